@@ -1,0 +1,319 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident aggregated params/s at K=8 neighbors (BASELINE.json metric).
+
+Workload (N=1, BASELINE config 3): 64 simulated devices on nx.random_regular_graph(8, 64,
+seed=0), ResNet-50 state_dicts (reference layout: 23,573,962 fp32 + 53 int64 elements), every
+device aggregating its 8 neighbors + itself (M = 9, self last, unweighted 1/M) — one step =
+one whole aggregation round (64 aggregation calls) executed by the K3 round kernel over the
+device-resident pool, inputs already in HBM, snapshot semantics, exact reference numerics.
+
+With --gpus N > 1 (launched by torch.distributed.run, one rank per GPU) the graph has 64*N
+devices (weak scaling: 64 per GPU, contiguous blocks); neighbor models owned by other GPUs
+arrive by RCCL send/recv over xGMI, overlapped with the interior rows' reduction.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md for the byte accounting.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--model", default="resnet50", choices=["resnet18", "resnet50", "vit_b16", "cifar10"])
+    p.add_argument("--devices-per-gpu", type=int, default=64)
+    p.add_argument("--degree", type=int, default=8)
+    p.add_argument("--mode", default="exact", choices=["exact", "fma"])
+    p.add_argument("--c4", type=int, default=0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU baseline sample")
+    p.add_argument("--no-k1", action="store_true", help="skip the per-call K1 side measurement")
+    p.add_argument("--host-path", action="store_true", help="also time the H2D+K1+D2H per-call path")
+    return p.parse_args()
+
+
+def round_spec(n_devices: int, degree: int, seed: int = 0):
+    import networkx as nx
+
+    g = nx.random_regular_graph(degree, n_devices, seed=seed)
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(n_devices)]
+    weights = [[1 / len(o)] * len(o) for o in orders]  # unweighted_module_avg, client.py:431
+    return orders, weights
+
+
+def fill_pool(pool, seed: int):
+    import torch
+
+    g = torch.Generator(device=pool.device)
+    g.manual_seed(seed)
+    pool.f32.normal_(generator=g)
+    pool.i64.random_(0, 1_000_000, generator=g)
+
+
+def cpu_baseline(layout_list, m: int, budget_s: float):
+    """The reference loop (clone/mul/add_/load_state_dict, oracle/torch_path.py) on host cores."""
+    import torch
+
+    from oracle import torch_path
+    from topology_aware_learning_amd import synth
+
+    sds = [synth.synth_state_dict(layout_list, 100 + i) for i in range(m)]
+    target = synth.synth_state_dict(layout_list, 99)
+    w = [1 / m] * m
+    torch_path.aggregate_call(sds, w, target)  # warm-up
+    n_out = sum(t.numel() for t in target.values())
+    calls = 0
+    t0 = time.perf_counter()
+    while True:
+        torch_path.aggregate_call(sds, w, target)
+        calls += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or calls >= 64:
+            break
+    return dict(value=calls * n_out / el, unit="params/s", cores=torch.get_num_threads(), kind="port",
+                sample=f"{calls} reference aggregation calls (M={m}, {n_out} params each, state_dicts in host "
+                       f"memory, torch CPU ops clone/mul/add_/copy_) in {el:.2f} s",
+                ms_per_call=1e3 * el / calls)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from topology_aware_learning_amd import ops, synth
+    from topology_aware_learning_amd.arena import ModelPool, StateLayout
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    lay = synth.get_layout(args.model)
+    layout = StateLayout.from_layout(lay)
+    n_params = layout.n_f32 + layout.n_i64
+    mode = ops.MODE_EXACT if args.mode == "exact" else ops.MODE_FMA
+    n_dev_total = args.devices_per_gpu * world
+    orders, weights = round_spec(n_dev_total, args.degree)
+    M = args.degree + 1
+
+    if world == 1:
+        from topology_aware_learning_amd import ops as _ops
+
+        rows = n_dev_total
+        pin = ModelPool(layout, rows, dev)
+        pout = ModelPool(layout, rows, dev)
+        fill_pool(pin, 1234)
+        row_ptr, col, w = _round_csr(orders, weights)
+        plan = _ops.build_plan(row_ptr, col, w, np.arange(rows, dtype=np.int32), c4=args.c4).to(dev)
+
+        def step(a, b):
+            _ops.round_f32(a.f32, b.f32, plan, n=layout.n_f32, mode=mode)
+            _ops.round_i64(a.i64, b.i64, plan, n=layout.n_i64)
+
+        # correctness spot check at full size: K3 row 0 == K1 on the same operands (bitwise)
+        step(pin, pout)
+        chk = torch.empty(layout.n_f32, dtype=torch.float32, device=dev)
+        _ops.agg_f32([pin.row_f32(j) for j in orders[0]], weights[0], chk, mode=mode)
+        parity_ok = bool(torch.equal(chk.view(torch.int32), pout.row_f32(0).view(torch.int32)))
+
+        pools = [pin, pout]
+        for i in range(args.warmup):
+            step(pools[i % 2], pools[(i + 1) % 2])
+        stream = torch.cuda.current_stream(dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            a, b = pools[i % 2], pools[(i + 1) % 2]
+            ev[i][0].record(stream)
+            _ops.round_f32(a.f32, b.f32, plan, n=layout.n_f32, mode=mode)
+            ev[i][1].record(stream)
+            _ops.round_i64(a.i64, b.i64, plan, n=layout.n_i64)
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        k_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+        staged = plan.info.total_src
+        bytes_round = 4 * layout.n_f32 * (staged + rows)  # compulsory: each staged source read once, each output written once
+        per_call_bytes = 4 * layout.n_f32 * (len(col) + rows)  # SURVEY §8(d) B summed over the round's calls
+        result_extra = dict(
+            kernel="k_round_tiled_f32", plan=dict(groups=plan.info.n_groups, staged_sources=staged,
+                                                  c4=plan.info.c4, lds_bytes=plan.info.lds_bytes),
+            per_call_equivalent_GBps=per_call_bytes / (k_ms * 1e-3) / 1e9, parity_k3_vs_k1_row0=parity_ok)
+        steps_done = args.steps
+        units = rows * n_params * steps_done
+        k1 = None
+        if not args.no_k1:
+            k1 = bench_k1(layout, pin, orders, weights, mode, dev)
+        hostp = bench_host_path(lay, M, dev) if args.host_path else None
+    else:
+        from topology_aware_learning_amd.distributed import ShardedRound
+
+        sr = ShardedRound(layout, orders, weights, rank, world, dev, mode=mode)
+        fill_pool(sr.pool_a, 1234 + rank)
+        for _ in range(args.warmup):
+            sr.step()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        k_ms_list = []
+        for _ in range(args.steps):
+            k_ms_list.append(sr.step(timed=True))
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        el_local = time.perf_counter() - t0
+        t = torch.tensor([el_local], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        torch.cuda.synchronize(dev)
+        k_ms = float(np.mean([x for x in k_ms_list if x is not None])) if any(k_ms_list) else float("nan")
+        staged = sr.staged_sources
+        rows = sr.local_rows
+        bytes_round = 4 * layout.n_f32 * (staged + rows)
+        result_extra = dict(kernel="k_round_tiled_f32", halo_rows_in=sr.halo_rows_in,
+                            halo_bytes_in=sr.halo_rows_in * 4 * layout.ld_f32)
+        units = n_dev_total * n_params * args.steps
+        parity_ok = None
+        k1 = None
+        hostp = None
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    achieved = bytes_round / (k_ms * 1e-3) / 1e9
+    traffic = load_traffic(args.model)
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(lay, M, args.cpu_seconds)
+    value = units / el
+    out = {
+        "metric": "device-resident aggregated params/s at K=8 neighbors",
+        "value": value,
+        "unit": "params/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * el / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if args.mode == "exact" else "f32-fma",
+        "data": "synthetic (random fp32 / int64 state_dicts of the reference layout in HBM)",
+        "config": {"workload": f"{n_dev_total}-device random {args.degree}-regular graph (seed 0), "
+                               f"{args.model} state_dicts, K={args.degree} (M={M}, self last), unweighted, "
+                               "one full aggregation round per step, snapshot semantics",
+                   "model_layout": args.model, "devices": n_dev_total, "devices_per_gpu": args.devices_per_gpu,
+                   "params_per_model": n_params, "parallelism": f"row-sharded x{world}" if world > 1 else "1 GPU"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                     "bytes_per_launch": bytes_round, "kernel_ms": k_ms},
+        "cpu_baseline": cpu,
+        "parity": parity_ok,
+        **result_extra,
+    }
+    if k1 is not None:
+        out["k1_per_call"] = k1
+    if hostp is not None:
+        out["host_path_per_call"] = hostp
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _round_csr(orders, weights):
+    from topology_aware_learning_amd.round import csr_from_lists
+
+    return csr_from_lists(orders, weights)
+
+
+def bench_k1(layout, pool, orders, weights, mode, dev, reps: int = 20):
+    """Per-call K1 (no cross-call reuse) on row 0's operands: SURVEY §8(d) B = 4N(M+1)."""
+    import torch
+
+    from topology_aware_learning_amd import ops
+
+    out = torch.empty(layout.n_f32, dtype=torch.float32, device=dev)
+    xs = [pool.row_f32(j) for j in orders[0]]
+    for _ in range(3):
+        ops.agg_f32(xs, weights[0], out, mode=mode)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ts = []
+    for r in range(reps):
+        xs = [pool.row_f32(j) for j in orders[r % len(orders)]]  # rotate rows: defeat the MALL
+        s.record()
+        ops.agg_f32(xs, weights[r % len(orders)], out, mode=mode)
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e))
+    ms = float(np.median(ts))
+    m = len(orders[0])
+    b = 4 * layout.n_f32 * (m + 1)
+    return dict(kernel="k_agg_f32_vec", ms=ms, bytes=b, GBps=b / (ms * 1e-3) / 1e9,
+                frac=b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, params_per_s=(layout.n_f32 + layout.n_i64) / (ms * 1e-3))
+
+
+def bench_host_path(lay, m, dev, reps: int = 5):
+    """Reference-shaped call: CPU state_dicts -> pinned H2D -> K1 -> D2H -> load into CPU model."""
+    import torch
+    import torch.nn as nn
+
+    from topology_aware_learning_amd import synth
+    from topology_aware_learning_amd.aggregate import aggregate_models
+
+    class Holder(nn.Module):
+        def __init__(self, sd):
+            super().__init__()
+            for i, (k, v) in enumerate(sd.items()):
+                self.register_buffer(f"b{i}", v.clone())
+
+    models = [Holder(synth.synth_state_dict(lay, 300 + i)) for i in range(m)]
+    w = [1 / m] * m
+    aggregate_models(models, w, models[-1])
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        aggregate_models(models, w, models[-1])
+    torch.cuda.synchronize(dev)
+    ms = 1e3 * (time.perf_counter() - t0) / reps
+    n = sum(v.numel() for v in models[0].state_dict().values())
+    return dict(ms=ms, params_per_s=n / (ms * 1e-3), note="includes pack, H2D, kernel, D2H, unpack")
+
+
+def load_traffic(model: str):
+    """HBM bytes per launch of k_round_tiled_f32 from the committed rocprofv3 PMC summary."""
+    f = ROOT / "profiles" / "traffic.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        return d.get(model, {}).get("bytes_per_launch")
+    except Exception:
+        return None
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,153 @@
+/*
+ * tal_agg.h — C-ABI of the MI355X (gfx950) neighbor-model aggregation library.
+ *
+ * The reference (msakarvadia/topology_aware_learning) is pure Python: its hot path is the
+ * inner loop shared by every aggregation app,
+ *
+ *     src/decentralized_client.py:399-413   (weighted_module_avg)
+ *     src/decentralized_client.py:433-446   (unweighted_module_avg)
+ *     src/decentralized_client.py:535-549   (sim_centrality_module_avg)
+ *     src/decentralized_client.py:597-611   (centrality_module_avg)
+ *     src/decentralized_client.py:630-645   (scale_agg)
+ *
+ *         avg[name]  = w_0 * clone(sd_0[name])            # fp32(w) * x, rounded to fp32
+ *         avg[name] += w_i * clone(sd_i[name])  (i=1..M-1) # separate fp32 add, no FMA
+ *         model.load_state_dict(avg)                       # int64 buffers: trunc toward 0
+ *
+ * and its caller, the round driver src/decentralized_app.py:605-641, which submits one such
+ * call per simulated device.  The reference binds no native code, so there is no FFI to
+ * mirror; the entry points below are what a ctypes binding of that loop would call (see
+ * INTEGRATION.md).  They replace the torch CPU ops clone/mul/add_/copy_ on that path.
+ *
+ * Conventions
+ *   - every function returns 0 (TAL_OK) or a TAL_ERR_* code; tal_last_error() gives a
+ *     thread-local message for the last failure on the calling thread.
+ *   - all data pointers are DEVICE pointers owned by the caller; host arrays are named *_host.
+ *   - `stream` is a hipStream_t (NULL = the default stream); calls are stream-ordered and
+ *     never synchronize the device; the library allocates no device memory.
+ *   - weights arrive as float64 (Python floats / numpy float64 in the reference) and are
+ *     rounded to fp32 exactly as torch does for `python_float * fp32_tensor`.
+ *   - mode: TAL_MODE_EXACT reproduces the reference bit for bit (ordered i=0..M-1,
+ *     separate fp32 multiply and add); TAL_MODE_FMA fuses them (tolerance M*2^-24*sum|w x|).
+ */
+#ifndef TAL_AGG_H
+#define TAL_AGG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TAL_OK 0
+#define TAL_ERR_INVALID 1   /* bad argument (null pointer, size, alias, plan mismatch) */
+#define TAL_ERR_HIP 2       /* HIP runtime error (launch / attribute) */
+#define TAL_ERR_CAPACITY 3  /* plan does not fit (a row has more sources than the LDS tile) */
+
+#define TAL_MODE_FMA 0
+#define TAL_MODE_EXACT 1
+
+/* Thread-local text of the last error on this thread ("" if none). */
+const char* tal_last_error(void);
+/* ABI version (bumped on any signature change). */
+int32_t tal_abi_version(void);
+
+/* ---- K1: one aggregation call over M flattened operands --------------------------------
+ * out[e] = sum_{i<M} fp32(w_host[i]) * x[i][e]   for e < n  (fp32 segment)
+ * Replaces decentralized_client.py:399-411 (+ the fp32 part of load_state_dict :413).
+ * x_host: host array of M device pointers.  out may alias any x[i] (the reference's
+ * aggregating client is itself the last operand, decentralized_app.py:625).  */
+int32_t tal_agg_f32(const float* const* x_host, const double* w_host, int32_t m,
+                    float* out, int64_t n, int32_t mode, void* stream);
+
+/* int64 buffers (num_batches_tracked): torch promotes `python_float * int64_tensor` to
+ * fp32, accumulates in fp32 and load_state_dict's copy_ truncates toward zero
+ * (decentralized_client.py:407-413).  NaN / out-of-range results give INT64_MIN, as the
+ * x86 cvttss2si the reference runs on does. */
+int32_t tal_agg_i64(const int64_t* const* x_host, const double* w_host, int32_t m,
+                    int64_t* out, int64_t n, void* stream);
+
+/* ---- K3: one whole aggregation round over a device-resident model pool -----------------
+ * Row r of the round computes pool_out[out_row[r]][e] = sum_k fp32(w[k]) * pool_in[col[k]][e]
+ * over k = row_ptr[r] .. row_ptr[r+1]-1 in that (reference) order, for e < n.  All rows read
+ * the pool as it was before the round ("snapshot" semantics).
+ *
+ * The host first turns the CSR into a tile plan (rows grouped so that each group's distinct
+ * sources fit one LDS tile); the plan is a flat int32 blob the caller copies to the device.
+ */
+typedef struct tal_round_plan_info {
+  int32_t rows;          /* rows in the round */
+  int32_t nnz;           /* operands over all rows */
+  int32_t n_groups;      /* row groups */
+  int32_t total_src;     /* staged sources summed over groups */
+  int32_t max_src;       /* largest group source count (sizes the LDS tile) */
+  int32_t max_rows;      /* largest group row count */
+  int32_t max_nnz;       /* largest group operand count */
+  int32_t c4;            /* float4 columns per staged source row per tile (16, 32 or 64) */
+  int32_t lds_bytes;     /* LDS per workgroup the round kernel will request */
+  /* offsets (in int32 words) of the plan's arrays inside the blob */
+  int32_t off_grp_row_ptr;  /* [n_groups+1] */
+  int32_t off_grp_src_ptr;  /* [n_groups+1] */
+  int32_t off_src_row;      /* [total_src]  pool_in row of each staged source */
+  int32_t off_row_ptr;      /* [rows+1] */
+  int32_t off_op_slot;      /* [nnz] staged-source slot of each operand (within its group) */
+  int32_t off_op_w;         /* [nnz] fp32 weight bits */
+  int32_t off_out_row;      /* [rows] pool_out row of each row */
+  int32_t words;            /* total int32 words of the blob */
+} tal_round_plan_info;
+
+/* Upper bound on the blob size in int32 words for a round of `rows` rows / `nnz` operands. */
+int64_t tal_round_plan_words(int32_t rows, int64_t nnz);
+
+/* Build the plan on the host.  row_ptr_host[rows+1], col_host[nnz], w_host[nnz] (float64),
+ * out_row_host[rows].  c4 in {16,32,64}; lds_bytes = LDS budget per workgroup for the tile
+ * (max sources per group = lds_bytes / (16*c4)).  Rows keep their order; consecutive rows
+ * share a group while the union of their sources fits.  Returns TAL_ERR_CAPACITY if one
+ * row alone has more distinct sources than fit. */
+int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host,
+                             const double* w_host, const int32_t* out_row_host, int32_t c4,
+                             int32_t lds_bytes, int32_t* plan_host, int64_t plan_capacity_words,
+                             tal_round_plan_info* info);
+
+/* Execute the round on the fp32 segment (n elements per model; row stride ld_in / ld_out in
+ * elements).  plan_dev = the blob copied to the device.  pool_out may equal pool_in only if
+ * the plan has a single group (each workgroup stages every source of its tile in LDS before
+ * it writes).  16-B aligned pools with ld % 4 == 0 take the float4 path; others the scalar
+ * tiled path. */
+int32_t tal_agg_round_f32(const float* pool_in, int64_t ld_in, float* pool_out, int64_t ld_out,
+                          int64_t n, const int32_t* plan_dev, const tal_round_plan_info* info,
+                          int32_t mode, void* stream);
+
+/* The same round on the int64 segment (fp32 accumulate, truncation, as tal_agg_i64). */
+int32_t tal_agg_round_i64(const int64_t* pool_in, int64_t ld_in, int64_t* pool_out,
+                          int64_t ld_out, int64_t n, const int32_t* plan_dev,
+                          const tal_round_plan_info* info, void* stream);
+
+/* ---- K2: cosine similarity of two models' parameters --------------------------------------
+ * Reference: cosine_similarity, decentralized_client.py:661-681: for each parameter tensor
+ * viewed as [A, I, B] (dim 1 = the reduced dim; 1-D tensors are unsqueezed to [n, 1]),
+ * nn.CosineSimilarity(dim=1, eps=1e-6) gives A*B values whose mean is taken; the result is
+ * the average of those means over tensors.
+ *
+ * seg_host: 4*n_seg int64 {offset (elements into the flat parameter arena), A, I, B}.
+ * The host cuts the segments into workgroup chunks (plan, int64 words, copied to the device
+ * by the caller); each chunk is either "row" work (B == 1, I > 1: one wavefront per output,
+ * lanes stride the contiguous row and reduce with cross-lane shuffles) or "column" work
+ * (one lane per output).  One pass reads each model once (dot, |a|^2, |b|^2 fused).
+ *
+ * a_ptrs_host / b_ptrs_host: n_pairs device pointers; pair j compares model a_j with b_j
+ * (flat fp32 parameter arenas of the same layout).  scratch: device buffer of at least
+ * tal_cosine_scratch_bytes(n_chunks, n_pairs) bytes.  out_dev: n_pairs fp32 results. */
+int64_t tal_cosine_plan_words(const int64_t* seg_host, int32_t n_seg);
+int32_t tal_cosine_plan_build(const int64_t* seg_host, int32_t n_seg, int64_t* plan_host,
+                              int64_t plan_capacity_words, int32_t* n_chunks);
+int64_t tal_cosine_scratch_bytes(int32_t n_chunks, int32_t n_pairs);
+int32_t tal_cosine_params(const float* const* a_ptrs_host, const float* const* b_ptrs_host,
+                          int32_t n_pairs, const int64_t* plan_dev, int32_t n_chunks,
+                          int32_t n_seg, void* scratch, float* out_dev, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TAL_AGG_H */

@@ -1,0 +1,103 @@
+"""TEST INFRASTRUCTURE — the CPU oracle for the aggregation hot path.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this package,
+and only as the checker / the timed CPU baseline: the product (topology_aware_learning_amd,
+src/) never imports it and has no CPU fallback.
+
+Contents
+  agg_oracle.c / Makefile  plain-C restatement of the reference arithmetic
+                           (src/decentralized_client.py:399-413) — `agg_f32`, `agg_i64`,
+                           `round_f32`, `round_i64` below are its numpy wrappers
+  reference_alg.py         numpy restatement of the host-side logic on the path: weight
+                           vectors of every app, cosine similarity, round semantics
+  torch_path.py            the reference loop restated with the same torch CPU ops
+                           (clone / mul / add_ / load_state_dict) — bench.py's cpu_baseline
+
+Pinning: tests/test_oracle_golden.py checks all of it against golden vectors generated from
+the reference itself (tests/golden/make_golden.py).
+"""
+from __future__ import annotations
+
+import ctypes
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "_build" / "liboracle_agg.so"
+
+
+def build() -> Path:
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        src = HERE / "agg_oracle.c"
+        if not LIB.exists() or LIB.stat().st_mtime < src.stat().st_mtime:
+            build()
+        L = ctypes.CDLL(str(LIB))
+        P = ctypes.c_void_p
+        L.oracle_agg_f32.argtypes = [P, P, ctypes.c_int32, P, ctypes.c_int64]
+        L.oracle_agg_i64.argtypes = [P, P, ctypes.c_int32, P, ctypes.c_int64]
+        rargs = [P, ctypes.c_int64, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, P, P, P, P]
+        L.oracle_round_f32.argtypes = rargs
+        L.oracle_round_i64.argtypes = rargs
+        _lib = L
+    return _lib
+
+
+def _ptrs(arrs):
+    a = (ctypes.c_void_p * len(arrs))()
+    for i, x in enumerate(arrs):
+        a[i] = x.ctypes.data
+    return a
+
+
+def agg_f32(xs, w) -> np.ndarray:
+    """One call, fp32 operands (list of equal-length 1-D arrays), float64 weights."""
+    xs = [np.ascontiguousarray(x, dtype=np.float32).reshape(-1) for x in xs]
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    out = np.empty_like(xs[0])
+    lib().oracle_agg_f32(_ptrs(xs), w.ctypes.data, len(xs), out.ctypes.data, out.size)
+    return out
+
+
+def agg_i64(xs, w) -> np.ndarray:
+    xs = [np.ascontiguousarray(x, dtype=np.int64).reshape(-1) for x in xs]
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    out = np.empty_like(xs[0])
+    lib().oracle_agg_i64(_ptrs(xs), w.ctypes.data, len(xs), out.ctypes.data, out.size)
+    return out
+
+
+def _round(fn, pool_in, row_ptr, col, w, out_row, pool_out):
+    row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int32)
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    out_row = np.ascontiguousarray(out_row, dtype=np.int32)
+    assert pool_in.flags.c_contiguous and pool_out.flags.c_contiguous
+    fn(pool_in.ctypes.data, pool_in.shape[1], pool_out.ctypes.data, pool_out.shape[1], pool_in.shape[1],
+       len(out_row), row_ptr.ctypes.data, col.ctypes.data, w.ctypes.data, out_row.ctypes.data)
+    return pool_out
+
+
+def round_f32(pool_in, row_ptr, col, w, out_row, pool_out=None) -> np.ndarray:
+    """Snapshot round over a [models, n] fp32 pool (pool_out defaults to a copy of pool_in)."""
+    pool_in = np.ascontiguousarray(pool_in, dtype=np.float32)
+    if pool_out is None:
+        pool_out = pool_in.copy()
+    return _round(lib().oracle_round_f32, pool_in, row_ptr, col, w, out_row, pool_out)
+
+
+def round_i64(pool_in, row_ptr, col, w, out_row, pool_out=None) -> np.ndarray:
+    pool_in = np.ascontiguousarray(pool_in, dtype=np.int64)
+    if pool_out is None:
+        pool_out = pool_in.copy()
+    return _round(lib().oracle_round_i64, pool_in, row_ptr, col, w, out_row, pool_out)

@@ -1,0 +1,329 @@
+"""Generate the golden fixtures under tests/golden/ FROM THE REFERENCE ITSELF.
+
+Runs only in the build container, where the read-only reference is mounted at
+/root/reference (it never travels to the GPU box; only the data files written here do).
+The reference imports with two shims: parsl and torchvision are absent, so
+`parsl.app.app.python_app` becomes the identity decorator and torchvision an empty module.
+
+Outputs (all data, no reference source):
+  tiny_cases.json / tiny_cases.npz   every aggregation app on small synthetic state_dicts:
+                                     inputs, outputs, kwargs, cosine values
+  layouts.json                       state_dict layouts of the reference's models
+  big_sha256.json                    ResNet-18 M=3 / ResNet-50 M=9 outputs as per-entry sha256
+  weights_onehot.json                fp32 aggregation weights the apps use on known graphs
+  centrality.json                    reference centrality dicts for those graphs
+  schedulers.json                    softmax_coeff sequences of every scheduler (100 rounds)
+  round_4ring.npz / .json            sequential in-place round driven through the reference
+
+Usage:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import sys
+import types
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+ROOT = HERE.parent.parent
+REF = Path("/root/reference")
+sys.path.insert(0, str(ROOT))
+
+
+def import_reference():
+    import transformers  # noqa: F401  (must precede the torchvision stub: it probes __spec__)
+
+    parsl = types.ModuleType("parsl")
+    app = types.ModuleType("parsl.app")
+    appapp = types.ModuleType("parsl.app.app")
+    appapp.python_app = lambda *a, **k: (lambda f: f)
+    sys.modules.update({"parsl": parsl, "parsl.app": app, "parsl.app.app": appapp})
+    tv = types.ModuleType("torchvision")
+    tvt = types.ModuleType("torchvision.transforms")
+    tvd = types.ModuleType("torchvision.datasets")
+    tv.transforms, tv.datasets = tvt, tvd
+    sys.modules.update({"torchvision": tv, "torchvision.transforms": tvt, "torchvision.datasets": tvd})
+    sys.path.insert(0, str(REF))
+    import src.decentralized_client as dc  # reference module
+    import src.aggregation_scheduler as sch
+    from src.models import resnet
+    from src import modules
+
+    return dc, sch, resnet, modules
+
+
+import torch  # noqa: E402
+import torch.nn as nn  # noqa: E402
+import networkx as nx  # noqa: E402
+from torch.utils.data import Subset, TensorDataset  # noqa: E402
+
+from topology_aware_learning_amd import synth  # noqa: E402
+
+
+class TinyNet(nn.Module):
+    """Small module covering every entry kind the reference models have."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv = nn.Conv2d(3, 4, 3)            # [4,3,3,3] + bias  (cosine: column kind, B=9)
+        self.bn = nn.BatchNorm2d(4)               # weight/bias/running_*/num_batches_tracked
+        self.pw = nn.Conv2d(4, 6, 1, bias=False)  # [6,4,1,1]          (row kind, B=1)
+        self.fc = nn.Linear(13, 5)                # [5,13] + bias (odd sizes -> n % 4 tails)
+        self.bn2 = nn.BatchNorm1d(5)
+
+
+class Vec(nn.Module):
+    def __init__(self, m):
+        super().__init__()
+        self.v = nn.Parameter(torch.zeros(m))
+
+
+DUMMY = TensorDataset(torch.zeros(4, 1), torch.zeros(4, dtype=torch.long))
+
+
+def make_client(dc, idx, model, n_train=10, neighbors=()):
+    data = TensorDataset(torch.zeros(n_train, 1), torch.zeros(n_train, dtype=torch.long))
+    return dc.DecentralClient(
+        idx=idx, prox_coeff=0.0, model=model, train_data=Subset(data, list(range(n_train))),
+        test_data=None, valid_data=None, global_test_data=DUMMY, global_backdoor_test_data=None,
+        neighbors=list(neighbors), neighbor_probs=[1.0] * len(neighbors),
+    )
+
+
+def sd_np(model):
+    return {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+
+
+def tiny_inputs(layout, seed, case_i, op_i, M):
+    sd = synth.synth_state_dict(layout, seed)
+    # special values on selected operands (still finite where NaN payloads would differ)
+    if op_i == 0 and case_i % 3 == 0:
+        sd["fc.weight"].view(-1)[0] = 1.0e-40      # fp32 denormal
+        sd["fc.weight"].view(-1)[1] = -0.0
+        sd["fc.weight"].view(-1)[2] = 3.0e38       # w*x and sums near overflow
+    if case_i % 4 == 1:
+        sd["fc.bias"].view(-1)[0] = float(2 ** 24 + 1)
+    for k in ("bn.num_batches_tracked", "bn2.num_batches_tracked"):
+        choices = {1: 7, 2: 1000, 3: 1000, 9: 1000, 17: 10}
+        v = choices.get(M, 123456)
+        if case_i % 5 == 4:
+            v = 123456789 + op_i * 1000003     # not representable in fp32
+        if case_i % 7 == 6:
+            v = 2 ** 31 + 5 + op_i
+        sd[k].fill_(v)
+    return sd
+
+
+def gen_tiny(dc, out_json, out_npz):
+    torch.manual_seed(0)
+    layout = synth.layout_of(TinyNet().state_dict())
+    g = nx.barabasi_albert_graph(20, 2, seed=0)
+    topo = nx.to_numpy_array(g)
+    rng = np.random.default_rng(0)
+    cent = dc.create_centrality_dict(topo, rng)
+    cases, arrays = [], {}
+    specs = []
+    for M in (1, 2, 3, 9, 17):
+        specs.append(("unweighted_module_avg", M, {}))
+        specs.append(("weighted_module_avg", M, {}))
+        specs.append(("scale_agg", M, {}))
+        specs.append(("test_agg", M, {}))
+        for metric in ("degree", "betweenness", "random"):
+            for sm, coeff in ((True, 10.0), (True, -10.0), (False, 10.0)):
+                specs.append(("centrality_module_avg", M, dict(centrality_metric=metric, softmax=sm, softmax_coeff=coeff)))
+        if M >= 2:
+            for metric in ("degree", "betweenness"):
+                for sm, coeff in ((True, 10.0), (True, -7.5), (False, 10.0)):
+                    specs.append(("sim_centrality_module_avg", M, dict(centrality_metric=metric, softmax=sm, softmax_coeff=coeff)))
+    for ci, (fn_name, M, kw) in enumerate(specs):
+        idxs = sorted(rng.choice(20, size=M, replace=False).tolist())
+        self_idx = idxs[-1]
+        order = idxs[:-1] + [self_idx]  # self last (decentralized_app.py:625)
+        lens = [int(x) for x in rng.integers(1, 500, size=M)]
+        clients = []
+        for oi, idx in enumerate(order):
+            m = TinyNet()
+            m.load_state_dict(tiny_inputs(layout, 1000 * ci + oi, ci, oi, M))
+            clients.append((["r"], make_client(dc, idx, m, n_train=lens[oi])))
+        for oi, c in enumerate(clients):
+            for k, v in sd_np(c[1].model).items():
+                arrays[f"c{ci}_in{oi}_{k}"] = v
+        cos = []
+        if fn_name == "sim_centrality_module_avg":
+            for c in clients[:-1]:
+                cos.append(float(dc.cosine_similarity(clients[-1][1].model, c[1].model)))
+        fn = getattr(dc, fn_name)
+        kwargs = dict(centrality_metric=kw.get("centrality_metric"), centrality_dict=cent,
+                      softmax=kw.get("softmax", False), softmax_coeff=kw.get("softmax_coeff", 10.0))
+        res = fn(clients[-1], 0, *clients, **kwargs)
+        assert res is clients[-1]
+        for k, v in sd_np(res[1].model).items():
+            arrays[f"c{ci}_out_{k}"] = v
+        cases.append(dict(case=ci, fn=fn_name, M=M, order=order, data_lens=lens,
+                          centrality_metric=kw.get("centrality_metric"),
+                          softmax=kw.get("softmax", False), softmax_coeff=kw.get("softmax_coeff", 10.0),
+                          cosine=cos))
+    meta = dict(layout=layout, graph="barabasi_albert_graph(20, 2, seed=0)",
+                centrality={k: {str(i): float(v) for i, v in d.items()} for k, d in cent.items()},
+                cases=cases)
+    out_json.write_text(json.dumps(meta, indent=1))
+    np.savez_compressed(out_npz, **arrays)
+    print(f"tiny: {len(cases)} cases")
+
+
+def gen_layouts(resnet, modules, out):
+    from src.types import DataChoices  # reference enum (imported via the reference path)
+
+    lay = {
+        "cifar10": synth.layout_of(modules.create_model(DataChoices.CIFAR10).state_dict()),
+        "resnet18": synth.layout_of(resnet.ResNet18().state_dict()),
+        "resnet50": synth.layout_of(resnet.ResNet50().state_dict()),
+    }
+    out.write_text(json.dumps(lay))
+    print({k: (len(v), synth.layout_counts(v)) for k, v in lay.items()})
+    return lay
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def gen_big(dc, resnet, out):
+    results = []
+    g = nx.random_regular_graph(8, 64, seed=0)
+    topo = nx.to_numpy_array(g)
+    cent = dc.create_centrality_dict(topo, np.random.default_rng(0))
+    specs = [
+        ("resnet18", 3, "unweighted_module_avg", [31, 1, 0], {}),
+        ("resnet50", 9, "unweighted_module_avg", sorted(g.neighbors(0)) + [0], {}),
+        ("resnet50", 9, "weighted_module_avg", sorted(g.neighbors(5)) + [5], {}),
+        ("resnet50", 9, "centrality_module_avg", sorted(g.neighbors(7)) + [7],
+         dict(centrality_metric="degree", softmax=True, softmax_coeff=10.0)),
+        ("resnet50", 9, "centrality_module_avg", sorted(g.neighbors(9)) + [9],
+         dict(centrality_metric="betweenness", softmax=True, softmax_coeff=-10.0)),
+    ]
+    ctor = {"resnet18": resnet.ResNet18, "resnet50": resnet.ResNet50}
+    for si, (model_name, M, fn_name, order, kw) in enumerate(specs):
+        layout = synth.layout_of(ctor[model_name]().state_dict())
+        clients = []
+        lens = [100 + 37 * i for i in range(M)]
+        for oi, idx in enumerate(order):
+            m = ctor[model_name]()
+            m.load_state_dict(synth.synth_state_dict(layout, 7000 + 100 * si + idx))
+            clients.append((["r"], make_client(dc, idx, m, n_train=lens[oi])))
+        kwargs = dict(centrality_metric=kw.get("centrality_metric"), centrality_dict=cent,
+                      softmax=kw.get("softmax", False), softmax_coeff=kw.get("softmax_coeff", 10.0))
+        res = getattr(dc, fn_name)(clients[-1], 0, *clients, **kwargs)
+        outsd = sd_np(res[1].model)
+        results.append(dict(model=model_name, M=M, fn=fn_name, order=order, data_lens=lens,
+                            seeds=[7000 + 100 * si + idx for idx in order],
+                            centrality_metric=kw.get("centrality_metric"), softmax=kw.get("softmax", False),
+                            softmax_coeff=kw.get("softmax_coeff", 10.0),
+                            graph="random_regular_graph(8, 64, seed=0)",
+                            sha256={k: sha(v) for k, v in outsd.items()},
+                            samples={k: [float(x) for x in v.reshape(-1)[:3]] for k, v in list(outsd.items())[:4]}))
+        print("big", model_name, fn_name)
+    out.write_text(json.dumps(dict(centrality={k: {str(i): float(v) for i, v in d.items()} for k, d in cent.items()},
+                                   cases=results), indent=1))
+
+
+def gen_weights(dc, out_w, out_c):
+    graphs = {
+        "cycle_graph(8)": nx.cycle_graph(8),
+        "barabasi_albert_graph(33, 2, seed=0)": nx.barabasi_albert_graph(33, 2, seed=0),
+    }
+    res, cents = [], {}
+    for gname, g in graphs.items():
+        topo = nx.to_numpy_array(g)
+        cent = dc.create_centrality_dict(topo, np.random.default_rng(0))
+        cents[gname] = {k: {str(i): float(v) for i, v in d.items()} for k, d in cent.items()}
+        for node in g.nodes:
+            order = np.where(topo[node] > 0)[0].tolist() + [node]
+            M = len(order)
+            for metric in ("degree", "betweenness"):
+                for sm, coeff in ((True, 10.0), (True, -10.0), (False, 10.0)):
+                    clients = []
+                    for oi, idx in enumerate(order):
+                        m = Vec(M)
+                        with torch.no_grad():
+                            m.v[oi] = 1.0
+                        clients.append((["r"], make_client(dc, idx, m)))
+                    r = dc.centrality_module_avg(clients[-1], 0, *clients, centrality_metric=metric,
+                                                 centrality_dict=cent, softmax=sm, softmax_coeff=coeff)
+                    w = r[1].model.v.detach().numpy()
+                    res.append(dict(graph=gname, node=int(node), order=order, metric=metric, softmax=sm,
+                                    coeff=coeff, w_f32_bits=[int(b) for b in w.view(np.uint32)]))
+    out_w.write_text(json.dumps(res))
+    out_c.write_text(json.dumps(cents))
+    print("weights:", len(res))
+
+
+def gen_schedulers(sch, out):
+    seqs = {}
+    specs = {
+        "base": lambda: sch.BaseScheduler(softmax_coeff=10.0),
+        "exp": lambda: sch.ExponentialScheduler(gamma=0.95, softmax_coeff=10.0),
+        "exp_eta": lambda: sch.ExponentialScheduler(gamma=0.9, eta_min=3, softmax_coeff=10.0),
+        "osc": lambda: sch.OscilateScheduler(T_0=5, softmax_coeff=10.0),
+        "ca": lambda: sch.CosineAnnealingWarmRestarts(T_0=10, eta_min=-5, softmax_coeff=10.0),
+        "ca_mult2": lambda: sch.CosineAnnealingWarmRestarts(T_0=4, T_mult=2, eta_min=1, softmax_coeff=100),
+    }
+    for name, mk in specs.items():
+        s = mk()
+        vals = []
+        for r in range(100):
+            vals.append(float(s.get_softmax_coeff()))
+            s.step(r)
+        seqs[name] = vals
+    # CosineAnnealingWarmRestarts rejects a float T_0 (decentralized_main.py passes --T_0 as float)
+    try:
+        sch.CosineAnnealingWarmRestarts(T_0=66.0)
+        seqs["ca_float_T0_raises"] = False
+    except ValueError:
+        seqs["ca_float_T0_raises"] = True
+    out.write_text(json.dumps(seqs))
+    print("schedulers:", list(seqs))
+
+
+def gen_round(dc, out_npz, out_json):
+    torch.manual_seed(0)
+    layout = synth.layout_of(TinyNet().state_dict())
+    n = 4
+    g = nx.cycle_graph(n)
+    topo = nx.to_numpy_array(g)
+    clients = []
+    arrays = {}
+    for i in range(n):
+        m = TinyNet()
+        m.load_state_dict(synth.synth_state_dict(layout, 500 + i))
+        clients.append((["r"], make_client(dc, i, m, neighbors=np.where(topo[i] > 0)[0].tolist())))
+        for k, v in sd_np(m).items():
+            arrays[f"in{i}_{k}"] = v
+    orders = []
+    for i in range(n):  # decentralized_app.py:605-641 with one thread, clients in index order
+        order = clients[i][1].neighbors + [i]
+        orders.append(order)
+        dc.unweighted_module_avg(clients[i], 0, *[clients[j] for j in order])
+    for i in range(n):
+        for k, v in sd_np(clients[i][1].model).items():
+            arrays[f"seq{i}_{k}"] = v
+    np.savez_compressed(out_npz, **arrays)
+    out_json.write_text(json.dumps(dict(layout=layout, orders=orders, graph="cycle_graph(4)")))
+    print("round: sequential in-place 4-ring")
+
+
+def main():
+    dc, sch, resnet, modules = import_reference()
+    gen_layouts(resnet, modules, HERE / "layouts.json")
+    gen_tiny(dc, HERE / "tiny_cases.json", HERE / "tiny_cases.npz")
+    gen_weights(dc, HERE / "weights_onehot.json", HERE / "centrality.json")
+    gen_schedulers(sch, HERE / "schedulers.json")
+    gen_round(dc, HERE / "round_4ring.npz", HERE / "round_4ring.json")
+    gen_big(dc, resnet, HERE / "big_sha256.json")
+
+
+if __name__ == "__main__":
+    main()

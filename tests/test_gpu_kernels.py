@@ -1,0 +1,264 @@
+"""GPU parity of the HIP kernels (through the C-ABI) against the C oracle.
+
+Bar: bit-exact in EXACT mode (fp32 and int64), M*2^-24*sum|w x| in FMA mode.
+"""
+import hashlib
+import json
+
+import networkx as nx
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from oracle import reference_alg as ra
+from topology_aware_learning_amd import ops, synth
+from topology_aware_learning_amd.arena import ModelPool, StateLayout
+from topology_aware_learning_amd.round import RoundExecutor
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand_f32(rng, n, special=False):
+    x = rng.standard_normal(n).astype(np.float32) * np.float32(3.0)
+    if special and n > 8:
+        x[0] = 1e-40
+        x[1] = -0.0
+        x[2] = 3e38
+        x[3] = -1e-45
+        x[4] = 65504.0
+    return x
+
+
+def _bits_equal(a, b):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    if a.dtype == np.float32:
+        na, nb = np.isnan(a), np.isnan(b)
+        assert np.array_equal(na, nb)
+        return np.array_equal(a[~na].view(np.uint32), b[~nb].view(np.uint32))
+    return np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("m", [1, 2, 3, 4, 8, 9, 16, 17, 18, 33, 64, 65, 130, 256, 300])
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 1027, 262147])
+def test_agg_f32_exact(cuda, m, n):
+    rng = np.random.default_rng(m * 1000 + n)
+    xs = [_rand_f32(rng, n, special=(i == 0)) for i in range(m)]
+    w = rng.random(m)
+    w = list(w / w.sum())
+    ref = oracle.agg_f32(xs, w)
+    dx = [torch.from_numpy(x).to(cuda) for x in xs]
+    out = torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.agg_f32(dx, w, out)
+    assert _bits_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("m", [1, 3, 9, 17, 70])
+def test_agg_f32_in_place_self_last(cuda, m):
+    """The aggregating client is the last operand and the output (decentralized_app.py:625)."""
+    rng = np.random.default_rng(m)
+    n = 100003
+    xs = [_rand_f32(rng, n) for _ in range(m)]
+    w = [1 / m] * m
+    ref = oracle.agg_f32(xs, w)
+    dx = [torch.from_numpy(x).to(cuda) for x in xs]
+    ops.agg_f32(dx, w, dx[-1])
+    assert _bits_equal(dx[-1].cpu().numpy(), ref)
+
+
+def test_agg_f32_unaligned(cuda):
+    rng = np.random.default_rng(5)
+    n, m = 50001, 9
+    base = [torch.from_numpy(_rand_f32(rng, n + 1)).to(cuda) for _ in range(m)]
+    xs = [b[1:] for b in base]  # 4-byte offset: scalar path
+    w = [1 / m] * m
+    ref = oracle.agg_f32([x.cpu().numpy() for x in xs], w)
+    out = torch.empty(n + 1, dtype=torch.float32, device=cuda)[1:]
+    ops.agg_f32(xs, w, out)
+    assert _bits_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("m", [2, 9, 17])
+def test_agg_f32_fma_tolerance(cuda, m):
+    rng = np.random.default_rng(11 + m)
+    n = 200000
+    xs = [_rand_f32(rng, n) for _ in range(m)]
+    w = list(rng.random(m))
+    ref = oracle.agg_f32(xs, w).astype(np.float64)
+    dx = [torch.from_numpy(x).to(cuda) for x in xs]
+    out = torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.agg_f32(dx, w, out, mode=ops.MODE_FMA)
+    bound = m * 2.0 ** -24 * sum(abs(np.float32(wi) * x.astype(np.float64)) for wi, x in zip(w, xs))
+    assert np.all(np.abs(out.cpu().numpy().astype(np.float64) - ref) <= 2 * bound + 1e-45)
+
+
+@pytest.mark.parametrize("m", [1, 3, 9, 17, 200])
+def test_agg_i64_truncation(cuda, m):
+    rng = np.random.default_rng(m)
+    n = 4099
+    xs = [rng.integers(-(2 ** 40), 2 ** 40, size=n).astype(np.int64) for _ in range(m)]
+    for x in xs:
+        x[:10] = [0, 1, 7, 10, 1000, 123456789, 2 ** 24 + 1, 2 ** 31 + 5, -1000, 999]
+    w = [1 / m] * m
+    ref = oracle.agg_i64(xs, w)
+    dx = [torch.from_numpy(x).to(cuda) for x in xs]
+    out = torch.empty(n, dtype=torch.int64, device=cuda)
+    ops.agg_i64(dx, w, out)
+    assert np.array_equal(out.cpu().numpy(), ref)
+    if m == 9:
+        assert ref[4] == 999  # nine copies of 1000 at w=1/9 come back as 999
+
+
+def _graph_csr(g, weights="unweighted"):
+    orders, ws = [], []
+    cent = nx.degree_centrality(g)
+    for i in sorted(g.nodes):
+        o = sorted(g.neighbors(i)) + [i]
+        orders.append(o)
+        if weights == "unweighted":
+            ws.append(ra.unweighted_weights(len(o)))
+        else:
+            ws.append(ra.centrality_weights(o, cent, True, 10.0))
+    return orders, ws
+
+
+@pytest.mark.parametrize("graph,n,c4,lds", [
+    ("ring", 1000, 0, ops.LDS_BUDGET),
+    ("regular", 4099, 64, ops.LDS_BUDGET),
+    ("regular", 4099, 32, ops.LDS_BUDGET),
+    ("regular", 4099, 16, ops.LDS_BUDGET),
+    ("regular", 70001, 64, 24 * 1024),      # forces several row groups
+    ("barbell", 3001, 0, ops.LDS_BUDGET),
+    ("complete", 515, 0, 160 * 1024),
+])
+def test_round_f32_vs_oracle(cuda, graph, n, c4, lds):
+    g = {
+        "ring": nx.cycle_graph(16),
+        "regular": nx.random_regular_graph(8, 64, seed=0),
+        "barbell": nx.barbell_graph(12, 4),
+        "complete": nx.complete_graph(40),
+    }[graph]
+    orders, ws = _graph_csr(g, "softmax" if graph == "regular" else "unweighted")
+    rows = len(orders)
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    out_rows = np.arange(rows, dtype=np.int32)
+    rng = np.random.default_rng(rows + n)
+    pool = np.stack([_rand_f32(rng, n) for _ in range(rows)])
+    ref = oracle.round_f32(pool, row_ptr, col, w, out_rows)
+    plan = ops.build_plan(row_ptr, col, w, out_rows, c4=c4, lds_bytes=lds)
+    pin = torch.from_numpy(pool).to(cuda)
+    pout = torch.zeros_like(pin)
+    ops.round_f32(pin, pout, plan)
+    assert _bits_equal(pout.cpu().numpy(), ref)
+    if plan.single_group:  # in place is snapshot-safe with one group
+        ops.round_f32(pin, pin, plan)
+        assert _bits_equal(pin.cpu().numpy(), ref)
+
+
+def test_round_f32_padded_ld_and_tail(cuda):
+    g = nx.random_regular_graph(4, 20, seed=1)
+    orders, ws = _graph_csr(g)
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    out_rows = np.arange(20, dtype=np.int32)
+    n, ld = 1030, 1088
+    rng = np.random.default_rng(3)
+    pool = np.zeros((20, ld), np.float32)
+    pool[:, :n] = rng.standard_normal((20, n)).astype(np.float32)
+    ref = oracle.round_f32(pool[:, :n].copy(), row_ptr, col, w, out_rows)
+    plan = ops.build_plan(row_ptr, col, w, out_rows)
+    pin = torch.from_numpy(pool).to(cuda)
+    pout = torch.full_like(pin, 7.0)
+    ops.round_f32(pin, pout, plan, n=n)
+    got = pout.cpu().numpy()
+    assert _bits_equal(got[:, :n], ref)
+    assert np.all(got[:, n:] == 7.0)  # padding untouched
+    # odd ld -> scalar tiled path
+    pin2 = torch.from_numpy(np.ascontiguousarray(pool[:, :n + 1])).to(cuda)
+    pout2 = torch.zeros_like(pin2)
+    ops.round_f32(pin2, pout2, plan, n=n)
+    assert _bits_equal(pout2.cpu().numpy()[:, :n], ref)
+
+
+def test_round_i64(cuda):
+    g = nx.random_regular_graph(8, 64, seed=0)
+    orders, ws = _graph_csr(g)
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    out_rows = np.arange(64, dtype=np.int32)
+    rng = np.random.default_rng(9)
+    pool = rng.integers(0, 10 ** 6, size=(64, 53)).astype(np.int64)
+    pool[:, 0] = 1000
+    ref = oracle.round_i64(pool, row_ptr, col, w, out_rows)
+    plan = ops.build_plan(row_ptr, col, w, out_rows)
+    pin = torch.from_numpy(pool).to(cuda)
+    pout = torch.zeros_like(pin)
+    ops.round_i64(pin, pout, plan)
+    assert np.array_equal(pout.cpu().numpy(), ref)
+    assert np.all(ref[:, 0] == 999)
+
+
+def test_round_sequential_matches_reference_fixture(cuda):
+    """Sequential in-place 4-ring round driven through the reference (tests/golden/round_4ring)."""
+    meta = json.loads((GOLDEN / "round_4ring.json").read_text())
+    z = np.load(GOLDEN / "round_4ring.npz")
+    layout = StateLayout.from_layout([(n, tuple(s), d) for n, s, d in meta["layout"]])
+    pool = ModelPool(layout, 4, cuda)
+    for i in range(4):
+        pool.load_row(i, {n: torch.from_numpy(z[f"in{i}_{n}"]) for n, _, _ in meta["layout"]})
+    ex = RoundExecutor(pool)
+    orders = meta["orders"]
+    ex.run(orders, [ra.unweighted_weights(len(o)) for o in orders], sequential=True)
+    for i in range(4):
+        sd = pool.state_dict(i)
+        for n, _, _ in meta["layout"]:
+            assert _bits_equal(sd[n].cpu().numpy(), z[f"seq{i}_{n}"]), (i, n)
+
+
+def test_big_sha256_k1(cuda):
+    """ResNet-18 M=3 / ResNet-50 M=9 reference outputs (sha256 per entry) through K1."""
+    meta = json.loads((GOLDEN / "big_sha256.json").read_text())
+    layouts = json.loads((GOLDEN / "layouts.json").read_text())
+    cent = {k: {int(i): v for i, v in d.items()} for k, d in meta["centrality"].items()}
+    for case in meta["cases"]:
+        lay = [(n, tuple(s), d) for n, s, d in layouts[case["model"]]]
+        layout = StateLayout.from_layout(lay)
+        order = case["order"]
+        if case["fn"] == "unweighted_module_avg":
+            w = ra.unweighted_weights(len(order))
+        elif case["fn"] == "weighted_module_avg":
+            w = ra.weighted_weights(case["data_lens"])
+        else:
+            w = ra.centrality_weights(order, cent[case["centrality_metric"]], case["softmax"], case["softmax_coeff"])
+        pool = ModelPool(layout, len(order), cuda)
+        for r, seed in enumerate(case["seeds"]):
+            pool.load_row(r, synth.synth_state_dict(lay, seed))
+        ops.agg_f32([pool.row_f32(r) for r in range(len(order))], w, pool.row_f32(len(order) - 1))
+        ops.agg_i64([pool.row_i64(r) for r in range(len(order))], w, pool.row_i64(len(order) - 1))
+        sd = pool.state_dict(len(order) - 1)
+        for name, digest in case["sha256"].items():
+            a = sd[name].cpu().numpy()
+            assert hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest() == digest, (case["fn"], name)
+
+
+def test_cosine_kernel_vs_numpy(cuda):
+    lay = synth.get_layout("resnet18")
+    layout = StateLayout.from_layout(lay)
+    names = synth.param_names(lay)
+    segs = layout.param_segments(names)
+    plan = ops.build_cosine_plan(segs)
+    a = synth.synth_state_dict(lay, 1)
+    bs = [synth.synth_state_dict(lay, 2 + j) for j in range(3)]
+    # make one pair strongly similar
+    for k in bs[0]:
+        if bs[0][k].dtype == torch.float32:
+            bs[0][k] = a[k] * 2 + 0.01 * bs[0][k]
+    pool = ModelPool(layout, 4, cuda)
+    pool.load_row(0, a)
+    for j, b in enumerate(bs):
+        pool.load_row(1 + j, b)
+    got = ops.cosine([pool.row_f32(0)] * 3, [pool.row_f32(1 + j) for j in range(3)], plan).cpu().numpy()
+    for j, b in enumerate(bs):
+        ref = ra.cosine_similarity([a[n].numpy() for n in names], [b[n].numpy() for n in names])
+        assert abs(got[j] - ref) < 2e-5, (j, got[j], ref)

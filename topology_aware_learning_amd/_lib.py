@@ -1,0 +1,153 @@
+"""ctypes binding of the gfx950 C-ABI library (include/tal_agg.h).
+
+This is the only way the package reaches the device: there is no CPU fallback.  If the
+library is missing or fails to load, every operation raises ``TalLibraryError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+
+# torch ships its own libamdhip64.so (soname libamdhip64.so.7, ROCm 7.0).  Loading torch first
+# makes the dynamic linker resolve our library's libamdhip64.so.7 dependency to that same
+# runtime, so torch's streams and device pointers are valid in our calls.
+import torch  # noqa: F401  (import order matters, see above)
+
+LIB_PATH = Path(__file__).resolve().parent / "libtal_agg.so"
+
+TAL_OK = 0
+TAL_ERR_INVALID = 1
+TAL_ERR_HIP = 2
+TAL_ERR_CAPACITY = 3
+TAL_MODE_FMA = 0
+TAL_MODE_EXACT = 1
+ABI_VERSION = 2
+
+EXPORTED = (
+    "tal_last_error",
+    "tal_abi_version",
+    "tal_agg_f32",
+    "tal_agg_i64",
+    "tal_round_plan_words",
+    "tal_round_plan_build",
+    "tal_agg_round_f32",
+    "tal_agg_round_i64",
+    "tal_cosine_plan_words",
+    "tal_cosine_plan_build",
+    "tal_cosine_scratch_bytes",
+    "tal_cosine_params",
+)
+
+
+class TalLibraryError(RuntimeError):
+    """The HIP library is unavailable (not built / not loadable)."""
+
+
+class TalError(RuntimeError):
+    """A C-ABI call returned a non-zero status."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[tal status {code}] {msg}")
+        self.code = code
+
+
+class RoundPlanInfo(ctypes.Structure):
+    _fields_ = [
+        ("rows", ctypes.c_int32),
+        ("nnz", ctypes.c_int32),
+        ("n_groups", ctypes.c_int32),
+        ("total_src", ctypes.c_int32),
+        ("max_src", ctypes.c_int32),
+        ("max_rows", ctypes.c_int32),
+        ("max_nnz", ctypes.c_int32),
+        ("c4", ctypes.c_int32),
+        ("lds_bytes", ctypes.c_int32),
+        ("off_grp_row_ptr", ctypes.c_int32),
+        ("off_grp_src_ptr", ctypes.c_int32),
+        ("off_src_row", ctypes.c_int32),
+        ("off_row_ptr", ctypes.c_int32),
+        ("off_op_slot", ctypes.c_int32),
+        ("off_op_w", ctypes.c_int32),
+        ("off_out_row", ctypes.c_int32),
+        ("words", ctypes.c_int32),
+    ]
+
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_PP = ctypes.POINTER(ctypes.c_void_p)
+_PD = ctypes.POINTER(ctypes.c_double)
+_PI32 = ctypes.POINTER(ctypes.c_int32)
+_PI64 = ctypes.POINTER(ctypes.c_int64)
+
+_SIGS = {
+    "tal_last_error": (ctypes.c_char_p, []),
+    "tal_abi_version": (_I32, []),
+    "tal_agg_f32": (_I32, [_PP, _PD, _I32, _P, _I64, _I32, _P]),
+    "tal_agg_i64": (_I32, [_PP, _PD, _I32, _P, _I64, _P]),
+    "tal_round_plan_words": (_I64, [_I32, _I64]),
+    "tal_round_plan_build": (
+        _I32,
+        [_I32, _PI32, _PI32, _PD, _PI32, _I32, _I32, _PI32, _I64, ctypes.POINTER(RoundPlanInfo)],
+    ),
+    "tal_agg_round_f32": (_I32, [_P, _I64, _P, _I64, _I64, _P, ctypes.POINTER(RoundPlanInfo), _I32, _P]),
+    "tal_agg_round_i64": (_I32, [_P, _I64, _P, _I64, _I64, _P, ctypes.POINTER(RoundPlanInfo), _P]),
+    "tal_cosine_plan_words": (_I64, [_PI64, _I32]),
+    "tal_cosine_plan_build": (_I32, [_PI64, _I32, _PI64, _I64, _PI32]),
+    "tal_cosine_scratch_bytes": (_I64, [_I32, _I32]),
+    "tal_cosine_params": (_I32, [_PP, _PP, _I32, _P, _I32, _I32, _P, _P, _P]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
+    """Load (once) and return the library; raises TalLibraryError if it is not there."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = Path(path) if path is not None else LIB_PATH
+        if not p.exists():
+            raise TalLibraryError(
+                f"{p} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(hipcc --offload-arch=gfx950). There is no CPU fallback."
+            )
+        try:
+            lib = ctypes.CDLL(str(p))
+        except OSError as exc:  # pragma: no cover - depends on the box
+            raise TalLibraryError(f"cannot load {p}: {exc}") from exc
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        ver = lib.tal_abi_version()
+        if ver != ABI_VERSION:
+            raise TalLibraryError(f"{p} has ABI {ver}, expected {ABI_VERSION}: rebuild it")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc: int) -> None:
+    if rc != TAL_OK:
+        msg = load().tal_last_error().decode(errors="replace")
+        raise TalError(rc, msg)
+
+
+def ptr_array(ptrs) -> ctypes.Array:
+    arr = (ctypes.c_void_p * len(ptrs))()
+    for i, p in enumerate(ptrs):
+        arr[i] = int(p)
+    return arr
+
+
+def double_array(vals) -> ctypes.Array:
+    arr = (ctypes.c_double * len(vals))()
+    for i, v in enumerate(vals):
+        arr[i] = float(v)
+    return arr

@@ -1,0 +1,228 @@
+"""Flattened state_dict layout and the device-resident model pool.
+
+A model's state_dict is split into two flat segments: every fp32 entry back to back (the
+"f32 segment", where the kernels stream) and every int64 entry (the "i64 segment",
+num_batches_tracked counters).  A ``ModelPool`` holds many models of one layout as rows of two
+2-D device tensors ``f32[rows, ld_f32]`` / ``i64[rows, ld_i64]`` (rows 256-B aligned), and can
+rebind an ``nn.Module``'s parameters and buffers to views of a row — so training, optimizers and
+the aggregation kernels all work on the same HBM bytes, with no pack/unpack per call
+(SURVEY §7 "state_dict flattening without re-packing every call", §8(f) rank 1).
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from dataclasses import dataclass
+from typing import Dict, List, Mapping, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+SUPPORTED = {torch.float32: "f32", torch.int64: "i64"}
+ROW_ALIGN = 64  # elements: 256 B for fp32 rows
+
+
+def _round_up(x: int, a: int) -> int:
+    return (x + a - 1) // a * a
+
+
+@dataclass(frozen=True)
+class Entry:
+    name: str
+    shape: Tuple[int, ...]
+    dtype: torch.dtype
+    seg: str          # "f32" | "i64"
+    offset: int       # element offset inside its segment
+    numel: int
+    alias_of: Optional[str] = None  # tied entry (same storage as an earlier key)
+
+
+class StateLayout:
+    """Segments of a state_dict (entry order = state_dict order)."""
+
+    def __init__(self, entries: Sequence[Entry]):
+        self.entries: List[Entry] = list(entries)
+        self.by_name: Dict[str, Entry] = {e.name: e for e in self.entries}
+        self.n_f32 = sum(e.numel for e in self.entries if e.seg == "f32" and e.alias_of is None)
+        self.n_i64 = sum(e.numel for e in self.entries if e.seg == "i64" and e.alias_of is None)
+        self.ld_f32 = max(_round_up(self.n_f32, ROW_ALIGN), ROW_ALIGN)
+        self.ld_i64 = max(_round_up(self.n_i64, 8), 8)
+        self.key = tuple((e.name, e.shape, str(e.dtype), e.alias_of) for e in self.entries)
+
+    def __eq__(self, other) -> bool:
+        return isinstance(other, StateLayout) and self.key == other.key
+
+    def __hash__(self) -> int:
+        return hash(self.key)
+
+    @classmethod
+    def from_state_dict(cls, sd: Mapping[str, torch.Tensor]) -> "StateLayout":
+        entries: List[Entry] = []
+        off = {"f32": 0, "i64": 0}
+        seen: Dict[Tuple[int, int, Tuple[int, ...]], str] = {}
+        for name, t in sd.items():
+            if t.dtype not in SUPPORTED:
+                raise NotImplementedError(
+                    f"state_dict entry {name!r} has dtype {t.dtype}; the aggregation kernels handle "
+                    "float32 and int64 entries (all the reference models have)")
+            seg = SUPPORTED[t.dtype]
+            key = (t.data_ptr(), t.storage_offset(), tuple(t.shape)) if t.numel() else None
+            if key is not None and key in seen and t.is_contiguous():
+                entries.append(Entry(name, tuple(t.shape), t.dtype, seg, by_name_offset(entries, seen[key]),
+                                     t.numel(), alias_of=seen[key]))
+                continue
+            entries.append(Entry(name, tuple(t.shape), t.dtype, seg, off[seg], t.numel()))
+            off[seg] += t.numel()
+            if key is not None:
+                seen[key] = name
+        return cls(entries)
+
+    @classmethod
+    def from_layout(cls, layout: Sequence[Tuple[str, Sequence[int], str]]) -> "StateLayout":
+        dt = {"float32": torch.float32, "int64": torch.int64}
+        sd = OrderedDict((n, torch.empty(tuple(s), dtype=dt[d], device="meta")) for n, s, d in layout)
+        entries: List[Entry] = []
+        off = {"f32": 0, "i64": 0}
+        for name, t in sd.items():
+            seg = SUPPORTED[t.dtype]
+            n = 1
+            for s in t.shape:
+                n *= int(s)
+            entries.append(Entry(name, tuple(t.shape), t.dtype, seg, off[seg], n))
+            off[seg] += n
+        return cls(entries)
+
+    def check_compatible(self, sd: Mapping[str, torch.Tensor], what: str = "state_dict") -> None:
+        """Same keys / shapes / dtypes as this layout (the reference would fail in `+=` or in
+        load_state_dict(strict=True) otherwise)."""
+        if len(sd) != len(self.entries):
+            raise RuntimeError(f"{what}: {len(sd)} entries, expected {len(self.entries)}")
+        for (name, t), e in zip(sd.items(), self.entries):
+            if name != e.name or tuple(t.shape) != e.shape or t.dtype != e.dtype:
+                raise RuntimeError(f"{what}: entry {name!r} {tuple(t.shape)} {t.dtype} does not match "
+                                   f"{e.name!r} {e.shape} {e.dtype}")
+
+    # ---------------------------------------------------------------------------------------
+    def views(self, f32: torch.Tensor, i64: torch.Tensor) -> "OrderedDict[str, torch.Tensor]":
+        out: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+        for e in self.entries:
+            base = f32 if e.seg == "f32" else i64
+            out[e.name] = base[e.offset: e.offset + e.numel].view(e.shape)
+        return out
+
+    def flatten_into(self, sd: Mapping[str, torch.Tensor], f32: torch.Tensor, i64: torch.Tensor,
+                     non_blocking: bool = False) -> None:
+        """Copy a state_dict's values into flat segment tensors (any devices)."""
+        for e in self.entries:
+            if e.alias_of is not None:
+                continue
+            base = f32 if e.seg == "f32" else i64
+            base[e.offset: e.offset + e.numel].copy_(sd[e.name].reshape(-1), non_blocking=non_blocking)
+
+    def flatten_cat(self, sd: Mapping[str, torch.Tensor], seg: str) -> List[torch.Tensor]:
+        return [sd[e.name].reshape(-1) for e in self.entries if e.seg == seg and e.alias_of is None]
+
+    def param_segments(self, param_names: Sequence[str]) -> List[Tuple[int, int, int, int]]:
+        """(offset, A, I, B) of each parameter for the cosine kernel: nn.CosineSimilarity(dim=1)
+        on the tensor, 1-D tensors unsqueezed to [n, 1] (decentralized_client.py:674-678)."""
+        segs = []
+        for name in param_names:
+            e = self.by_name[name]
+            if e.seg != "f32":
+                raise NotImplementedError(f"parameter {name} is not fp32")
+            s = e.shape
+            if len(s) < 2:
+                A, I, B = max(e.numel, 1), 1, 1
+            else:
+                A, I = s[0], s[1]
+                B = 1
+                for x in s[2:]:
+                    B *= x
+            segs.append((e.offset, int(A), int(I), int(B)))
+        return segs
+
+
+def by_name_offset(entries: Sequence[Entry], name: str) -> int:
+    for e in entries:
+        if e.name == name:
+            return e.offset
+    raise KeyError(name)
+
+
+def _resolve(module: nn.Module, name: str) -> Tuple[nn.Module, str]:
+    parts = name.split(".")
+    mod = module
+    for p in parts[:-1]:
+        mod = getattr(mod, p)
+    return mod, parts[-1]
+
+
+class ModelPool:
+    """Rows of flat model state on one GPU: f32[rows, ld_f32], i64[rows, ld_i64]."""
+
+    def __init__(self, layout: StateLayout, rows: int, device, f32: Optional[torch.Tensor] = None,
+                 i64: Optional[torch.Tensor] = None):
+        self.layout = layout
+        self.rows = rows
+        self.device = torch.device(device)
+        self.f32 = f32 if f32 is not None else torch.zeros(rows, layout.ld_f32, dtype=torch.float32, device=self.device)
+        self.i64 = i64 if i64 is not None else torch.zeros(rows, layout.ld_i64, dtype=torch.int64, device=self.device)
+        self._bound: Dict[int, int] = {}  # id(module) -> row
+
+    def row_f32(self, r: int) -> torch.Tensor:
+        return self.f32[r, : self.layout.n_f32]
+
+    def row_i64(self, r: int) -> torch.Tensor:
+        return self.i64[r, : self.layout.n_i64]
+
+    def load_row(self, r: int, sd: Mapping[str, torch.Tensor]) -> None:
+        self.layout.check_compatible(sd)
+        self.layout.flatten_into(sd, self.f32[r], self.i64[r])
+
+    def state_dict(self, r: int) -> "OrderedDict[str, torch.Tensor]":
+        return self.layout.views(self.f32[r], self.i64[r])
+
+    def bind(self, module: nn.Module, r: int) -> nn.Module:
+        """Copy `module`'s state into row r and make its parameters / buffers views of that row.
+
+        Parameter objects keep their identity (``param.data`` is re-pointed) so optimizers built
+        before or after binding keep working; buffers are re-registered as views."""
+        sd = module.state_dict()
+        self.layout.check_compatible(sd, "module")
+        with torch.no_grad():
+            self.layout.flatten_into(sd, self.f32[r], self.i64[r])
+        views = self.state_dict(r)
+        for e in self.layout.entries:
+            if e.alias_of is not None:
+                continue
+            mod, attr = _resolve(module, e.name)
+            v = views[e.name]
+            if attr in mod._parameters and mod._parameters[attr] is not None:
+                mod._parameters[attr].data = v
+            elif attr in mod._buffers:
+                mod._buffers[attr] = v
+            else:  # pragma: no cover - state_dict keys always resolve to a param or buffer
+                raise KeyError(e.name)
+        module._tal_pool = self  # type: ignore[attr-defined]
+        module._tal_row = r  # type: ignore[attr-defined]
+        self._bound[id(module)] = r
+        return module
+
+    def row_of(self, module: nn.Module) -> Optional[int]:
+        """Row the module is bound to, if its state still lives there (checked per entry)."""
+        if getattr(module, "_tal_pool", None) is not self:
+            return None
+        r = module._tal_row  # type: ignore[attr-defined]
+        views = self.state_dict(r)
+        for name, t in module.state_dict().items():
+            v = views.get(name)
+            if v is None or t.data_ptr() != v.data_ptr() or t.device != self.device:
+                return None
+        return r
+
+
+def bound_row(module: nn.Module) -> Optional[Tuple[ModelPool, int]]:
+    pool = getattr(module, "_tal_pool", None)
+    if pool is None:
+        return None
+    r = pool.row_of(module)
+    return None if r is None else (pool, r)

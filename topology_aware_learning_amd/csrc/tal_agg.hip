@@ -1,0 +1,855 @@
+// tal_agg.hip — MI355X (gfx950 / CDNA4) kernels + C-ABI for topology-weighted neighbor-model
+// aggregation.  See include/tal_agg.h for the contract and DESIGN.md for the roofline.
+//
+// Reference semantics (msakarvadia/topology_aware_learning, pure Python/PyTorch CPU):
+//   src/decentralized_client.py:399-413   avg  = fp32(w0)*x0 ; avg += fp32(wi)*xi ; load_state_dict
+//   src/decentralized_client.py:661-681   cosine_similarity (K2)
+//   src/decentralized_app.py:605-641      one call per simulated device per round (K3 batches them)
+//
+// Numerics: EXACT mode = one rounded fp32 multiply then one rounded fp32 add per operand, in
+// operand order — bit-identical to torch's `w * clone(v)` / `+=` on CPU.  This file is built
+// with -ffp-contract=off and the exact kernels use explicit __fmul_rn / __fadd_rn so no FMA can
+// be formed; the FMA mode uses __builtin_fmaf explicitly.
+//
+// The op is element-wise with arithmetic intensity ~0.1 flop/B: every kernel here is bound by
+// HBM3E bandwidth (no MFMA — nothing here is a contraction).
+
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/tal_agg.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kAbiVersion = 2;
+constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
+constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
+constexpr int kMaxGrid = 256 * 8; // 256 CUs x 8 resident 256-thread blocks
+
+thread_local std::string g_err;
+
+int32_t fail(int32_t code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int32_t check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(TAL_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  g_err.clear();
+  return TAL_OK;
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// ------------------------------------------------------------------------------------------
+// element arithmetic
+// ------------------------------------------------------------------------------------------
+template <bool EXACT>
+__device__ __forceinline__ float first_term(float w, float x) {
+  return __fmul_rn(w, x);
+}
+
+template <bool EXACT>
+__device__ __forceinline__ float next_term(float acc, float w, float x) {
+  if constexpr (EXACT) {
+    return __fadd_rn(acc, __fmul_rn(w, x));
+  } else {
+    return __builtin_fmaf(w, x, acc);
+  }
+}
+
+template <bool EXACT>
+__device__ __forceinline__ float4 first4(float w, float4 x) {
+  return make_float4(first_term<EXACT>(w, x.x), first_term<EXACT>(w, x.y),
+                     first_term<EXACT>(w, x.z), first_term<EXACT>(w, x.w));
+}
+
+template <bool EXACT>
+__device__ __forceinline__ float4 next4(float4 a, float w, float4 x) {
+  return make_float4(next_term<EXACT>(a.x, w, x.x), next_term<EXACT>(a.y, w, x.y),
+                     next_term<EXACT>(a.z, w, x.z), next_term<EXACT>(a.w, w, x.w));
+}
+
+// fp32 accumulator -> int64 the way load_state_dict's copy_ does it on x86: truncation toward
+// zero; NaN and out-of-range give INT64_MIN (cvttss2si "integer indefinite").
+__device__ __forceinline__ int64_t trunc_i64(float v) {
+  if (!(v >= -9.2233720368547758e18f && v < 9.2233720368547758e18f)) return INT64_MIN;
+  return static_cast<int64_t>(v);
+}
+
+// ------------------------------------------------------------------------------------------
+// K1: one aggregation call, M operands given as a pointer table in the kernel arguments
+// ------------------------------------------------------------------------------------------
+struct OpTableF32 {
+  const float* x[kMaxOps];
+  float w[kMaxOps];
+};
+
+struct OpTableI64 {
+  const int64_t* x[kMaxOps];
+  float w[kMaxOps];
+};
+
+// M_STATIC > 0: operand count known at compile time -> every operand's float4 load of an
+// element chunk is issued before the ordered accumulate (M loads in flight per lane).
+// M_STATIC == 0: runtime count, loads issued in batches of 8.
+// CONT: accumulate onto `out` (second and later passes when M > kMaxOps; keeps the exact order).
+template <int M_STATIC, bool EXACT, bool CONT>
+__global__ __launch_bounds__(kBlock) void k_agg_f32_vec(OpTableF32 t, int m_rt, float* out,
+                                                        int64_t n4) {
+  const int m = M_STATIC > 0 ? M_STATIC : m_rt;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n4; i += stride) {
+    float4 acc;
+    if constexpr (M_STATIC > 0) {
+      float4 v[M_STATIC];
+#pragma unroll
+      for (int k = 0; k < M_STATIC; ++k) v[k] = reinterpret_cast<const float4*>(t.x[k])[i];
+      int k0 = 0;
+      if constexpr (CONT) {
+        acc = reinterpret_cast<const float4*>(out)[i];
+      } else {
+        acc = first4<EXACT>(t.w[0], v[0]);
+        k0 = 1;
+      }
+#pragma unroll
+      for (int k = k0; k < M_STATIC; ++k) acc = next4<EXACT>(acc, t.w[k], v[k]);
+    } else {
+      int k = 0;
+      if constexpr (CONT) {
+        acc = reinterpret_cast<const float4*>(out)[i];
+      } else {
+        acc = first4<EXACT>(t.w[0], reinterpret_cast<const float4*>(t.x[0])[i]);
+        k = 1;
+      }
+      for (; k < m; k += 8) {
+        float4 v[8];
+        const int kn = min(8, m - k);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j < kn) v[j] = reinterpret_cast<const float4*>(t.x[k + j])[i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j < kn) acc = next4<EXACT>(acc, t.w[k + j], v[j]);
+      }
+    }
+    reinterpret_cast<float4*>(out)[i] = acc;
+  }
+}
+
+// Scalar form: unaligned pointers and the n % 4 tail.
+template <bool EXACT, bool CONT>
+__global__ __launch_bounds__(kBlock) void k_agg_f32_scalar(OpTableF32 t, int m, float* out,
+                                                           int64_t e0, int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t e = e0 + static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n;
+       e += stride) {
+    float acc;
+    int k = 0;
+    if constexpr (CONT) {
+      acc = out[e];
+    } else {
+      acc = first_term<EXACT>(t.w[0], t.x[0][e]);
+      k = 1;
+    }
+    for (; k < m; ++k) acc = next_term<EXACT>(acc, t.w[k], t.x[k][e]);
+    out[e] = acc;
+  }
+}
+
+// int64 buffers (num_batches_tracked): every operand converted to fp32 (round to nearest,
+// as torch's type promotion does), fp32 multiply-add chain, truncation on the store.
+// Single pass: all M <= kMaxOps operands are in the table, so `out` may alias any of them.
+__global__ __launch_bounds__(kBlock) void k_agg_i64(OpTableI64 t, int m, int64_t* out, int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n; e += stride) {
+    float acc = __fmul_rn(t.w[0], static_cast<float>(t.x[0][e]));
+    for (int k = 1; k < m; ++k)
+      acc = __fadd_rn(acc, __fmul_rn(t.w[k], static_cast<float>(t.x[k][e])));
+    out[e] = trunc_i64(acc);
+  }
+}
+
+int grid_for(int64_t work) {
+  int64_t b = (work + kBlock - 1) / kBlock;
+  if (b < 1) b = 1;
+  if (b > kMaxGrid) b = kMaxGrid;
+  return static_cast<int>(b);
+}
+
+template <bool EXACT, bool CONT>
+void launch_vec(const OpTableF32& t, int m, float* out, int64_t n4, hipStream_t s) {
+  const dim3 g(grid_for(n4)), b(kBlock);
+#define TAL_VEC_CASE(MM) \
+  case MM:               \
+    k_agg_f32_vec<MM, EXACT, CONT><<<g, b, 0, s>>>(t, m, out, n4); \
+    return;
+  switch (m) {
+    TAL_VEC_CASE(1) TAL_VEC_CASE(2) TAL_VEC_CASE(3) TAL_VEC_CASE(4) TAL_VEC_CASE(5)
+    TAL_VEC_CASE(6) TAL_VEC_CASE(7) TAL_VEC_CASE(8) TAL_VEC_CASE(9) TAL_VEC_CASE(10)
+    TAL_VEC_CASE(11) TAL_VEC_CASE(12) TAL_VEC_CASE(13) TAL_VEC_CASE(14) TAL_VEC_CASE(15)
+    TAL_VEC_CASE(16) TAL_VEC_CASE(17)
+    default:
+      k_agg_f32_vec<0, EXACT, CONT><<<g, b, 0, s>>>(t, m, out, n4);
+  }
+#undef TAL_VEC_CASE
+}
+
+template <bool EXACT, bool CONT>
+void launch_scalar(const OpTableF32& t, int m, float* out, int64_t e0, int64_t n, hipStream_t s) {
+  if (n <= e0) return;
+  k_agg_f32_scalar<EXACT, CONT><<<grid_for(n - e0), kBlock, 0, s>>>(t, m, out, e0, n);
+}
+
+template <bool EXACT>
+void launch_pass(const OpTableF32& t, int m, bool cont, bool vec, float* out, int64_t n,
+                 hipStream_t s) {
+  const int64_t n4 = vec ? n / 4 : 0;
+  if (cont) {
+    if (n4) launch_vec<EXACT, true>(t, m, out, n4, s);
+    launch_scalar<EXACT, true>(t, m, out, n4 * 4, n, s);
+  } else {
+    if (n4) launch_vec<EXACT, false>(t, m, out, n4, s);
+    launch_scalar<EXACT, false>(t, m, out, n4 * 4, n, s);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K3: whole-round aggregation over a device pool, LDS-tiled.
+//   grid = (column tiles, row groups).  A workgroup stages tile c (C4 float4 per source) of
+//   every distinct source of its group into LDS (one HBM read per source per tile, however
+//   many rows of the group use it), plus the group's slice of the plan; after one barrier
+//   each wavefront walks rows and emits out[row][tile c] with the operands in reference order.
+//   HBM traffic per tile = (sources + rows) * C4 * 16 B instead of (nnz + rows) * C4 * 16 B.
+// ------------------------------------------------------------------------------------------
+struct PlanView {
+  const int32_t* grp_row_ptr;
+  const int32_t* grp_src_ptr;
+  const int32_t* src_row;
+  const int32_t* row_ptr;
+  const int32_t* op_slot;
+  const float* op_w;
+  const int32_t* out_row;
+};
+
+PlanView make_view(const int32_t* plan, const tal_round_plan_info& in) {
+  PlanView v;
+  v.grp_row_ptr = plan + in.off_grp_row_ptr;
+  v.grp_src_ptr = plan + in.off_grp_src_ptr;
+  v.src_row = plan + in.off_src_row;
+  v.row_ptr = plan + in.off_row_ptr;
+  v.op_slot = plan + in.off_op_slot;
+  v.op_w = reinterpret_cast<const float*>(plan + in.off_op_w);
+  v.out_row = plan + in.off_out_row;
+  return v;
+}
+
+// LDS layout of one workgroup: [max_src * C4 float4 data][row_ptr (rows+1)][slot (nnz)][w (nnz)]
+template <int C4, bool EXACT>
+__global__ __launch_bounds__(kBlock) void k_round_tiled_f32(const float* __restrict__ pin,
+                                                            int64_t ld_in4,
+                                                            float* __restrict__ pout,
+                                                            int64_t ld_out4, int64_t n4,
+                                                            PlanView p, int max_src) {
+  extern __shared__ float4 s_data[];
+  const int g = blockIdx.y;
+  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * C4;
+
+  const int s_beg = p.grp_src_ptr[g];
+  const int ns = p.grp_src_ptr[g + 1] - s_beg;
+  const int r_beg = p.grp_row_ptr[g];
+  const int nr = p.grp_row_ptr[g + 1] - r_beg;
+  const int o_beg = p.row_ptr[r_beg];
+  const int no = p.row_ptr[r_beg + nr] - o_beg;
+
+  int32_t* s_rowptr = reinterpret_cast<int32_t*>(s_data + static_cast<size_t>(max_src) * C4);
+  int32_t* s_slot = s_rowptr + (nr + 1);
+  float* s_w = reinterpret_cast<float*>(s_slot + no);
+
+  // stage the plan slice
+  for (int k = threadIdx.x; k <= nr; k += kBlock) s_rowptr[k] = p.row_ptr[r_beg + k] - o_beg;
+  for (int k = threadIdx.x; k < no; k += kBlock) {
+    s_slot[k] = p.op_slot[o_beg + k] * C4;
+    s_w[k] = p.op_w[o_beg + k];
+  }
+  // stage tile c0 of every source of the group (each wave reads C4*16 contiguous bytes/source)
+  const int64_t cols = min(static_cast<int64_t>(C4), n4 - c0);
+  for (int k = threadIdx.x; k < ns * C4; k += kBlock) {
+    const int s = k / C4;
+    const int c = k % C4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < cols) {
+      const int64_t row = p.src_row[s_beg + s];
+      v = reinterpret_cast<const float4*>(pin)[row * ld_in4 + c0 + c];
+    }
+    s_data[k] = v;
+  }
+  __syncthreads();
+
+  constexpr int kRowsPerPass = kBlock / C4;
+  const int c = threadIdx.x % C4;
+  const int rsub = threadIdx.x / C4;
+  if (c >= cols) return;
+  for (int r = rsub; r < nr; r += kRowsPerPass) {
+    const int q0 = s_rowptr[r];
+    const int q1 = s_rowptr[r + 1];
+    float4 acc = first4<EXACT>(s_w[q0], s_data[s_slot[q0] + c]);
+    for (int q = q0 + 1; q < q1; ++q) acc = next4<EXACT>(acc, s_w[q], s_data[s_slot[q] + c]);
+    const int64_t orow = p.out_row[r_beg + r];
+    reinterpret_cast<float4*>(pout)[orow * ld_out4 + c0 + c] = acc;
+  }
+}
+
+// Scalar tiled round: the fp32 tail (elements e0..n-1 when the float4 path ran) or whole
+// unaligned pools, and the int64 segment (IS_I64: fp32 accumulate, truncation).  The tile is
+// 4*c4 elements so one staged source costs the same 16*c4 LDS bytes as in the float4 kernel.
+template <bool IS_I64, bool EXACT>
+__global__ __launch_bounds__(kBlock) void k_round_tiled_scalar(const void* __restrict__ pin_v,
+                                                               int64_t ld_in,
+                                                               void* __restrict__ pout_v,
+                                                               int64_t ld_out, int64_t e0,
+                                                               int64_t n, PlanView p,
+                                                               int max_src, int tile) {
+  extern __shared__ float s_f[];
+  const int g = blockIdx.y;
+  const int64_t t0 = e0 + static_cast<int64_t>(blockIdx.x) * tile;
+
+  const int s_beg = p.grp_src_ptr[g];
+  const int ns = p.grp_src_ptr[g + 1] - s_beg;
+  const int r_beg = p.grp_row_ptr[g];
+  const int nr = p.grp_row_ptr[g + 1] - r_beg;
+  const int o_beg = p.row_ptr[r_beg];
+  const int no = p.row_ptr[r_beg + nr] - o_beg;
+
+  int32_t* s_rowptr = reinterpret_cast<int32_t*>(s_f + static_cast<size_t>(max_src) * tile);
+  int32_t* s_slot = s_rowptr + (nr + 1);
+  float* s_w = reinterpret_cast<float*>(s_slot + no);
+
+  for (int k = threadIdx.x; k <= nr; k += kBlock) s_rowptr[k] = p.row_ptr[r_beg + k] - o_beg;
+  for (int k = threadIdx.x; k < no; k += kBlock) {
+    s_slot[k] = p.op_slot[o_beg + k] * tile;
+    s_w[k] = p.op_w[o_beg + k];
+  }
+  const int64_t cols = min(static_cast<int64_t>(tile), n - t0);
+  for (int k = threadIdx.x; k < ns * tile; k += kBlock) {
+    const int s = k / tile;
+    const int c = k % tile;
+    float v = 0.f;
+    if (c < cols) {
+      const int64_t row = p.src_row[s_beg + s];
+      if constexpr (IS_I64) {
+        v = static_cast<float>(static_cast<const int64_t*>(pin_v)[row * ld_in + t0 + c]);
+      } else {
+        v = static_cast<const float*>(pin_v)[row * ld_in + t0 + c];
+      }
+    }
+    s_f[k] = v;
+  }
+  __syncthreads();
+
+  const int rows_per_pass = kBlock / tile;
+  const int c = threadIdx.x % tile;
+  const int rsub = threadIdx.x / tile;
+  if (c >= cols) return;
+  for (int r = rsub; r < nr; r += rows_per_pass) {
+    const int q0 = s_rowptr[r];
+    const int q1 = s_rowptr[r + 1];
+    float acc;
+    if constexpr (IS_I64) {
+      acc = __fmul_rn(s_w[q0], s_f[s_slot[q0] + c]);
+      for (int q = q0 + 1; q < q1; ++q)
+        acc = __fadd_rn(acc, __fmul_rn(s_w[q], s_f[s_slot[q] + c]));
+    } else {
+      acc = first_term<EXACT>(s_w[q0], s_f[s_slot[q0] + c]);
+      for (int q = q0 + 1; q < q1; ++q) acc = next_term<EXACT>(acc, s_w[q], s_f[s_slot[q] + c]);
+    }
+    const int64_t orow = p.out_row[r_beg + r];
+    if constexpr (IS_I64) {
+      static_cast<int64_t*>(pout_v)[orow * ld_out + t0 + c] = trunc_i64(acc);
+    } else {
+      static_cast<float*>(pout_v)[orow * ld_out + t0 + c] = acc;
+    }
+  }
+}
+
+size_t plan_lds_bytes(const tal_round_plan_info& in, int tile_bytes_per_src) {
+  return static_cast<size_t>(in.max_src) * tile_bytes_per_src +
+         static_cast<size_t>(in.max_rows + 1 + 2 * in.max_nnz) * 4;
+}
+
+std::mutex g_lds_mu;
+std::vector<const void*> g_lds_raised;
+
+int32_t ensure_lds(const void* kernel, size_t bytes) {
+  // Dynamic LDS above 64 KiB must be opted in per kernel (gfx950 allows 160 KiB per workgroup).
+  if (bytes > 160 * 1024) return fail(TAL_ERR_CAPACITY, "round plan needs more than 160 KiB LDS");
+  if (bytes <= 64 * 1024) return TAL_OK;
+  std::lock_guard<std::mutex> lk(g_lds_mu);
+  if (std::find(g_lds_raised.begin(), g_lds_raised.end(), kernel) != g_lds_raised.end()) return TAL_OK;
+  hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess)
+    return fail(TAL_ERR_HIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
+  g_lds_raised.push_back(kernel);
+  return TAL_OK;
+}
+
+int32_t validate_info(const tal_round_plan_info* info) {
+  if (!info) return fail(TAL_ERR_INVALID, "null plan info");
+  if (info->rows <= 0 || info->n_groups <= 0 || info->max_src <= 0)
+    return fail(TAL_ERR_INVALID, "empty round plan");
+  if (info->c4 != 16 && info->c4 != 32 && info->c4 != 64)
+    return fail(TAL_ERR_INVALID, "plan c4 must be 16, 32 or 64");
+  return TAL_OK;
+}
+
+template <bool IS_I64>
+int32_t launch_round_scalar(const void* pin, int64_t ld_in, void* pout, int64_t ld_out,
+                            int64_t e0, int64_t n, const PlanView& v,
+                            const tal_round_plan_info& in, bool exact, hipStream_t s) {
+  if (n <= e0) return TAL_OK;
+  const int tile = 4 * in.c4;
+  const size_t lds = plan_lds_bytes(in, tile * 4);
+  const int64_t tiles = (n - e0 + tile - 1) / tile;
+  if (tiles > 0x7fffffff) return fail(TAL_ERR_INVALID, "too many tiles");
+  const dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(in.n_groups));
+  auto k = (IS_I64 || exact) ? k_round_tiled_scalar<IS_I64, true> : k_round_tiled_scalar<IS_I64, false>;
+  int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
+  if (rc) return rc;
+  k<<<grid, kBlock, lds, s>>>(pin, ld_in, pout, ld_out, e0, n, v, in.max_src, tile);
+  return check_launch("round scalar kernel");
+}
+
+template <int C4, bool EXACT>
+int32_t launch_round_vec(const float* pin, int64_t ld_in, float* pout, int64_t ld_out, int64_t n4,
+                         const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
+  const size_t lds = plan_lds_bytes(in, C4 * 16);
+  auto k = k_round_tiled_f32<C4, EXACT>;
+  int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
+  if (rc) return rc;
+  const int64_t tiles = (n4 + C4 - 1) / C4;
+  if (tiles > 0x7fffffff) return fail(TAL_ERR_INVALID, "too many tiles");
+  const dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(in.n_groups));
+  k<<<grid, kBlock, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, in.max_src);
+  return check_launch("round kernel");
+}
+
+// ------------------------------------------------------------------------------------------
+// K2: cosine similarity of parameter tensors (plan of chunks; see tal_agg.h)
+// ------------------------------------------------------------------------------------------
+constexpr int kCosMaxPairs = 32;
+constexpr int64_t kCosRowsPerChunk = 32;     // ROW kind: 8 rows per wave
+constexpr int64_t kCosColsPerChunk = 1024;   // COL kind: 4 outputs per lane
+enum { kCosRow = 0, kCosCol = 1 };
+
+struct CosPairs {
+  const float* a[kCosMaxPairs];
+  const float* b[kCosMaxPairs];
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float cos_value(float dot, float na2, float nb2) {
+  // nn.CosineSimilarity(eps=1e-6): x/max(|x|,eps) . y/max(|y|,eps)
+  const float na = fmaxf(sqrtf(na2), 1e-6f);
+  const float nb = fmaxf(sqrtf(nb2), 1e-6f);
+  return dot / (na * nb);
+}
+
+// plan: [n_seg x {off, A, I, B}] then [n_chunks x {seg, first, count, kind}]  (int64 words)
+__global__ __launch_bounds__(kBlock) void k_cosine_chunks(CosPairs pr, const int64_t* __restrict__ plan,
+                                                          int n_seg, int n_chunks,
+                                                          double* __restrict__ partial) {
+  __shared__ double s_part[kBlock / 64];
+  const int chunk = blockIdx.x;
+  const int pair = blockIdx.y;
+  const int64_t* ch = plan + 4 * static_cast<int64_t>(n_seg) + 4 * static_cast<int64_t>(chunk);
+  const int64_t seg = ch[0], first = ch[1], count = ch[2], kind = ch[3];
+  const int64_t off = plan[4 * seg + 0];
+  const int64_t I = plan[4 * seg + 2];
+  const int64_t B = plan[4 * seg + 3];
+  const float* a = pr.a[pair] + off;
+  const float* b = pr.b[pair] + off;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  double sum = 0.0;
+  if (kind == kCosRow) {
+    for (int64_t r = first + wave; r < first + count; r += kBlock / 64) {
+      float dot = 0.f, na = 0.f, nb = 0.f;
+      const float* ar = a + r * I;
+      const float* br = b + r * I;
+      for (int64_t i = lane; i < I; i += 64) {
+        const float x = ar[i], y = br[i];
+        dot += x * y;
+        na += x * x;
+        nb += y * y;
+      }
+      dot = wave_sum(dot);
+      na = wave_sum(na);
+      nb = wave_sum(nb);
+      if (lane == 0) sum += static_cast<double>(cos_value(dot, na, nb));
+    }
+  } else {
+    for (int64_t o = first + threadIdx.x; o < first + count; o += kBlock) {
+      const int64_t ai = o / B, bi = o % B;
+      const float* ap = a + ai * I * B + bi;
+      const float* bp = b + ai * I * B + bi;
+      float dot = 0.f, na = 0.f, nb = 0.f;
+      for (int64_t i = 0; i < I; ++i) {
+        const float x = ap[i * B], y = bp[i * B];
+        dot += x * y;
+        na += x * x;
+        nb += y * y;
+      }
+      sum += static_cast<double>(cos_value(dot, na, nb));
+    }
+    // reduce lanes of the wave
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  }
+  if (lane == 0) s_part[wave] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < kBlock / 64; ++w) t += s_part[w];
+    partial[static_cast<int64_t>(pair) * n_chunks + chunk] = t;
+  }
+}
+
+__global__ void k_cosine_finish(const int64_t* __restrict__ plan, int n_seg, int n_chunks,
+                                const double* __restrict__ partial, float* __restrict__ out,
+                                int pair0) {
+  if (threadIdx.x != 0) return;
+  const int pair = blockIdx.x;
+  const int64_t* chunks = plan + 4 * static_cast<int64_t>(n_seg);
+  double total = 0.0, seg_sum = 0.0;
+  int64_t cur = -1;
+  for (int c = 0; c < n_chunks; ++c) {
+    const int64_t seg = chunks[4 * c];
+    if (seg != cur) {
+      if (cur >= 0) total += seg_sum / static_cast<double>(plan[4 * cur + 1] * plan[4 * cur + 3]);
+      cur = seg;
+      seg_sum = 0.0;
+    }
+    seg_sum += partial[static_cast<int64_t>(pair) * n_chunks + c];
+  }
+  if (cur >= 0) total += seg_sum / static_cast<double>(plan[4 * cur + 1] * plan[4 * cur + 3]);
+  out[pair0 + pair] = static_cast<float>(total / static_cast<double>(n_seg));
+}
+
+}  // namespace
+
+// ==========================================================================================
+// C-ABI
+// ==========================================================================================
+extern "C" {
+
+const char* tal_last_error(void) { return g_err.c_str(); }
+
+int32_t tal_abi_version(void) { return kAbiVersion; }
+
+int32_t tal_agg_f32(const float* const* x_host, const double* w_host, int32_t m, float* out,
+                    int64_t n, int32_t mode, void* stream) {
+  if (m <= 0) return fail(TAL_ERR_INVALID, "tal_agg_f32: m must be >= 1");
+  if (n < 0) return fail(TAL_ERR_INVALID, "tal_agg_f32: n < 0");
+  if (!x_host || !w_host || (n > 0 && !out)) return fail(TAL_ERR_INVALID, "tal_agg_f32: null pointer");
+  if (n == 0) { g_err.clear(); return TAL_OK; }
+  bool vec = aligned16(out);
+  for (int i = 0; i < m; ++i) {
+    if (!x_host[i]) return fail(TAL_ERR_INVALID, "tal_agg_f32: null operand pointer");
+    vec = vec && aligned16(x_host[i]);
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool exact = mode == TAL_MODE_EXACT;
+  // Operands beyond kMaxOps are folded in by further passes that continue the same ordered
+  // chain from `out` (stored exactly in fp32, so the result is unchanged).
+  for (int base = 0; base < m; base += kMaxOps) {
+    OpTableF32 t;
+    const int cnt = std::min(kMaxOps, m - base);
+    for (int i = 0; i < cnt; ++i) {
+      t.x[i] = x_host[base + i];
+      t.w[i] = static_cast<float>(w_host[base + i]);
+    }
+    for (int i = cnt; i < kMaxOps; ++i) { t.x[i] = nullptr; t.w[i] = 0.f; }
+    // a later pass must not read an operand that aliases `out` after out was overwritten
+    if (base > 0)
+      for (int i = 0; i < cnt; ++i)
+        if (t.x[i] == out)
+          return fail(TAL_ERR_INVALID, "tal_agg_f32: out aliases an operand beyond the first 256");
+    if (exact) launch_pass<true>(t, cnt, base > 0, vec, out, n, s);
+    else launch_pass<false>(t, cnt, base > 0, vec, out, n, s);
+  }
+  return check_launch("tal_agg_f32");
+}
+
+int32_t tal_agg_i64(const int64_t* const* x_host, const double* w_host, int32_t m, int64_t* out,
+                    int64_t n, void* stream) {
+  if (m <= 0) return fail(TAL_ERR_INVALID, "tal_agg_i64: m must be >= 1");
+  if (n < 0) return fail(TAL_ERR_INVALID, "tal_agg_i64: n < 0");
+  if (!x_host || !w_host || (n > 0 && !out)) return fail(TAL_ERR_INVALID, "tal_agg_i64: null pointer");
+  if (n == 0) { g_err.clear(); return TAL_OK; }
+  if (m > kMaxOps)
+    return fail(TAL_ERR_INVALID, "tal_agg_i64: more than 256 operands: use tal_agg_round_i64");
+  OpTableI64 t;
+  for (int i = 0; i < m; ++i) {
+    if (!x_host[i]) return fail(TAL_ERR_INVALID, "tal_agg_i64: null operand pointer");
+    t.x[i] = x_host[i];
+    t.w[i] = static_cast<float>(w_host[i]);
+  }
+  for (int i = m; i < kMaxOps; ++i) { t.x[i] = nullptr; t.w[i] = 0.f; }
+  k_agg_i64<<<grid_for(n), kBlock, 0, static_cast<hipStream_t>(stream)>>>(t, m, out, n);
+  return check_launch("tal_agg_i64");
+}
+
+int64_t tal_round_plan_words(int32_t rows, int64_t nnz) {
+  if (rows < 0 || nnz < 0) return -1;
+  // grp_row_ptr + grp_src_ptr (<= rows+1 each) + src_row (<= nnz) + row_ptr + slot + w + out_row
+  return 2 * (static_cast<int64_t>(rows) + 1) + nnz + (rows + 1) + 2 * nnz + rows + 16;
+}
+
+int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host,
+                             const double* w_host, const int32_t* out_row_host, int32_t c4,
+                             int32_t lds_bytes, int32_t* plan_host, int64_t plan_capacity_words,
+                             tal_round_plan_info* info) {
+  if (rows <= 0 || !row_ptr_host || !col_host || !w_host || !out_row_host || !plan_host || !info)
+    return fail(TAL_ERR_INVALID, "tal_round_plan_build: bad arguments");
+  if (c4 != 16 && c4 != 32 && c4 != 64)
+    return fail(TAL_ERR_INVALID, "tal_round_plan_build: c4 must be 16, 32 or 64");
+  if (row_ptr_host[0] != 0) return fail(TAL_ERR_INVALID, "tal_round_plan_build: row_ptr[0] != 0");
+  for (int r = 0; r < rows; ++r)
+    if (row_ptr_host[r + 1] <= row_ptr_host[r])
+      return fail(TAL_ERR_INVALID, "tal_round_plan_build: every row needs >= 1 operand");
+  const int64_t nnz = row_ptr_host[rows];
+  for (int64_t k = 0; k < nnz; ++k)
+    if (col_host[k] < 0) return fail(TAL_ERR_INVALID, "tal_round_plan_build: negative source row");
+  if (plan_capacity_words < tal_round_plan_words(rows, nnz))
+    return fail(TAL_ERR_INVALID, "tal_round_plan_build: plan buffer too small");
+
+  // Both round kernels stage 16*c4 bytes per source (c4 float4 or 4*c4 scalars).
+  const int64_t per_src = 16LL * c4;
+  std::vector<int32_t> grp_row_ptr{0}, grp_src_ptr{0}, src_row, slot(nnz);
+  std::vector<int32_t> map;  // source row -> slot in current group (-1 absent)
+  int32_t max_col = 0;
+  for (int64_t k = 0; k < nnz; ++k) max_col = std::max(max_col, col_host[k]);
+  map.assign(static_cast<size_t>(max_col) + 1, -1);
+  std::vector<int32_t> cur_src;
+  int64_t cur_rows = 0, cur_nnz = 0;
+  int32_t max_src = 0, max_rows = 0, max_nnz = 0;
+  auto need = [&](int64_t ns, int64_t nr, int64_t no) {
+    return ns * per_src + (nr + 1 + 2 * no) * 4;
+  };
+  auto close_group = [&](int r_end) {
+    grp_row_ptr.push_back(r_end);
+    for (int32_t sr : cur_src) { src_row.push_back(sr); map[sr] = -1; }
+    grp_src_ptr.push_back(static_cast<int32_t>(src_row.size()));
+    max_src = std::max<int32_t>(max_src, static_cast<int32_t>(cur_src.size()));
+    max_rows = std::max<int32_t>(max_rows, static_cast<int32_t>(cur_rows));
+    max_nnz = std::max<int32_t>(max_nnz, static_cast<int32_t>(cur_nnz));
+    cur_src.clear();
+    cur_rows = cur_nnz = 0;
+  };
+  for (int r = 0; r < rows; ++r) {
+    // sources this row would add
+    int64_t add = 0;
+    std::vector<int32_t> fresh;
+    for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1]; ++k) {
+      const int32_t sr = col_host[k];
+      if (map[sr] < 0 && std::find(fresh.begin(), fresh.end(), sr) == fresh.end()) {
+        fresh.push_back(sr);
+        ++add;
+      }
+    }
+    const int64_t row_nnz = row_ptr_host[r + 1] - row_ptr_host[r];
+    if (cur_rows > 0 &&
+        need(static_cast<int64_t>(cur_src.size()) + add, cur_rows + 1, cur_nnz + row_nnz) > lds_bytes) {
+      close_group(r);
+      fresh.clear();
+      for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1]; ++k) {
+        const int32_t sr = col_host[k];
+        if (std::find(fresh.begin(), fresh.end(), sr) == fresh.end()) fresh.push_back(sr);
+      }
+    }
+    if (need(static_cast<int64_t>(cur_src.size() + fresh.size()), cur_rows + 1, cur_nnz + row_nnz) >
+        lds_bytes)
+      return fail(TAL_ERR_CAPACITY, "tal_round_plan_build: row " + std::to_string(r) +
+                                        " has more distinct sources than one LDS tile holds");
+    for (int32_t sr : fresh) {
+      map[sr] = static_cast<int32_t>(cur_src.size());
+      cur_src.push_back(sr);
+    }
+    for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1]; ++k) slot[k] = map[col_host[k]];
+    ++cur_rows;
+    cur_nnz += row_nnz;
+  }
+  close_group(rows);
+
+  const int32_t G = static_cast<int32_t>(grp_row_ptr.size()) - 1;
+  tal_round_plan_info in;
+  memset(&in, 0, sizeof(in));
+  in.rows = rows;
+  in.nnz = static_cast<int32_t>(nnz);
+  in.n_groups = G;
+  in.total_src = static_cast<int32_t>(src_row.size());
+  in.max_src = max_src;
+  in.max_rows = max_rows;
+  in.max_nnz = max_nnz;
+  in.c4 = c4;
+  int32_t off = 0;
+  in.off_grp_row_ptr = off; off += G + 1;
+  in.off_grp_src_ptr = off; off += G + 1;
+  in.off_src_row = off; off += in.total_src;
+  in.off_row_ptr = off; off += rows + 1;
+  in.off_op_slot = off; off += static_cast<int32_t>(nnz);
+  in.off_op_w = off; off += static_cast<int32_t>(nnz);
+  in.off_out_row = off; off += rows;
+  in.words = off;
+  in.lds_bytes = static_cast<int32_t>(plan_lds_bytes(in, 16 * c4));
+  if (off > plan_capacity_words) return fail(TAL_ERR_INVALID, "tal_round_plan_build: overflow");
+
+  memcpy(plan_host + in.off_grp_row_ptr, grp_row_ptr.data(), 4 * (G + 1));
+  memcpy(plan_host + in.off_grp_src_ptr, grp_src_ptr.data(), 4 * (G + 1));
+  memcpy(plan_host + in.off_src_row, src_row.data(), 4 * src_row.size());
+  memcpy(plan_host + in.off_row_ptr, row_ptr_host, 4 * (static_cast<size_t>(rows) + 1));
+  memcpy(plan_host + in.off_op_slot, slot.data(), 4 * nnz);
+  for (int64_t k = 0; k < nnz; ++k) {
+    const float wf = static_cast<float>(w_host[k]);
+    memcpy(plan_host + in.off_op_w + k, &wf, 4);
+  }
+  memcpy(plan_host + in.off_out_row, out_row_host, 4 * static_cast<size_t>(rows));
+  *info = in;
+  g_err.clear();
+  return TAL_OK;
+}
+
+int32_t tal_agg_round_f32(const float* pool_in, int64_t ld_in, float* pool_out, int64_t ld_out,
+                          int64_t n, const int32_t* plan_dev, const tal_round_plan_info* info,
+                          int32_t mode, void* stream) {
+  int32_t rc = validate_info(info);
+  if (rc) return rc;
+  if (!pool_in || !pool_out || !plan_dev) return fail(TAL_ERR_INVALID, "tal_agg_round_f32: null pointer");
+  if (n < 0 || ld_in < n || ld_out < n) return fail(TAL_ERR_INVALID, "tal_agg_round_f32: bad n / ld");
+  if (pool_in == pool_out && info->n_groups > 1)
+    return fail(TAL_ERR_INVALID,
+                "tal_agg_round_f32: in-place round needs a single-group plan (snapshot semantics)");
+  if (n == 0) { g_err.clear(); return TAL_OK; }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const PlanView v = make_view(plan_dev, *info);
+  const bool exact = mode == TAL_MODE_EXACT;
+  const bool vec = aligned16(pool_in) && aligned16(pool_out) && ld_in % 4 == 0 && ld_out % 4 == 0;
+  int64_t e_vec = 0;
+  if (vec) {
+    const int64_t n4 = n / 4;
+    e_vec = n4 * 4;
+    if (n4 > 0) {
+      switch (info->c4 * 2 + (exact ? 1 : 0)) {
+        case 129: rc = launch_round_vec<64, true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        case 128: rc = launch_round_vec<64, false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        case 65: rc = launch_round_vec<32, true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        case 64: rc = launch_round_vec<32, false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        case 33: rc = launch_round_vec<16, true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        default: rc = launch_round_vec<16, false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+      }
+      if (rc) return rc;
+    }
+  }
+  return launch_round_scalar<false>(pool_in, ld_in, pool_out, ld_out, e_vec, n, v, *info, exact, s);
+}
+
+int32_t tal_agg_round_i64(const int64_t* pool_in, int64_t ld_in, int64_t* pool_out, int64_t ld_out,
+                          int64_t n, const int32_t* plan_dev, const tal_round_plan_info* info,
+                          void* stream) {
+  int32_t rc = validate_info(info);
+  if (rc) return rc;
+  if (!pool_in || !pool_out || !plan_dev) return fail(TAL_ERR_INVALID, "tal_agg_round_i64: null pointer");
+  if (n < 0 || ld_in < n || ld_out < n) return fail(TAL_ERR_INVALID, "tal_agg_round_i64: bad n / ld");
+  if (pool_in == pool_out && info->n_groups > 1)
+    return fail(TAL_ERR_INVALID,
+                "tal_agg_round_i64: in-place round needs a single-group plan (snapshot semantics)");
+  if (n == 0) { g_err.clear(); return TAL_OK; }
+  const PlanView v = make_view(plan_dev, *info);
+  return launch_round_scalar<true>(pool_in, ld_in, pool_out, ld_out, 0, n, v, *info, true,
+                                   static_cast<hipStream_t>(stream));
+}
+
+int64_t tal_cosine_plan_words(const int64_t* seg_host, int32_t n_seg) {
+  if (!seg_host || n_seg <= 0) return -1;
+  int64_t chunks = 0;
+  for (int s = 0; s < n_seg; ++s) {
+    const int64_t A = seg_host[4 * s + 1], I = seg_host[4 * s + 2], B = seg_host[4 * s + 3];
+    if (A <= 0 || I <= 0 || B <= 0) return -1;
+    if (B == 1 && I > 1) chunks += (A + kCosRowsPerChunk - 1) / kCosRowsPerChunk;
+    else chunks += (A * B + kCosColsPerChunk - 1) / kCosColsPerChunk;
+  }
+  return 4 * (static_cast<int64_t>(n_seg) + chunks);
+}
+
+int32_t tal_cosine_plan_build(const int64_t* seg_host, int32_t n_seg, int64_t* plan_host,
+                              int64_t plan_capacity_words, int32_t* n_chunks) {
+  const int64_t words = tal_cosine_plan_words(seg_host, n_seg);
+  if (words < 0 || !plan_host || !n_chunks)
+    return fail(TAL_ERR_INVALID, "tal_cosine_plan_build: bad segments");
+  if (plan_capacity_words < words) return fail(TAL_ERR_INVALID, "tal_cosine_plan_build: buffer too small");
+  memcpy(plan_host, seg_host, sizeof(int64_t) * 4 * n_seg);
+  int64_t* ch = plan_host + 4 * n_seg;
+  int64_t c = 0;
+  for (int s = 0; s < n_seg; ++s) {
+    const int64_t A = seg_host[4 * s + 1], I = seg_host[4 * s + 2], B = seg_host[4 * s + 3];
+    const bool row = (B == 1 && I > 1);
+    const int64_t total = row ? A : A * B;
+    const int64_t per = row ? kCosRowsPerChunk : kCosColsPerChunk;
+    for (int64_t f = 0; f < total; f += per) {
+      ch[4 * c + 0] = s;
+      ch[4 * c + 1] = f;
+      ch[4 * c + 2] = std::min(per, total - f);
+      ch[4 * c + 3] = row ? kCosRow : kCosCol;
+      ++c;
+    }
+  }
+  if (c > 0x7fffffff) return fail(TAL_ERR_INVALID, "tal_cosine_plan_build: too many chunks");
+  *n_chunks = static_cast<int32_t>(c);
+  g_err.clear();
+  return TAL_OK;
+}
+
+int64_t tal_cosine_scratch_bytes(int32_t n_chunks, int32_t n_pairs) {
+  if (n_chunks <= 0 || n_pairs <= 0) return -1;
+  return static_cast<int64_t>(sizeof(double)) * n_chunks * std::min(n_pairs, kCosMaxPairs);
+}
+
+int32_t tal_cosine_params(const float* const* a_ptrs_host, const float* const* b_ptrs_host,
+                          int32_t n_pairs, const int64_t* plan_dev, int32_t n_chunks,
+                          int32_t n_seg, void* scratch, float* out_dev, void* stream) {
+  if (!a_ptrs_host || !b_ptrs_host || !plan_dev || !scratch || !out_dev || n_pairs <= 0 ||
+      n_chunks <= 0 || n_seg <= 0)
+    return fail(TAL_ERR_INVALID, "tal_cosine_params: bad arguments");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  for (int base = 0; base < n_pairs; base += kCosMaxPairs) {
+    const int cnt = std::min(kCosMaxPairs, n_pairs - base);
+    CosPairs pr;
+    for (int j = 0; j < kCosMaxPairs; ++j) {
+      pr.a[j] = j < cnt ? a_ptrs_host[base + j] : nullptr;
+      pr.b[j] = j < cnt ? b_ptrs_host[base + j] : nullptr;
+      if (j < cnt && (!pr.a[j] || !pr.b[j]))
+        return fail(TAL_ERR_INVALID, "tal_cosine_params: null model pointer");
+    }
+    double* part = static_cast<double*>(scratch);
+    k_cosine_chunks<<<dim3(n_chunks, cnt), kBlock, 0, s>>>(pr, plan_dev, n_seg, n_chunks, part);
+    k_cosine_finish<<<cnt, 64, 0, s>>>(plan_dev, n_seg, n_chunks, part, out_dev, base);
+  }
+  return check_launch("tal_cosine_params");
+}
+
+}  // extern "C"

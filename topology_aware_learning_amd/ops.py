@@ -1,0 +1,225 @@
+"""Device operations: thin, checked wrappers over the C-ABI (include/tal_agg.h).
+
+Every function takes torch tensors that already live on the GPU and launches on the current
+torch stream of their device.  Nothing here falls back to the CPU: without the HIP library
+the first call raises ``TalLibraryError``; with a CPU tensor it raises ``ValueError``.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import RoundPlanInfo, check
+
+MODE_EXACT = _lib.TAL_MODE_EXACT
+MODE_FMA = _lib.TAL_MODE_FMA
+
+
+def _stream(device: torch.device, stream: Optional[torch.cuda.Stream] = None) -> ctypes.c_void_p:
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _require_gpu(t: torch.Tensor, name: str, dtype: torch.dtype) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name} must be a GPU tensor (got {t.device}); the aggregation has no CPU path")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype} (got {t.dtype})")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def _ptrs_and_weights(xs, weights, n, dtype, out):
+    if len(xs) == 0:
+        raise ValueError("at least one operand is required")
+    if len(weights) != len(xs):
+        raise ValueError(f"{len(xs)} operands but {len(weights)} weights")
+    for i, x in enumerate(xs):
+        _require_gpu(x, f"operand {i}", dtype)
+        if x.numel() != n:
+            raise ValueError(f"operand {i} has {x.numel()} elements, expected {n}")
+        if x.device != out.device:
+            raise ValueError(f"operand {i} is on {x.device}, out on {out.device}")
+    return _lib.ptr_array([x.data_ptr() for x in xs]), _lib.double_array(weights)
+
+
+def agg_f32(xs: Sequence[torch.Tensor], weights: Sequence[float], out: torch.Tensor,
+            mode: int = MODE_EXACT, stream=None) -> torch.Tensor:
+    """K1: out = sum_i fp32(w_i) * xs[i] (reference order; decentralized_client.py:399-411)."""
+    _require_gpu(out, "out", torch.float32)
+    n = out.numel()
+    P, W = _ptrs_and_weights(xs, weights, n, torch.float32, out)
+    L = _lib.load()
+    check(L.tal_agg_f32(P, W, len(xs), ctypes.c_void_p(out.data_ptr()), n, int(mode),
+                        _stream(out.device, stream)))
+    return out
+
+
+def agg_i64(xs: Sequence[torch.Tensor], weights: Sequence[float], out: torch.Tensor,
+            stream=None) -> torch.Tensor:
+    """K1 on int64 buffers: fp32 accumulate, truncation (decentralized_client.py:407-413)."""
+    _require_gpu(out, "out", torch.int64)
+    n = out.numel()
+    P, W = _ptrs_and_weights(xs, weights, n, torch.int64, out)
+    L = _lib.load()
+    check(L.tal_agg_i64(P, W, len(xs), ctypes.c_void_p(out.data_ptr()), n, _stream(out.device, stream)))
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# K3 round plans
+# ------------------------------------------------------------------------------------------
+LDS_BUDGET = 64 * 1024  # two workgroups per CU overlap one's HBM staging with the other's math
+
+
+@dataclass
+class RoundPlan:
+    info: RoundPlanInfo
+    host: np.ndarray           # int32 blob
+    device: Optional[torch.Tensor] = None
+    rows: int = 0
+    nnz: int = 0
+
+    @property
+    def single_group(self) -> bool:
+        return self.info.n_groups == 1
+
+    def to(self, device) -> "RoundPlan":
+        self.device = torch.from_numpy(self.host).to(device, non_blocking=False)
+        return self
+
+    def staged_rows(self) -> int:
+        """Source rows read from HBM per column tile (sum over groups)."""
+        return int(self.info.total_src)
+
+
+def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = LDS_BUDGET) -> RoundPlan:
+    """Tile plan for a round given as CSR (row r: operands col[row_ptr[r]:row_ptr[r+1]] with
+    float64 weights w, written to pool row out_row[r]).
+
+    c4 = 0 picks the float4 tile width (64, 32 or 16 float4 per source) that stages the fewest
+    source rows in total (ties -> the widest tile, i.e. the longest contiguous HBM segments)."""
+    row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int32)
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    out_row = np.ascontiguousarray(out_row, dtype=np.int32)
+    rows = len(out_row)
+    if len(row_ptr) != rows + 1 or row_ptr[-1] != len(col) or len(w) != len(col):
+        raise ValueError("inconsistent CSR arrays")
+    L = _lib.load()
+    cap = L.tal_round_plan_words(rows, len(col))
+    best = None
+    last_err = None
+    for cand in ([c4] if c4 else [64, 32, 16]):
+        blob = np.zeros(cap, dtype=np.int32)
+        info = RoundPlanInfo()
+        P32 = ctypes.POINTER(ctypes.c_int32)
+        rc = L.tal_round_plan_build(rows, row_ptr.ctypes.data_as(P32), col.ctypes.data_as(P32),
+                                    w.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                    out_row.ctypes.data_as(P32), cand, int(lds_bytes),
+                                    blob.ctypes.data_as(P32), cap, ctypes.byref(info))
+        if rc != _lib.TAL_OK:
+            last_err = _lib.TalError(rc, L.tal_last_error().decode())
+            continue
+        plan = RoundPlan(info=info, host=blob[: info.words].copy(), rows=rows, nnz=len(col))
+        if best is None or plan.info.total_src < best.info.total_src:
+            best = plan
+    if best is None:
+        raise last_err
+    return best
+
+
+def round_f32(pool_in: torch.Tensor, pool_out: torch.Tensor, plan: RoundPlan, n: Optional[int] = None,
+              mode: int = MODE_EXACT, stream=None) -> torch.Tensor:
+    """K3 on [models, ld] fp32 pools (snapshot semantics; see tal_agg.h)."""
+    return _round(pool_in, pool_out, plan, n, torch.float32, mode, stream)
+
+
+def round_i64(pool_in: torch.Tensor, pool_out: torch.Tensor, plan: RoundPlan, n: Optional[int] = None,
+              stream=None) -> torch.Tensor:
+    return _round(pool_in, pool_out, plan, n, torch.int64, MODE_EXACT, stream)
+
+
+def _round(pool_in, pool_out, plan, n, dtype, mode, stream):
+    _require_gpu(pool_in, "pool_in", dtype)
+    _require_gpu(pool_out, "pool_out", dtype)
+    if pool_in.dim() != 2 or pool_out.dim() != 2:
+        raise ValueError("pools must be 2-D [models, ld]")
+    if pool_in.device != pool_out.device:
+        raise ValueError("pools on different devices")
+    if plan.device is None or plan.device.device != pool_in.device:
+        plan.to(pool_in.device)
+    n = pool_in.shape[1] if n is None else int(n)
+    rows_in = pool_in.shape[0]
+    rows_out = pool_out.shape[0]
+    h = plan.host
+    i = plan.info
+    if h[i.off_src_row: i.off_src_row + i.total_src].max(initial=-1) >= rows_in:
+        raise ValueError("plan reads a pool row beyond pool_in")
+    if h[i.off_out_row: i.off_out_row + i.rows].max(initial=-1) >= rows_out:
+        raise ValueError("plan writes a pool row beyond pool_out")
+    L = _lib.load()
+    fn = L.tal_agg_round_f32 if dtype == torch.float32 else L.tal_agg_round_i64
+    args = [ctypes.c_void_p(pool_in.data_ptr()), pool_in.stride(0), ctypes.c_void_p(pool_out.data_ptr()),
+            pool_out.stride(0), n, ctypes.c_void_p(plan.device.data_ptr()), ctypes.byref(plan.info)]
+    if dtype == torch.float32:
+        args.append(int(mode))
+    args.append(_stream(pool_in.device, stream))
+    check(fn(*args))
+    return pool_out
+
+
+# ------------------------------------------------------------------------------------------
+# K2 cosine similarity
+# ------------------------------------------------------------------------------------------
+@dataclass
+class CosinePlan:
+    n_seg: int
+    n_chunks: int
+    host: np.ndarray
+    device: Optional[torch.Tensor] = None
+
+
+def build_cosine_plan(segments: Sequence[Sequence[int]]) -> CosinePlan:
+    """segments: (offset, A, I, B) per parameter tensor (see tal_agg.h K2)."""
+    seg = np.ascontiguousarray(np.asarray(segments, dtype=np.int64).reshape(-1, 4))
+    L = _lib.load()
+    P64 = ctypes.POINTER(ctypes.c_int64)
+    words = L.tal_cosine_plan_words(seg.ctypes.data_as(P64), len(seg))
+    if words < 0:
+        raise ValueError("bad cosine segments")
+    blob = np.zeros(words, dtype=np.int64)
+    nch = ctypes.c_int32()
+    check(L.tal_cosine_plan_build(seg.ctypes.data_as(P64), len(seg), blob.ctypes.data_as(P64), words,
+                                  ctypes.byref(nch)))
+    return CosinePlan(n_seg=len(seg), n_chunks=nch.value, host=blob)
+
+
+def cosine(a_list: Sequence[torch.Tensor], b_list: Sequence[torch.Tensor], plan: CosinePlan,
+           stream=None) -> torch.Tensor:
+    """K2: cosine_similarity(a_j, b_j) for every pair (flat fp32 parameter arenas)."""
+    if len(a_list) != len(b_list) or not a_list:
+        raise ValueError("need matching, non-empty a/b lists")
+    dev = a_list[0].device
+    for i, t in enumerate(list(a_list) + list(b_list)):
+        _require_gpu(t, f"model {i}", torch.float32)
+        if t.device != dev:
+            raise ValueError("models on different devices")
+    if plan.device is None or plan.device.device != dev:
+        plan.device = torch.from_numpy(plan.host).to(dev)
+    L = _lib.load()
+    scratch = torch.empty(int(L.tal_cosine_scratch_bytes(plan.n_chunks, len(a_list))), dtype=torch.uint8, device=dev)
+    out = torch.empty(len(a_list), dtype=torch.float32, device=dev)
+    check(L.tal_cosine_params(_lib.ptr_array([t.data_ptr() for t in a_list]),
+                              _lib.ptr_array([t.data_ptr() for t in b_list]), len(a_list),
+                              ctypes.c_void_p(plan.device.data_ptr()), plan.n_chunks, plan.n_seg,
+                              ctypes.c_void_p(scratch.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                              _stream(dev, stream)))
+    return out

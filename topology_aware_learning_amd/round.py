@@ -1,0 +1,89 @@
+"""A whole aggregation round over a device-resident model pool (K3).
+
+The reference submits one aggregation app per selected client per round
+(src/decentralized_app.py:605-641); each reads its neighbors' freshly trained models and the
+client's own (self last, :625).  With every model of the round resident in one ``ModelPool``
+the round is one sparse mix ``OUT = W . X``: row r of W holds the round's weights for client r
+in reference operand order.  ``RoundExecutor`` turns that into a tile plan once per distinct
+operand/weight pattern and launches one LDS-tiled kernel per segment, reading each source
+model once per column tile instead of once per aggregation that uses it.
+
+Round semantics ("snapshot"): every aggregation of the round reads the models as they were
+before the round.  The reference's in-place writes from two threads make
+its own round order-dependent; ``sequential=True`` reproduces its single-thread order
+(client index order, each call seeing the previous calls' writes) as one K1 call per client.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import ops
+from .arena import ModelPool
+
+
+def csr_from_lists(orders: Sequence[Sequence[int]], weights: Sequence[Sequence[float]]):
+    row_ptr = [0]
+    col: List[int] = []
+    w: List[float] = []
+    for o, ws in zip(orders, weights):
+        if len(o) != len(ws) or len(o) == 0:
+            raise ValueError("each aggregation needs one weight per operand and >= 1 operand")
+        col.extend(int(x) for x in o)
+        w.extend(float(x) for x in ws)
+        row_ptr.append(len(col))
+    return np.array(row_ptr, np.int32), np.array(col, np.int32), np.array(w, np.float64)
+
+
+class RoundExecutor:
+    def __init__(self, pool: ModelPool, scratch: Optional[ModelPool] = None, mode: int = ops.MODE_EXACT):
+        self.pool = pool
+        self.scratch = scratch
+        self.mode = mode
+        self._plans: Dict[Tuple, ops.RoundPlan] = {}
+
+    def plan(self, orders, weights, out_rows) -> ops.RoundPlan:
+        key = (tuple(tuple(o) for o in orders), tuple(tuple(float(x) for x in w) for w in weights), tuple(out_rows))
+        p = self._plans.get(key)
+        if p is None:
+            row_ptr, col, w = csr_from_lists(orders, weights)
+            p = ops.build_plan(row_ptr, col, w, np.asarray(out_rows, np.int32)).to(self.pool.device)
+            if len(self._plans) > 64:
+                self._plans.clear()
+            self._plans[key] = p
+        return p
+
+    def run(self, orders: Sequence[Sequence[int]], weights: Sequence[Sequence[float]],
+            out_rows: Optional[Sequence[int]] = None, sequential: bool = False) -> None:
+        """Aggregate pool rows: out_rows[r] <- sum_k weights[r][k] * pool[orders[r][k]]."""
+        if out_rows is None:
+            out_rows = list(range(len(orders)))
+        if len(orders) == 0:
+            return
+        lay = self.pool.layout
+        if sequential:
+            for r, o, w in zip(out_rows, orders, weights):
+                if lay.n_f32:
+                    ops.agg_f32([self.pool.row_f32(j) for j in o], w, self.pool.row_f32(r), mode=self.mode)
+                if lay.n_i64:
+                    ops.agg_i64([self.pool.row_i64(j) for j in o], w, self.pool.row_i64(r))
+            return
+        plan = self.plan(orders, weights, out_rows)
+        if plan.single_group:
+            # every workgroup stages all sources of its tile before writing: in place is safe
+            if lay.n_f32:
+                ops.round_f32(self.pool.f32, self.pool.f32, plan, n=lay.n_f32, mode=self.mode)
+            if lay.n_i64:
+                ops.round_i64(self.pool.i64, self.pool.i64, plan, n=lay.n_i64)
+            return
+        if self.scratch is None:
+            self.scratch = ModelPool(lay, self.pool.rows, self.pool.device)
+        if lay.n_f32:
+            ops.round_f32(self.pool.f32, self.scratch.f32, plan, n=lay.n_f32, mode=self.mode)
+        if lay.n_i64:
+            ops.round_i64(self.pool.i64, self.scratch.i64, plan, n=lay.n_i64)
+        idx = torch.as_tensor(list(out_rows), dtype=torch.long, device=self.pool.device)
+        self.pool.f32.index_copy_(0, idx, self.scratch.f32.index_select(0, idx))
+        self.pool.i64.index_copy_(0, idx, self.scratch.i64.index_select(0, idx))

@@ -1,0 +1,206 @@
+"""Deterministic synthetic state_dicts and model layouts.
+
+The values come from a counter-based integer generator (splitmix64 of (seed, index)) turned
+into fp32 by bit assembly, so the same (layout, seed) gives the same bytes on any machine —
+the golden sha256 fixtures in tests/golden were produced from exactly these inputs by the
+reference's own aggregation functions.
+
+Layouts are lists of (name, shape, dtype) in state_dict order.  The CIFAR CNN / ResNet-18 /
+ResNet-50 layouts match the reference's models (src/modules.py:18-54, src/models/resnet.py:122,130;
+pinned by tests/golden/layouts.json); ViT-B/16 is not in the reference and follows the
+torchvision vit_b_16 state_dict (BASELINE config 5).
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Iterable, List, Sequence, Tuple
+
+import numpy as np
+import torch
+
+Layout = List[Tuple[str, Tuple[int, ...], str]]  # dtype in {"float32", "int64"}
+
+_M1 = np.uint64(0x9E3779B97F4A7C15)
+_M2 = np.uint64(0xBF58476D1CE4E5B9)
+_M3 = np.uint64(0x94D049BB133111EB)
+
+
+def _splitmix(x: np.ndarray) -> np.ndarray:
+    x = x + _M1
+    x = (x ^ (x >> np.uint64(30))) * _M2
+    x = (x ^ (x >> np.uint64(27))) * _M3
+    return x ^ (x >> np.uint64(31))
+
+
+def counter_bits(seed: int, start: int, n: int) -> np.ndarray:
+    idx = np.arange(start, start + n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        return _splitmix(idx ^ (np.uint64(seed & 0xFFFFFFFF) << np.uint64(40)))
+
+
+def counter_f32(seed: int, start: int, n: int) -> np.ndarray:
+    """fp32 values with random sign, exponent in [2^-6, 2^2) and full random mantissa."""
+    u = counter_bits(seed, start, n)
+    mant = (u & np.uint64(0x7FFFFF)).astype(np.uint32)
+    expo = (np.uint64(121) + ((u >> np.uint64(23)) % np.uint64(8))).astype(np.uint32)
+    sign = ((u >> np.uint64(31)) & np.uint64(1)).astype(np.uint32)
+    bits = (sign << np.uint32(31)) | (expo << np.uint32(23)) | mant
+    return bits.view(np.float32)
+
+
+def counter_i64(seed: int, start: int, n: int, hi: int = 1_000_000) -> np.ndarray:
+    return (counter_bits(seed, start, n) % np.uint64(hi)).astype(np.int64)
+
+
+def layout_of(sd) -> Layout:
+    out: Layout = []
+    for k, v in sd.items():
+        dt = str(v.dtype).replace("torch.", "")
+        out.append((k, tuple(int(s) for s in v.shape), dt))
+    return out
+
+
+def numel(shape: Sequence[int]) -> int:
+    n = 1
+    for s in shape:
+        n *= int(s)
+    return n
+
+
+def layout_counts(layout: Layout) -> Tuple[int, int]:
+    nf = sum(numel(s) for _, s, d in layout if d == "float32")
+    ni = sum(numel(s) for _, s, d in layout if d == "int64")
+    return nf, ni
+
+
+def synth_state_dict(layout: Layout, seed: int) -> "OrderedDict[str, torch.Tensor]":
+    """CPU tensors for `layout`; entry values depend only on (seed, position in the layout)."""
+    sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    pos = 0
+    for name, shape, dt in layout:
+        n = numel(shape)
+        if dt == "float32":
+            a = counter_f32(seed, pos, n)
+            if name.endswith("running_var"):
+                a = np.abs(a) + np.float32(0.5)
+        elif dt == "int64":
+            a = counter_i64(seed, pos, n)
+        else:
+            raise ValueError(f"unsupported dtype {dt} for {name}")
+        sd[name] = torch.from_numpy(a.reshape(shape).copy())
+        pos += n
+    return sd
+
+
+# ------------------------------------------------------------------------------------------
+# layouts
+# ------------------------------------------------------------------------------------------
+def _bn(prefix: str, c: int) -> Layout:
+    return [
+        (f"{prefix}.weight", (c,), "float32"),
+        (f"{prefix}.bias", (c,), "float32"),
+        (f"{prefix}.running_mean", (c,), "float32"),
+        (f"{prefix}.running_var", (c,), "float32"),
+        (f"{prefix}.num_batches_tracked", (), "int64"),
+    ]
+
+
+def cifar_cnn_layout(num_classes: int = 10) -> Layout:
+    """CifarModule (reference src/modules.py:18-54): conv stack in `network` Sequential."""
+    convs = [(0, 3, 32), (2, 32, 64), (5, 64, 128), (7, 128, 128), (10, 128, 256), (12, 256, 256)]
+    out: Layout = []
+    for idx, cin, cout in convs:
+        out.append((f"network.{idx}.weight", (cout, cin, 3, 3), "float32"))
+        out.append((f"network.{idx}.bias", (cout,), "float32"))
+    for idx, fin, fout in [(16, 4096, 1024), (18, 1024, 512), (20, 512, num_classes)]:
+        out.append((f"network.{idx}.weight", (fout, fin), "float32"))
+        out.append((f"network.{idx}.bias", (fout,), "float32"))
+    return out
+
+
+def resnet_layout(kind: str, num_classes: int = 10) -> Layout:
+    """CIFAR ResNet-18 / ResNet-50 (reference src/models/resnet.py:122,130)."""
+    if kind == "resnet18":
+        blocks, expansion, bottleneck = [2, 2, 2, 2], 1, False
+    elif kind == "resnet50":
+        blocks, expansion, bottleneck = [3, 4, 6, 3], 4, True
+    else:
+        raise ValueError(kind)
+    out: Layout = [("conv1.weight", (64, 3, 3, 3), "float32")] + _bn("bn1", 64)
+    in_planes = 64
+    for li, (planes, nb) in enumerate(zip([64, 128, 256, 512], blocks), start=1):
+        for bi in range(nb):
+            stride = 1 if (li == 1 or bi > 0) else 2
+            p = f"layer{li}.{bi}"
+            if bottleneck:
+                out.append((f"{p}.conv1.weight", (planes, in_planes, 1, 1), "float32"))
+                out += _bn(f"{p}.bn1", planes)
+                out.append((f"{p}.conv2.weight", (planes, planes, 3, 3), "float32"))
+                out += _bn(f"{p}.bn2", planes)
+                out.append((f"{p}.conv3.weight", (planes * expansion, planes, 1, 1), "float32"))
+                out += _bn(f"{p}.bn3", planes * expansion)
+            else:
+                out.append((f"{p}.conv1.weight", (planes, in_planes, 3, 3), "float32"))
+                out += _bn(f"{p}.bn1", planes)
+                out.append((f"{p}.conv2.weight", (planes, planes, 3, 3), "float32"))
+                out += _bn(f"{p}.bn2", planes)
+            if stride != 1 or in_planes != planes * expansion:
+                out.append((f"{p}.shortcut.0.weight", (planes * expansion, in_planes, 1, 1), "float32"))
+                out += _bn(f"{p}.shortcut.1", planes * expansion)
+            in_planes = planes * expansion
+    out.append(("linear.weight", (num_classes, 512 * expansion), "float32"))
+    out.append(("linear.bias", (num_classes,), "float32"))
+    return out
+
+
+def vit_b16_layout(num_classes: int = 1000, image_size: int = 224) -> Layout:
+    """torchvision vit_b_16 state_dict layout (BASELINE config 5; not in the reference)."""
+    d, mlp, layers, patch = 768, 3072, 12, 16
+    seq = (image_size // patch) ** 2 + 1
+    out: Layout = [
+        ("class_token", (1, 1, d), "float32"),
+        ("conv_proj.weight", (d, 3, patch, patch), "float32"),
+        ("conv_proj.bias", (d,), "float32"),
+        ("encoder.pos_embedding", (1, seq, d), "float32"),
+    ]
+    for i in range(layers):
+        p = f"encoder.layers.encoder_layer_{i}"
+        out += [
+            (f"{p}.ln_1.weight", (d,), "float32"),
+            (f"{p}.ln_1.bias", (d,), "float32"),
+            (f"{p}.self_attention.in_proj_weight", (3 * d, d), "float32"),
+            (f"{p}.self_attention.in_proj_bias", (3 * d,), "float32"),
+            (f"{p}.self_attention.out_proj.weight", (d, d), "float32"),
+            (f"{p}.self_attention.out_proj.bias", (d,), "float32"),
+            (f"{p}.ln_2.weight", (d,), "float32"),
+            (f"{p}.ln_2.bias", (d,), "float32"),
+            (f"{p}.mlp.0.weight", (mlp, d), "float32"),
+            (f"{p}.mlp.0.bias", (mlp,), "float32"),
+            (f"{p}.mlp.3.weight", (d, mlp), "float32"),
+            (f"{p}.mlp.3.bias", (d,), "float32"),
+        ]
+    out += [
+        ("encoder.ln.weight", (d,), "float32"),
+        ("encoder.ln.bias", (d,), "float32"),
+        ("heads.head.weight", (num_classes, d), "float32"),
+        ("heads.head.bias", (num_classes,), "float32"),
+    ]
+    return out
+
+
+LAYOUTS = {
+    "cifar10": cifar_cnn_layout,
+    "resnet18": lambda: resnet_layout("resnet18"),
+    "resnet50": lambda: resnet_layout("resnet50"),
+    "vit_b16": vit_b16_layout,
+}
+
+
+def get_layout(name: str) -> Layout:
+    return LAYOUTS[name]()
+
+
+def param_names(layout: Layout, buffers: Iterable[str] = ("running_mean", "running_var", "num_batches_tracked")) -> List[str]:
+    """Entries that are nn.Parameters (named_parameters order = state_dict order minus buffers)."""
+    bufs = tuple(buffers)
+    return [n for n, _, _ in layout if not n.endswith(bufs)]
