@@ -157,7 +157,7 @@ def main():
         bytes_round = 4 * layout.n_f32 * (staged + rows)  # compulsory: each staged source read once, each output written once
         per_call_bytes = 4 * layout.n_f32 * (len(col) + rows)  # SURVEY §8(d) B summed over the round's calls
         result_extra = dict(
-            kernel="k_round_tiled_f32", plan=dict(groups=plan.info.n_groups, staged_sources=staged,
+            kernel="k_round_f32_persistent", plan=dict(groups=plan.info.n_groups, staged_sources=staged,
                                                   c4=plan.info.c4, lds_bytes=plan.info.lds_bytes),
             per_call_equivalent_GBps=per_call_bytes / (k_ms * 1e-3) / 1e9, parity_k3_vs_k1_row0=parity_ok)
         steps_done = args.steps
@@ -190,7 +190,7 @@ def main():
         staged = sr.staged_sources
         rows = sr.local_rows
         bytes_round = 4 * layout.n_f32 * (staged + rows)
-        result_extra = dict(kernel="k_round_tiled_f32", halo_rows_in=sr.halo_rows_in,
+        result_extra = dict(kernel="k_round_f32_persistent", halo_rows_in=sr.halo_rows_in,
                             halo_bytes_in=sr.halo_rows_in * 4 * layout.ld_f32)
         units = n_dev_total * n_params * args.steps
         parity_ok = None

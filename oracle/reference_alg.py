@@ -60,19 +60,22 @@ def sim_centrality_weights(order: Sequence[int], self_idx: int, cent: Dict[int, 
 
 
 def cosine_similarity(params_a: Sequence[np.ndarray], params_b: Sequence[np.ndarray]) -> float:
-    """decentralized_client.py:661-681 in float64: per parameter, 1-D tensors get a trailing
-    unit dim, nn.CosineSimilarity(dim=1, eps=1e-6) (x/max(|x|,eps) . y/max(|y|,eps) along dim 1),
-    mean over the remaining elements; then the average over parameters."""
+    """decentralized_client.py:661-681 in fp32 like torch: per parameter, 1-D tensors get a
+    trailing unit dim, nn.CosineSimilarity(dim=1, eps=1e-6) = sum over dim 1 of
+    (x / max(|x|, eps)) * (y / max(|y|, eps)) with the norms computed first (an fp32 norm that
+    overflows is inf and zeroes its row, as in torch), mean over the remaining elements, then
+    the average over parameters."""
     total = 0.0
-    for a, b in zip(params_a, params_b):
-        a = np.asarray(a, dtype=np.float64)
-        b = np.asarray(b, dtype=np.float64)
-        if a.ndim < 2:
-            a = a.reshape(-1, 1)
-            b = b.reshape(-1, 1)
-        na = np.maximum(np.sqrt((a * a).sum(axis=1, keepdims=True)), 1e-6)
-        nb = np.maximum(np.sqrt((b * b).sum(axis=1, keepdims=True)), 1e-6)
-        total += float(((a / na) * (b / nb)).sum(axis=1).mean())
+    with np.errstate(over="ignore", invalid="ignore"):
+        for a, b in zip(params_a, params_b):
+            a = np.asarray(a, dtype=np.float32)
+            b = np.asarray(b, dtype=np.float32)
+            if a.ndim < 2:
+                a = a.reshape(-1, 1)
+                b = b.reshape(-1, 1)
+            na = np.maximum(np.sqrt((a * a).sum(axis=1, keepdims=True, dtype=np.float32)), np.float32(1e-6))
+            nb = np.maximum(np.sqrt((b * b).sum(axis=1, keepdims=True, dtype=np.float32)), np.float32(1e-6))
+            total += float(((a / na) * (b / nb)).sum(axis=1, dtype=np.float32).astype(np.float64).mean())
     return total / len(params_a)
 
 

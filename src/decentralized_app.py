@@ -1,0 +1,243 @@
+"""Experiment driver — mirror of the reference's src/decentralized_app.py.
+
+Round structure, operand order, RNG draws, strategy dispatch, scheduler stepping and the
+checkpoint/resume protocol follow the reference (decentralized_app.py:96-644).  MI355X
+difference: when a GPU is visible every client's model is bound to one device-resident
+ModelPool row (topology_aware_learning_amd.arena), so local training and the aggregation
+kernels work on the same HBM bytes and no model crosses PCIe between rounds
+(TAL_DEVICE_POOL=0 keeps the reference's CPU-resident models).
+"""
+from __future__ import annotations
+
+import glob
+import json
+import logging
+import os
+import pathlib
+import shutil
+from pathlib import Path
+
+import numpy
+import torch
+
+from src.aggregation_scheduler import (BaseScheduler, CosineAnnealingWarmRestarts, ExponentialScheduler,
+                                       OscilateScheduler)
+from src.decentralized_client import (DecentralClient, centrality_module_avg, create_centrality_dict,  # noqa: F401
+                                      create_clients, scale_agg, sim_centrality_module_avg, test_agg,
+                                      unweighted_module_avg, update_random_agg_coeffs, weighted_module_avg)
+from src.modules import create_model, load_data
+from src.tasks import local_train, no_local_train
+from src.types import DataChoices, Result
+from src.utils import load_checkpoint, process_futures_and_ckpt, set_file_logger
+
+APP_LOG_LEVEL = 21
+logger = logging.getLogger("decentral_app")
+
+# strategy string -> (aggregation app, centrality metric); reference :318-353
+STRATEGIES = {
+    "betCent_sim": (sim_centrality_module_avg, "betweenness"),
+    "degCent_sim": (sim_centrality_module_avg, "degree"),
+    "random": (centrality_module_avg, "random"),
+    "betCent": (centrality_module_avg, "betweenness"),
+    "degCent": (centrality_module_avg, "degree"),
+    "weighted": (weighted_module_avg, None),
+    "unweighted": (unweighted_module_avg, None),
+    "unweighted_fl": (unweighted_module_avg, None),
+    "test_agg": (test_agg, None),
+    "scale_agg": (scale_agg, None),
+}
+
+_DATASETS = {
+    "mnist": (DataChoices.MNIST, 10), "fmnist": (DataChoices.FMNIST, 10), "cifar10": (DataChoices.CIFAR10, 10),
+    "cifar10_mobile": (DataChoices.CIFAR10_MOBILE, 10), "cifar10_vit": (DataChoices.CIFAR10_VIT, 10),
+    "cifar10_resnet18": (DataChoices.CIFAR10_RESTNET18, 10), "cifar10_resnet50": (DataChoices.CIFAR10_RESTNET50, 10),
+    "cifar10_augment": (DataChoices.CIFAR10_AUGMENT, 10), "cifar10_augment_vgg": (DataChoices.CIFAR10_AUGMENT_VGG, 10),
+    "cifar10_vgg": (DataChoices.CIFAR10_VGG, 10), "cifar100_vgg": (DataChoices.CIFAR100_VGG, 100),
+    "cifar10_dropout": (DataChoices.CIFAR10_DROPOUT, 10),
+    "cifar10_augment_dropout": (DataChoices.CIFAR10_AUGMENT_DROPOUT, 10),
+}
+
+
+class DecentrallearnApp:
+    """Decentralized learning experiment (reference :58-454)."""
+
+    def __init__(self, data_dir: str = "../data", topology_path: str = "topology/topo_1.txt",
+                 dataset: str = "mnist", rounds: int = 5, batch_size: int = 16, epochs: int = 2,
+                 lr: float = 1e-3, download: bool = False, train: bool = True, label_alpha: float = 100,
+                 sample_alpha: float = 100, participation: float = 1.0, seed: int | None = 0,
+                 log_dir: str = "./logs", aggregation_strategy: str = "weighted", prox_coeff: float = 0.1,
+                 train_test_val: tuple = None, backdoor: bool = False, backdoor_proportion: float = 0.1,
+                 backdoor_node_idx: int = 0, random_bd: bool = False, many_to_one: bool = True,
+                 offset_clients_data_placement: int = 0, centrality_metric_data_placement: str = "degree",
+                 random_data_placement: bool = True, softmax: bool = False, tiny_mem_num_labels: int = 50,
+                 momentum: float = 0, softmax_coeff: float = 10, optimizer: str = "sgd",
+                 weight_decay: float = 0, beta_1: float = 0.9, beta_2: float = 0.98, scheduler: str = None,
+                 gamma: float = 0.95, T_0: float = 66, T_mult: float = 1, eta_min: float = 1,
+                 trigger: int = 100, num_test: int = 1000, num_example: int = 5000, modulo: int = 16381,
+                 length: int = 20, max_ctx: int = 150, n_layer: int = 4, task_type: str = "multiply",
+                 data_dis: str = "evens", checkpoint_every: int = 5) -> None:
+        args = dict(locals())
+        args.pop("self", None)
+        args["topology_path"] = os.path.basename(args["topology_path"])
+        for k in ("log_dir", "rounds", "checkpoint_every"):
+            args.pop(k, None)
+        # run dir = every other ctor argument joined with "_" (reference :151-162)
+        arg_path = "_".join(map(str, args.values())).replace(".", "").replace("/", "")
+        self.run_dir = Path(f"{log_dir}/{arg_path}/")
+        os.makedirs(self.run_dir, exist_ok=True)
+        with open(f"{self.run_dir}/args.txt", "w") as f:
+            json.dump(args, f)
+
+        if dataset not in _DATASETS and "tiny_mem" not in dataset:
+            raise ValueError(f"unknown dataset {dataset}")
+        self.dataset, self.num_labels = _DATASETS.get(dataset, (None, tiny_mem_num_labels))
+        set_file_logger(filename=f"{self.run_dir}/experiment.log", name="decentral_app")
+
+        self.rng = numpy.random.default_rng(seed)
+        self.seed = seed
+        self.train_test_val = train_test_val
+        if seed is not None:
+            torch.manual_seed(seed)
+        self.max_ctx, self.n_layer = max_ctx, n_layer
+        self.global_model = create_model(data=self.dataset, n_layer=n_layer, max_ctx=max_ctx)
+        self.checkpoint_every = checkpoint_every
+        self.train = train
+        root = pathlib.Path(data_dir)
+        self.train_data = load_data(self.dataset, root, train=True, download=True)
+        self.test_data = load_data(self.dataset, root, train=False, download=True)
+
+        self.topology = numpy.loadtxt(topology_path, dtype=float)
+        num_clients = self.topology.shape[0]
+        self.backdoor = backdoor
+        if backdoor:
+            raise NotImplementedError("backdoor experiments are outside the accelerated path")
+
+        self.aggregation_strategy = aggregation_strategy
+        self.softmax = softmax
+        self.softmax_coeff = softmax_coeff
+        self.aggregation_scheduler = BaseScheduler(self.softmax_coeff)
+        if aggregation_strategy not in STRATEGIES:
+            raise ValueError(f"unknown aggregation strategy {aggregation_strategy}")
+        self.aggregation_function, self.centrality_metric = STRATEGIES[aggregation_strategy]
+        if scheduler == "CA":
+            self.aggregation_scheduler = CosineAnnealingWarmRestarts(T_0=T_0, T_mult=T_mult, eta_min=eta_min,
+                                                                     last_round=-1, softmax_coeff=self.softmax_coeff)
+        if scheduler == "exp":
+            self.aggregation_scheduler = ExponentialScheduler(gamma=gamma, softmax_coeff=self.softmax_coeff)
+        if scheduler == "osc":
+            self.aggregation_scheduler = OscilateScheduler(T_0=T_0, softmax_coeff=self.softmax_coeff)
+
+        self.epochs, self.batch_size, self.lr = epochs, batch_size, lr
+        self.momentum, self.optimizer, self.weight_decay = momentum, optimizer, weight_decay
+        self.beta_1, self.beta_2 = beta_1, beta_2
+        self.prox_coeff = prox_coeff
+        self.participation = participation
+        if aggregation_strategy == "unweighted_fl":  # fully connected, no self loops (:386-389)
+            self.topology = numpy.ones(self.topology.shape)
+            numpy.fill_diagonal(self.topology, 0)
+        self.rounds = rounds
+        self.start_round = 0
+        if sample_alpha <= 0 or label_alpha <= 0:
+            raise ValueError("Argument `alpha` must be greater than 0.")
+        self.label_alpha, self.sample_alpha = label_alpha, sample_alpha
+        if backdoor_node_idx >= num_clients:
+            raise ValueError("Backdoor node index must be less than the # of clients.")
+
+        self.clients = create_clients(num_clients, self.dataset, self.train_data, self.num_labels, self.test_data,
+                                      label_alpha, sample_alpha, self.rng, self.topology, prox_coeff, self.run_dir,
+                                      train_test_val)
+        self.pool = self._bind_device_pool()
+        self.centrality_dict = create_centrality_dict(self.topology, self.rng)
+        logger.log(APP_LOG_LEVEL, f"Created {len(self.clients)} clients")
+        self.client_results: list[Result] = []
+
+        ckpts = glob.glob(f"{self.run_dir}/*.pth")
+        if ckpts:
+            path = max(ckpts, key=os.path.getctime)
+            logger.log(APP_LOG_LEVEL, f"Loading lastest checkpoint from:  {path}")
+            try:
+                (self.start_round, self.clients, self.client_results,
+                 self.aggregation_scheduler) = load_checkpoint(path, self.clients, self.aggregation_scheduler)
+            except Exception as exc:  # corrupt checkpoint: the reference deletes the run dir (:449-452)
+                shutil.rmtree(self.run_dir, ignore_errors=True)
+                raise RuntimeError(f"corrupt checkpoint {path}: run directory removed") from exc
+            self.start_round += 1
+            print(f"loaded latest ckpt from: {path}")
+
+    def _bind_device_pool(self):
+        if os.environ.get("TAL_DEVICE_POOL", "1") == "0" or not torch.cuda.is_available():
+            return None
+        from topology_aware_learning_amd.aggregate import layout_of_module
+        from topology_aware_learning_amd.arena import ModelPool
+
+        layout = layout_of_module(self.clients[0].model)
+        pool = ModelPool(layout, len(self.clients), torch.device("cuda", torch.cuda.current_device()))
+        for c in self.clients:
+            c.model.to(pool.device)
+            pool.bind(c.model, c.idx)
+        return pool
+
+    def close(self) -> None:
+        pass
+
+    def run(self):
+        """Round loop with periodic checkpoints (reference :460-518)."""
+        self.round_states = {self.start_round: {i: {"agg": ([{}], self.clients[i])} for i in range(len(self.clients))}}
+        train_result_futures = []
+        if self.start_round >= self.rounds:
+            return 0
+        for round_idx in range(self.start_round, self.rounds):
+            train_result_futures.extend(self._federated_round(round_idx))
+            if round_idx % self.checkpoint_every == 0 and round_idx != 0:
+                process_futures_and_ckpt(self.client_results, train_result_futures, self.round_states, round_idx,
+                                         self.run_dir)
+            self.round_states.pop(round_idx - 1, None)
+        process_futures_and_ckpt(self.client_results, train_result_futures, self.round_states, self.rounds,
+                                 self.run_dir)
+        return 0
+
+    def _federated_round(self, round_idx: int):
+        """Client selection, local training, aggregation (reference :520-644)."""
+        print("round idx: ", round_idx)
+        job = local_train if self.train else no_local_train
+        size = int(max(1, len(self.clients) * self.participation))
+        selected = self.rng.choice(list(range(len(self.clients))), size=size, replace=False).tolist()
+        print(f"{selected=}")
+        futures = []
+        nxt = self.round_states[round_idx + 1] = {}
+        cur = self.round_states[round_idx]
+        for client in self.clients:
+            train_input = cur[client.idx]["agg"]
+            if client.idx not in selected:
+                nxt[client.idx] = {"train": train_input}
+                continue
+            prox_neighbors = [cur[i]["agg"] for i in client.get_neighbors()]
+            nxt[client.idx] = {"train": job(train_input, round_idx, self.epochs, self.batch_size, self.lr,
+                                            self.momentum, self.prox_coeff, self.seed, self.backdoor, self.dataset,
+                                            self.optimizer, self.weight_decay, self.beta_1, self.beta_2,
+                                            *prox_neighbors)}
+        if self.centrality_metric == "random":
+            self.centrality_dict = update_random_agg_coeffs(seed=self.seed, round_idx=round_idx,
+                                                            num_clients=len(self.clients),
+                                                            centrality_dict=self.centrality_dict)
+        for client in self.clients:
+            agg_client = nxt[client.idx]["train"]
+            if client.idx not in selected:
+                nxt[client.idx]["agg"] = agg_client
+                futures.append(agg_client)
+                continue
+            neighbor_idxs = client.get_neighbors()  # second, independent draw (:616)
+            if len(neighbor_idxs) == 0:
+                nxt[client.idx]["agg"] = agg_client
+                futures.append(agg_client)
+                continue
+            neighbor_idxs.append(client.idx)  # self is the last operand (:625)
+            agg_neighbors = [nxt[i]["train"] for i in neighbor_idxs]
+            future = self.aggregation_function(
+                agg_client, self.seed, *agg_neighbors, centrality_metric=self.centrality_metric,
+                centrality_dict=self.centrality_dict, softmax=self.softmax,
+                softmax_coeff=self.aggregation_scheduler.get_softmax_coeff())
+            futures.append(future)
+            nxt[client.idx]["agg"] = future
+        self.aggregation_scheduler.step(round_idx)
+        return futures

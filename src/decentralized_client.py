@@ -1,0 +1,225 @@
+"""Client object and neighbor-aggregation apps — mirror of the reference's
+src/decentralized_client.py with the aggregation arithmetic on the MI355X.
+
+Every app keeps the reference's signature, return value and side effects
+(`fn(client_future, seed, *neighbor_futures, **kwargs) -> client_future`, the aggregating
+client's model overwritten in place, the self model being the last operand), computes its
+weight vector on the host with the reference's float64 arithmetic
+(topology_aware_learning_amd.weights) and hands the reduction
+`sum_i fp32(w_i) * state_dict_i` to the HIP library (topology_aware_learning_amd.aggregate):
+exact mode, bit-identical to the reference's clone/mul/add_/load_state_dict on CPU.
+
+Deliberate difference: the reference calls `model.to("cpu")` on every operand
+(decentralized_client.py:404); here models stay where they are (GPU pool rows are read in
+place, CPU models are staged through pinned memory) — the values are the same.
+"""
+from __future__ import annotations
+
+import json
+from typing import List, Optional
+
+import networkx as nx
+import numpy as np
+import torch
+from numpy.random import Generator
+from pydantic import BaseModel, ConfigDict, Field
+from torch.utils.data import Dataset, Subset
+
+from src._parsl_compat import python_app
+from src.types import DataChoices, Result  # noqa: F401  (Result is part of the interface)
+from topology_aware_learning_amd import weights as _w
+from topology_aware_learning_amd.aggregate import aggregate_models
+from topology_aware_learning_amd.similarity import cosine_pairs
+
+
+class DecentralClient(BaseModel):
+    """Client class (reference :30-71)."""
+
+    model_config = ConfigDict(arbitrary_types_allowed=True)
+
+    idx: int = Field(description="Client ID.")
+    prox_coeff: float = Field(description="Proximal term coefficient (FedProx).")
+    model: torch.nn.Module = Field(description="Client local model.")
+    train_data: Optional[Subset] = Field(description="Subset of data this client will train on.")
+    test_data: Optional[Subset] = Field(description="Subset of local data this client will test on.")
+    valid_data: Optional[Subset] = Field(description="Subset of local data this client will validate on.")
+    global_test_data: Dataset = Field(description="Global test set every client is evaluated on.")
+    global_backdoor_test_data: Optional[Subset] = Field(description="Backdoored global test subset.")
+    neighbors: list[int] = Field(description="list of this clients neighbors")
+    neighbor_probs: list[float] = Field(description="neighbors' link survival probabilities")
+
+    def get_neighbors(self) -> list[int]:
+        """Neighbors whose link survives this draw: one Bernoulli(p) per neighbor from the
+        global NumPy RNG (reference :63-71, faulty-network simulation)."""
+        keep = np.random.binomial(1, self.neighbor_probs)
+        return [a for a, b in zip(self.neighbors, keep) if b > 0]
+
+
+# ------------------------------------------------------------------------------------------
+# setup helpers (outside the hot path; reference :74-381)
+# ------------------------------------------------------------------------------------------
+def update_random_agg_coeffs(seed: int, round_idx: int, num_clients: int,
+                             centrality_dict: dict[str, dict[int, float]]) -> dict[str, dict[int, float]]:
+    """Fresh U(0,1) coefficient per client for the "random" strategy, seeded by
+    seed + round_idx (reference :161-181)."""
+    draws = np.random.default_rng(seed=(seed + round_idx)).uniform(low=0.0, high=1.0, size=num_clients)
+    centrality_dict["random"] = {i: draws[i].item() for i in range(num_clients)}
+    return centrality_dict
+
+
+def create_centrality_dict(topology: np.ndarray, rng: Generator) -> dict[str, dict[int, float]]:
+    """degree / betweenness (normalized, endpoints) / random centrality per node
+    (reference :184-221).  Pinned by tests/golden/centrality.json."""
+    g = nx.from_numpy_array(topology)
+    out: dict[str, dict[int, float]] = {
+        "degree": nx.degree_centrality(g),
+        "betweenness": nx.betweenness_centrality(g, normalized=True, endpoints=True),
+    }
+    draws = rng.uniform(low=0.0, high=1.0, size=len(g))
+    out["random"] = {i: draws[i].item() for i in range(len(g))}
+    return out
+
+
+def _split_indices(n: int, num_clients: int, sample_alpha: float, rng: Generator) -> List[List[int]]:
+    """Disjoint client shards with Dirichlet(sample_alpha) sizes, >= 1 sample each.
+
+    The reference's federated_split (src/data.py:136-344) also skews labels (label_alpha);
+    data partitioning is outside the accelerated path and only this simpler split is provided.
+    """
+    props = rng.dirichlet(np.full(num_clients, float(sample_alpha)))
+    counts = np.maximum(1, np.floor(props * n).astype(int))
+    while counts.sum() > n:
+        counts[np.argmax(counts)] -= 1
+    perm = rng.permutation(n)
+    out, pos = [], 0
+    for c in counts:
+        out.append(perm[pos: pos + c].tolist())
+        pos += c
+    return out
+
+
+def create_clients(num_clients: int, data_name: DataChoices, train_data: Dataset, num_labels: int,
+                   global_test_data: Dataset, label_alpha: float, sample_alpha: float, rng: Generator,
+                   topology: np.ndarray, prox_coeff: float, run_dir, train_test_val_split: tuple = None,
+                   backdoor_test_data: Dataset = None, backdoor: bool = False, backdoor_proportion: float = 0.1,
+                   backdoor_node_idx: int = 0, random_bd: bool = False, many_to_one: bool = True,
+                   offset_clients_data_placement: int = 0, centrality_metric_data_placement: str = "degree",
+                   random_data_placement: bool = True, ckpt_dir: str = "./ckpt", trigger: int = 100,
+                   ) -> list[DecentralClient]:
+    """Clients with disjoint data and their topology neighbors (reference :224-380).
+    neighbors = columns with topology[idx] > 0, probabilities = those entries (:348-350)."""
+    from src.modules import create_model
+
+    if backdoor:
+        raise NotImplementedError("backdoor data placement is outside the accelerated path")
+    shards = _split_indices(len(train_data), num_clients, sample_alpha, rng)
+    clients = []
+    label_counts = {lab: [0] * num_clients for lab in range(num_labels)}
+    targets = getattr(train_data, "targets", None)
+    for idx in range(num_clients):
+        neighbors = np.where(topology[idx] > 0)[0].tolist()
+        probs = topology[idx][np.argwhere(topology[idx] > 0)].flatten().tolist()
+        sub = Subset(train_data, shards[idx])
+        if targets is not None:
+            for i in shards[idx]:
+                label_counts[int(targets[i])][idx] += 1
+        clients.append(DecentralClient(
+            idx=idx, model=create_model(data_name), train_data=sub, test_data=None, valid_data=None,
+            global_test_data=global_test_data, neighbors=neighbors, neighbor_probs=probs,
+            prox_coeff=prox_coeff, global_backdoor_test_data=backdoor_test_data,
+        ))
+    with open(f"{run_dir}/label_counts_per_worker.txt", "w") as f:
+        json.dump(label_counts, f)
+    return clients
+
+
+# ------------------------------------------------------------------------------------------
+# the aggregation apps (hot path)
+# ------------------------------------------------------------------------------------------
+def _models(futures) -> list:
+    return [f[1].model for f in futures]
+
+
+@python_app(executors=["threadpool_executor"])
+def weighted_module_avg(client_future, seed: int, *neighbor_futures, **kwargs):
+    """Data-size weighted average (reference :383-415)."""
+    if seed is not None:
+        torch.manual_seed(seed)
+    print("weighted aggregate round")
+    w = _w.weighted([len(f[1].train_data) for f in neighbor_futures])
+    aggregate_models(_models(neighbor_futures), w, client_future[1].model)
+    return client_future
+
+
+@python_app(executors=["threadpool_executor"])
+def unweighted_module_avg(client_future, seed: int, *neighbor_futures, **kwargs):
+    """Plain average, w = 1/M (reference :418-448)."""
+    if seed is not None:
+        torch.manual_seed(seed)
+    print("unweighted aggregate round")
+    aggregate_models(_models(neighbor_futures), _w.unweighted(len(neighbor_futures)), client_future[1].model)
+    return client_future
+
+
+@python_app(executors=["threadpool_executor"])
+def sim_centrality_module_avg(client_future, seed: int, *neighbor_futures, **kwargs):
+    """Centrality weights whose softmax sign follows the least similar neighbor
+    (reference :451-550); the similarities come from one K2 launch."""
+    if seed is not None:
+        torch.manual_seed(seed)
+    cent_dict = kwargs["centrality_dict"]
+    metric = kwargs["centrality_metric"]
+    softmax = kwargs["softmax"]
+    coeff = kwargs["softmax_coeff"]
+    print(f"{metric} aggregate round w/ {softmax=}")
+    me = client_future[1]
+    others = [f[1] for f in neighbor_futures if f[1].idx != me.idx]
+    sims_list = cosine_pairs(me.model, [c.model for c in others])
+    sims = {c.idx: s for c, s in zip(others, sims_list)}
+    order = [f[1].idx for f in neighbor_futures]
+    w, coeff = _w.sim_centrality(order, me.idx, cent_dict[metric], sims, softmax, coeff)
+    if softmax:
+        print(f"client_idx={me.idx} softmaxing aggregation weights w/ softmax_coeff={coeff}")
+    else:
+        print("1/N aggregation weights")
+    aggregate_models(_models(neighbor_futures), w, me.model)
+    return client_future
+
+
+@python_app(executors=["threadpool_executor"])
+def centrality_module_avg(client_future, seed: int, *neighbor_futures, **kwargs):
+    """Centrality weights, softmax(coeff * c) or c / sum(c) (reference :553-612)."""
+    if seed is not None:
+        torch.manual_seed(seed)
+    cent_dict = kwargs["centrality_dict"]
+    metric = kwargs["centrality_metric"]
+    softmax = kwargs["softmax"]
+    coeff = kwargs["softmax_coeff"]
+    print(f"{metric} aggregate round w/ {softmax=}")
+    order = [f[1].idx for f in neighbor_futures]
+    w = _w.centrality(order, cent_dict[metric], softmax, coeff)
+    aggregate_models(_models(neighbor_futures), w, client_future[1].model)
+    return client_future
+
+
+@python_app(executors=["threadpool_executor"])
+def scale_agg(client_future, seed: int, *neighbor_futures, **kwargs):
+    """Self model scaled by 1/M (only self is read; reference :615-647)."""
+    if seed is not None:
+        torch.manual_seed(seed)
+    print("unweighted aggregate round")
+    w = 1 / len(neighbor_futures)
+    aggregate_models([client_future[1].model], [w], client_future[1].model)
+    return client_future
+
+
+@python_app(executors=["threadpool_executor"])
+def test_agg(client_future, seed: int, *neighbor_futures, **kwargs):
+    """No-op aggregation (reference :650-658)."""
+    return client_future
+
+
+def cosine_similarity(model_1, model_2):
+    """Average per-parameter cosine similarity of two models (reference :661-681), as a 0-d
+    fp32 tensor like the reference's."""
+    return torch.tensor(cosine_pairs(model_1, [model_2])[0], dtype=torch.float32)

@@ -52,6 +52,8 @@ def import_reference():
     from src.models import resnet
     from src import modules
 
+    # this repo also has a `src` package (the interface mirror): make sure the reference's won
+    assert str(REF) in dc.__file__, dc.__file__
     return dc, sch, resnet, modules
 
 
@@ -63,22 +65,8 @@ from torch.utils.data import Subset, TensorDataset  # noqa: E402
 from topology_aware_learning_amd import synth  # noqa: E402
 
 
-class TinyNet(nn.Module):
-    """Small module covering every entry kind the reference models have."""
-
-    def __init__(self):
-        super().__init__()
-        self.conv = nn.Conv2d(3, 4, 3)            # [4,3,3,3] + bias  (cosine: column kind, B=9)
-        self.bn = nn.BatchNorm2d(4)               # weight/bias/running_*/num_batches_tracked
-        self.pw = nn.Conv2d(4, 6, 1, bias=False)  # [6,4,1,1]          (row kind, B=1)
-        self.fc = nn.Linear(13, 5)                # [5,13] + bias (odd sizes -> n % 4 tails)
-        self.bn2 = nn.BatchNorm1d(5)
-
-
-class Vec(nn.Module):
-    def __init__(self, m):
-        super().__init__()
-        self.v = nn.Parameter(torch.zeros(m))
+sys.path.insert(0, str(HERE.parent))
+from _models import TinyNet, Vec  # noqa: E402
 
 
 DUMMY = TensorDataset(torch.zeros(4, 1), torch.zeros(4, dtype=torch.long))

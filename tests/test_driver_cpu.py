@@ -1,0 +1,73 @@
+"""BASELINE config 1 plumbing: 8-device ring, CIFAR-10 CNN, one round through
+src/experiments/decentralized_main.py on the CPU.
+
+There is no GPU here, so the test swaps the device reduction for a recorder that checks what
+the driver hands it (operands in reference order, self last, weights) and applies the
+reference's own CPU loop (oracle/torch_path.py) — test infrastructure only.  The same run
+goes through the HIP library in tests/test_gpu_interface.py."""
+import numpy as np
+import networkx as nx
+import pytest
+import torch
+
+from oracle import torch_path
+
+
+@pytest.fixture()
+def recorder(monkeypatch):
+    import src.decentralized_client as dc
+
+    calls = []
+
+    def fake_aggregate(operands, weights, target, mode=None):
+        sds = [{k: v.detach().clone() for k, v in m.state_dict().items()} for m in operands]
+        torch_path.aggregate_call(sds, weights, target.state_dict())
+        calls.append(dict(ids=[id(m) for m in operands], target=id(target), weights=list(weights),
+                          out={k: v.detach().clone() for k, v in target.state_dict().items()}))
+        return target
+
+    monkeypatch.setattr(dc, "aggregate_models", fake_aggregate)
+    return calls
+
+
+def test_config1_one_round(tmp_path, monkeypatch, recorder):
+    monkeypatch.setenv("TAL_SYNTHETIC_DATA", "1")
+    monkeypatch.setenv("TAL_SYNTHETIC_SAMPLES", "64")
+    monkeypatch.setenv("TAL_DEVICE_POOL", "0")
+    topo = tmp_path / "ring8.txt"
+    np.savetxt(topo, nx.to_numpy_array(nx.cycle_graph(8)), fmt="%d")
+    from src.experiments import decentralized_main
+
+    rc = decentralized_main.main(["--dataset", "cifar10", "--aggregation_strategy", "unweighted", "--rounds", "1",
+                                  "--epochs", "1", "--topology_file", str(topo), "--out_dir", str(tmp_path / "logs"),
+                                  "--batch_size", "32"])
+    assert rc == 0
+    assert len(recorder) == 8
+    for c in recorder:
+        assert len(c["ids"]) == 3 and c["ids"][-1] == c["target"]  # self last, aggregated in place
+        assert c["weights"] == [1 / 3] * 3
+    ckpts = list((tmp_path / "logs").rglob("0_ckpt.pth"))
+    assert len(ckpts) == 1
+    ck = torch.load(ckpts[0], weights_only=False)
+    assert ck["round_idx"] == 0 and len(ck["client_state_dicts"]) == 8
+    outs = sorted((tuple(c["out"]["network.0.bias"][:3].tolist()) for c in recorder))
+    saved = sorted(tuple(sd["network.0.bias"][:3].tolist()) for sd in ck["client_state_dicts"])
+    assert outs == saved
+
+
+def test_strategy_dispatch_and_unweighted_fl_topology(tmp_path, monkeypatch, recorder):
+    monkeypatch.setenv("TAL_SYNTHETIC_DATA", "1")
+    monkeypatch.setenv("TAL_SYNTHETIC_SAMPLES", "32")
+    monkeypatch.setenv("TAL_DEVICE_POOL", "0")
+    topo = tmp_path / "ring4.txt"
+    np.savetxt(topo, nx.to_numpy_array(nx.cycle_graph(4)), fmt="%d")
+    from src.decentralized_app import DecentrallearnApp, STRATEGIES
+    from src.decentralized_client import centrality_module_avg, unweighted_module_avg
+
+    assert STRATEGIES["degCent"] == (centrality_module_avg, "degree")
+    app = DecentrallearnApp(dataset="cifar10", topology_path=str(topo), rounds=1, epochs=1, batch_size=32,
+                            aggregation_strategy="unweighted_fl", log_dir=str(tmp_path / "l"), train=False)
+    assert app.aggregation_function is unweighted_module_avg
+    assert np.array_equal(app.topology, np.ones((4, 4)) - np.eye(4))
+    app.run()
+    assert len(recorder) == 4 and all(len(c["ids"]) == 4 for c in recorder)

@@ -1,0 +1,148 @@
+"""The reference interface (src/decentralized_client.py apps, cosine_similarity, the round
+driver) running on the HIP library, bit-compared with the reference's own outputs
+(tests/golden/tiny_cases.*) for every app and every model placement."""
+import json
+
+import networkx as nx
+import numpy as np
+import pytest
+import torch
+from torch.utils.data import Subset, TensorDataset
+
+from oracle import reference_alg as ra
+from oracle import torch_path
+from topology_aware_learning_amd.arena import ModelPool, StateLayout
+from topology_aware_learning_amd.round import RoundExecutor
+
+from _models import TinyNet
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+TINY = json.loads((GOLDEN / "tiny_cases.json").read_text())
+TINYZ = np.load(GOLDEN / "tiny_cases.npz")
+CENT = {k: {int(i): v for i, v in d.items()} for k, d in TINY["centrality"].items()}
+LAYOUT = [(n, tuple(s), d) for n, s, d in TINY["layout"]]
+DUMMY = TensorDataset(torch.zeros(4, 1), torch.zeros(4, dtype=torch.long))
+
+
+def make_client(idx, model, n_train):
+    from src.decentralized_client import DecentralClient
+
+    data = TensorDataset(torch.zeros(n_train, 1), torch.zeros(n_train, dtype=torch.long))
+    return DecentralClient(idx=idx, prox_coeff=0.0, model=model, train_data=Subset(data, list(range(n_train))),
+                           test_data=None, valid_data=None, global_test_data=DUMMY,
+                           global_backdoor_test_data=None, neighbors=[], neighbor_probs=[])
+
+
+def bits_equal(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    if a.dtype == np.float32:
+        return np.array_equal(np.isnan(a), np.isnan(b)) and np.array_equal(
+            a[~np.isnan(a)].view(np.uint32), b[~np.isnan(b)].view(np.uint32))
+    return np.array_equal(a, b)
+
+
+def build_clients(case, placement, cuda):
+    ci, M = case["case"], case["M"]
+    layout = StateLayout.from_layout(LAYOUT)
+    pool = ModelPool(layout, M, cuda) if placement == "pool" else None
+    clients = []
+    for oi, idx in enumerate(case["order"]):
+        m = TinyNet()
+        m.load_state_dict({n: torch.from_numpy(TINYZ[f"c{ci}_in{oi}_{n}"].copy()) for n, _, _ in LAYOUT})
+        if placement == "gpu":
+            m = m.to(cuda)
+        elif placement == "pool":
+            m = m.to(cuda)
+            pool.bind(m, oi)
+        clients.append((["r"], make_client(idx, m, case["data_lens"][oi])))
+    return clients, pool
+
+
+@pytest.mark.parametrize("placement", ["cpu", "gpu", "pool"])
+def test_every_app_bit_exact(cuda, placement):
+    import src.decentralized_client as dc
+
+    for case in TINY["cases"]:
+        clients, pool = build_clients(case, placement, cuda)
+        fn = getattr(dc, case["fn"])
+        res = fn(clients[-1], 0, *clients, centrality_metric=case["centrality_metric"], centrality_dict=CENT,
+                 softmax=case["softmax"], softmax_coeff=case["softmax_coeff"]).result()
+        assert res is clients[-1]
+        sd = res[1].model.state_dict()
+        if placement == "pool":
+            assert pool.row_of(res[1].model) == case["M"] - 1  # written in place, still bound
+        for name, _, _ in LAYOUT:
+            assert bits_equal(sd[name].detach().cpu().numpy(), TINYZ[f"c{case['case']}_out_{name}"]), \
+                (case["case"], case["fn"], name)
+
+
+def test_cosine_similarity_matches_reference(cuda):
+    import src.decentralized_client as dc
+
+    for case in [c for c in TINY["cases"] if c["fn"] == "sim_centrality_module_avg"]:
+        for placement in ("cpu", "pool"):
+            clients, _ = build_clients(case, placement, cuda)
+            for j, ref in enumerate(case["cosine"]):
+                got = float(dc.cosine_similarity(clients[-1][1].model, clients[j][1].model))
+                assert abs(got - ref) < 2e-5, (case["case"], j, got, ref)
+
+
+def test_round_executor_snapshot_and_sequential(cuda):
+    """K3 over a pool == per-call oracle on the pre-round snapshot; sequential mode == the
+    reference driven in client order (tests/golden/round_4ring)."""
+    meta = json.loads((GOLDEN / "round_4ring.json").read_text())
+    z = np.load(GOLDEN / "round_4ring.npz")
+    layout = StateLayout.from_layout([(n, tuple(s), d) for n, s, d in meta["layout"]])
+    orders = meta["orders"]
+    ws = [ra.unweighted_weights(len(o)) for o in orders]
+    pool = ModelPool(layout, 4, cuda)
+    for i in range(4):
+        pool.load_row(i, {n: torch.from_numpy(z[f"in{i}_{n}"]) for n, _, _ in meta["layout"]})
+    before = [{k: v.cpu().clone() for k, v in pool.state_dict(i).items()} for i in range(4)]
+    RoundExecutor(pool).run(orders, ws)
+    for i in range(4):
+        target = {k: v.clone() for k, v in before[i].items()}
+        torch_path.aggregate_call([before[j] for j in orders[i]], ws[i], target)
+        got = pool.state_dict(i)
+        for k in target:
+            assert bits_equal(got[k].cpu().numpy(), target[k].numpy()), (i, k)
+
+
+def test_driver_config1_on_gpu(cuda, tmp_path, monkeypatch):
+    """decentralized_main.py, 8-ring CIFAR CNN, one round, device-resident pool: every
+    aggregation the driver issues goes through the HIP library and equals the reference loop
+    applied to the same operands."""
+    import src.decentralized_client as dc
+    from topology_aware_learning_amd.aggregate import aggregate_models as real
+
+    monkeypatch.setenv("TAL_SYNTHETIC_DATA", "1")
+    monkeypatch.setenv("TAL_SYNTHETIC_SAMPLES", "64")
+    checked = []
+
+    def checked_aggregate(operands, weights, target, mode=0):
+        sds = [{k: v.detach().cpu().clone() for k, v in m.state_dict().items()} for m in operands]
+        ref = {k: v.clone() for k, v in sds[-1].items()}
+        torch_path.aggregate_call(sds, weights, ref)
+        out = real(operands, weights, target)
+        assert getattr(target, "_tal_pool", None) is not None  # device-resident path
+        for k, v in target.state_dict().items():
+            assert bits_equal(v.detach().cpu().numpy(), ref[k].numpy()), k
+        checked.append(len(operands))
+        return out
+
+    monkeypatch.setattr(dc, "aggregate_models", checked_aggregate)
+    from src import _parsl_compat
+
+    _parsl_compat.shutdown()
+    _parsl_compat.configure({"threadpool_executor": 1})  # no in-place race between snapshot and kernel
+    topo = tmp_path / "ring8.txt"
+    np.savetxt(topo, nx.to_numpy_array(nx.cycle_graph(8)), fmt="%d")
+    from src.experiments import decentralized_main
+
+    rc = decentralized_main.main(["--dataset", "cifar10", "--aggregation_strategy", "degCent", "--softmax",
+                                  "--rounds", "2", "--epochs", "1", "--topology_file", str(topo), "--out_dir",
+                                  str(tmp_path / "logs"), "--batch_size", "32"])
+    _parsl_compat.configure({"threadpool_executor": 2})
+    assert rc == 0 and checked == [3] * 16

@@ -1,0 +1,89 @@
+"""The C-ABI library loads and exports every symbol include/tal_agg.h declares; argument
+errors are reported through status codes + tal_last_error (no GPU needed); the product path
+refuses CPU tensors instead of computing on the CPU."""
+import ctypes
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from topology_aware_learning_amd import _lib, ops
+
+from conftest import ROOT
+
+
+def header_functions():
+    text = (ROOT / "include" / "tal_agg.h").read_text()
+    return sorted(set(re.findall(r"^\s*(?:const char\*|int32_t|int64_t)\s+(tal_\w+)\(", text, re.M)))
+
+
+def test_exports_every_declared_symbol():
+    L = _lib.load()
+    declared = header_functions()
+    assert len(declared) >= 12
+    for name in declared:
+        assert hasattr(L, name), name
+    assert sorted(_lib.EXPORTED) == declared
+    assert L.tal_abi_version() == _lib.ABI_VERSION
+
+
+def test_library_is_gfx950_code():
+    data = (ROOT / "topology_aware_learning_amd" / "libtal_agg.so").read_bytes()
+    assert b"gfx950" in data
+
+
+def test_error_status_and_message():
+    L = _lib.load()
+    P = (ctypes.c_void_p * 1)()
+    W = (ctypes.c_double * 1)(1.0)
+    rc = L.tal_agg_f32(P, W, 0, None, 10, 1, None)
+    assert rc == _lib.TAL_ERR_INVALID and b"m must be" in L.tal_last_error()
+    rc = L.tal_agg_i64(P, W, 1, None, 10, None)
+    assert rc == _lib.TAL_ERR_INVALID and b"null" in L.tal_last_error()
+    rc = L.tal_agg_f32(P, W, 1, None, 0, 1, None)  # n == 0: nothing to do
+    assert rc == _lib.TAL_OK
+    info = _lib.RoundPlanInfo()
+    rc = L.tal_agg_round_f32(None, 4, None, 4, 4, None, ctypes.byref(info), 1, None)
+    assert rc == _lib.TAL_ERR_INVALID
+    assert L.tal_round_plan_words(-1, 0) == -1
+    assert L.tal_cosine_scratch_bytes(0, 1) == -1
+
+
+def test_in_place_multi_group_rejected():
+    import networkx as nx
+
+    g = nx.random_regular_graph(8, 64, seed=0)
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(64)]
+    row_ptr = np.cumsum([0] + [len(o) for o in orders]).astype(np.int32)
+    col = np.concatenate(orders).astype(np.int32)
+    w = np.full(len(col), 1 / 9)
+    plan = ops.build_plan(row_ptr, col, w, np.arange(64, dtype=np.int32), c4=64, lds_bytes=16 * 1024)
+    assert plan.info.n_groups > 1
+    L = _lib.load()
+    buf = ctypes.c_void_p(0x1000)
+    rc = L.tal_agg_round_f32(buf, 64, buf, 64, 64, buf, ctypes.byref(plan.info), 1, None)
+    assert rc == _lib.TAL_ERR_INVALID and b"in-place" in L.tal_last_error()
+
+
+def test_ops_refuse_cpu_tensors():
+    x = torch.zeros(8)
+    with pytest.raises(ValueError, match="GPU"):
+        ops.agg_f32([x], [1.0], torch.zeros(8))
+    with pytest.raises(ValueError, match="GPU"):
+        ops.agg_i64([x.long()], [1.0], torch.zeros(8, dtype=torch.int64))
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(_lib.TalLibraryError, match="no CPU fallback"):
+        _lib.load(tmp_path / "libtal_agg.so")
+
+
+def test_aggregate_without_gpu_fails_loudly():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from topology_aware_learning_amd.aggregate import aggregate_models
+
+    m = torch.nn.Linear(2, 2)
+    with pytest.raises(RuntimeError, match="GPU"):
+        aggregate_models([m, m], [0.5, 0.5], m)

@@ -34,6 +34,10 @@ constexpr int kAbiVersion = 2;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr int kMaxGrid = 256 * 8; // 256 CUs x 8 resident 256-thread blocks
+constexpr int kK1Unroll = 2;     // float4 chunks per lane per K1 grid-stride step
+constexpr int kK1Grid = 4096;    // K1 grid cap (16 blocks per CU in flight)
+
+typedef float v4f __attribute__((ext_vector_type(4)));
 
 thread_local std::string g_err;
 
@@ -100,50 +104,79 @@ struct OpTableI64 {
   float w[kMaxOps];
 };
 
-// M_STATIC > 0: operand count known at compile time -> every operand's float4 load of an
-// element chunk is issued before the ordered accumulate (M loads in flight per lane).
-// M_STATIC == 0: runtime count, loads issued in batches of 8.
-// CONT: accumulate onto `out` (second and later passes when M > kMaxOps; keeps the exact order).
+// Streamed operand loads are non-temporal: every operand byte is read exactly once per call,
+// so keeping it out of the caches leaves L2/MALL to the output stream (measured +15-20 % at
+// M = 9 on MI355X, tools/tune/k1_variants.hip).
+__device__ __forceinline__ float4 ld_stream(const float* base, int64_t i) {
+  const v4f q = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(base) + i);
+  return make_float4(q.x, q.y, q.z, q.w);
+}
+
+// K1 vector kernel.  Each lane owns kK1Unroll float4 chunks per grid-stride step and issues the
+// loads of every operand of both chunks before the ordered accumulate: M * kK1Unroll 16-B loads
+// in flight per lane.
+// M_STATIC > 0: operand count known at compile time; 0: runtime count, loads in batches of 8.
+// CONT: accumulate onto `out` (passes after the first when M > kMaxOps; keeps the exact order).
 template <int M_STATIC, bool EXACT, bool CONT>
 __global__ __launch_bounds__(kBlock) void k_agg_f32_vec(OpTableF32 t, int m_rt, float* out,
                                                         int64_t n4) {
   const int m = M_STATIC > 0 ? M_STATIC : m_rt;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n4; i += stride) {
-    float4 acc;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock * kK1Unroll;
+  for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * kBlock * kK1Unroll + threadIdx.x; i0 < n4;
+       i0 += stride) {
     if constexpr (M_STATIC > 0) {
-      float4 v[M_STATIC];
+      float4 v[kK1Unroll][M_STATIC];
 #pragma unroll
-      for (int k = 0; k < M_STATIC; ++k) v[k] = reinterpret_cast<const float4*>(t.x[k])[i];
-      int k0 = 0;
-      if constexpr (CONT) {
-        acc = reinterpret_cast<const float4*>(out)[i];
-      } else {
-        acc = first4<EXACT>(t.w[0], v[0]);
-        k0 = 1;
+      for (int u = 0; u < kK1Unroll; ++u) {
+        const int64_t i = i0 + u * kBlock;
+        if (i < n4) {
+#pragma unroll
+          for (int k = 0; k < M_STATIC; ++k) v[u][k] = ld_stream(t.x[k], i);
+        }
       }
 #pragma unroll
-      for (int k = k0; k < M_STATIC; ++k) acc = next4<EXACT>(acc, t.w[k], v[k]);
+      for (int u = 0; u < kK1Unroll; ++u) {
+        const int64_t i = i0 + u * kBlock;
+        if (i < n4) {
+          float4 acc;
+          int k0 = 0;
+          if constexpr (CONT) {
+            acc = reinterpret_cast<const float4*>(out)[i];
+          } else {
+            acc = first4<EXACT>(t.w[0], v[u][0]);
+            k0 = 1;
+          }
+#pragma unroll
+          for (int k = k0; k < M_STATIC; ++k) acc = next4<EXACT>(acc, t.w[k], v[u][k]);
+          reinterpret_cast<float4*>(out)[i] = acc;
+        }
+      }
     } else {
-      int k = 0;
-      if constexpr (CONT) {
-        acc = reinterpret_cast<const float4*>(out)[i];
-      } else {
-        acc = first4<EXACT>(t.w[0], reinterpret_cast<const float4*>(t.x[0])[i]);
-        k = 1;
-      }
-      for (; k < m; k += 8) {
-        float4 v[8];
-        const int kn = min(8, m - k);
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (j < kn) v[j] = reinterpret_cast<const float4*>(t.x[k + j])[i];
+      for (int u = 0; u < kK1Unroll; ++u) {
+        const int64_t i = i0 + u * kBlock;
+        if (i >= n4) break;
+        float4 acc;
+        int k = 0;
+        if constexpr (CONT) {
+          acc = reinterpret_cast<const float4*>(out)[i];
+        } else {
+          acc = first4<EXACT>(t.w[0], ld_stream(t.x[0], i));
+          k = 1;
+        }
+        for (; k < m; k += 8) {
+          float4 v[8];
+          const int kn = min(8, m - k);
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (j < kn) acc = next4<EXACT>(acc, t.w[k + j], v[j]);
+          for (int j = 0; j < 8; ++j)
+            if (j < kn) v[j] = ld_stream(t.x[k + j], i);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (j < kn) acc = next4<EXACT>(acc, t.w[k + j], v[j]);
+        }
+        reinterpret_cast<float4*>(out)[i] = acc;
       }
     }
-    reinterpret_cast<float4*>(out)[i] = acc;
   }
 }
 
@@ -189,7 +222,9 @@ int grid_for(int64_t work) {
 
 template <bool EXACT, bool CONT>
 void launch_vec(const OpTableF32& t, int m, float* out, int64_t n4, hipStream_t s) {
-  const dim3 g(grid_for(n4)), b(kBlock);
+  int64_t nb = (n4 + kBlock * kK1Unroll - 1) / (kBlock * kK1Unroll);
+  nb = std::max<int64_t>(1, std::min<int64_t>(nb, kK1Grid));
+  const dim3 g(static_cast<unsigned>(nb)), b(kBlock);
 #define TAL_VEC_CASE(MM) \
   case MM:               \
     k_agg_f32_vec<MM, EXACT, CONT><<<g, b, 0, s>>>(t, m, out, n4); \
@@ -254,60 +289,138 @@ PlanView make_view(const int32_t* plan, const tal_round_plan_info& in) {
   return v;
 }
 
-// LDS layout of one workgroup: [max_src * C4 float4 data][row_ptr (rows+1)][slot (nnz)][w (nnz)]
-template <int C4, bool EXACT>
-__global__ __launch_bounds__(kBlock) void k_round_tiled_f32(const float* __restrict__ pin,
-                                                            int64_t ld_in4,
-                                                            float* __restrict__ pout,
-                                                            int64_t ld_out4, int64_t n4,
-                                                            PlanView p, int max_src) {
-  extern __shared__ float4 s_data[];
-  const int g = blockIdx.y;
-  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * C4;
+// LDS carve of one workgroup (both float4 kernels and the scalar one):
+//   [max_src * tile data][row_ptr (rows+1)][slot (nnz)][w (nnz)][src_row (ns)][out_row (rows)]
+struct GroupLds {
+  int32_t* rowptr;
+  int32_t* slot;
+  float* w;
+  int32_t* src;
+  int32_t* out;
+  int ns, nr, s_beg, r_beg;
+};
 
-  const int s_beg = p.grp_src_ptr[g];
-  const int ns = p.grp_src_ptr[g + 1] - s_beg;
-  const int r_beg = p.grp_row_ptr[g];
-  const int nr = p.grp_row_ptr[g + 1] - r_beg;
-  const int o_beg = p.row_ptr[r_beg];
-  const int no = p.row_ptr[r_beg + nr] - o_beg;
-
-  int32_t* s_rowptr = reinterpret_cast<int32_t*>(s_data + static_cast<size_t>(max_src) * C4);
-  int32_t* s_slot = s_rowptr + (nr + 1);
-  float* s_w = reinterpret_cast<float*>(s_slot + no);
-
-  // stage the plan slice
-  for (int k = threadIdx.x; k <= nr; k += kBlock) s_rowptr[k] = p.row_ptr[r_beg + k] - o_beg;
-  for (int k = threadIdx.x; k < no; k += kBlock) {
-    s_slot[k] = p.op_slot[o_beg + k] * C4;
-    s_w[k] = p.op_w[o_beg + k];
+// Stage group g's plan slice into LDS (slots pre-multiplied by the tile width).
+__device__ __forceinline__ GroupLds stage_group(const PlanView& p, int g, void* lds_tail, int tile,
+                                                int nthreads) {
+  GroupLds L;
+  L.s_beg = p.grp_src_ptr[g];
+  L.ns = p.grp_src_ptr[g + 1] - L.s_beg;
+  L.r_beg = p.grp_row_ptr[g];
+  L.nr = p.grp_row_ptr[g + 1] - L.r_beg;
+  const int o_beg = p.row_ptr[L.r_beg];
+  const int no = p.row_ptr[L.r_beg + L.nr] - o_beg;
+  L.rowptr = static_cast<int32_t*>(lds_tail);
+  L.slot = L.rowptr + (L.nr + 1);
+  L.w = reinterpret_cast<float*>(L.slot + no);
+  L.src = reinterpret_cast<int32_t*>(L.w + no);
+  L.out = L.src + L.ns;
+  for (int k = threadIdx.x; k <= L.nr; k += nthreads) L.rowptr[k] = p.row_ptr[L.r_beg + k] - o_beg;
+  for (int k = threadIdx.x; k < no; k += nthreads) {
+    L.slot[k] = p.op_slot[o_beg + k] * tile;
+    L.w[k] = p.op_w[o_beg + k];
   }
-  // stage tile c0 of every source of the group (each wave reads C4*16 contiguous bytes/source)
-  const int64_t cols = min(static_cast<int64_t>(C4), n4 - c0);
-  for (int k = threadIdx.x; k < ns * C4; k += kBlock) {
-    const int s = k / C4;
-    const int c = k % C4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c < cols) {
-      const int64_t row = p.src_row[s_beg + s];
-      v = reinterpret_cast<const float4*>(pin)[row * ld_in4 + c0 + c];
-    }
-    s_data[k] = v;
-  }
-  __syncthreads();
+  for (int k = threadIdx.x; k < L.ns; k += nthreads) L.src[k] = p.src_row[L.s_beg + k];
+  for (int k = threadIdx.x; k < L.nr; k += nthreads) L.out[k] = p.out_row[L.r_beg + k];
+  return L;
+}
 
-  constexpr int kRowsPerPass = kBlock / C4;
+__device__ __forceinline__ void st_stream(float* base, int64_t i, float4 v) {
+  const v4f q = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(base) + i);
+}
+
+// Compute one column tile from LDS: every row of the group, operands in reference order.
+template <int C4, int NT, bool EXACT>
+__device__ __forceinline__ void emit_tile(const float4* s_data, const GroupLds& L, float* pout,
+                                          int64_t ld_out4, int64_t c0, int64_t n4) {
+  constexpr int kRowsPerPass = NT / C4;
   const int c = threadIdx.x % C4;
   const int rsub = threadIdx.x / C4;
-  if (c >= cols) return;
-  for (int r = rsub; r < nr; r += kRowsPerPass) {
-    const int q0 = s_rowptr[r];
-    const int q1 = s_rowptr[r + 1];
-    float4 acc = first4<EXACT>(s_w[q0], s_data[s_slot[q0] + c]);
-    for (int q = q0 + 1; q < q1; ++q) acc = next4<EXACT>(acc, s_w[q], s_data[s_slot[q] + c]);
-    const int64_t orow = p.out_row[r_beg + r];
-    reinterpret_cast<float4*>(pout)[orow * ld_out4 + c0 + c] = acc;
+  if (c0 + c >= n4) return;
+  for (int r = rsub; r < L.nr; r += kRowsPerPass) {
+    const int q0 = L.rowptr[r];
+    const int q1 = L.rowptr[r + 1];
+    float4 acc = first4<EXACT>(L.w[q0], s_data[L.slot[q0] + c]);
+    for (int q = q0 + 1; q < q1; ++q) acc = next4<EXACT>(acc, L.w[q], s_data[L.slot[q] + c]);
+    st_stream(pout, static_cast<int64_t>(L.out[r]) * ld_out4 + c0 + c, acc);
   }
+}
+
+// Persistent form (the fast path): each workgroup walks column tiles t, t+gridDim.x, ...;
+// every lane owns J fixed staging slots (source, column) and keeps the next tile's J float4
+// loads in flight in registers while the workgroup computes the current tile from LDS.
+template <int C4, int NT, int J, bool EXACT>
+__global__ __launch_bounds__(NT) void k_round_f32_persistent(const float* __restrict__ pin,
+                                                             int64_t ld_in4,
+                                                             float* __restrict__ pout,
+                                                             int64_t ld_out4, int64_t n4,
+                                                             PlanView p, int max_src,
+                                                             int64_t n_tiles) {
+  extern __shared__ float4 s_data[];
+  const GroupLds L = stage_group(p, blockIdx.y, s_data + static_cast<size_t>(max_src) * C4, C4, NT);
+  const float* base[J];
+  int slotk[J];
+  bool live[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int k = j * NT + threadIdx.x;
+    const int s = k / C4;
+    live[j] = s < L.ns;
+    slotk[j] = k;
+    base[j] = pin + 4 * ((live[j] ? static_cast<int64_t>(p.src_row[L.s_beg + s]) * ld_in4 : 0) + (k % C4));
+  }
+  float4 v[J];
+  auto load_tile = [&](int64_t tt) {
+    const int64_t c0 = tt * C4;
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+      if (live[j] && c0 + (slotk[j] % C4) < n4) v[j] = ld_stream(base[j], c0);
+  };
+  int64_t t = blockIdx.x;
+  if (t < n_tiles) load_tile(t);
+  for (; t < n_tiles; t += gridDim.x) {
+    __syncthreads();  // the previous tile's readers are done with s_data (and the plan is staged)
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+      if (live[j]) s_data[slotk[j]] = v[j];
+    __syncthreads();
+    if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
+    emit_tile<C4, NT, EXACT>(s_data, L, pout, ld_out4, t * C4, n4);
+  }
+}
+
+// General form (groups whose staging needs more than 8 loads per lane): one tile per
+// workgroup, staging in batches of 4 independent loads per lane.
+template <int C4, int NT, bool EXACT>
+__global__ __launch_bounds__(NT) void k_round_f32_tiled(const float* __restrict__ pin,
+                                                        int64_t ld_in4, float* __restrict__ pout,
+                                                        int64_t ld_out4, int64_t n4, PlanView p,
+                                                        int max_src) {
+  extern __shared__ float4 s_data[];
+  const GroupLds L = stage_group(p, blockIdx.y, s_data + static_cast<size_t>(max_src) * C4, C4, NT);
+  __syncthreads();
+  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * C4;
+  const int total = L.ns * C4;
+  constexpr int U = 4;
+  for (int k0 = 0; k0 < total; k0 += NT * U) {
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u * NT + threadIdx.x;
+      const int c = k % C4;
+      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k < total && c0 + c < n4)
+        v[u] = ld_stream(pin, static_cast<int64_t>(L.src[k / C4]) * ld_in4 + c0 + c);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u * NT + threadIdx.x;
+      if (k < total) s_data[k] = v[u];
+    }
+  }
+  __syncthreads();
+  emit_tile<C4, NT, EXACT>(s_data, L, pout, ld_out4, c0, n4);
 }
 
 // Scalar tiled round: the fp32 tail (elements e0..n-1 when the float4 path ran) or whole
@@ -321,32 +434,16 @@ __global__ __launch_bounds__(kBlock) void k_round_tiled_scalar(const void* __res
                                                                int64_t n, PlanView p,
                                                                int max_src, int tile) {
   extern __shared__ float s_f[];
-  const int g = blockIdx.y;
+  const GroupLds L = stage_group(p, blockIdx.y, s_f + static_cast<size_t>(max_src) * tile, tile, kBlock);
+  __syncthreads();
   const int64_t t0 = e0 + static_cast<int64_t>(blockIdx.x) * tile;
-
-  const int s_beg = p.grp_src_ptr[g];
-  const int ns = p.grp_src_ptr[g + 1] - s_beg;
-  const int r_beg = p.grp_row_ptr[g];
-  const int nr = p.grp_row_ptr[g + 1] - r_beg;
-  const int o_beg = p.row_ptr[r_beg];
-  const int no = p.row_ptr[r_beg + nr] - o_beg;
-
-  int32_t* s_rowptr = reinterpret_cast<int32_t*>(s_f + static_cast<size_t>(max_src) * tile);
-  int32_t* s_slot = s_rowptr + (nr + 1);
-  float* s_w = reinterpret_cast<float*>(s_slot + no);
-
-  for (int k = threadIdx.x; k <= nr; k += kBlock) s_rowptr[k] = p.row_ptr[r_beg + k] - o_beg;
-  for (int k = threadIdx.x; k < no; k += kBlock) {
-    s_slot[k] = p.op_slot[o_beg + k] * tile;
-    s_w[k] = p.op_w[o_beg + k];
-  }
   const int64_t cols = min(static_cast<int64_t>(tile), n - t0);
-  for (int k = threadIdx.x; k < ns * tile; k += kBlock) {
+  for (int k = threadIdx.x; k < L.ns * tile; k += kBlock) {
     const int s = k / tile;
     const int c = k % tile;
     float v = 0.f;
     if (c < cols) {
-      const int64_t row = p.src_row[s_beg + s];
+      const int64_t row = L.src[s];
       if constexpr (IS_I64) {
         v = static_cast<float>(static_cast<const int64_t*>(pin_v)[row * ld_in + t0 + c]);
       } else {
@@ -361,19 +458,19 @@ __global__ __launch_bounds__(kBlock) void k_round_tiled_scalar(const void* __res
   const int c = threadIdx.x % tile;
   const int rsub = threadIdx.x / tile;
   if (c >= cols) return;
-  for (int r = rsub; r < nr; r += rows_per_pass) {
-    const int q0 = s_rowptr[r];
-    const int q1 = s_rowptr[r + 1];
+  for (int r = rsub; r < L.nr; r += rows_per_pass) {
+    const int q0 = L.rowptr[r];
+    const int q1 = L.rowptr[r + 1];
     float acc;
     if constexpr (IS_I64) {
-      acc = __fmul_rn(s_w[q0], s_f[s_slot[q0] + c]);
+      acc = __fmul_rn(L.w[q0], s_f[L.slot[q0] + c]);
       for (int q = q0 + 1; q < q1; ++q)
-        acc = __fadd_rn(acc, __fmul_rn(s_w[q], s_f[s_slot[q] + c]));
+        acc = __fadd_rn(acc, __fmul_rn(L.w[q], s_f[L.slot[q] + c]));
     } else {
-      acc = first_term<EXACT>(s_w[q0], s_f[s_slot[q0] + c]);
-      for (int q = q0 + 1; q < q1; ++q) acc = next_term<EXACT>(acc, s_w[q], s_f[s_slot[q] + c]);
+      acc = first_term<EXACT>(L.w[q0], s_f[L.slot[q0] + c]);
+      for (int q = q0 + 1; q < q1; ++q) acc = next_term<EXACT>(acc, L.w[q], s_f[L.slot[q] + c]);
     }
-    const int64_t orow = p.out_row[r_beg + r];
+    const int64_t orow = L.out[r];
     if constexpr (IS_I64) {
       static_cast<int64_t*>(pout_v)[orow * ld_out + t0 + c] = trunc_i64(acc);
     } else {
@@ -384,7 +481,7 @@ __global__ __launch_bounds__(kBlock) void k_round_tiled_scalar(const void* __res
 
 size_t plan_lds_bytes(const tal_round_plan_info& in, int tile_bytes_per_src) {
   return static_cast<size_t>(in.max_src) * tile_bytes_per_src +
-         static_cast<size_t>(in.max_rows + 1 + 2 * in.max_nnz) * 4;
+         static_cast<size_t>(in.max_rows + 1 + 2 * in.max_nnz + in.max_src + in.max_rows) * 4;
 }
 
 std::mutex g_lds_mu;
@@ -429,17 +526,40 @@ int32_t launch_round_scalar(const void* pin, int64_t ld_in, void* pout, int64_t 
   return check_launch("round scalar kernel");
 }
 
+constexpr int kRoundThreads = 512;  // 8 wavefronts; up to 4 workgroups per CU (LDS permitting)
+
+template <int C4, int J, bool EXACT>
+int32_t launch_round_persistent(const float* pin, int64_t ld_in, float* pout, int64_t ld_out,
+                                int64_t n4, const PlanView& v, const tal_round_plan_info& in,
+                                size_t lds, hipStream_t s) {
+  auto k = k_round_f32_persistent<C4, kRoundThreads, J, EXACT>;
+  int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
+  if (rc) return rc;
+  const int64_t tiles = (n4 + C4 - 1) / C4;
+  const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(4, (160 * 1024) / static_cast<int64_t>(lds)));
+  int64_t gx = std::max<int64_t>(1, 256 * per_cu / in.n_groups);
+  gx = std::min<int64_t>(gx, tiles);
+  const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(in.n_groups));
+  k<<<grid, kRoundThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, in.max_src, tiles);
+  return check_launch("round kernel (persistent)");
+}
+
 template <int C4, bool EXACT>
 int32_t launch_round_vec(const float* pin, int64_t ld_in, float* pout, int64_t ld_out, int64_t n4,
                          const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
   const size_t lds = plan_lds_bytes(in, C4 * 16);
-  auto k = k_round_tiled_f32<C4, EXACT>;
+  const int64_t loads = static_cast<int64_t>(in.max_src) * C4;  // float4 staging loads per tile
+  if (loads <= 1LL * kRoundThreads) return launch_round_persistent<C4, 1, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+  if (loads <= 2LL * kRoundThreads) return launch_round_persistent<C4, 2, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+  if (loads <= 4LL * kRoundThreads) return launch_round_persistent<C4, 4, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+  if (loads <= 8LL * kRoundThreads) return launch_round_persistent<C4, 8, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+  auto k = k_round_f32_tiled<C4, kRoundThreads, EXACT>;
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;
   const int64_t tiles = (n4 + C4 - 1) / C4;
   if (tiles > 0x7fffffff) return fail(TAL_ERR_INVALID, "too many tiles");
   const dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(in.n_groups));
-  k<<<grid, kBlock, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, in.max_src);
+  k<<<grid, kRoundThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, in.max_src);
   return check_launch("round kernel");
 }
 
@@ -462,11 +582,18 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-__device__ __forceinline__ float cos_value(float dot, float na2, float nb2) {
-  // nn.CosineSimilarity(eps=1e-6): x/max(|x|,eps) . y/max(|y|,eps)
-  const float na = fmaxf(sqrtf(na2), 1e-6f);
-  const float nb = fmaxf(sqrtf(nb2), 1e-6f);
-  return dot / (na * nb);
+__device__ __forceinline__ float clamp_norm(float n2) { return fmaxf(sqrtf(n2), 1e-6f); }
+
+// nn.CosineSimilarity(eps=1e-6) = sum_i (x_i/max(|x|,eps)) * (y_i/max(|y|,eps)).  The fused
+// one-pass value dot/|x|/|y| equals it up to rounding whenever the fp32 sums stayed finite;
+// when a sum of squares (or the dot) overflowed, torch's fp32 norm is inf and zeroes the row's
+// terms, so the caller recomputes that row in the normalize-first form (rare path).
+__device__ __forceinline__ bool fused_ok(float dot, float na2, float nb2) {
+  return isfinite(dot) && isfinite(na2) && isfinite(nb2);
+}
+
+__device__ __forceinline__ float cos_fused(float dot, float na2, float nb2) {
+  return (dot / clamp_norm(na2)) / clamp_norm(nb2);
 }
 
 // plan: [n_seg x {off, A, I, B}] then [n_chunks x {seg, first, count, kind}]  (int64 words)
@@ -500,7 +627,16 @@ __global__ __launch_bounds__(kBlock) void k_cosine_chunks(CosPairs pr, const int
       dot = wave_sum(dot);
       na = wave_sum(na);
       nb = wave_sum(nb);
-      if (lane == 0) sum += static_cast<double>(cos_value(dot, na, nb));
+      float cv;
+      if (fused_ok(dot, na, nb)) {
+        cv = cos_fused(dot, na, nb);
+      } else {
+        const float ia = clamp_norm(na), ib = clamp_norm(nb);
+        float t = 0.f;
+        for (int64_t i = lane; i < I; i += 64) t += (ar[i] / ia) * (br[i] / ib);
+        cv = wave_sum(t);
+      }
+      if (lane == 0) sum += static_cast<double>(cv);
     }
   } else {
     for (int64_t o = first + threadIdx.x; o < first + count; o += kBlock) {
@@ -514,7 +650,14 @@ __global__ __launch_bounds__(kBlock) void k_cosine_chunks(CosPairs pr, const int
         na += x * x;
         nb += y * y;
       }
-      sum += static_cast<double>(cos_value(dot, na, nb));
+      if (fused_ok(dot, na, nb)) {
+        sum += static_cast<double>(cos_fused(dot, na, nb));
+      } else {
+        const float ia = clamp_norm(na), ib = clamp_norm(nb);
+        float t = 0.f;
+        for (int64_t i = 0; i < I; ++i) t += (ap[i * B] / ia) * (bp[i * B] / ib);
+        sum += static_cast<double>(t);
+      }
     }
     // reduce lanes of the wave
 #pragma unroll
@@ -649,7 +792,7 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
   int64_t cur_rows = 0, cur_nnz = 0;
   int32_t max_src = 0, max_rows = 0, max_nnz = 0;
   auto need = [&](int64_t ns, int64_t nr, int64_t no) {
-    return ns * per_src + (nr + 1 + 2 * no) * 4;
+    return ns * per_src + (nr + 1 + 2 * no + ns + nr) * 4;
   };
   auto close_group = [&](int r_end) {
     grp_row_ptr.push_back(r_end);

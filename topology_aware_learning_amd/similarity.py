@@ -1,0 +1,58 @@
+"""Model-to-model cosine similarity on the GPU (K2), for the `*_sim` aggregation strategies.
+
+Reference: cosine_similarity, src/decentralized_client.py:661-681 — over `named_parameters`
+(buffers excluded), nn.CosineSimilarity(dim=1, eps=1e-6) per tensor (1-D tensors get a
+trailing unit dim), mean per tensor, average over tensors.  The kernel fuses dot and both
+squared norms in one pass over each model (reference: normalise-then-dot in fp32); results
+agree with the reference to ~1e-6 (tests: tolerance 2e-5), which is what the only consumer
+— the arg-min neighbour of sim_centrality_module_avg (:511) — needs.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .aggregate import _device_for, _stage, layout_of_module
+from .arena import bound_row
+
+_plans: Dict[Tuple, ops.CosinePlan] = {}
+
+
+def _param_names(model: nn.Module) -> List[str]:
+    return [n for n, _ in model.named_parameters()]
+
+
+def _flat(models: Sequence[nn.Module], layout, device) -> List[torch.Tensor]:
+    out: List = [None] * len(models)
+    rest = []
+    for j, m in enumerate(models):
+        b = bound_row(m)
+        if b is not None and b[0].device == device and b[0].layout == layout:
+            out[j] = b[0].row_f32(b[1])
+        else:
+            rest.append(j)
+    if rest:
+        df, _ = _stage([models[j] for j in rest], layout, device)
+        for k, j in enumerate(rest):
+            out[j] = df[k]
+    return out
+
+
+def cosine_pairs(model: nn.Module, others: Sequence[nn.Module]) -> List[float]:
+    """[cosine_similarity(model, o) for o in others] in one kernel launch."""
+    if not others:
+        return []
+    layout = layout_of_module(model)
+    names = _param_names(model)
+    key = (layout.key, tuple(names))
+    plan = _plans.get(key)
+    if plan is None:
+        plan = ops.build_cosine_plan(layout.param_segments(names))
+        _plans[key] = plan
+    device = _device_for([model, *others])
+    flats = _flat([model, *others], layout, device)
+    res = ops.cosine([flats[0]] * len(others), flats[1:], plan)
+    return [float(x) for x in res.cpu().tolist()]
