@@ -38,6 +38,11 @@ def parse():
     p.add_argument("--model", default="resnet50", choices=["resnet18", "resnet50", "vit_b16", "cifar10"])
     p.add_argument("--devices-per-gpu", type=int, default=64)
     p.add_argument("--degree", type=int, default=8)
+    p.add_argument("--graph", default="random", choices=["random", "ring", "barbell", "sbm"],
+                   help="random: nx.random_regular_graph(degree, devices, 0) (configs 3 / weak scaling); "
+                        "ring: cycle (config 2); barbell: nx.barbell_graph(60, 8) (config 4); "
+                        "sbm: 8 blocks of 32, p_in=14/31, p_out=2/224 (config 5)")
+    p.add_argument("--devices", type=int, default=0, help="total devices (overrides devices-per-gpu x N)")
     p.add_argument("--mode", default="exact", choices=["exact", "fma"])
     p.add_argument("--c4", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -47,10 +52,24 @@ def parse():
     return p.parse_args()
 
 
-def round_spec(n_devices: int, degree: int, seed: int = 0):
+def make_graph(kind: str, n_devices: int, degree: int, seed: int = 0):
+    """BASELINE configs' topologies (SURVEY §8(d) synthetic inputs)."""
     import networkx as nx
 
-    g = nx.random_regular_graph(degree, n_devices, seed=seed)
+    if kind == "random":
+        return nx.random_regular_graph(degree, n_devices, seed=seed)
+    if kind == "ring":
+        return nx.cycle_graph(n_devices)
+    if kind == "barbell":
+        return nx.barbell_graph(60, 8)
+    sizes = [32] * max(1, n_devices // 32)
+    p = [[14 / 31 if a == b else 2 / 224 for b in range(len(sizes))] for a in range(len(sizes))]
+    return nx.stochastic_block_model(sizes, p, seed=seed)
+
+
+def round_spec(n_devices: int, degree: int, seed: int = 0, kind: str = "random"):
+    g = make_graph(kind, n_devices, degree, seed)
+    n_devices = g.number_of_nodes()
     orders = [sorted(g.neighbors(i)) + [i] for i in range(n_devices)]
     weights = [[1 / len(o)] * len(o) for o in orders]  # unweighted_module_avg, client.py:431
     return orders, weights
@@ -113,9 +132,10 @@ def main():
     layout = StateLayout.from_layout(lay)
     n_params = layout.n_f32 + layout.n_i64
     mode = ops.MODE_EXACT if args.mode == "exact" else ops.MODE_FMA
-    n_dev_total = args.devices_per_gpu * world
-    orders, weights = round_spec(n_dev_total, args.degree)
-    M = args.degree + 1
+    n_dev_total = args.devices or args.devices_per_gpu * world
+    orders, weights = round_spec(n_dev_total, args.degree, kind=args.graph)
+    n_dev_total = len(orders)
+    M = max(len(o) for o in orders)
 
     if world == 1:
         from topology_aware_learning_amd import ops as _ops
@@ -162,6 +182,8 @@ def main():
             per_call_equivalent_GBps=per_call_bytes / (k_ms * 1e-3) / 1e9, parity_k3_vs_k1_row0=parity_ok)
         steps_done = args.steps
         units = rows * n_params * steps_done
+        copy_ceiling = bench_copy(pin, pout, bytes_round, dev)
+        result_extra["copy_ceiling"] = copy_ceiling
         k1 = None
         if not args.no_k1:
             k1 = bench_k1(layout, pin, orders, weights, mode, dev)
@@ -171,14 +193,21 @@ def main():
 
         sr = ShardedRound(layout, orders, weights, rank, world, dev, mode=mode)
         fill_pool(sr.pool_a, 1234 + rank)
+        sr.step()
+        # spot check: one (boundary if any) row of this rank == K1 on its operands as received
+        k = (sr.spec.boundary or sr.spec.interior)[0]
+        chk = torch.empty(layout.n_f32, dtype=torch.float32, device=dev)
+        ops.agg_f32([sr.pool_b.row_f32(j) for j in sr.spec.orders_local[k]], sr.spec.weights[k], chk, mode=mode)
+        ok = torch.tensor([int(torch.equal(chk.view(torch.int32), sr.pool_a.row_f32(k).view(torch.int32)))], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        parity_dist = bool(ok.item())
         for _ in range(args.warmup):
             sr.step()
         torch.cuda.synchronize(dev)
         dist.barrier()
         t0 = time.perf_counter()
-        k_ms_list = []
         for _ in range(args.steps):
-            k_ms_list.append(sr.step(timed=True))
+            sr.step(timed=True)
         torch.cuda.synchronize(dev)
         dist.barrier()
         el_local = time.perf_counter() - t0
@@ -186,14 +215,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
         torch.cuda.synchronize(dev)
-        k_ms = float(np.mean([x for x in k_ms_list if x is not None])) if any(k_ms_list) else float("nan")
+        k_ms = float(np.mean(sr.kernel_ms()))
         staged = sr.staged_sources
         rows = sr.local_rows
         bytes_round = 4 * layout.n_f32 * (staged + rows)
         result_extra = dict(kernel="k_round_f32_persistent", halo_rows_in=sr.halo_rows_in,
                             halo_bytes_in=sr.halo_rows_in * 4 * layout.ld_f32)
         units = n_dev_total * n_params * args.steps
-        parity_ok = None
+        parity_ok = parity_dist
         k1 = None
         hostp = None
 
@@ -204,6 +233,8 @@ def main():
         return
 
     achieved = bytes_round / (k_ms * 1e-3) / 1e9
+    if "copy_ceiling" in result_extra:
+        result_extra["frac_of_copy_ceiling"] = achieved / result_extra["copy_ceiling"]["GBps"]
     traffic = load_traffic(args.model)
     cpu = None
     if not args.no_cpu_baseline and world == 1:
@@ -222,8 +253,9 @@ def main():
         "vs_baseline": None,
         "dtype": "f32" if args.mode == "exact" else "f32-fma",
         "data": "synthetic (random fp32 / int64 state_dicts of the reference layout in HBM)",
-        "config": {"workload": f"{n_dev_total}-device random {args.degree}-regular graph (seed 0), "
-                               f"{args.model} state_dicts, K={args.degree} (M={M}, self last), unweighted, "
+        "config": {"workload": f"{n_dev_total}-device {args.graph} graph"
+                               + (f" ({args.degree}-regular, seed 0)" if args.graph == "random" else "")
+                               + f", {args.model} state_dicts, max M={M} (self last), unweighted, "
                                "one full aggregation round per step, snapshot semantics",
                    "model_layout": args.model, "devices": n_dev_total, "devices_per_gpu": args.devices_per_gpu,
                    "params_per_model": n_params, "parallelism": f"row-sharded x{world}" if world > 1 else "1 GPU"},
@@ -248,6 +280,29 @@ def _round_csr(orders, weights):
     from topology_aware_learning_amd.round import csr_from_lists
 
     return csr_from_lists(orders, weights)
+
+
+def bench_copy(pin, pout, bytes_round, dev, reps: int = 5):
+    """Same-device reference: a plain device copy moving the round's compulsory bytes (read
+    every staged source row once, write every output row once) — what a 50/50 read/write
+    stream achieves on this particular GPU (MI355X boards differ by several %)."""
+    import torch
+
+    n = min(pin.f32.numel(), bytes_round // 8)
+    a = pin.f32.view(-1)[:n]
+    b = pout.f32.view(-1)[:n]
+    b.copy_(a)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ts = []
+    for _ in range(reps):
+        s.record()
+        b.copy_(a)
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e))
+    ms = float(np.median(ts))
+    gbps = 8 * n / (ms * 1e-3) / 1e9
+    return dict(GBps=gbps, frac_of_peak=gbps / HBM_PEAK_GBPS, bytes=8 * n, ms=ms, kernel="torch copy_ (D2D)")
 
 
 def bench_k1(layout, pool, orders, weights, mode, dev, reps: int = 20):

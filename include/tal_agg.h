@@ -83,7 +83,7 @@ typedef struct tal_round_plan_info {
   int32_t max_src;       /* largest group source count (sizes the LDS tile) */
   int32_t max_rows;      /* largest group row count */
   int32_t max_nnz;       /* largest group operand count */
-  int32_t c4;            /* float4 columns per staged source row per tile (16, 32 or 64) */
+  int32_t c4;            /* float4 columns per staged source row per tile (64 or 128) */
   int32_t lds_bytes;     /* LDS per workgroup the round kernel will request */
   /* offsets (in int32 words) of the plan's arrays inside the blob */
   int32_t off_grp_row_ptr;  /* [n_groups+1] */
@@ -100,8 +100,8 @@ typedef struct tal_round_plan_info {
 int64_t tal_round_plan_words(int32_t rows, int64_t nnz);
 
 /* Build the plan on the host.  row_ptr_host[rows+1], col_host[nnz], w_host[nnz] (float64),
- * out_row_host[rows].  c4 in {16,32,64}; lds_bytes = LDS budget per workgroup for the tile
- * (max sources per group = lds_bytes / (16*c4)).  Rows keep their order; consecutive rows
+ * out_row_host[rows].  c4 in {64,128}; lds_bytes = LDS budget per workgroup (staged tile
+ * 16*c4 B per source plus the scalar kernels' plan slice).  Rows keep their order; consecutive rows
  * share a group while the union of their sources fits.  Returns TAL_ERR_CAPACITY if one
  * row alone has more distinct sources than fit. */
 int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host,

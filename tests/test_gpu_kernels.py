@@ -126,12 +126,13 @@ def _graph_csr(g, weights="unweighted"):
 
 
 @pytest.mark.parametrize("graph,n,c4,lds", [
-    ("ring", 1000, 0, ops.LDS_BUDGET),
+    ("ring", 1000, 0, 0),
     ("regular", 4099, 64, ops.LDS_BUDGET),
-    ("regular", 4099, 32, ops.LDS_BUDGET),
-    ("regular", 4099, 16, ops.LDS_BUDGET),
+    ("regular", 4099, 128, 160 * 1024),
     ("regular", 70001, 64, 24 * 1024),      # forces several row groups
-    ("barbell", 3001, 0, ops.LDS_BUDGET),
+    ("regular", 70001, 128, 40 * 1024),     # several groups, 2 float4 columns per lane
+    ("regular", 1000003, 64, 48 * 1024),    # persistent kernel with J < 8
+    ("barbell", 3001, 0, 0),
     ("complete", 515, 0, 160 * 1024),
 ])
 def test_round_f32_vs_oracle(cuda, graph, n, c4, lds):

@@ -177,7 +177,7 @@ def test_round_plan_reconstructs_csr():
     ws = [W.unweighted(len(o)) for o in orders]
     row_ptr, col, w = ra.round_csr(orders, ws)
     out_rows = np.arange(64, dtype=np.int32)[::-1].copy()
-    for c4, budget in ((32, ops.LDS_BUDGET), (64, 20 * 1024), (16, 8 * 1024)):
+    for c4, budget in ((64, ops.LDS_BUDGET), (64, 20 * 1024), (128, 40 * 1024)):
         plan = ops.build_plan(row_ptr, col, w, out_rows, c4=c4, lds_bytes=budget)
         i, h = plan.info, plan.host
         grp_row = h[i.off_grp_row_ptr: i.off_grp_row_ptr + i.n_groups + 1]

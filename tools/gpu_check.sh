@@ -1,6 +1,7 @@
 # GPU check: kernel parity tests, smoke, bench (short).  Usage: bash tools/gpu_check.sh [tag]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
+python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo BUILD FAILED; exit 1; }
 TAG=${1:-chk}
 mkdir -p gpurun_out
 timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/${TAG}_tests.log 2>&1 && \

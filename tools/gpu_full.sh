@@ -2,6 +2,7 @@
 # Usage: bash tools/gpu_full.sh <tag>
 set -o pipefail
 cd $GRAFT_REPO_ROOT
+python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo BUILD FAILED; exit 1; }
 TAG=${1:-full}
 OUT=$GRAFT_REPO_ROOT/gpurun_out
 mkdir -p $OUT

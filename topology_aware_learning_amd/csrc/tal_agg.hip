@@ -330,20 +330,70 @@ __device__ __forceinline__ void st_stream(float* base, int64_t i, float4 v) {
   __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(base) + i);
 }
 
-// Compute one column tile from LDS: every row of the group, operands in reference order.
+// Compute one column tile from LDS.  A wavefront owns whole rows (row index wave-uniform, so
+// the plan entries — row extent, operand slots and weights — are scalar loads from the plan in
+// global memory, served by the scalar cache); each lane owns C4/64 float4 columns.  Operands are
+// consumed in reference order, four LDS reads in flight ahead of the ordered accumulate.
+// The plan is read-only for the whole launch: reading it through the constant address space
+// lets the backend use scalar (SMEM) loads for the wave-uniform entries.
+typedef __attribute__((address_space(4))) const int32_t* ConstI32;
+typedef __attribute__((address_space(4))) const float* ConstF32;
+
 template <int C4, int NT, bool EXACT>
-__device__ __forceinline__ void emit_tile(const float4* s_data, const GroupLds& L, float* pout,
-                                          int64_t ld_out4, int64_t c0, int64_t n4) {
-  constexpr int kRowsPerPass = NT / C4;
-  const int c = threadIdx.x % C4;
-  const int rsub = threadIdx.x / C4;
-  if (c0 + c >= n4) return;
-  for (int r = rsub; r < L.nr; r += kRowsPerPass) {
-    const int q0 = L.rowptr[r];
-    const int q1 = L.rowptr[r + 1];
-    float4 acc = first4<EXACT>(L.w[q0], s_data[L.slot[q0] + c]);
-    for (int q = q0 + 1; q < q1; ++q) acc = next4<EXACT>(acc, L.w[q], s_data[L.slot[q] + c]);
-    st_stream(pout, static_cast<int64_t>(L.out[r]) * ld_out4 + c0 + c, acc);
+__device__ __forceinline__ void emit_tile(const float4* s_data, const PlanView& p, int r_beg, int nr,
+                                          float* pout, int64_t ld_out4, int64_t c0, int64_t n4) {
+  constexpr int kB = C4 >= 128 ? 8 : 4;  // operands per batch (LDS reads in flight per lane)
+  static_assert(C4 % 64 == 0, "a wavefront covers 64 float4 columns");
+  constexpr int kWaves = NT / 64;
+  constexpr int kCpl = C4 / 64;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const ConstI32 row_ptr = (ConstI32)p.row_ptr;
+  const ConstI32 out_row = (ConstI32)p.out_row;
+  const ConstI32 op_slot = (ConstI32)p.op_slot;
+  const ConstF32 op_w = (ConstF32)p.op_w;
+  for (int r = wave; r < nr; r += kWaves) {
+    const int gr = r_beg + r;
+    const int q0 = row_ptr[gr];
+    const int q1 = row_ptr[gr + 1];
+    const int64_t orow = out_row[gr];
+    float4 acc[kCpl];
+    {
+      const float w = op_w[q0];
+      const int sl = op_slot[q0] * C4 + lane;
+#pragma unroll
+      for (int j = 0; j < kCpl; ++j) acc[j] = first4<EXACT>(w, s_data[sl + 64 * j]);
+    }
+    int q = q0 + 1;
+    for (; q + kB <= q1; q += kB) {
+      float w[kB];
+      int sl[kB];
+      float4 x[kB][kCpl];
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        w[u] = op_w[q + u];
+        sl[u] = op_slot[q + u] * C4 + lane;
+      }
+#pragma unroll
+      for (int u = 0; u < kB; ++u)
+#pragma unroll
+        for (int j = 0; j < kCpl; ++j) x[u][j] = s_data[sl[u] + 64 * j];
+#pragma unroll
+      for (int u = 0; u < kB; ++u)
+#pragma unroll
+        for (int j = 0; j < kCpl; ++j) acc[j] = next4<EXACT>(acc[j], w[u], x[u][j]);
+    }
+    for (; q < q1; ++q) {
+      const float w = op_w[q];
+      const int sl = op_slot[q] * C4 + lane;
+#pragma unroll
+      for (int j = 0; j < kCpl; ++j) acc[j] = next4<EXACT>(acc[j], w, s_data[sl + 64 * j]);
+    }
+#pragma unroll
+    for (int j = 0; j < kCpl; ++j) {
+      const int64_t col = c0 + lane + 64 * j;
+      if (col < n4) st_stream(pout, orow * ld_out4 + col, acc[j]);
+    }
   }
 }
 
@@ -355,10 +405,13 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const float* __rest
                                                              int64_t ld_in4,
                                                              float* __restrict__ pout,
                                                              int64_t ld_out4, int64_t n4,
-                                                             PlanView p, int max_src,
-                                                             int64_t n_tiles) {
+                                                             PlanView p, int64_t n_tiles) {
   extern __shared__ float4 s_data[];
-  const GroupLds L = stage_group(p, blockIdx.y, s_data + static_cast<size_t>(max_src) * C4, C4, NT);
+  const int g = blockIdx.y;
+  const int s_beg = p.grp_src_ptr[g];
+  const int ns = p.grp_src_ptr[g + 1] - s_beg;
+  const int r_beg = p.grp_row_ptr[g];
+  const int nr = p.grp_row_ptr[g + 1] - r_beg;
   const float* base[J];
   int slotk[J];
   bool live[J];
@@ -366,9 +419,9 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const float* __rest
   for (int j = 0; j < J; ++j) {
     const int k = j * NT + threadIdx.x;
     const int s = k / C4;
-    live[j] = s < L.ns;
+    live[j] = s < ns;
     slotk[j] = k;
-    base[j] = pin + 4 * ((live[j] ? static_cast<int64_t>(p.src_row[L.s_beg + s]) * ld_in4 : 0) + (k % C4));
+    base[j] = pin + 4 * ((live[j] ? static_cast<int64_t>(p.src_row[s_beg + s]) * ld_in4 : 0) + (k % C4));
   }
   float4 v[J];
   auto load_tile = [&](int64_t tt) {
@@ -380,13 +433,13 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const float* __rest
   int64_t t = blockIdx.x;
   if (t < n_tiles) load_tile(t);
   for (; t < n_tiles; t += gridDim.x) {
-    __syncthreads();  // the previous tile's readers are done with s_data (and the plan is staged)
+    __syncthreads();  // the previous tile's readers are done with s_data
 #pragma unroll
     for (int j = 0; j < J; ++j)
       if (live[j]) s_data[slotk[j]] = v[j];
     __syncthreads();
     if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
-    emit_tile<C4, NT, EXACT>(s_data, L, pout, ld_out4, t * C4, n4);
+    emit_tile<C4, NT, EXACT>(s_data, p, r_beg, nr, pout, ld_out4, t * C4, n4);
   }
 }
 
@@ -395,13 +448,15 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const float* __rest
 template <int C4, int NT, bool EXACT>
 __global__ __launch_bounds__(NT) void k_round_f32_tiled(const float* __restrict__ pin,
                                                         int64_t ld_in4, float* __restrict__ pout,
-                                                        int64_t ld_out4, int64_t n4, PlanView p,
-                                                        int max_src) {
+                                                        int64_t ld_out4, int64_t n4, PlanView p) {
   extern __shared__ float4 s_data[];
-  const GroupLds L = stage_group(p, blockIdx.y, s_data + static_cast<size_t>(max_src) * C4, C4, NT);
-  __syncthreads();
+  const int g = blockIdx.y;
+  const int s_beg = p.grp_src_ptr[g];
+  const int ns = p.grp_src_ptr[g + 1] - s_beg;
+  const int r_beg = p.grp_row_ptr[g];
+  const int nr = p.grp_row_ptr[g + 1] - r_beg;
   const int64_t c0 = static_cast<int64_t>(blockIdx.x) * C4;
-  const int total = L.ns * C4;
+  const int total = ns * C4;
   constexpr int U = 4;
   for (int k0 = 0; k0 < total; k0 += NT * U) {
     float4 v[U];
@@ -411,7 +466,7 @@ __global__ __launch_bounds__(NT) void k_round_f32_tiled(const float* __restrict_
       const int c = k % C4;
       v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (k < total && c0 + c < n4)
-        v[u] = ld_stream(pin, static_cast<int64_t>(L.src[k / C4]) * ld_in4 + c0 + c);
+        v[u] = ld_stream(pin, static_cast<int64_t>(p.src_row[s_beg + k / C4]) * ld_in4 + c0 + c);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -420,7 +475,7 @@ __global__ __launch_bounds__(NT) void k_round_f32_tiled(const float* __restrict_
     }
   }
   __syncthreads();
-  emit_tile<C4, NT, EXACT>(s_data, L, pout, ld_out4, c0, n4);
+  emit_tile<C4, NT, EXACT>(s_data, p, r_beg, nr, pout, ld_out4, c0, n4);
 }
 
 // Scalar tiled round: the fp32 tail (elements e0..n-1 when the float4 path ran) or whole
@@ -454,27 +509,25 @@ __global__ __launch_bounds__(kBlock) void k_round_tiled_scalar(const void* __res
   }
   __syncthreads();
 
-  const int rows_per_pass = kBlock / tile;
-  const int c = threadIdx.x % tile;
-  const int rsub = threadIdx.x / tile;
-  if (c >= cols) return;
-  for (int r = rsub; r < L.nr; r += rows_per_pass) {
-    const int q0 = L.rowptr[r];
-    const int q1 = L.rowptr[r + 1];
-    float acc;
-    if constexpr (IS_I64) {
-      acc = __fmul_rn(L.w[q0], s_f[L.slot[q0] + c]);
-      for (int q = q0 + 1; q < q1; ++q)
-        acc = __fadd_rn(acc, __fmul_rn(L.w[q], s_f[L.slot[q] + c]));
-    } else {
-      acc = first_term<EXACT>(L.w[q0], s_f[L.slot[q0] + c]);
-      for (int q = q0 + 1; q < q1; ++q) acc = next_term<EXACT>(acc, L.w[q], s_f[L.slot[q] + c]);
-    }
-    const int64_t orow = L.out[r];
-    if constexpr (IS_I64) {
-      static_cast<int64_t*>(pout_v)[orow * ld_out + t0 + c] = trunc_i64(acc);
-    } else {
-      static_cast<float*>(pout_v)[orow * ld_out + t0 + c] = acc;
+  for (int c = threadIdx.x; c < cols; c += kBlock) {
+    for (int r = 0; r < L.nr; ++r) {
+      const int q0 = L.rowptr[r];
+      const int q1 = L.rowptr[r + 1];
+      float acc;
+      if constexpr (IS_I64) {
+        acc = __fmul_rn(L.w[q0], s_f[L.slot[q0] + c]);
+        for (int q = q0 + 1; q < q1; ++q)
+          acc = __fadd_rn(acc, __fmul_rn(L.w[q], s_f[L.slot[q] + c]));
+      } else {
+        acc = first_term<EXACT>(L.w[q0], s_f[L.slot[q0] + c]);
+        for (int q = q0 + 1; q < q1; ++q) acc = next_term<EXACT>(acc, L.w[q], s_f[L.slot[q] + c]);
+      }
+      const int64_t orow = L.out[r];
+      if constexpr (IS_I64) {
+        static_cast<int64_t*>(pout_v)[orow * ld_out + t0 + c] = trunc_i64(acc);
+      } else {
+        static_cast<float*>(pout_v)[orow * ld_out + t0 + c] = acc;
+      }
     }
   }
 }
@@ -504,8 +557,8 @@ int32_t validate_info(const tal_round_plan_info* info) {
   if (!info) return fail(TAL_ERR_INVALID, "null plan info");
   if (info->rows <= 0 || info->n_groups <= 0 || info->max_src <= 0)
     return fail(TAL_ERR_INVALID, "empty round plan");
-  if (info->c4 != 16 && info->c4 != 32 && info->c4 != 64)
-    return fail(TAL_ERR_INVALID, "plan c4 must be 16, 32 or 64");
+  if (info->c4 != 64 && info->c4 != 128)
+    return fail(TAL_ERR_INVALID, "plan c4 must be 64 or 128");
   return TAL_OK;
 }
 
@@ -526,12 +579,17 @@ int32_t launch_round_scalar(const void* pin, int64_t ld_in, void* pout, int64_t 
   return check_launch("round scalar kernel");
 }
 
-constexpr int kRoundThreads = 512;  // 8 wavefronts; up to 4 workgroups per CU (LDS permitting)
+// Threads per round workgroup: 16 wavefronts at c4 = 64 (a 64-source tile is 4 loads per lane),
+// 8 at c4 = 128 (dense rows: fewer, longer rows per wavefront).  Tuned on MI355X with
+// tools/tune/round_variants.hip (config 3: 2.0-2.1 ms / round, config 4: 7.8 ms).
+template <int C4>
+constexpr int round_threads() { return C4 >= 128 ? 512 : 1024; }
 
 template <int C4, int J, bool EXACT>
 int32_t launch_round_persistent(const float* pin, int64_t ld_in, float* pout, int64_t ld_out,
                                 int64_t n4, const PlanView& v, const tal_round_plan_info& in,
                                 size_t lds, hipStream_t s) {
+  constexpr int kRoundThreads = round_threads<C4>();
   auto k = k_round_f32_persistent<C4, kRoundThreads, J, EXACT>;
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;
@@ -540,26 +598,30 @@ int32_t launch_round_persistent(const float* pin, int64_t ld_in, float* pout, in
   int64_t gx = std::max<int64_t>(1, 256 * per_cu / in.n_groups);
   gx = std::min<int64_t>(gx, tiles);
   const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(in.n_groups));
-  k<<<grid, kRoundThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, in.max_src, tiles);
+  k<<<grid, kRoundThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles);
   return check_launch("round kernel (persistent)");
 }
 
 template <int C4, bool EXACT>
 int32_t launch_round_vec(const float* pin, int64_t ld_in, float* pout, int64_t ld_out, int64_t n4,
                          const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
-  const size_t lds = plan_lds_bytes(in, C4 * 16);
+  constexpr int kRoundThreads = round_threads<C4>();
+  const size_t lds = static_cast<size_t>(in.max_src) * C4 * 16;
   const int64_t loads = static_cast<int64_t>(in.max_src) * C4;  // float4 staging loads per tile
   if (loads <= 1LL * kRoundThreads) return launch_round_persistent<C4, 1, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
   if (loads <= 2LL * kRoundThreads) return launch_round_persistent<C4, 2, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
   if (loads <= 4LL * kRoundThreads) return launch_round_persistent<C4, 4, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
   if (loads <= 8LL * kRoundThreads) return launch_round_persistent<C4, 8, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+  if constexpr (kRoundThreads <= 512) {  // 16 float4 in flight per lane: 512-thread blocks only (VGPRs)
+    if (loads <= 16LL * kRoundThreads) return launch_round_persistent<C4, 16, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+  }
   auto k = k_round_f32_tiled<C4, kRoundThreads, EXACT>;
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;
   const int64_t tiles = (n4 + C4 - 1) / C4;
   if (tiles > 0x7fffffff) return fail(TAL_ERR_INVALID, "too many tiles");
   const dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(in.n_groups));
-  k<<<grid, kRoundThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, in.max_src);
+  k<<<grid, kRoundThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v);
   return check_launch("round kernel");
 }
 
@@ -769,8 +831,8 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
                              tal_round_plan_info* info) {
   if (rows <= 0 || !row_ptr_host || !col_host || !w_host || !out_row_host || !plan_host || !info)
     return fail(TAL_ERR_INVALID, "tal_round_plan_build: bad arguments");
-  if (c4 != 16 && c4 != 32 && c4 != 64)
-    return fail(TAL_ERR_INVALID, "tal_round_plan_build: c4 must be 16, 32 or 64");
+  if (c4 != 64 && c4 != 128)
+    return fail(TAL_ERR_INVALID, "tal_round_plan_build: c4 must be 64 or 128");
   if (row_ptr_host[0] != 0) return fail(TAL_ERR_INVALID, "tal_round_plan_build: row_ptr[0] != 0");
   for (int r = 0; r < rows; ++r)
     if (row_ptr_host[r + 1] <= row_ptr_host[r])
@@ -898,12 +960,10 @@ int32_t tal_agg_round_f32(const float* pool_in, int64_t ld_in, float* pool_out, 
     e_vec = n4 * 4;
     if (n4 > 0) {
       switch (info->c4 * 2 + (exact ? 1 : 0)) {
+        case 257: rc = launch_round_vec<128, true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        case 256: rc = launch_round_vec<128, false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
         case 129: rc = launch_round_vec<64, true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
-        case 128: rc = launch_round_vec<64, false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
-        case 65: rc = launch_round_vec<32, true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
-        case 64: rc = launch_round_vec<32, false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
-        case 33: rc = launch_round_vec<16, true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
-        default: rc = launch_round_vec<16, false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        default: rc = launch_round_vec<64, false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
       }
       if (rc) return rc;
     }

@@ -1,0 +1,167 @@
+"""Aggregation rounds with the simulated devices sharded over GPUs (one process per GPU).
+
+Partitioning: every rank owns a contiguous block of simulated devices (or any owner map the
+caller gives) and keeps their models as rows of a local pool.  A round needs, on rank g, the
+models of every remote neighbor of its rows — the halo.  The exchange is point-to-point: for
+each ordered pair (g -> h), g sends the unique set of its own rows that h's rows reference,
+once, however many of h's rows use it (torch.distributed P2P, i.e. RCCL ncclSend/ncclRecv in
+one group over xGMI with the "nccl" backend, gloo on CPU for tests).  There is no all-reduce:
+the round is a sparse W·X whose outputs stay sharded.
+
+Overlap: the rows whose operands are all local ("interior") are reduced by the K3 kernel on
+the compute stream while the halo is in flight; the remaining ("boundary") rows run after the
+receives complete.  Inputs are double-buffered (pool a -> pool b, then swap) so snapshot
+semantics hold across the two launches.  Exactness is unchanged: every row still sums its
+operands in reference order (neighbors ascending, self last).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import ops
+from .arena import ModelPool, StateLayout
+from .round import csr_from_lists
+
+
+def partition_contiguous(n: int, world: int) -> np.ndarray:
+    """owner[i] for n devices over `world` ranks in contiguous, near-equal blocks."""
+    return (np.arange(n, dtype=np.int64) * world // n).astype(np.int32)
+
+
+@dataclass
+class ShardSpec:
+    rank: int
+    world: int
+    own: List[int]                      # global ids owned, ascending
+    halo: List[int]                     # global ids received, grouped by owner, ascending
+    local_of: Dict[int, int]            # global id -> local pool row
+    send: Dict[int, List[int]] = field(default_factory=dict)  # peer -> local rows to send
+    recv: Dict[int, List[int]] = field(default_factory=dict)  # peer -> local rows to fill
+    interior: List[int] = field(default_factory=list)         # own-row indices, all operands local
+    boundary: List[int] = field(default_factory=list)
+    orders_local: List[List[int]] = field(default_factory=list)  # per own row, local source rows
+    weights: List[List[float]] = field(default_factory=list)
+
+    @property
+    def rows(self) -> int:
+        return len(self.own) + len(self.halo)
+
+
+def build_shard(orders: Sequence[Sequence[int]], weights: Sequence[Sequence[float]], owner: np.ndarray,
+                rank: int, world: Optional[int] = None) -> ShardSpec:
+    """Rank `rank`'s part of a round.  orders[i] = operands of device i in reference order."""
+    owner = np.asarray(owner)
+    if world is None:
+        world = int(owner.max()) + 1 if len(owner) else 1
+    own = [i for i in range(len(orders)) if owner[i] == rank]
+    own_set = set(own)
+    need = sorted({j for i in own for j in orders[i] if j not in own_set}, key=lambda j: (owner[j], j))
+    local_of = {g: k for k, g in enumerate(own)}
+    for k, g in enumerate(need):
+        local_of[g] = len(own) + k
+    spec = ShardSpec(rank=rank, world=world, own=own, halo=need, local_of=local_of)
+    for p in range(world):
+        if p == rank:
+            continue
+        # what p needs from me: my rows referenced by p's rows (same sorted list on both sides)
+        p_rows = [i for i in range(len(orders)) if owner[i] == p]
+        give = sorted({j for i in p_rows for j in orders[i] if owner[j] == rank})
+        if give:
+            spec.send[p] = [local_of[j] for j in give]
+        take = [j for j in need if owner[j] == p]
+        if take:
+            spec.recv[p] = [local_of[j] for j in take]
+    for k, i in enumerate(own):
+        spec.orders_local.append([local_of[j] for j in orders[i]])
+        spec.weights.append([float(x) for x in weights[i]])
+        (spec.interior if all(owner[j] == rank for j in orders[i]) else spec.boundary).append(k)
+    return spec
+
+
+def post_exchange(spec: ShardSpec, tensors: Sequence[torch.Tensor], group=None) -> list:
+    """Post the halo sends/receives of one round for each [rows, ld] pool tensor; returns the
+    requests (wait on them before reading halo rows).  One P2P group: RCCL batches it into a
+    single ncclGroupStart/End."""
+    p2p = []
+    for peer in sorted(set(spec.send) | set(spec.recv)):
+        for t in tensors:
+            for r in spec.send.get(peer, []):
+                p2p.append(dist.P2POp(dist.isend, t[r], peer, group=group))
+            for r in spec.recv.get(peer, []):
+                p2p.append(dist.P2POp(dist.irecv, t[r], peer, group=group))
+    if not p2p:
+        return []
+    return dist.batch_isend_irecv(p2p)
+
+
+class ShardedRound:
+    """One rank's device-resident round over its shard (K3 kernels + halo exchange)."""
+
+    def __init__(self, layout: StateLayout, orders, weights, rank: int, world: int, device,
+                 mode: int = ops.MODE_EXACT, owner: Optional[np.ndarray] = None, group=None,
+                 exchange: Optional[Callable[["ShardedRound"], list]] = None):
+        self.layout = layout
+        self.device = torch.device(device)
+        self.mode = mode
+        self.group = group
+        # exchange(self) -> requests; default: RCCL/gloo P2P.  Tests may pass an in-process copy.
+        self._exchange = exchange or (lambda sr: post_exchange(sr.spec, [sr.pool_a.f32, sr.pool_a.i64], sr.group))
+        owner = partition_contiguous(len(orders), world) if owner is None else np.asarray(owner, np.int32)
+        self.spec = build_shard(orders, weights, owner, rank, world)
+        self.pool_a = ModelPool(layout, self.spec.rows, self.device)
+        self.pool_b = ModelPool(layout, self.spec.rows, self.device)
+        self.plans = {}
+        for name, idx in (("interior", self.spec.interior), ("boundary", self.spec.boundary)):
+            if idx:
+                rp, col, w = csr_from_lists([self.spec.orders_local[k] for k in idx],
+                                            [self.spec.weights[k] for k in idx])
+                self.plans[name] = ops.build_plan(rp, col, w, np.asarray(idx, np.int32)).to(self.device)
+        self.local_rows = len(self.spec.own)
+        self.halo_rows_in = len(self.spec.halo)
+        self.staged_sources = sum(p.info.total_src for p in self.plans.values())
+        self._events: list = []
+
+    def _run(self, name: str, a: ModelPool, b: ModelPool) -> None:
+        plan = self.plans.get(name)
+        if plan is None:
+            return
+        if self.layout.n_f32:
+            ops.round_f32(a.f32, b.f32, plan, n=self.layout.n_f32, mode=self.mode)
+        if self.layout.n_i64:
+            ops.round_i64(a.i64, b.i64, plan, n=self.layout.n_i64)
+
+    def step(self, timed: bool = False) -> None:
+        """One round: halo exchange overlapped with the interior rows, then the boundary rows.
+        With timed=True the kernels are bracketed by events (read them with kernel_ms())."""
+        a, b = self.pool_a, self.pool_b
+        reqs = self._exchange(self)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None
+        if ev:
+            ev[0].record()
+        self._run("interior", a, b)
+        if ev:
+            ev[1].record()
+        for r in reqs:
+            r.wait()
+        if ev:
+            ev[2].record()
+        self._run("boundary", a, b)
+        if ev:
+            ev[3].record()
+            self._events.append(ev)
+        self.pool_a, self.pool_b = b, a
+
+    def kernel_ms(self) -> List[float]:
+        """Per timed step: interior + boundary kernel time (ms); call after synchronizing."""
+        out = [e[0].elapsed_time(e[1]) + e[2].elapsed_time(e[3]) for e in self._events]
+        self._events = []
+        return out
+
+    def own_rows(self) -> ModelPool:
+        """Pool whose rows [0, local_rows) hold this rank's current models."""
+        return self.pool_a

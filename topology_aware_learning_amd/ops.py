@@ -76,7 +76,8 @@ def agg_i64(xs: Sequence[torch.Tensor], weights: Sequence[float], out: torch.Ten
 # ------------------------------------------------------------------------------------------
 # K3 round plans
 # ------------------------------------------------------------------------------------------
-LDS_BUDGET = 64 * 1024  # two workgroups per CU overlap one's HBM staging with the other's math
+LDS_BUDGET = 80 * 1024  # two workgroups per CU overlap one's HBM staging with the other's math
+LDS_BUDGETS = (80 * 1024, 160 * 1024)  # candidates: 2 workgroups / CU, or 1 with bigger groups
 
 
 @dataclass
@@ -100,12 +101,16 @@ class RoundPlan:
         return int(self.info.total_src)
 
 
-def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = LDS_BUDGET) -> RoundPlan:
+def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0) -> RoundPlan:
     """Tile plan for a round given as CSR (row r: operands col[row_ptr[r]:row_ptr[r+1]] with
     float64 weights w, written to pool row out_row[r]).
 
-    c4 = 0 picks the float4 tile width (64, 32 or 16 float4 per source) that stages the fewest
-    source rows in total (ties -> the widest tile, i.e. the longest contiguous HBM segments)."""
+    c4 = 0 / lds_bytes = 0 search the float4 tile width (64 or 128 float4 per source) and the
+    LDS budget (LDS_BUDGETS) for the plan with the lowest estimated time per element:
+      HBM  = 4 B x (staged sources + rows)                     at ~5.5 TB/s
+      LDS  = 4 B x operands (one LDS read per operand)         at ~150 TB/s x eff(workgroups/CU)
+    (eff = 0.33 / 0.6 / 0.8 for 1 / 2 / >= 3 resident workgroups, halved at c4 = 64; fitted to
+    tools/tune/round_variants.hip on MI355X); ties go to more resident workgroups."""
     row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int32)
     col = np.ascontiguousarray(col, dtype=np.int32)
     w = np.ascontiguousarray(w, dtype=np.float64)
@@ -117,23 +122,40 @@ def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = LDS_BUDGE
     cap = L.tal_round_plan_words(rows, len(col))
     best = None
     last_err = None
-    for cand in ([c4] if c4 else [64, 32, 16]):
+    cands = [(c, b) for b in ([lds_bytes] if lds_bytes else LDS_BUDGETS) for c in ([c4] if c4 else [64, 128])]
+    for cand, budget in cands:
         blob = np.zeros(cap, dtype=np.int32)
         info = RoundPlanInfo()
         P32 = ctypes.POINTER(ctypes.c_int32)
         rc = L.tal_round_plan_build(rows, row_ptr.ctypes.data_as(P32), col.ctypes.data_as(P32),
                                     w.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
-                                    out_row.ctypes.data_as(P32), cand, int(lds_bytes),
+                                    out_row.ctypes.data_as(P32), cand, int(budget),
                                     blob.ctypes.data_as(P32), cap, ctypes.byref(info))
         if rc != _lib.TAL_OK:
             last_err = _lib.TalError(rc, L.tal_last_error().decode())
             continue
         plan = RoundPlan(info=info, host=blob[: info.words].copy(), rows=rows, nnz=len(col))
-        if best is None or plan.info.total_src < best.info.total_src:
-            best = plan
+        key = (_plan_cost(plan.info), -_blocks_per_cu(plan.info))
+        if best is None or key < best[0]:
+            best = (key, plan)
     if best is None:
         raise last_err
-    return best
+    return best[1]
+
+
+def _blocks_per_cu(info: RoundPlanInfo) -> int:
+    lds = max(1, info.max_src * info.c4 * 16)
+    return max(1, min(4, (160 * 1024) // lds))
+
+
+def _plan_cost(info: RoundPlanInfo) -> float:
+    """Estimated seconds per element column of the round (see build_plan)."""
+    eff = {1: 0.33, 2: 0.6}.get(_blocks_per_cu(info), 0.8)
+    if info.c4 == 64:
+        eff *= 0.5  # one float4 column per lane: half the LDS reads in flight of the c4=128 form
+    hbm = 4.0 * (info.total_src + info.rows) / 5.5e12
+    lds = 4.0 * info.nnz / (150e12 * eff)
+    return max(hbm, lds)
 
 
 def round_f32(pool_in: torch.Tensor, pool_out: torch.Tensor, plan: RoundPlan, n: Optional[int] = None,
