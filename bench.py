@@ -45,6 +45,7 @@ def parse():
     p.add_argument("--devices", type=int, default=0, help="total devices (overrides devices-per-gpu x N)")
     p.add_argument("--mode", default="exact", choices=["exact", "fma"])
     p.add_argument("--c4", type=int, default=0)
+    p.add_argument("--no-tune", action="store_true", help="use the model-based plan choice instead of timing candidates")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU baseline sample")
     p.add_argument("--no-k1", action="store_true", help="skip the per-call K1 side measurement")
@@ -145,7 +146,11 @@ def main():
         pout = ModelPool(layout, rows, dev)
         fill_pool(pin, 1234)
         row_ptr, col, w = _round_csr(orders, weights)
-        plan = _ops.build_plan(row_ptr, col, w, np.arange(rows, dtype=np.int32), c4=args.c4).to(dev)
+        out_rows = np.arange(rows, dtype=np.int32)
+        if args.no_tune or args.c4:
+            plan = _ops.build_plan(row_ptr, col, w, out_rows, c4=args.c4).to(dev)
+        else:  # time every plan candidate on the real pools (a few rounds, once per topology)
+            plan = _ops.tune_plan(row_ptr, col, w, out_rows, pin.f32, pout.f32, n=layout.n_f32, mode=mode)
 
         def step(a, b):
             _ops.round_f32(a.f32, b.f32, plan, n=layout.n_f32, mode=mode)
@@ -177,13 +182,13 @@ def main():
         bytes_round = 4 * layout.n_f32 * (staged + rows)  # compulsory: each staged source read once, each output written once
         per_call_bytes = 4 * layout.n_f32 * (len(col) + rows)  # SURVEY §8(d) B summed over the round's calls
         result_extra = dict(
-            kernel="k_round_f32_persistent", plan=dict(groups=plan.info.n_groups, staged_sources=staged,
-                                                  c4=plan.info.c4, lds_bytes=plan.info.lds_bytes),
+            kernel=_ops.round_kernel_name(plan.info), plan=dict(groups=plan.info.n_groups, staged_sources=staged,
+                                                  c4=plan.info.c4, dense_rb=plan.info.dense_rb,
+                                                  lds_reads_per_column=plan.info.dense_reads,
+                                                  tuned_ms=plan.tuned_ms, candidates=plan.candidates),
             per_call_equivalent_GBps=per_call_bytes / (k_ms * 1e-3) / 1e9, parity_k3_vs_k1_row0=parity_ok)
         steps_done = args.steps
         units = rows * n_params * steps_done
-        copy_ceiling = bench_copy(pin, pout, bytes_round, dev)
-        result_extra["copy_ceiling"] = copy_ceiling
         k1 = None
         if not args.no_k1:
             k1 = bench_k1(layout, pin, orders, weights, mode, dev)
@@ -191,7 +196,7 @@ def main():
     else:
         from topology_aware_learning_amd.distributed import ShardedRound
 
-        sr = ShardedRound(layout, orders, weights, rank, world, dev, mode=mode)
+        sr = ShardedRound(layout, orders, weights, rank, world, dev, mode=mode, tune=not args.no_tune)
         fill_pool(sr.pool_a, 1234 + rank)
         sr.step()
         # spot check: one (boundary if any) row of this rank == K1 on its operands as received
@@ -233,8 +238,6 @@ def main():
         return
 
     achieved = bytes_round / (k_ms * 1e-3) / 1e9
-    if "copy_ceiling" in result_extra:
-        result_extra["frac_of_copy_ceiling"] = achieved / result_extra["copy_ceiling"]["GBps"]
     traffic = load_traffic(args.model)
     cpu = None
     if not args.no_cpu_baseline and world == 1:

@@ -94,20 +94,40 @@ typedef struct tal_round_plan_info {
   int32_t off_op_w;         /* [nnz] fp32 weight bits */
   int32_t off_out_row;      /* [rows] pool_out row of each row */
   int32_t words;            /* total int32 words of the blob */
+  /* dense row-block form (dense_rb > 0): a wavefront computes dense_rb rows per pass over its
+   * group's staged sources, each LDS read serving every row that uses that source.  Valid
+   * when every row lists its operands as sources in ascending order followed by the row's own
+   * (reference order: sorted neighbors, then self). */
+  int32_t dense_rb;         /* rows per block (0 = sparse form only) */
+  int32_t n_blocks;         /* row blocks over all groups */
+  int32_t off_grp_blk_ptr;  /* [n_groups+1] first block of each group */
+  int32_t off_blk_tab;      /* [n_blocks] word offset of each block's table inside the blob */
+  int32_t off_dense;        /* start of the tables (32-B aligned): per block {n_used, 7 pad words,
+                             * slot[n_used] (staged slots
+                             * the block's rows use, ascending), mask[n_used] (bit r = row r of
+                             * the block uses that slot, own model excluded),
+                             * w[n_used][dense_rb] fp32}; n_used padded to a multiple of 4
+                             * with mask-0 entries */
+  int32_t dense_reads;      /* LDS operand reads per column in the dense form (sparse: nnz) */
 } tal_round_plan_info;
 
-/* Upper bound on the blob size in int32 words for a round of `rows` rows / `nnz` operands. */
+/* Blob size in int32 words of the sparse form for `rows` rows / `nnz` operands (an upper
+ * bound); the dense tables come on top — tal_round_plan_build reports the exact need. */
 int64_t tal_round_plan_words(int32_t rows, int64_t nnz);
 
 /* Build the plan on the host.  row_ptr_host[rows+1], col_host[nnz], w_host[nnz] (float64),
  * out_row_host[rows].  c4 in {64,128}; lds_bytes = LDS budget per workgroup (staged tile
  * 16*c4 B per source plus the scalar kernels' plan slice).  Rows keep their order; consecutive rows
- * share a group while the union of their sources fits.  Returns TAL_ERR_CAPACITY if one
- * row alone has more distinct sources than fit. */
+ * share a group while the union of their sources fits; a group's staged sources are in
+ * ascending pool row order.  dense_rb: 0 = sparse form, 8 = dense row blocks of 8 (falls back
+ * to sparse if a row is not in reference order), -1 = dense when it cuts the LDS operand reads
+ * by at least a quarter.  Returns
+ * TAL_ERR_CAPACITY if one row alone has more distinct sources than fit, or if plan_capacity_words
+ * is too small (info->words then holds the size needed). */
 int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host,
                              const double* w_host, const int32_t* out_row_host, int32_t c4,
-                             int32_t lds_bytes, int32_t* plan_host, int64_t plan_capacity_words,
-                             tal_round_plan_info* info);
+                             int32_t lds_bytes, int32_t dense_rb, int32_t* plan_host,
+                             int64_t plan_capacity_words, tal_round_plan_info* info);
 
 /* Execute the round on the fp32 segment (n elements per model; row stride ld_in / ld_out in
  * elements).  plan_dev = the blob copied to the device.  pool_out may equal pool_in only if

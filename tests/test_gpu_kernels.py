@@ -125,6 +125,7 @@ def _graph_csr(g, weights="unweighted"):
     return orders, ws
 
 
+@pytest.mark.parametrize("dense", [0, 8])
 @pytest.mark.parametrize("graph,n,c4,lds", [
     ("ring", 1000, 0, 0),
     ("regular", 4099, 64, ops.LDS_BUDGET),
@@ -135,7 +136,7 @@ def _graph_csr(g, weights="unweighted"):
     ("barbell", 3001, 0, 0),
     ("complete", 515, 0, 160 * 1024),
 ])
-def test_round_f32_vs_oracle(cuda, graph, n, c4, lds):
+def test_round_f32_vs_oracle(cuda, graph, n, c4, lds, dense):
     g = {
         "ring": nx.cycle_graph(16),
         "regular": nx.random_regular_graph(8, 64, seed=0),
@@ -149,7 +150,8 @@ def test_round_f32_vs_oracle(cuda, graph, n, c4, lds):
     rng = np.random.default_rng(rows + n)
     pool = np.stack([_rand_f32(rng, n) for _ in range(rows)])
     ref = oracle.round_f32(pool, row_ptr, col, w, out_rows)
-    plan = ops.build_plan(row_ptr, col, w, out_rows, c4=c4, lds_bytes=lds)
+    plan = ops.build_plan(row_ptr, col, w, out_rows, c4=c4, lds_bytes=lds, dense=dense)
+    assert plan.info.dense_rb == dense
     pin = torch.from_numpy(pool).to(cuda)
     pout = torch.zeros_like(pin)
     ops.round_f32(pin, pout, plan)

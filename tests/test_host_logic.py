@@ -177,8 +177,9 @@ def test_round_plan_reconstructs_csr():
     ws = [W.unweighted(len(o)) for o in orders]
     row_ptr, col, w = ra.round_csr(orders, ws)
     out_rows = np.arange(64, dtype=np.int32)[::-1].copy()
-    for c4, budget in ((64, ops.LDS_BUDGET), (64, 20 * 1024), (128, 40 * 1024)):
-        plan = ops.build_plan(row_ptr, col, w, out_rows, c4=c4, lds_bytes=budget)
+    for c4, budget, dense in ((64, ops.LDS_BUDGET, 0), (64, 20 * 1024, 0), (128, 40 * 1024, 0),
+                              (64, ops.LDS_BUDGET, 8), (128, 40 * 1024, 8)):
+        plan = ops.build_plan(row_ptr, col, w, out_rows, c4=c4, lds_bytes=budget, dense=dense)
         i, h = plan.info, plan.host
         grp_row = h[i.off_grp_row_ptr: i.off_grp_row_ptr + i.n_groups + 1]
         grp_src = h[i.off_grp_src_ptr: i.off_grp_src_ptr + i.n_groups + 1]
@@ -193,10 +194,44 @@ def test_round_plan_reconstructs_csr():
         for gi in range(i.n_groups):
             srcs = src_row[grp_src[gi]: grp_src[gi + 1]]
             assert len(set(srcs.tolist())) == len(srcs) <= i.max_src
+            assert np.all(np.diff(srcs) > 0)  # staged in ascending pool-row order
             for r in range(grp_row[gi], grp_row[gi + 1]):
                 for k in range(rp[r], rp[r + 1]):
                     rec[k] = srcs[slot[k]]
         assert np.array_equal(rec, col)
+        assert i.dense_rb == dense
+        if dense:
+            blk_ptr = h[i.off_grp_blk_ptr: i.off_grp_blk_ptr + i.n_groups + 1]
+            tabs = h[i.off_blk_tab: i.off_blk_tab + i.n_blocks]
+            reads = 0
+            for gi in range(i.n_groups):
+                for lb in range(blk_ptr[gi + 1] - blk_ptr[gi]):
+                    t0 = tabs[blk_ptr[gi] + lb]
+                    n_used = h[t0]
+                    assert n_used % 4 == 0 and t0 % 8 == 0
+                    e_slot = h[t0 + 8: t0 + 8 + n_used]
+                    e_mask = h[t0 + 8 + n_used: t0 + 8 + 2 * n_used]
+                    e_w = h[t0 + 8 + 2 * n_used: t0 + 8 + 2 * n_used + n_used * dense].reshape(n_used, dense)
+                    ent = np.concatenate([e_slot[:, None], e_mask[:, None], e_w], axis=1)
+                    real = ent[:, 1] != 0
+                    assert np.all(np.diff(ent[real, 0]) > 0) and np.all(ent[~real, 2:] == 0)
+                    ent = ent[real]
+                    n_used = len(ent)
+                    rows_here = 0
+                    for rr in range(dense):
+                        r = grp_row[gi] + lb * dense + rr
+                        if r >= grp_row[gi + 1]:
+                            assert not np.any(ent[:, 1] & (1 << rr))
+                            continue
+                        rows_here += 1
+                        used = {slot[k]: w[k] for k in range(rp[r], rp[r + 1] - 1)}  # self excluded
+                        for e in range(n_used):
+                            bit = bool(ent[e, 1] & (1 << rr))
+                            assert bit == (int(ent[e, 0]) in used)
+                            if bit:
+                                assert ent[e, 2 + rr].view(np.float32) == np.float32(used[int(ent[e, 0])])
+                    reads += n_used + rows_here
+            assert reads == i.dense_reads
         assert i.lds_bytes <= budget
         if budget == ops.LDS_BUDGET:
             assert i.n_groups == 1 and i.total_src == 64

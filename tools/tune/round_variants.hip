@@ -251,7 +251,7 @@ int main(int argc, char** argv) {
   };
   for (int c4 : {64, 128}) for (int lds : {80 * 1024, 160 * 1024}) {
     std::vector<int> plan(tal_round_plan_words(nrows, col.size())); tal_round_plan_info info;
-    if (tal_round_plan_build(nrows, row_ptr.data(), col.data(), w.data(), out_row.data(), c4, lds, plan.data(), plan.size(), &info)) { printf("plan c4=%d lds=%d: %s\n", c4, lds, tal_last_error()); continue; }
+    if (tal_round_plan_build(nrows, row_ptr.data(), col.data(), w.data(), out_row.data(), c4, lds, 0, plan.data(), plan.size(), &info)) { printf("plan c4=%d lds=%d: %s\n", c4, lds, tal_last_error()); continue; }
     int* dplan; CK(hipMalloc(&dplan, info.words * 4)); CK(hipMemcpy(dplan, plan.data(), info.words * 4, hipMemcpyHostToDevice));
     bytes = 4.0 * n * (info.total_src + nrows);
     printf("== c4=%d lds_budget=%d groups=%d staged=%d max_src=%d\n", c4, lds, info.n_groups, info.total_src, info.max_src);

@@ -23,7 +23,7 @@ TAL_ERR_HIP = 2
 TAL_ERR_CAPACITY = 3
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 EXPORTED = (
     "tal_last_error",
@@ -72,6 +72,12 @@ class RoundPlanInfo(ctypes.Structure):
         ("off_op_w", ctypes.c_int32),
         ("off_out_row", ctypes.c_int32),
         ("words", ctypes.c_int32),
+        ("dense_rb", ctypes.c_int32),
+        ("n_blocks", ctypes.c_int32),
+        ("off_grp_blk_ptr", ctypes.c_int32),
+        ("off_blk_tab", ctypes.c_int32),
+        ("off_dense", ctypes.c_int32),
+        ("dense_reads", ctypes.c_int32),
     ]
 
 
@@ -91,7 +97,7 @@ _SIGS = {
     "tal_round_plan_words": (_I64, [_I32, _I64]),
     "tal_round_plan_build": (
         _I32,
-        [_I32, _PI32, _PI32, _PD, _PI32, _I32, _I32, _PI32, _I64, ctypes.POINTER(RoundPlanInfo)],
+        [_I32, _PI32, _PI32, _PD, _PI32, _I32, _I32, _I32, _PI32, _I64, ctypes.POINTER(RoundPlanInfo)],
     ),
     "tal_agg_round_f32": (_I32, [_P, _I64, _P, _I64, _I64, _P, ctypes.POINTER(RoundPlanInfo), _I32, _P]),
     "tal_agg_round_i64": (_I32, [_P, _I64, _P, _I64, _I64, _P, ctypes.POINTER(RoundPlanInfo), _P]),

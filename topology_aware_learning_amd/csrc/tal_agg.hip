@@ -30,7 +30,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 2;
+constexpr int kAbiVersion = 3;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr int kMaxGrid = 256 * 8; // 256 CUs x 8 resident 256-thread blocks
@@ -275,6 +275,9 @@ struct PlanView {
   const int32_t* op_slot;
   const float* op_w;
   const int32_t* out_row;
+  const int32_t* grp_blk_ptr;  // dense form only
+  const int32_t* blk_tab;
+  const int32_t* base;         // the blob (dense tables are addressed from it)
 };
 
 PlanView make_view(const int32_t* plan, const tal_round_plan_info& in) {
@@ -286,6 +289,9 @@ PlanView make_view(const int32_t* plan, const tal_round_plan_info& in) {
   v.op_slot = plan + in.off_op_slot;
   v.op_w = reinterpret_cast<const float*>(plan + in.off_op_w);
   v.out_row = plan + in.off_out_row;
+  v.grp_blk_ptr = plan + in.off_grp_blk_ptr;
+  v.blk_tab = plan + in.off_blk_tab;
+  v.base = plan;
   return v;
 }
 
@@ -338,6 +344,10 @@ __device__ __forceinline__ void st_stream(float* base, int64_t i, float4 v) {
 // lets the backend use scalar (SMEM) loads for the wave-uniform entries.
 typedef __attribute__((address_space(4))) const int32_t* ConstI32;
 typedef __attribute__((address_space(4))) const float* ConstF32;
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(4))) const i32x4* ConstI32x4;
+typedef __attribute__((address_space(4))) const f32x8* ConstF32x8;
 
 template <int C4, int NT, bool EXACT>
 __device__ __forceinline__ void emit_tile(const float4* s_data, const PlanView& p, int r_beg, int nr,
@@ -397,10 +407,90 @@ __device__ __forceinline__ void emit_tile(const float4* s_data, const PlanView& 
   }
 }
 
+// Dense form: a wavefront owns a block of RB rows and walks, once, the staged sources any of
+// them uses (ascending); each source's LDS read serves every row of the block that uses it (row
+// mask), so a row's operands are still consumed in its reference order (sorted neighbors), and
+// the row's own model — the reference's last operand — is added last.  Accumulators start at
+// -0.0f: -0 + fl(w*x) == fl(w*x) exactly for every x, so the first term needs no special case
+// and the result is bit-identical.  Sources are walked four at a time (their LDS reads in flight
+// together); masks, slots and weights are wave-uniform scalar loads.
+// Block table (32-B aligned): {n_used, 7 pad words, slot[n_used], mask[n_used], w[n_used][RB]},
+// n_used padded to a multiple of 4 with mask-0 entries so every vector load is aligned.
+template <int C4, int NT, int RB, bool EXACT>
+__device__ __forceinline__ void emit_tile_dense(const float4* s_data, const PlanView& p, int g, int r_beg,
+                                                int nr, int ns, float* pout, int64_t ld_out4,
+                                                int64_t c0, int64_t n4) {
+  constexpr int kWaves = NT / 64;
+  constexpr int kCpl = C4 / 64;
+  constexpr int kU = 4;
+  static_assert(RB == 8, "weights are loaded as 8-wide vectors");
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const ConstI32 row_ptr = (ConstI32)p.row_ptr;
+  const ConstI32 out_row = (ConstI32)p.out_row;
+  const ConstI32 op_slot = (ConstI32)p.op_slot;
+  const ConstF32 op_w = (ConstF32)p.op_w;
+  const ConstI32 base = (ConstI32)p.base;
+  const int blk0 = ((ConstI32)p.grp_blk_ptr)[g];
+  const int nblk = (nr + RB - 1) / RB;
+  for (int lb = wave; lb < nblk; lb += kWaves) {
+    const ConstI32 tab = base + ((ConstI32)p.blk_tab)[blk0 + lb];
+    const int rows_here = min(RB, nr - lb * RB);
+    const int n_used = tab[0];                        // multiple of kU
+    const ConstI32x4 slots4 = (ConstI32x4)(tab + 8);    // 32-B aligned (see the builder)
+    const ConstI32x4 masks4 = (ConstI32x4)(tab + 8 + n_used);
+    const ConstF32x8 wts8 = (ConstF32x8)(tab + 8 + 2 * n_used);
+    float4 acc[RB][kCpl];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int j = 0; j < kCpl; ++j) acc[r][j] = make_float4(-0.f, -0.f, -0.f, -0.f);
+    for (int e = 0; e < n_used; e += kU) {
+      const i32x4 sl = slots4[e / kU];                 // s_load_dwordx4
+      const i32x4 mk = masks4[e / kU];
+      float4 x[kU][kCpl];
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+#pragma unroll
+        for (int j = 0; j < kCpl; ++j) x[u][j] = s_data[sl[u] * C4 + lane + 64 * j];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const f32x8 wv = wts8[e + u];                   // s_load_dwordx8
+        const uint32_t m = static_cast<uint32_t>(mk[u]);
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          if (m & (1u << r)) {
+#pragma unroll
+            for (int j = 0; j < kCpl; ++j) acc[r][j] = next4<EXACT>(acc[r][j], wv[r], x[u][j]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      if (r < rows_here) {
+        const int gr = r_beg + lb * RB + r;
+        const int q = row_ptr[gr + 1] - 1;  // the row's own model, last in reference order
+        const float w = op_w[q];
+        const int sl = op_slot[q] * C4 + lane;
+        const int64_t orow = out_row[gr];
+#pragma unroll
+        for (int j = 0; j < kCpl; ++j) {
+          acc[r][j] = next4<EXACT>(acc[r][j], w, s_data[sl + 64 * j]);
+          const int64_t col = c0 + lane + 64 * j;
+          if (col < n4) st_stream(pout, orow * ld_out4 + col, acc[r][j]);
+        }
+      }
+    }
+  }
+}
+
+constexpr int kDenseRb = 8;
+
 // Persistent form (the fast path): each workgroup walks column tiles t, t+gridDim.x, ...;
 // every lane owns J fixed staging slots (source, column) and keeps the next tile's J float4
 // loads in flight in registers while the workgroup computes the current tile from LDS.
-template <int C4, int NT, int J, bool EXACT>
+template <int C4, int NT, int J, bool EXACT, bool DENSE>
 __global__ __launch_bounds__(NT) void k_round_f32_persistent(const float* __restrict__ pin,
                                                              int64_t ld_in4,
                                                              float* __restrict__ pout,
@@ -412,23 +502,24 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const float* __rest
   const int ns = p.grp_src_ptr[g + 1] - s_beg;
   const int r_beg = p.grp_row_ptr[g];
   const int nr = p.grp_row_ptr[g + 1] - r_beg;
-  const float* base[J];
-  int slotk[J];
-  bool live[J];
+  // lane-fixed staging slots: slot k = j*NT + tid holds column c = tid % C4 (NT is a multiple
+  // of C4) of staged source k / C4; only the source's pool row is kept per slot (-1 = unused)
+  static_assert(NT % C4 == 0, "a block stages whole source tiles");
+  const int c = threadIdx.x % C4;
+  int srow[J];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const int k = j * NT + threadIdx.x;
-    const int s = k / C4;
-    live[j] = s < ns;
-    slotk[j] = k;
-    base[j] = pin + 4 * ((live[j] ? static_cast<int64_t>(p.src_row[s_beg + s]) * ld_in4 : 0) + (k % C4));
+    const int src = (j * NT + threadIdx.x) / C4;
+    srow[j] = src < ns ? p.src_row[s_beg + src] : -1;
   }
   float4 v[J];
   auto load_tile = [&](int64_t tt) {
-    const int64_t c0 = tt * C4;
+    const int64_t col = tt * C4 + c;
+    if (col < n4) {
 #pragma unroll
-    for (int j = 0; j < J; ++j)
-      if (live[j] && c0 + (slotk[j] % C4) < n4) v[j] = ld_stream(base[j], c0);
+      for (int j = 0; j < J; ++j)
+        if (srow[j] >= 0) v[j] = ld_stream(pin, static_cast<int64_t>(srow[j]) * ld_in4 + col);
+    }
   };
   int64_t t = blockIdx.x;
   if (t < n_tiles) load_tile(t);
@@ -436,16 +527,19 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const float* __rest
     __syncthreads();  // the previous tile's readers are done with s_data
 #pragma unroll
     for (int j = 0; j < J; ++j)
-      if (live[j]) s_data[slotk[j]] = v[j];
+      if (srow[j] >= 0) s_data[j * NT + threadIdx.x] = v[j];
     __syncthreads();
     if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
-    emit_tile<C4, NT, EXACT>(s_data, p, r_beg, nr, pout, ld_out4, t * C4, n4);
+    if constexpr (DENSE)
+      emit_tile_dense<C4, NT, kDenseRb, EXACT>(s_data, p, g, r_beg, nr, ns, pout, ld_out4, t * C4, n4);
+    else
+      emit_tile<C4, NT, EXACT>(s_data, p, r_beg, nr, pout, ld_out4, t * C4, n4);
   }
 }
 
 // General form (groups whose staging needs more than 8 loads per lane): one tile per
 // workgroup, staging in batches of 4 independent loads per lane.
-template <int C4, int NT, bool EXACT>
+template <int C4, int NT, bool EXACT, bool DENSE>
 __global__ __launch_bounds__(NT) void k_round_f32_tiled(const float* __restrict__ pin,
                                                         int64_t ld_in4, float* __restrict__ pout,
                                                         int64_t ld_out4, int64_t n4, PlanView p) {
@@ -475,7 +569,10 @@ __global__ __launch_bounds__(NT) void k_round_f32_tiled(const float* __restrict_
     }
   }
   __syncthreads();
-  emit_tile<C4, NT, EXACT>(s_data, p, r_beg, nr, pout, ld_out4, c0, n4);
+  if constexpr (DENSE)
+    emit_tile_dense<C4, NT, kDenseRb, EXACT>(s_data, p, g, r_beg, nr, ns, pout, ld_out4, c0, n4);
+  else
+    emit_tile<C4, NT, EXACT>(s_data, p, r_beg, nr, pout, ld_out4, c0, n4);
 }
 
 // Scalar tiled round: the fp32 tail (elements e0..n-1 when the float4 path ran) or whole
@@ -559,6 +656,8 @@ int32_t validate_info(const tal_round_plan_info* info) {
     return fail(TAL_ERR_INVALID, "empty round plan");
   if (info->c4 != 64 && info->c4 != 128)
     return fail(TAL_ERR_INVALID, "plan c4 must be 64 or 128");
+  if (info->dense_rb != 0 && info->dense_rb != kDenseRb)
+    return fail(TAL_ERR_INVALID, "plan dense_rb must be 0 or 8");
   return TAL_OK;
 }
 
@@ -585,12 +684,12 @@ int32_t launch_round_scalar(const void* pin, int64_t ld_in, void* pout, int64_t 
 template <int C4>
 constexpr int round_threads() { return C4 >= 128 ? 512 : 1024; }
 
-template <int C4, int J, bool EXACT>
+template <int C4, int J, bool EXACT, bool DENSE>
 int32_t launch_round_persistent(const float* pin, int64_t ld_in, float* pout, int64_t ld_out,
                                 int64_t n4, const PlanView& v, const tal_round_plan_info& in,
                                 size_t lds, hipStream_t s) {
   constexpr int kRoundThreads = round_threads<C4>();
-  auto k = k_round_f32_persistent<C4, kRoundThreads, J, EXACT>;
+  auto k = k_round_f32_persistent<C4, kRoundThreads, J, EXACT, DENSE>;
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;
   const int64_t tiles = (n4 + C4 - 1) / C4;
@@ -602,20 +701,21 @@ int32_t launch_round_persistent(const float* pin, int64_t ld_in, float* pout, in
   return check_launch("round kernel (persistent)");
 }
 
-template <int C4, bool EXACT>
+template <int C4, bool EXACT, bool DENSE>
 int32_t launch_round_vec(const float* pin, int64_t ld_in, float* pout, int64_t ld_out, int64_t n4,
                          const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
   constexpr int kRoundThreads = round_threads<C4>();
   const size_t lds = static_cast<size_t>(in.max_src) * C4 * 16;
   const int64_t loads = static_cast<int64_t>(in.max_src) * C4;  // float4 staging loads per tile
-  if (loads <= 1LL * kRoundThreads) return launch_round_persistent<C4, 1, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
-  if (loads <= 2LL * kRoundThreads) return launch_round_persistent<C4, 2, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
-  if (loads <= 4LL * kRoundThreads) return launch_round_persistent<C4, 4, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
-  if (loads <= 8LL * kRoundThreads) return launch_round_persistent<C4, 8, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
-  if constexpr (kRoundThreads <= 512) {  // 16 float4 in flight per lane: 512-thread blocks only (VGPRs)
-    if (loads <= 16LL * kRoundThreads) return launch_round_persistent<C4, 16, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+  if (loads <= 1LL * kRoundThreads) return launch_round_persistent<C4, 1, EXACT, DENSE>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+  if (loads <= 2LL * kRoundThreads) return launch_round_persistent<C4, 2, EXACT, DENSE>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+  if (loads <= 4LL * kRoundThreads) return launch_round_persistent<C4, 4, EXACT, DENSE>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+  if (loads <= 8LL * kRoundThreads) return launch_round_persistent<C4, 8, EXACT, DENSE>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+  if constexpr (kRoundThreads <= 512) {  // 16-20 float4 in flight per lane: 512-thread blocks only (VGPRs)
+    if (loads <= 16LL * kRoundThreads) return launch_round_persistent<C4, 16, EXACT, DENSE>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+    if (loads <= 20LL * kRoundThreads) return launch_round_persistent<C4, 20, EXACT, DENSE>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
   }
-  auto k = k_round_f32_tiled<C4, kRoundThreads, EXACT>;
+  auto k = k_round_f32_tiled<C4, kRoundThreads, EXACT, DENSE>;
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;
   const int64_t tiles = (n4 + C4 - 1) / C4;
@@ -827,12 +927,14 @@ int64_t tal_round_plan_words(int32_t rows, int64_t nnz) {
 
 int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host,
                              const double* w_host, const int32_t* out_row_host, int32_t c4,
-                             int32_t lds_bytes, int32_t* plan_host, int64_t plan_capacity_words,
-                             tal_round_plan_info* info) {
-  if (rows <= 0 || !row_ptr_host || !col_host || !w_host || !out_row_host || !plan_host || !info)
+                             int32_t lds_bytes, int32_t dense_rb, int32_t* plan_host,
+                             int64_t plan_capacity_words, tal_round_plan_info* info) {
+  if (rows <= 0 || !row_ptr_host || !col_host || !w_host || !out_row_host || !info)
     return fail(TAL_ERR_INVALID, "tal_round_plan_build: bad arguments");
   if (c4 != 64 && c4 != 128)
     return fail(TAL_ERR_INVALID, "tal_round_plan_build: c4 must be 64 or 128");
+  if (dense_rb != 0 && dense_rb != kDenseRb && dense_rb != -1)
+    return fail(TAL_ERR_INVALID, "tal_round_plan_build: dense_rb must be 0, 8 or -1");
   if (row_ptr_host[0] != 0) return fail(TAL_ERR_INVALID, "tal_round_plan_build: row_ptr[0] != 0");
   for (int r = 0; r < rows; ++r)
     if (row_ptr_host[r + 1] <= row_ptr_host[r])
@@ -840,68 +942,111 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
   const int64_t nnz = row_ptr_host[rows];
   for (int64_t k = 0; k < nnz; ++k)
     if (col_host[k] < 0) return fail(TAL_ERR_INVALID, "tal_round_plan_build: negative source row");
-  if (plan_capacity_words < tal_round_plan_words(rows, nnz))
-    return fail(TAL_ERR_INVALID, "tal_round_plan_build: plan buffer too small");
 
-  // Both round kernels stage 16*c4 bytes per source (c4 float4 or 4*c4 scalars).
+  // 1. group consecutive rows while the union of their sources fits the LDS budget
+  //    (both round kernels stage 16*c4 bytes per source; the scalar one also the plan slice)
   const int64_t per_src = 16LL * c4;
-  std::vector<int32_t> grp_row_ptr{0}, grp_src_ptr{0}, src_row, slot(nnz);
-  std::vector<int32_t> map;  // source row -> slot in current group (-1 absent)
-  int32_t max_col = 0;
-  for (int64_t k = 0; k < nnz; ++k) max_col = std::max(max_col, col_host[k]);
-  map.assign(static_cast<size_t>(max_col) + 1, -1);
-  std::vector<int32_t> cur_src;
-  int64_t cur_rows = 0, cur_nnz = 0;
-  int32_t max_src = 0, max_rows = 0, max_nnz = 0;
   auto need = [&](int64_t ns, int64_t nr, int64_t no) {
     return ns * per_src + (nr + 1 + 2 * no + ns + nr) * 4;
   };
-  auto close_group = [&](int r_end) {
-    grp_row_ptr.push_back(r_end);
-    for (int32_t sr : cur_src) { src_row.push_back(sr); map[sr] = -1; }
-    grp_src_ptr.push_back(static_cast<int32_t>(src_row.size()));
-    max_src = std::max<int32_t>(max_src, static_cast<int32_t>(cur_src.size()));
-    max_rows = std::max<int32_t>(max_rows, static_cast<int32_t>(cur_rows));
-    max_nnz = std::max<int32_t>(max_nnz, static_cast<int32_t>(cur_nnz));
-    cur_src.clear();
-    cur_rows = cur_nnz = 0;
-  };
+  int32_t max_col = 0;
+  for (int64_t k = 0; k < nnz; ++k) max_col = std::max(max_col, col_host[k]);
+  std::vector<int32_t> seen(static_cast<size_t>(max_col) + 1, -1);  // source -> group id that has it
+  std::vector<int32_t> grp_row_ptr{0};
+  std::vector<std::vector<int32_t>> grp_srcs(1);
+  int64_t cur_nnz = 0;
   for (int r = 0; r < rows; ++r) {
-    // sources this row would add
-    int64_t add = 0;
+    const int g = static_cast<int>(grp_srcs.size()) - 1;
     std::vector<int32_t> fresh;
     for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1]; ++k) {
       const int32_t sr = col_host[k];
-      if (map[sr] < 0 && std::find(fresh.begin(), fresh.end(), sr) == fresh.end()) {
-        fresh.push_back(sr);
-        ++add;
-      }
+      if (seen[sr] != g && std::find(fresh.begin(), fresh.end(), sr) == fresh.end()) fresh.push_back(sr);
     }
     const int64_t row_nnz = row_ptr_host[r + 1] - row_ptr_host[r];
+    const int64_t cur_rows = r - grp_row_ptr.back();
     if (cur_rows > 0 &&
-        need(static_cast<int64_t>(cur_src.size()) + add, cur_rows + 1, cur_nnz + row_nnz) > lds_bytes) {
-      close_group(r);
+        need(static_cast<int64_t>(grp_srcs[g].size() + fresh.size()), cur_rows + 1, cur_nnz + row_nnz) > lds_bytes) {
+      grp_row_ptr.push_back(r);
+      grp_srcs.emplace_back();
+      cur_nnz = 0;
+      const int g2 = static_cast<int>(grp_srcs.size()) - 1;
       fresh.clear();
       for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1]; ++k) {
         const int32_t sr = col_host[k];
-        if (std::find(fresh.begin(), fresh.end(), sr) == fresh.end()) fresh.push_back(sr);
+        if (seen[sr] != g2 && std::find(fresh.begin(), fresh.end(), sr) == fresh.end()) fresh.push_back(sr);
       }
-    }
-    if (need(static_cast<int64_t>(cur_src.size() + fresh.size()), cur_rows + 1, cur_nnz + row_nnz) >
-        lds_bytes)
+      if (need(static_cast<int64_t>(fresh.size()), 1, row_nnz) > lds_bytes)
+        return fail(TAL_ERR_CAPACITY, "tal_round_plan_build: row " + std::to_string(r) +
+                                          " has more distinct sources than one LDS tile holds");
+    } else if (need(static_cast<int64_t>(grp_srcs[g].size() + fresh.size()), cur_rows + 1, cur_nnz + row_nnz) >
+               lds_bytes) {
       return fail(TAL_ERR_CAPACITY, "tal_round_plan_build: row " + std::to_string(r) +
                                         " has more distinct sources than one LDS tile holds");
-    for (int32_t sr : fresh) {
-      map[sr] = static_cast<int32_t>(cur_src.size());
-      cur_src.push_back(sr);
     }
-    for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1]; ++k) slot[k] = map[col_host[k]];
-    ++cur_rows;
+    const int gg = static_cast<int>(grp_srcs.size()) - 1;
+    for (int32_t sr : fresh) {
+      seen[sr] = gg;
+      grp_srcs[gg].push_back(sr);
+    }
     cur_nnz += row_nnz;
   }
-  close_group(rows);
+  grp_row_ptr.push_back(rows);
+  const int32_t G = static_cast<int32_t>(grp_srcs.size());
 
-  const int32_t G = static_cast<int32_t>(grp_row_ptr.size()) - 1;
+  // 2. staged sources of a group in ascending pool-row order; operand slots
+  std::vector<int32_t> grp_src_ptr{0}, src_row, slot(nnz);
+  std::vector<int32_t> map(static_cast<size_t>(max_col) + 1, -1);
+  int32_t max_src = 0, max_rows = 0, max_nnz = 0;
+  for (int g = 0; g < G; ++g) {
+    std::vector<int32_t>& ss = grp_srcs[g];
+    std::sort(ss.begin(), ss.end());
+    for (size_t i = 0; i < ss.size(); ++i) map[ss[i]] = static_cast<int32_t>(i);
+    for (int r = grp_row_ptr[g]; r < grp_row_ptr[g + 1]; ++r)
+      for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1]; ++k) slot[k] = map[col_host[k]];
+    src_row.insert(src_row.end(), ss.begin(), ss.end());
+    grp_src_ptr.push_back(static_cast<int32_t>(src_row.size()));
+    max_src = std::max<int32_t>(max_src, static_cast<int32_t>(ss.size()));
+    max_rows = std::max<int32_t>(max_rows, grp_row_ptr[g + 1] - grp_row_ptr[g]);
+    max_nnz = std::max<int32_t>(max_nnz, row_ptr_host[grp_row_ptr[g + 1]] - row_ptr_host[grp_row_ptr[g]]);
+  }
+
+  // 3. dense row blocks: valid when every row's operands are strictly ascending sources followed
+  //    by one more (its own model) that does not occur before it
+  bool dense_ok = dense_rb != 0;
+  for (int r = 0; r < rows && dense_ok; ++r) {
+    const int32_t k0 = row_ptr_host[r], k1 = row_ptr_host[r + 1];
+    for (int32_t k = k0 + 1; k < k1 - 1 && dense_ok; ++k) dense_ok = col_host[k] > col_host[k - 1];
+    for (int32_t k = k0; k < k1 - 1 && dense_ok; ++k) dense_ok = col_host[k] != col_host[k1 - 1];
+  }
+  // dense walk: per block of kDenseRb rows, one LDS read per distinct (non-self) source the
+  // block uses plus one per row for its own model
+  std::vector<std::vector<int32_t>> blk_used;  // per block: used slots, ascending
+  int64_t dense_reads = 0;
+  if (dense_ok) {
+    for (int g = 0; g < G; ++g) {
+      for (int r0 = grp_row_ptr[g]; r0 < grp_row_ptr[g + 1]; r0 += kDenseRb) {
+        std::vector<int32_t> used;
+        const int r1 = std::min(r0 + kDenseRb, grp_row_ptr[g + 1]);
+        for (int r = r0; r < r1; ++r)
+          for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1] - 1; ++k) used.push_back(slot[k]);
+        std::sort(used.begin(), used.end());
+        used.erase(std::unique(used.begin(), used.end()), used.end());
+        dense_reads += static_cast<int64_t>(used.size()) + (r1 - r0);
+        blk_used.push_back(std::move(used));
+      }
+    }
+    if (dense_rb == -1) dense_ok = dense_reads * 4 <= nnz * 3;
+  }
+  const int32_t rb = dense_ok ? kDenseRb : 0;
+  std::vector<int32_t> grp_blk_ptr{0};
+  int64_t dense_words = 0;
+  if (rb) {
+    for (int g = 0; g < G; ++g)
+      grp_blk_ptr.push_back(grp_blk_ptr.back() + (grp_row_ptr[g + 1] - grp_row_ptr[g] + rb - 1) / rb);
+    for (const auto& u : blk_used) dense_words += 8 + ((static_cast<int64_t>(u.size()) + 3) / 4 * 4) * (rb + 2);
+  }
+  const int32_t n_blocks = rb ? grp_blk_ptr.back() : 0;
+
   tal_round_plan_info in;
   memset(&in, 0, sizeof(in));
   in.rows = rows;
@@ -912,17 +1057,29 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
   in.max_rows = max_rows;
   in.max_nnz = max_nnz;
   in.c4 = c4;
-  int32_t off = 0;
-  in.off_grp_row_ptr = off; off += G + 1;
-  in.off_grp_src_ptr = off; off += G + 1;
-  in.off_src_row = off; off += in.total_src;
-  in.off_row_ptr = off; off += rows + 1;
-  in.off_op_slot = off; off += static_cast<int32_t>(nnz);
-  in.off_op_w = off; off += static_cast<int32_t>(nnz);
-  in.off_out_row = off; off += rows;
-  in.words = off;
+  in.dense_rb = rb;
+  in.n_blocks = n_blocks;
+  in.dense_reads = static_cast<int32_t>(rb ? dense_reads : nnz);
+  int64_t off = 0;
+  in.off_grp_row_ptr = static_cast<int32_t>(off); off += G + 1;
+  in.off_grp_src_ptr = static_cast<int32_t>(off); off += G + 1;
+  in.off_src_row = static_cast<int32_t>(off); off += in.total_src;
+  in.off_row_ptr = static_cast<int32_t>(off); off += rows + 1;
+  in.off_op_slot = static_cast<int32_t>(off); off += nnz;
+  in.off_op_w = static_cast<int32_t>(off); off += nnz;
+  in.off_out_row = static_cast<int32_t>(off); off += rows;
+  in.off_grp_blk_ptr = static_cast<int32_t>(off); off += rb ? G + 1 : 0;
+  in.off_blk_tab = static_cast<int32_t>(off); off += n_blocks;
+  off = (off + 7) / 8 * 8;  // dense tables 32-B aligned (vector scalar loads)
+  in.off_dense = static_cast<int32_t>(off); off += dense_words;
+  if (off > 0x7fffffff) return fail(TAL_ERR_INVALID, "tal_round_plan_build: plan larger than 2^31 words");
+  in.words = static_cast<int32_t>(off);
   in.lds_bytes = static_cast<int32_t>(plan_lds_bytes(in, 16 * c4));
-  if (off > plan_capacity_words) return fail(TAL_ERR_INVALID, "tal_round_plan_build: overflow");
+  if (!plan_host || off > plan_capacity_words) {
+    *info = in;
+    return fail(TAL_ERR_CAPACITY, "tal_round_plan_build: plan buffer too small: need " +
+                                      std::to_string(off) + " words");
+  }
 
   memcpy(plan_host + in.off_grp_row_ptr, grp_row_ptr.data(), 4 * (G + 1));
   memcpy(plan_host + in.off_grp_src_ptr, grp_src_ptr.data(), 4 * (G + 1));
@@ -934,6 +1091,35 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
     memcpy(plan_host + in.off_op_w + k, &wf, 4);
   }
   memcpy(plan_host + in.off_out_row, out_row_host, 4 * static_cast<size_t>(rows));
+  if (rb) {
+    memcpy(plan_host + in.off_grp_blk_ptr, grp_blk_ptr.data(), 4 * (G + 1));
+    int64_t pos = in.off_dense;
+    int b = 0;
+    for (int g = 0; g < G; ++g) {
+      for (int r0 = grp_row_ptr[g]; r0 < grp_row_ptr[g + 1]; r0 += rb, ++b) {
+        const std::vector<int32_t>& used = blk_used[b];
+        const int64_t nu = (static_cast<int64_t>(used.size()) + 3) / 4 * 4;  // padded (mask-0 entries)
+        plan_host[in.off_blk_tab + b] = static_cast<int32_t>(pos);
+        int32_t* tab = plan_host + pos;
+        const int64_t words = 8 + nu * (rb + 2);  // multiple of 8: the next table stays aligned
+        memset(tab, 0, 4 * static_cast<size_t>(words));
+        tab[0] = static_cast<int32_t>(nu);
+        int32_t* t_slot = tab + 8;
+        int32_t* t_mask = t_slot + nu;
+        int32_t* t_w = t_mask + nu;
+        for (size_t e = 0; e < used.size(); ++e) t_slot[e] = used[e];
+        for (int r = r0; r < std::min(r0 + rb, grp_row_ptr[g + 1]); ++r) {
+          for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1] - 1; ++k) {  // self excluded
+            const int64_t e = std::lower_bound(used.begin(), used.end(), slot[k]) - used.begin();
+            t_mask[e] |= static_cast<int32_t>(1u << (r - r0));
+            const float wf = static_cast<float>(w_host[k]);
+            memcpy(t_w + e * rb + (r - r0), &wf, 4);
+          }
+        }
+        pos += words;
+      }
+    }
+  }
   *info = in;
   g_err.clear();
   return TAL_OK;
@@ -959,11 +1145,16 @@ int32_t tal_agg_round_f32(const float* pool_in, int64_t ld_in, float* pool_out, 
     const int64_t n4 = n / 4;
     e_vec = n4 * 4;
     if (n4 > 0) {
-      switch (info->c4 * 2 + (exact ? 1 : 0)) {
-        case 257: rc = launch_round_vec<128, true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
-        case 256: rc = launch_round_vec<128, false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
-        case 129: rc = launch_round_vec<64, true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
-        default: rc = launch_round_vec<64, false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+      const bool dense = info->dense_rb > 0;
+      switch (info->c4 * 4 + (exact ? 2 : 0) + (dense ? 1 : 0)) {
+        case 515: rc = launch_round_vec<128, true, true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        case 514: rc = launch_round_vec<128, true, false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        case 513: rc = launch_round_vec<128, false, true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        case 512: rc = launch_round_vec<128, false, false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        case 259: rc = launch_round_vec<64, true, true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        case 258: rc = launch_round_vec<64, true, false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        case 257: rc = launch_round_vec<64, false, true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        default: rc = launch_round_vec<64, false, false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
       }
       if (rc) return rc;
     }

@@ -104,7 +104,7 @@ class ShardedRound:
 
     def __init__(self, layout: StateLayout, orders, weights, rank: int, world: int, device,
                  mode: int = ops.MODE_EXACT, owner: Optional[np.ndarray] = None, group=None,
-                 exchange: Optional[Callable[["ShardedRound"], list]] = None):
+                 exchange: Optional[Callable[["ShardedRound"], list]] = None, tune: bool = False):
         self.layout = layout
         self.device = torch.device(device)
         self.mode = mode
@@ -120,7 +120,9 @@ class ShardedRound:
             if idx:
                 rp, col, w = csr_from_lists([self.spec.orders_local[k] for k in idx],
                                             [self.spec.weights[k] for k in idx])
-                self.plans[name] = ops.build_plan(rp, col, w, np.asarray(idx, np.int32)).to(self.device)
+                self.plans[name] = (ops.tune_plan(rp, col, w, np.asarray(idx, np.int32), self.pool_a.f32,
+                                                  self.pool_b.f32, n=layout.n_f32, mode=mode)
+                                    if tune else ops.build_plan(rp, col, w, np.asarray(idx, np.int32)).to(self.device))
         self.local_rows = len(self.spec.own)
         self.halo_rows_in = len(self.spec.halo)
         self.staged_sources = sum(p.info.total_src for p in self.plans.values())

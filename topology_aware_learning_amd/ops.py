@@ -87,6 +87,8 @@ class RoundPlan:
     device: Optional[torch.Tensor] = None
     rows: int = 0
     nnz: int = 0
+    tuned_ms: Optional[float] = None
+    candidates: Optional[list] = None  # tune_plan's measured candidates
 
     @property
     def single_group(self) -> bool:
@@ -101,7 +103,7 @@ class RoundPlan:
         return int(self.info.total_src)
 
 
-def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0) -> RoundPlan:
+def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0, dense: int = -1) -> RoundPlan:
     """Tile plan for a round given as CSR (row r: operands col[row_ptr[r]:row_ptr[r+1]] with
     float64 weights w, written to pool row out_row[r]).
 
@@ -110,7 +112,9 @@ def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0) -> Rou
       HBM  = 4 B x (staged sources + rows)                     at ~5.5 TB/s
       LDS  = 4 B x operands (one LDS read per operand)         at ~150 TB/s x eff(workgroups/CU)
     (eff = 0.33 / 0.6 / 0.8 for 1 / 2 / >= 3 resident workgroups, halved at c4 = 64; fitted to
-    tools/tune/round_variants.hip on MI355X); ties go to more resident workgroups."""
+    tools/tune/round_variants.hip on MI355X); ties go to more resident workgroups.
+    dense: -1 lets the library pick the dense row-block form by density (rows that use a large
+    share of their group's sources: cliques), 0 forces the sparse form, 8 requests dense."""
     row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int32)
     col = np.ascontiguousarray(col, dtype=np.int32)
     w = np.ascontiguousarray(w, dtype=np.float64)
@@ -124,13 +128,19 @@ def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0) -> Rou
     last_err = None
     cands = [(c, b) for b in ([lds_bytes] if lds_bytes else LDS_BUDGETS) for c in ([c4] if c4 else [64, 128])]
     for cand, budget in cands:
-        blob = np.zeros(cap, dtype=np.int32)
         info = RoundPlanInfo()
         P32 = ctypes.POINTER(ctypes.c_int32)
-        rc = L.tal_round_plan_build(rows, row_ptr.ctypes.data_as(P32), col.ctypes.data_as(P32),
-                                    w.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
-                                    out_row.ctypes.data_as(P32), cand, int(budget),
-                                    blob.ctypes.data_as(P32), cap, ctypes.byref(info))
+        size = cap
+        for _ in range(2):  # the dense tables' size is known only after grouping: retry once
+            blob = np.zeros(size, dtype=np.int32)
+            rc = L.tal_round_plan_build(rows, row_ptr.ctypes.data_as(P32), col.ctypes.data_as(P32),
+                                        w.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                        out_row.ctypes.data_as(P32), cand, int(budget), int(dense),
+                                        blob.ctypes.data_as(P32), size, ctypes.byref(info))
+            if rc == _lib.TAL_ERR_CAPACITY and info.words > size:
+                size = int(info.words)
+                continue
+            break
         if rc != _lib.TAL_OK:
             last_err = _lib.TalError(rc, L.tal_last_error().decode())
             continue
@@ -141,6 +151,62 @@ def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0) -> Rou
     if best is None:
         raise last_err
     return best[1]
+
+
+def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.Tensor,
+              n: Optional[int] = None, reps: int = 2, mode: int = MODE_EXACT) -> RoundPlan:
+    """Pick the plan by measurement: every (tile width, LDS budget, sparse/dense) candidate that
+    builds runs `reps` times on the real pools (pool_out must not alias pool_in) and the fastest
+    median wins.  Costs a few rounds once per topology; the model-based choice of build_plan is
+    the fallback when only one candidate builds."""
+    if pool_in.data_ptr() == pool_out.data_ptr():
+        raise ValueError("tune_plan needs distinct input / output pools")
+    cands = []
+    for c4 in (64, 128):
+        for budget in LDS_BUDGETS:
+            for dense in (0, 8):
+                try:
+                    p = build_plan(row_ptr, col, w, out_row, c4=c4, lds_bytes=budget, dense=dense)
+                except _lib.TalError:
+                    continue
+                if dense and not p.info.dense_rb:
+                    continue
+                key = (p.info.c4, p.info.n_groups, p.info.total_src, p.info.dense_rb, p.info.max_src)
+                if all(key != k for k, _ in cands):
+                    cands.append((key, p))
+    if not cands:
+        return build_plan(row_ptr, col, w, out_row)
+    if len(cands) == 1:
+        return cands[0][1].to(pool_in.device)
+    best, best_t = None, None
+    timings = []
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for key, p in cands:
+        p.to(pool_in.device)
+        round_f32(pool_in, pool_out, p, n=n, mode=mode)  # warm (LDS attribute, code load)
+        ts = []
+        for _ in range(reps):
+            s.record()
+            round_f32(pool_in, pool_out, p, n=n, mode=mode)
+            e.record()
+            e.synchronize()
+            ts.append(s.elapsed_time(e))
+        t = float(np.median(ts))
+        timings.append({"c4": key[0], "groups": key[1], "staged": key[2], "dense_rb": key[3],
+                        "max_src": key[4], "ms": round(t, 4)})
+        if best_t is None or t < best_t:
+            best, best_t = p, t
+    best.tuned_ms = best_t
+    best.candidates = timings
+    return best
+
+
+def round_kernel_name(info: RoundPlanInfo) -> str:
+    """Which K3 kernel tal_agg_round_f32 launches for this plan (mirrors launch_round_vec)."""
+    threads = 1024 if info.c4 == 64 else 512
+    j_max = 20 if threads <= 512 else 8
+    loads = info.max_src * info.c4
+    return "k_round_f32_persistent" if loads <= j_max * threads else "k_round_f32_tiled"
 
 
 def _blocks_per_cu(info: RoundPlanInfo) -> int:
@@ -154,7 +220,7 @@ def _plan_cost(info: RoundPlanInfo) -> float:
     if info.c4 == 64:
         eff *= 0.5  # one float4 column per lane: half the LDS reads in flight of the c4=128 form
     hbm = 4.0 * (info.total_src + info.rows) / 5.5e12
-    lds = 4.0 * info.nnz / (150e12 * eff)
+    lds = 4.0 * info.dense_reads / (150e12 * eff)
     return max(hbm, lds)
 
 
