@@ -105,10 +105,19 @@ typedef struct tal_round_plan_info {
   int32_t off_dense;        /* start of the tables (32-B aligned): per block {n_used, 7 pad words,
                              * slot[n_used] (staged slots
                              * the block's rows use, ascending), mask[n_used] (bit r = row r of
-                             * the block uses that slot, own model excluded),
+                             * the block uses that slot, own model excluded; bit 31 set
+                             * when all those rows have the same fp32 weight, which then
+                             * fills every w slot: one product w*x serves them all),
                              * w[n_used][dense_rb] fp32}; n_used padded to a multiple of 4
                              * with mask-0 entries */
   int32_t dense_reads;      /* LDS operand reads per column in the dense form (sparse: nnz) */
+  /* streamed form (stream_cs > 0, built by tal_round_plan_build_stream): a workgroup of
+   * stream_cs wavefronts owns a group of at most 8*stream_cs rows (one dense row block per
+   * wavefront) and streams the group's staged sources through a ring of LDS chunks of
+   * stream_cs sources x 64 float4 columns (one global->LDS DMA per wavefront per chunk), so a
+   * group's source count is not bounded by LDS.  Each block's table lists its entries chunk by
+   * chunk, every chunk's run padded to a multiple of 4 with mask-0 entries. */
+  int32_t stream_cs;        /* sources per chunk = wavefronts per workgroup (8 or 16); 0 = LDS-resident groups */
 } tal_round_plan_info;
 
 /* Blob size in int32 words of the sparse form for `rows` rows / `nnz` operands (an upper
@@ -128,6 +137,17 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
                              const double* w_host, const int32_t* out_row_host, int32_t c4,
                              int32_t lds_bytes, int32_t dense_rb, int32_t* plan_host,
                              int64_t plan_capacity_words, tal_round_plan_info* info);
+
+/* Streamed plan (see stream_cs above).  Rows keep their order; consecutive rows share a group
+ * while the group has at most max_group_rows rows (<= 128) and, if max_group_src > 0, at
+ * most max_group_src distinct sources.  Every row must list its operands in reference order
+ * (ascending distinct sources, then its own model, which does not occur before): otherwise
+ * TAL_ERR_INVALID.  c4 is 64.  TAL_ERR_CAPACITY as for tal_round_plan_build. */
+int32_t tal_round_plan_build_stream(int32_t rows, const int32_t* row_ptr_host,
+                                    const int32_t* col_host, const double* w_host,
+                                    const int32_t* out_row_host, int32_t max_group_rows,
+                                    int32_t max_group_src, int32_t* plan_host,
+                                    int64_t plan_capacity_words, tal_round_plan_info* info);
 
 /* Execute the round on the fp32 segment (n elements per model; row stride ld_in / ld_out in
  * elements).  plan_dev = the blob copied to the device.  pool_out may equal pool_in only if

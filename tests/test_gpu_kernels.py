@@ -161,6 +161,92 @@ def test_round_f32_vs_oracle(cuda, graph, n, c4, lds, dense):
         assert _bits_equal(pin.cpu().numpy(), ref)
 
 
+_STREAM_GRAPHS = {
+    "ring": lambda: nx.cycle_graph(16),
+    "regular": lambda: nx.random_regular_graph(8, 64, seed=0),
+    "barbell": lambda: nx.barbell_graph(30, 4),
+    "complete40": lambda: nx.complete_graph(40),
+    "complete100": lambda: nx.complete_graph(100),
+    "gnp": lambda: nx.gnp_random_graph(150, 0.08, seed=2),
+}
+
+
+@pytest.mark.parametrize("grouping", [(64, 0), (128, 0), (16, 24)])
+@pytest.mark.parametrize("n", [4099, 70001])
+@pytest.mark.parametrize("graph", list(_STREAM_GRAPHS))
+def test_round_stream_vs_oracle(cuda, graph, n, grouping):
+    g = _STREAM_GRAPHS[graph]()
+    orders, ws = _graph_csr(g, "softmax" if graph in ("regular", "gnp") else "unweighted")
+    rows = len(orders)
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    out_rows = np.random.default_rng(rows).permutation(rows).astype(np.int32)
+    rng = np.random.default_rng(rows + n)
+    pool = np.stack([_rand_f32(rng, n, special=(rows % 3 == 0)) for _ in range(rows)])
+    ref = oracle.round_f32(pool, row_ptr, col, w, out_rows)
+    plan = ops.build_stream_plan(row_ptr, col, w, out_rows, *grouping)
+    assert plan.info.stream_cs in (8, 16) and ops.round_kernel_name(plan.info) == "k_round_stream"
+    pin = torch.from_numpy(pool).to(cuda)
+    pout = torch.zeros_like(pin)
+    ops.round_f32(pin, pout, plan)
+    assert _bits_equal(pout.cpu().numpy(), ref)
+    if plan.single_group:
+        ops.round_f32(pin, pin, plan)
+        assert _bits_equal(pin.cpu().numpy(), ref)
+
+
+def test_round_stream_large_and_fma(cuda):
+    g = nx.barbell_graph(60, 8)
+    orders, ws = _graph_csr(g)
+    rows = len(orders)
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    out_rows = np.arange(rows, dtype=np.int32)
+    n = 1 << 20
+    rng = np.random.default_rng(11)
+    pool = rng.standard_normal((rows, n)).astype(np.float32)
+    plan = ops.build_stream_plan(row_ptr, col, w, out_rows, 64, 0)
+    pin = torch.from_numpy(pool).to(cuda)
+    pout = torch.zeros_like(pin)
+    ops.round_f32(pin, pout, plan)
+    ref = oracle.round_f32(pool, row_ptr, col, w, out_rows)
+    assert _bits_equal(pout.cpu().numpy(), ref)
+    ops.round_f32(pin, pout, plan, mode=ops.MODE_FMA)
+    m = max(len(o) for o in orders)
+    tol = m * 2.0 ** -24 * np.abs(pool).max() * 1.0 + 1e-30
+    assert np.max(np.abs(pout.cpu().numpy() - ref)) <= tol
+
+
+def test_round_stream_padded_ld_tail_unaligned_i64(cuda):
+    g = nx.barbell_graph(9, 2)
+    orders, ws = _graph_csr(g)
+    rows = len(orders)
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    out_rows = np.arange(rows, dtype=np.int32)[::-1].copy()
+    plan = ops.build_stream_plan(row_ptr, col, w, out_rows, 8, 0)
+    assert plan.info.n_groups > 1
+    n, ld = 1030, 1088
+    rng = np.random.default_rng(4)
+    pool = np.zeros((rows, ld), np.float32)
+    pool[:, :n] = rng.standard_normal((rows, n)).astype(np.float32)
+    ref = oracle.round_f32(pool[:, :n].copy(), row_ptr, col, w, out_rows)
+    pin = torch.from_numpy(pool).to(cuda)
+    pout = torch.full_like(pin, 7.0)
+    ops.round_f32(pin, pout, plan, n=n)
+    got = pout.cpu().numpy()
+    assert _bits_equal(got[:, :n], ref)
+    assert np.all(got[:, n:] == 7.0)
+    pin2 = torch.from_numpy(np.ascontiguousarray(pool[:, :n + 1])).to(cuda)  # odd ld: scalar path
+    pout2 = torch.zeros_like(pin2)
+    ops.round_f32(pin2, pout2, plan, n=n)
+    assert _bits_equal(pout2.cpu().numpy()[:, :n], ref)
+    ipool = rng.integers(0, 10 ** 6, size=(rows, 53)).astype(np.int64)
+    ipool[:, 0] = 1000
+    iref = oracle.round_i64(ipool, row_ptr, col, w, out_rows)
+    ipin = torch.from_numpy(ipool).to(cuda)
+    ipout = torch.zeros_like(ipin)
+    ops.round_i64(ipin, ipout, plan)
+    assert np.array_equal(ipout.cpu().numpy(), iref)
+
+
 def test_round_f32_padded_ld_and_tail(cuda):
     g = nx.random_regular_graph(4, 20, seed=1)
     orders, ws = _graph_csr(g)

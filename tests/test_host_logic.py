@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 import torch
 
+import oracle
 from oracle import reference_alg as ra
 from topology_aware_learning_amd import ops, synth
 from topology_aware_learning_amd import weights as W
@@ -235,6 +236,91 @@ def test_round_plan_reconstructs_csr():
         assert i.lds_bytes <= budget
         if budget == ops.LDS_BUDGET:
             assert i.n_groups == 1 and i.total_src == 64
+
+
+def _emulate_stream(plan, pool):
+    """The streamed kernel's walk (k_round_stream) in numpy fp32: chunk by chunk, batches of 4
+    table entries, own model captured when its chunk passes and added last."""
+    i, h = plan.info, plan.host
+    cs = i.stream_cs
+    grp_row = h[i.off_grp_row_ptr: i.off_grp_row_ptr + i.n_groups + 1]
+    grp_src = h[i.off_grp_src_ptr: i.off_grp_src_ptr + i.n_groups + 1]
+    src_row = h[i.off_src_row: i.off_src_row + i.total_src]
+    rp = h[i.off_row_ptr: i.off_row_ptr + i.rows + 1]
+    slot = h[i.off_op_slot: i.off_op_slot + i.nnz]
+    wf = h[i.off_op_w: i.off_op_w + i.nnz].view(np.float32)
+    out_row = h[i.off_out_row: i.off_out_row + i.rows]
+    blk_ptr = h[i.off_grp_blk_ptr: i.off_grp_blk_ptr + i.n_groups + 1]
+    tabs = h[i.off_blk_tab: i.off_blk_tab + i.n_blocks]
+    out = np.zeros_like(pool)
+    for gi in range(i.n_groups):
+        srcs = src_row[grp_src[gi]: grp_src[gi + 1]]
+        nch = (len(srcs) + cs - 1) // cs
+        for lb in range(blk_ptr[gi + 1] - blk_ptr[gi]):
+            t0 = tabs[blk_ptr[gi] + lb]
+            nu = h[t0]
+            e_slot = h[t0 + 8: t0 + 8 + nu]
+            e_mask = h[t0 + 8 + nu: t0 + 8 + 2 * nu]
+            e_w = h[t0 + 8 + 2 * nu: t0 + 8 + 2 * nu + 8 * nu].view(np.float32).reshape(nu, 8)
+            rows = [grp_row[gi] + lb * 8 + r for r in range(8) if grp_row[gi] + lb * 8 + r < grp_row[gi + 1]]
+            acc = np.full((8, pool.shape[1]), -0.0, np.float32)
+            e = 0
+            for k in range(nch):
+                lo, hi = k * cs, k * cs + cs
+                while e < nu:
+                    if e_slot[e] >= hi:
+                        break
+                    assert np.all((e_slot[e: e + 4] >= lo) & (e_slot[e: e + 4] < hi))  # one chunk per batch
+                    for u in range(4):
+                        x = pool[srcs[e_slot[e + u]]]
+                        for r in range(8):
+                            if e_mask[e + u] & (1 << r):
+                                acc[r] = acc[r] + np.float32(e_w[e + u, r]) * x
+                    e += 4
+            assert e == nu
+            for r, gr in enumerate(rows):
+                q = rp[gr + 1] - 1
+                out[out_row[gr]] = acc[r] + wf[q] * pool[srcs[slot[q]]]
+    return out
+
+
+@pytest.mark.parametrize("graph", ["clique", "barbell", "ring", "random"])
+def test_stream_plan_walk_matches_oracle(graph):
+    rng = np.random.default_rng(5)
+    if graph == "clique":
+        n_dev = 40
+        orders = [[j for j in range(n_dev) if j != i] + [i] for i in range(n_dev)]
+    elif graph == "barbell":
+        g = nx.barbell_graph(30, 3)
+        n_dev = g.number_of_nodes()
+        orders = [sorted(g.neighbors(i)) + [i] for i in range(n_dev)]
+    elif graph == "ring":
+        n_dev = 70
+        orders = [sorted({(i - 1) % n_dev, (i + 1) % n_dev}) + [i] for i in range(n_dev)]
+    else:
+        g = nx.gnp_random_graph(150, 0.1, seed=3)
+        n_dev = 150
+        orders = [sorted(g.neighbors(i)) + [i] for i in range(n_dev)]
+    ws = [[float(x) for x in rng.dirichlet(np.ones(len(o)))] for o in orders]
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    out_rows = np.arange(n_dev, dtype=np.int32)
+    pool = rng.standard_normal((n_dev, 7)).astype(np.float32)
+    pool[0, 0] = -0.0
+    ref = oracle.round_f32(pool, row_ptr, col, w, out_rows)
+    for max_rows, max_src in ((64, 0), (128, 0), (16, 0), (64, 24)):
+        plan = ops.build_stream_plan(row_ptr, col, w, out_rows, max_rows, max_src)
+        i = plan.info
+        assert i.stream_cs in (8, 16) and i.c4 == 64 and i.dense_rb == 8
+        assert i.max_rows <= min(max_rows, 8 * i.stream_cs)
+        got = _emulate_stream(plan, pool)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (graph, max_rows, max_src)
+
+
+def test_stream_plan_rejects_non_reference_order():
+    row_ptr = np.array([0, 3], np.int32)
+    col = np.array([2, 1, 0], np.int32)  # unsorted neighbors
+    with pytest.raises(Exception, match="reference order"):
+        ops.build_stream_plan(row_ptr, col, np.full(3, 1 / 3), np.zeros(1, np.int32))
 
 
 def test_round_plan_capacity_error():

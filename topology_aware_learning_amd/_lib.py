@@ -23,7 +23,7 @@ TAL_ERR_HIP = 2
 TAL_ERR_CAPACITY = 3
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 EXPORTED = (
     "tal_last_error",
@@ -32,6 +32,7 @@ EXPORTED = (
     "tal_agg_i64",
     "tal_round_plan_words",
     "tal_round_plan_build",
+    "tal_round_plan_build_stream",
     "tal_agg_round_f32",
     "tal_agg_round_i64",
     "tal_cosine_plan_words",
@@ -78,6 +79,7 @@ class RoundPlanInfo(ctypes.Structure):
         ("off_blk_tab", ctypes.c_int32),
         ("off_dense", ctypes.c_int32),
         ("dense_reads", ctypes.c_int32),
+        ("stream_cs", ctypes.c_int32),
     ]
 
 
@@ -98,6 +100,10 @@ _SIGS = {
     "tal_round_plan_build": (
         _I32,
         [_I32, _PI32, _PI32, _PD, _PI32, _I32, _I32, _I32, _PI32, _I64, ctypes.POINTER(RoundPlanInfo)],
+    ),
+    "tal_round_plan_build_stream": (
+        _I32,
+        [_I32, _PI32, _PI32, _PD, _PI32, _I32, _I32, _PI32, _I64, ctypes.POINTER(RoundPlanInfo)],
     ),
     "tal_agg_round_f32": (_I32, [_P, _I64, _P, _I64, _I64, _P, ctypes.POINTER(RoundPlanInfo), _I32, _P]),
     "tal_agg_round_i64": (_I32, [_P, _I64, _P, _I64, _I64, _P, ctypes.POINTER(RoundPlanInfo), _P]),

@@ -30,9 +30,10 @@
 
 namespace {
 
-constexpr int kAbiVersion = 3;
+constexpr int kAbiVersion = 4;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
+constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
 constexpr int kMaxGrid = 256 * 8; // 256 CUs x 8 resident 256-thread blocks
 constexpr int kK1Unroll = 2;     // float4 chunks per lane per K1 grid-stride step
 constexpr int kK1Grid = 4096;    // K1 grid cap (16 blocks per CU in flight)
@@ -82,6 +83,14 @@ template <bool EXACT>
 __device__ __forceinline__ float4 next4(float4 a, float w, float4 x) {
   return make_float4(next_term<EXACT>(a.x, w, x.x), next_term<EXACT>(a.y, w, x.y),
                      next_term<EXACT>(a.z, w, x.z), next_term<EXACT>(a.w, w, x.w));
+}
+
+__device__ __forceinline__ float4 mul4(float w, float4 x) {
+  return make_float4(__fmul_rn(w, x.x), __fmul_rn(w, x.y), __fmul_rn(w, x.z), __fmul_rn(w, x.w));
+}
+
+__device__ __forceinline__ float4 add4(float4 a, float4 p) {
+  return make_float4(__fadd_rn(a.x, p.x), __fadd_rn(a.y, p.y), __fadd_rn(a.z, p.z), __fadd_rn(a.w, p.w));
 }
 
 // fp32 accumulator -> int64 the way load_state_dict's copy_ does it on x86: truncation toward
@@ -486,6 +495,9 @@ __device__ __forceinline__ void emit_tile_dense(const float4* s_data, const Plan
 }
 
 constexpr int kDenseRb = 8;
+constexpr int kStreamDepth = 3;        // chunks in flight ahead of the one being read
+constexpr int kStreamMaxRows = 128;    // 16 wavefronts x one 8-row block
+constexpr size_t stream_lds_bytes(int cs) { return static_cast<size_t>(kStreamDepth + 1) * cs * 64 * 16; }
 
 // Persistent form (the fast path): each workgroup walks column tiles t, t+gridDim.x, ...;
 // every lane owns J fixed staging slots (source, column) and keeps the next tile's J float4
@@ -629,6 +641,235 @@ __global__ __launch_bounds__(kBlock) void k_round_tiled_scalar(const void* __res
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// K3, streamed form: sources pass through a ring of LDS chunks (global->LDS DMA), so a
+// group's source count is unbounded and the workgroup needs no staging registers.
+//
+// Workgroup = CS wavefronts = one group of <= 8*CS rows (wavefront w owns dense row block w).
+// Per column tile of 64 float4, the group's sources are consumed CS at a time: wavefront w
+// DMAs source k*CS+w of chunk k (64 lanes x 16 B = 1 KiB, lane-linear in LDS) into ring slot
+// (chunk index mod NBUF).  Chunks are prefetched kStreamDepth ahead across tile boundaries.
+// A row's operands are ascending sources then itself, so accumulating chunk by chunk keeps the
+// reference order; each row's own model is captured in registers when its chunk passes and
+// added last.  The DMA is issued from inline asm (hipcc would otherwise drain vmcnt before
+// every LDS read), so the kernel counts vmcnt itself: every VMEM op of a wavefront (DMA and
+// output stores) retires in issue order, and chunk q is resident once at most
+// (DMAs issued after it) + (stores issued after it) ops are outstanding.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_byte_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_byte_addr)
+      : "memory");
+}
+
+// s_waitcnt vmcnt(n) lgkmcnt(0) + s_barrier, n wave-uniform (clamped: waiting longer is safe)
+__device__ __forceinline__ void wait_vm_barrier(int n) {
+#define TAL_WB(k) case k: asm volatile("s_waitcnt vmcnt(" #k ") lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+  switch (n < 0 ? 0 : (n > 15 ? 15 : n)) {
+    TAL_WB(0) TAL_WB(1) TAL_WB(2) TAL_WB(3) TAL_WB(4) TAL_WB(5) TAL_WB(6) TAL_WB(7)
+    TAL_WB(8) TAL_WB(9) TAL_WB(10) TAL_WB(11) TAL_WB(12) TAL_WB(13) TAL_WB(14) TAL_WB(15)
+  }
+#undef TAL_WB
+}
+
+template <int NT, bool EXACT>
+__global__ __launch_bounds__(NT) void k_round_stream(const float* __restrict__ pin, int64_t ld_in4,
+                                                     float* __restrict__ pout, int64_t ld_out4,
+                                                     int64_t n4, PlanView p, int64_t n_tiles) {
+  constexpr int CS = NT / 64;
+  constexpr int P = kStreamDepth;
+  constexpr int NBUF = P + 1;
+  constexpr int RB = kDenseRb;
+  extern __shared__ float4 s_data[];
+  const int g = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const ConstI32 grp_src_ptr = (ConstI32)p.grp_src_ptr;
+  const ConstI32 grp_row_ptr = (ConstI32)p.grp_row_ptr;
+  const ConstI32 src_row = (ConstI32)p.src_row;
+  const int s_beg = grp_src_ptr[g];
+  const int ns = grp_src_ptr[g + 1] - s_beg;
+  const int r_beg = grp_row_ptr[g];
+  const int nr = grp_row_ptr[g + 1] - r_beg;
+  const int nch = (ns + CS - 1) / CS;
+  const int64_t bx = blockIdx.x, gx = gridDim.x;
+  const int64_t n_mine = bx < n_tiles ? (n_tiles - 1 - bx) / gx + 1 : 0;
+  const int64_t total = n_mine * nch;  // chunk steps of this workgroup
+  const float4* pin4 = reinterpret_cast<const float4*>(pin);
+  const uint32_t lds0 = static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)s_data));
+
+  // DMA cursor: (tile i, chunk k) of step qi
+  int64_t qi = 0, ii = 0;
+  int ik = 0;
+  auto issue = [&]() {
+    const int64_t t = bx + ii * gx;
+    const int s = min(ik * CS + wave, ns - 1);  // past the last source: a duplicate (L2 hit)
+    const int64_t row = src_row[s_beg + s];
+    const int64_t col = min(t * 64 + lane, n4 - 1);
+    dma16(pin4 + row * ld_in4 + col, lds0 + static_cast<uint32_t>(((qi % NBUF) * CS + wave) * 1024));
+    ++qi;
+    if (++ik == nch) { ik = 0; ++ii; }
+  };
+  for (int d = 0; d < P; ++d)
+    if (qi < total) issue();
+
+  // my row block
+  const int nblk = (nr + RB - 1) / RB;
+  const bool has_blk = wave < nblk;
+  const int rows_here = has_blk ? min(RB, nr - wave * RB) : 0;
+  const ConstI32 base = (ConstI32)p.base;
+  const ConstI32 tab = has_blk ? base + ((ConstI32)p.blk_tab)[((ConstI32)p.grp_blk_ptr)[g] + wave] : base;
+  const int n_used = has_blk ? tab[0] : 0;
+  const ConstI32x4 slots4 = (ConstI32x4)(tab + 8);
+  const ConstI32x4 masks4 = (ConstI32x4)(tab + 8 + n_used);
+  const ConstF32x8 wts8 = (ConstF32x8)(tab + 8 + 2 * n_used);
+  int self_slot[RB];
+  float self_w[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    self_slot[r] = -1;
+    self_w[r] = 0.f;
+    if (r < rows_here) {
+      const int q = ((ConstI32)p.row_ptr)[r_beg + wave * RB + r + 1] - 1;  // own model: last operand
+      self_slot[r] = ((ConstI32)p.op_slot)[q];
+      self_w[r] = ((ConstF32)p.op_w)[q];
+    }
+  }
+  float4 acc[RB], self_x[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    acc[r] = make_float4(-0.f, -0.f, -0.f, -0.f);
+    self_x[r] = acc[r];
+  }
+
+  int64_t ci = 0;   // compute cursor: tile i, chunk k
+  int ck = 0;
+  int e = 0;        // table cursor (entries of chunks < ck consumed)
+  uint32_t ends = 0;  // bit j: the step j+1 before this one ended a tile (issued stores)
+  for (int64_t q = 0; q < total; ++q) {
+    const int younger_dma = static_cast<int>(min<int64_t>(P - 1, total - 1 - q));
+    const int younger_st = rows_here * __builtin_popcount(ends & ((1u << P) - 1));
+    wait_vm_barrier(younger_dma + younger_st);  // chunk q resident; step q-1's readers done
+    if (qi < total) issue();                    // into the slot step q-1 read
+    if (has_blk) {
+      const float4* buf = s_data + (q % NBUF) * CS * 64 + lane;
+      const int lo = ck * CS, hi = lo + CS;
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+        if (self_slot[r] >= lo && self_slot[r] < hi) self_x[r] = buf[(self_slot[r] - lo) * 64];
+      for (; e < n_used; e += 4) {
+        const i32x4 sl = slots4[e >> 2];
+        if (sl.x >= hi) break;
+        const i32x4 mk = masks4[e >> 2];
+        float4 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = buf[(sl[u] - lo) * 64];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const f32x8 wv = wts8[e + u];
+          const uint32_t m = static_cast<uint32_t>(mk[u]);
+          if (EXACT && (m & kMaskUniform)) {  // one product serves every row
+            const float4 pr = x[u] = mul4(wv[0], x[u]);
+            if ((m & 0xffu) == 0xffu) {
+#pragma unroll
+              for (int r = 0; r < RB; ++r) acc[r] = add4(acc[r], pr);
+            } else {
+#pragma unroll
+              for (int r = 0; r < RB; ++r)
+                if (m & (1u << r)) acc[r] = add4(acc[r], pr);
+            }
+          } else if (m == (1u << RB) - 1) {  // cliques: every row of the block takes this source
+#pragma unroll
+            for (int r = 0; r < RB; ++r) acc[r] = next4<EXACT>(acc[r], wv[r], x[u]);
+          } else if (m) {
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+              if (m & (1u << r)) acc[r] = next4<EXACT>(acc[r], wv[r], x[u]);
+          }
+        }
+      }
+    }
+    ends <<= 1;
+    if (ck == nch - 1) {  // tile done: own model last, store, reset
+      if (has_blk) {
+        const int64_t col = (bx + ci * gx) * 64 + lane;
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          if (r < rows_here) {
+            acc[r] = next4<EXACT>(acc[r], self_w[r], self_x[r]);
+            const int64_t orow = ((ConstI32)p.out_row)[r_beg + wave * RB + r];
+            if (col < n4) st_stream(pout, orow * ld_out4 + col, acc[r]);
+            acc[r] = make_float4(-0.f, -0.f, -0.f, -0.f);
+          }
+        }
+      }
+      ends |= 1u;
+      ck = 0;
+      ++ci;
+      e = 0;
+    } else {
+      ++ck;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Tail / int64 columns of a streamed plan: per (column chunk, group) workgroup, the group's
+// sources' columns are staged in LDS (as fp32), then each thread computes (row, column) pairs
+// walking the row's operands in reference order from the plan in global memory.
+template <bool IS_I64, bool EXACT>
+__global__ __launch_bounds__(kBlock) void k_round_stream_scalar(const void* __restrict__ pin_v,
+                                                                int64_t ld_in,
+                                                                void* __restrict__ pout_v,
+                                                                int64_t ld_out, int64_t e0,
+                                                                int64_t n, PlanView p, int tc) {
+  extern __shared__ float s_f[];
+  const int g = blockIdx.y;
+  const int s_beg = p.grp_src_ptr[g];
+  const int ns = p.grp_src_ptr[g + 1] - s_beg;
+  const int r_beg = p.grp_row_ptr[g];
+  const int nr = p.grp_row_ptr[g + 1] - r_beg;
+  const int64_t t0 = e0 + static_cast<int64_t>(blockIdx.x) * tc;
+  const int cols = static_cast<int>(min(static_cast<int64_t>(tc), n - t0));
+  for (int k = threadIdx.x; k < ns * tc; k += kBlock) {
+    const int sidx = k / tc;
+    const int c = k % tc;
+    float v = 0.f;
+    if (c < cols) {
+      const int64_t row = p.src_row[s_beg + sidx];
+      if constexpr (IS_I64) {
+        v = static_cast<float>(static_cast<const int64_t*>(pin_v)[row * ld_in + t0 + c]);
+      } else {
+        v = static_cast<const float*>(pin_v)[row * ld_in + t0 + c];
+      }
+    }
+    s_f[k] = v;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < nr * cols; k += kBlock) {
+    const int r = k / cols;
+    const int c = k % cols;
+    const int gr = r_beg + r;
+    const int q0 = p.row_ptr[gr], q1 = p.row_ptr[gr + 1];
+    float acc = first_term<EXACT || IS_I64>(p.op_w[q0], s_f[p.op_slot[q0] * tc + c]);
+    for (int q = q0 + 1; q < q1; ++q) acc = next_term<EXACT || IS_I64>(acc, p.op_w[q], s_f[p.op_slot[q] * tc + c]);
+    const int64_t orow = p.out_row[gr];
+    if constexpr (IS_I64) {
+      static_cast<int64_t*>(pout_v)[orow * ld_out + t0 + c] = trunc_i64(acc);
+    } else {
+      static_cast<float*>(pout_v)[orow * ld_out + t0 + c] = acc;
+    }
+  }
+}
+
 size_t plan_lds_bytes(const tal_round_plan_info& in, int tile_bytes_per_src) {
   return static_cast<size_t>(in.max_src) * tile_bytes_per_src +
          static_cast<size_t>(in.max_rows + 1 + 2 * in.max_nnz + in.max_src + in.max_rows) * 4;
@@ -658,6 +899,11 @@ int32_t validate_info(const tal_round_plan_info* info) {
     return fail(TAL_ERR_INVALID, "plan c4 must be 64 or 128");
   if (info->dense_rb != 0 && info->dense_rb != kDenseRb)
     return fail(TAL_ERR_INVALID, "plan dense_rb must be 0 or 8");
+  if (info->stream_cs != 0 && (info->stream_cs != 8 && info->stream_cs != 16))
+    return fail(TAL_ERR_INVALID, "plan stream_cs must be 0, 8 or 16");
+  if (info->stream_cs != 0 && (info->c4 != 64 || info->dense_rb != kDenseRb ||
+                               info->max_rows > kDenseRb * info->stream_cs))
+    return fail(TAL_ERR_INVALID, "streamed plan: c4 64, dense row blocks, <= 8 rows per wavefront");
   return TAL_OK;
 }
 
@@ -699,6 +945,55 @@ int32_t launch_round_persistent(const float* pin, int64_t ld_in, float* pout, in
   const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(in.n_groups));
   k<<<grid, kRoundThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles);
   return check_launch("round kernel (persistent)");
+}
+
+template <int NT, bool EXACT>
+int32_t launch_round_stream_nt(const float* pin, int64_t ld_in, float* pout, int64_t ld_out, int64_t n4,
+                               const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
+  auto k = k_round_stream<NT, EXACT>;
+  const size_t lds = stream_lds_bytes(NT / 64);
+  int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
+  if (rc) return rc;
+  static int per_cu = 0;  // resident workgroups per CU (registers / LDS), asked once
+  if (per_cu == 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(k), NT, lds) != hipSuccess)
+      nb = 1;
+    per_cu = std::max(1, nb);
+  }
+  const int64_t tiles = (n4 + 63) / 64;
+  int64_t gx = std::max<int64_t>(1, 256LL * per_cu / in.n_groups);
+  gx = std::min<int64_t>(gx, tiles);
+  const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(in.n_groups));
+  k<<<grid, NT, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles);
+  return check_launch("round kernel (streamed)");
+}
+
+int32_t launch_round_stream(const float* pin, int64_t ld_in, float* pout, int64_t ld_out, int64_t n4,
+                            const PlanView& v, const tal_round_plan_info& in, bool exact, hipStream_t s) {
+  if (in.stream_cs == 8)
+    return exact ? launch_round_stream_nt<512, true>(pin, ld_in, pout, ld_out, n4, v, in, s)
+                 : launch_round_stream_nt<512, false>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  return exact ? launch_round_stream_nt<1024, true>(pin, ld_in, pout, ld_out, n4, v, in, s)
+               : launch_round_stream_nt<1024, false>(pin, ld_in, pout, ld_out, n4, v, in, s);
+}
+
+template <bool IS_I64>
+int32_t launch_round_stream_scalar(const void* pin, int64_t ld_in, void* pout, int64_t ld_out, int64_t e0,
+                                   int64_t n, const PlanView& v, const tal_round_plan_info& in, bool exact,
+                                   hipStream_t s) {
+  if (n <= e0) return TAL_OK;
+  const int64_t tc = std::max<int64_t>(1, std::min<int64_t>(64, (160 * 1024) / (4LL * in.max_src)));
+  if (in.max_src > 160 * 1024 / 4) return fail(TAL_ERR_CAPACITY, "streamed plan: group too large for the tail kernel");
+  const size_t lds = static_cast<size_t>(in.max_src) * tc * 4;
+  const int64_t tiles = (n - e0 + tc - 1) / tc;
+  if (tiles > 0x7fffffff) return fail(TAL_ERR_INVALID, "too many tiles");
+  auto k = (IS_I64 || exact) ? k_round_stream_scalar<IS_I64, true> : k_round_stream_scalar<IS_I64, false>;
+  int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
+  if (rc) return rc;
+  const dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(in.n_groups));
+  k<<<grid, kBlock, lds, s>>>(pin, ld_in, pout, ld_out, e0, n, v, static_cast<int>(tc));
+  return check_launch("round scalar kernel (streamed plan)");
 }
 
 template <int C4, bool EXACT, bool DENSE>
@@ -860,6 +1155,267 @@ __global__ void k_cosine_finish(const int64_t* __restrict__ plan, int n_seg, int
 // ==========================================================================================
 // C-ABI
 // ==========================================================================================
+namespace {
+
+// Row groups: consecutive rows and the union of their sources (ascending pool rows after
+// finish_plan sorts them).
+struct Groups {
+  std::vector<int32_t> row_ptr{0};
+  std::vector<std::vector<int32_t>> srcs;
+};
+
+int32_t check_csr(const char* fn, int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host,
+                  const double* w_host, const int32_t* out_row_host, int32_t* max_col) {
+  if (rows <= 0 || !row_ptr_host || !col_host || !w_host || !out_row_host)
+    return fail(TAL_ERR_INVALID, std::string(fn) + ": bad arguments");
+  if (row_ptr_host[0] != 0) return fail(TAL_ERR_INVALID, std::string(fn) + ": row_ptr[0] != 0");
+  for (int r = 0; r < rows; ++r)
+    if (row_ptr_host[r + 1] <= row_ptr_host[r])
+      return fail(TAL_ERR_INVALID, std::string(fn) + ": every row needs >= 1 operand");
+  const int64_t nnz = row_ptr_host[rows];
+  *max_col = 0;
+  for (int64_t k = 0; k < nnz; ++k) {
+    if (col_host[k] < 0) return fail(TAL_ERR_INVALID, std::string(fn) + ": negative source row");
+    *max_col = std::max(*max_col, col_host[k]);
+  }
+  return TAL_OK;
+}
+
+// Reference operand order (decentralized_app.py:618-625): ascending distinct neighbors, then
+// the row's own model, which does not occur among them.
+bool reference_order(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host) {
+  for (int r = 0; r < rows; ++r) {
+    const int32_t k0 = row_ptr_host[r], k1 = row_ptr_host[r + 1];
+    for (int32_t k = k0 + 1; k < k1 - 1; ++k)
+      if (col_host[k] <= col_host[k - 1]) return false;
+    for (int32_t k = k0; k < k1 - 1; ++k)
+      if (col_host[k] == col_host[k1 - 1]) return false;
+  }
+  return true;
+}
+
+// Greedy grouping: a row joins the current group unless that breaks `fits(n_src, n_rows, n_ops)`.
+template <class Fits>
+int32_t group_rows(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host, int32_t max_col,
+                   Fits fits, Groups* out) {
+  std::vector<int32_t> seen(static_cast<size_t>(max_col) + 1, -1);  // source -> group that has it
+  Groups& G = *out;
+  G.srcs.assign(1, {});
+  int64_t cur_nnz = 0;
+  auto fresh_of = [&](int r, int g, std::vector<int32_t>* fresh) {
+    fresh->clear();
+    for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1]; ++k) {
+      const int32_t sr = col_host[k];
+      if (seen[sr] != g && std::find(fresh->begin(), fresh->end(), sr) == fresh->end()) fresh->push_back(sr);
+    }
+  };
+  std::vector<int32_t> fresh;
+  for (int r = 0; r < rows; ++r) {
+    int g = static_cast<int>(G.srcs.size()) - 1;
+    fresh_of(r, g, &fresh);
+    const int64_t row_nnz = row_ptr_host[r + 1] - row_ptr_host[r];
+    const int64_t cur_rows = r - G.row_ptr.back();
+    if (!fits(static_cast<int64_t>(G.srcs[g].size() + fresh.size()), cur_rows + 1, cur_nnz + row_nnz)) {
+      if (cur_rows > 0) {
+        G.row_ptr.push_back(r);
+        G.srcs.emplace_back();
+        cur_nnz = 0;
+        g = static_cast<int>(G.srcs.size()) - 1;
+        fresh_of(r, g, &fresh);
+      }
+      if (!fits(static_cast<int64_t>(fresh.size()), 1, row_nnz))
+        return fail(TAL_ERR_CAPACITY, "tal_round_plan_build: row " + std::to_string(r) +
+                                          " has more distinct sources than one LDS tile holds");
+    }
+    for (int32_t sr : fresh) {
+      seen[sr] = g;
+      G.srcs[g].push_back(sr);
+    }
+    cur_nnz += row_nnz;
+  }
+  G.row_ptr.push_back(rows);
+  return TAL_OK;
+}
+
+// Lay the plan blob out (see tal_round_plan_info).  rb = dense row-block size (0 = sparse
+// form only, -1 = dense when it saves LDS reads); stream_cs > 0 pads each block's entries
+// chunk by chunk for the streamed kernel.
+int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host,
+                    const double* w_host, const int32_t* out_row_host, int32_t max_col,
+                    Groups& grp, int32_t c4, int32_t dense_rb, int32_t stream_cs,
+                    int32_t* plan_host, int64_t plan_capacity_words, tal_round_plan_info* info) {
+  const int64_t nnz = row_ptr_host[rows];
+  const int32_t G = static_cast<int32_t>(grp.srcs.size());
+  const std::vector<int32_t>& grp_row_ptr = grp.row_ptr;
+
+  // staged sources of a group in ascending pool-row order; operand slots
+  std::vector<int32_t> grp_src_ptr{0}, src_row, slot(nnz);
+  std::vector<int32_t> map(static_cast<size_t>(max_col) + 1, -1);
+  int32_t max_src = 0, max_rows = 0, max_nnz = 0;
+  for (int g = 0; g < G; ++g) {
+    std::vector<int32_t>& ss = grp.srcs[g];
+    std::sort(ss.begin(), ss.end());
+    for (size_t i = 0; i < ss.size(); ++i) map[ss[i]] = static_cast<int32_t>(i);
+    for (int r = grp_row_ptr[g]; r < grp_row_ptr[g + 1]; ++r)
+      for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1]; ++k) slot[k] = map[col_host[k]];
+    src_row.insert(src_row.end(), ss.begin(), ss.end());
+    grp_src_ptr.push_back(static_cast<int32_t>(src_row.size()));
+    max_src = std::max<int32_t>(max_src, static_cast<int32_t>(ss.size()));
+    max_rows = std::max<int32_t>(max_rows, grp_row_ptr[g + 1] - grp_row_ptr[g]);
+    max_nnz = std::max<int32_t>(max_nnz, row_ptr_host[grp_row_ptr[g + 1]] - row_ptr_host[grp_row_ptr[g]]);
+  }
+
+  // dense row blocks need reference order; per block of kDenseRb rows, one LDS read per
+  // table entry (distinct non-self source the block uses, padded) plus one per row for its
+  // own model
+  bool dense_ok = dense_rb != 0 && reference_order(rows, row_ptr_host, col_host);
+  std::vector<std::vector<int32_t>> blk_used;  // per block: table slots (padded), ascending
+  int64_t dense_reads = 0;
+  if (dense_ok) {
+    for (int g = 0; g < G; ++g) {
+      for (int r0 = grp_row_ptr[g]; r0 < grp_row_ptr[g + 1]; r0 += kDenseRb) {
+        std::vector<int32_t> used;
+        const int r1 = std::min(r0 + kDenseRb, grp_row_ptr[g + 1]);
+        for (int r = r0; r < r1; ++r)
+          for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1] - 1; ++k) used.push_back(slot[k]);
+        std::sort(used.begin(), used.end());
+        used.erase(std::unique(used.begin(), used.end()), used.end());
+        std::vector<int32_t> tab;
+        if (stream_cs > 0) {  // each chunk's run starts on a multiple of 4 entries
+          for (size_t i = 0; i < used.size();) {
+            const int32_t chunk = used[i] / stream_cs;
+            const int32_t first = used[i];
+            while (i < used.size() && used[i] / stream_cs == chunk) tab.push_back(used[i++]);
+            while (tab.size() % 4) tab.push_back(first);  // a repeated slot marks padding (mask 0)
+          }
+        } else {
+          tab = used;
+          while (tab.size() % 4) tab.push_back(-1);
+        }
+        dense_reads += static_cast<int64_t>(stream_cs > 0 ? tab.size() : used.size()) + (r1 - r0);
+        blk_used.push_back(std::move(tab));
+      }
+    }
+    if (dense_rb == -1) dense_ok = dense_reads * 4 <= nnz * 3;
+  }
+  if (stream_cs > 0 && !dense_ok)
+    return fail(TAL_ERR_INVALID, "tal_round_plan_build_stream: rows must list operands in reference order");
+  const int32_t rb = dense_ok ? kDenseRb : 0;
+  std::vector<int32_t> grp_blk_ptr{0};
+  int64_t dense_words = 0;
+  if (rb) {
+    for (int g = 0; g < G; ++g)
+      grp_blk_ptr.push_back(grp_blk_ptr.back() + (grp_row_ptr[g + 1] - grp_row_ptr[g] + rb - 1) / rb);
+    for (const auto& u : blk_used) dense_words += 8 + static_cast<int64_t>(u.size()) * (rb + 2);
+  }
+  const int32_t n_blocks = rb ? grp_blk_ptr.back() : 0;
+
+  tal_round_plan_info in;
+  memset(&in, 0, sizeof(in));
+  in.rows = rows;
+  in.nnz = static_cast<int32_t>(nnz);
+  in.n_groups = G;
+  in.total_src = static_cast<int32_t>(src_row.size());
+  in.max_src = max_src;
+  in.max_rows = max_rows;
+  in.max_nnz = max_nnz;
+  in.c4 = c4;
+  in.dense_rb = rb;
+  in.n_blocks = n_blocks;
+  in.dense_reads = static_cast<int32_t>(rb ? dense_reads : nnz);
+  in.stream_cs = stream_cs;
+  int64_t off = 0;
+  in.off_grp_row_ptr = static_cast<int32_t>(off); off += G + 1;
+  in.off_grp_src_ptr = static_cast<int32_t>(off); off += G + 1;
+  in.off_src_row = static_cast<int32_t>(off); off += in.total_src;
+  in.off_row_ptr = static_cast<int32_t>(off); off += rows + 1;
+  in.off_op_slot = static_cast<int32_t>(off); off += nnz;
+  in.off_op_w = static_cast<int32_t>(off); off += nnz;
+  in.off_out_row = static_cast<int32_t>(off); off += rows;
+  in.off_grp_blk_ptr = static_cast<int32_t>(off); off += rb ? G + 1 : 0;
+  in.off_blk_tab = static_cast<int32_t>(off); off += n_blocks;
+  off = (off + 7) / 8 * 8;  // dense tables 32-B aligned (vector scalar loads)
+  in.off_dense = static_cast<int32_t>(off); off += dense_words;
+  if (off > 0x7fffffff) return fail(TAL_ERR_INVALID, "tal_round_plan_build: plan larger than 2^31 words");
+  in.words = static_cast<int32_t>(off);
+  in.lds_bytes = static_cast<int32_t>(stream_cs > 0 ? stream_lds_bytes(stream_cs) : plan_lds_bytes(in, 16 * c4));
+  if (!plan_host || off > plan_capacity_words) {
+    *info = in;
+    return fail(TAL_ERR_CAPACITY, "tal_round_plan_build: plan buffer too small: need " +
+                                      std::to_string(off) + " words");
+  }
+
+  memcpy(plan_host + in.off_grp_row_ptr, grp_row_ptr.data(), 4 * (G + 1));
+  memcpy(plan_host + in.off_grp_src_ptr, grp_src_ptr.data(), 4 * (G + 1));
+  memcpy(plan_host + in.off_src_row, src_row.data(), 4 * src_row.size());
+  memcpy(plan_host + in.off_row_ptr, row_ptr_host, 4 * (static_cast<size_t>(rows) + 1));
+  memcpy(plan_host + in.off_op_slot, slot.data(), 4 * nnz);
+  for (int64_t k = 0; k < nnz; ++k) {
+    const float wf = static_cast<float>(w_host[k]);
+    memcpy(plan_host + in.off_op_w + k, &wf, 4);
+  }
+  memcpy(plan_host + in.off_out_row, out_row_host, 4 * static_cast<size_t>(rows));
+  if (rb) {
+    memcpy(plan_host + in.off_grp_blk_ptr, grp_blk_ptr.data(), 4 * (G + 1));
+    int64_t pos = in.off_dense;
+    int b = 0;
+    for (int g = 0; g < G; ++g) {
+      for (int r0 = grp_row_ptr[g]; r0 < grp_row_ptr[g + 1]; r0 += rb, ++b) {
+        const std::vector<int32_t>& tabs = blk_used[b];
+        const int64_t nu = static_cast<int64_t>(tabs.size());  // multiple of 4
+        plan_host[in.off_blk_tab + b] = static_cast<int32_t>(pos);
+        int32_t* tab = plan_host + pos;
+        const int64_t words = 8 + nu * (rb + 2);  // multiple of 8: the next table stays aligned
+        memset(tab, 0, 4 * static_cast<size_t>(words));
+        tab[0] = static_cast<int32_t>(nu);
+        int32_t* t_slot = tab + 8;
+        int32_t* t_mask = t_slot + nu;
+        int32_t* t_w = t_mask + nu;
+        // real entries ascend strictly; padding repeats an earlier slot (or is -1: repeat the last)
+        std::vector<int64_t> entry_of;  // parallel to the sorted distinct slots
+        std::vector<int32_t> distinct;
+        for (int64_t e = 0; e < nu; ++e) {
+          const int32_t sl = tabs[e];
+          const bool pad = sl < 0 || (!distinct.empty() && sl <= distinct.back());  // real slots ascend
+          t_slot[e] = sl < 0 ? (e > 0 ? t_slot[e - 1] : 0) : sl;
+          if (!pad) {
+            distinct.push_back(sl);
+            entry_of.push_back(e);
+          }
+        }
+        std::vector<uint32_t> wbits(static_cast<size_t>(nu), 0);
+        std::vector<uint8_t> uniform(static_cast<size_t>(nu), 1);
+        for (int r = r0; r < std::min(r0 + rb, grp_row_ptr[g + 1]); ++r) {
+          for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1] - 1; ++k) {  // self excluded
+            const int64_t d = std::lower_bound(distinct.begin(), distinct.end(), slot[k]) - distinct.begin();
+            const int64_t e = entry_of[d];
+            const float wf = static_cast<float>(w_host[k]);
+            uint32_t wb;
+            memcpy(&wb, &wf, 4);
+            if (t_mask[e] != 0 && wb != wbits[e]) uniform[e] = 0;
+            wbits[e] = wb;
+            t_mask[e] |= static_cast<int32_t>(1u << (r - r0));
+            memcpy(t_w + e * rb + (r - r0), &wf, 4);
+          }
+        }
+        // every row using the entry has the same fp32 weight: one product w*x serves them all
+        // (identical operands round identically); the weight then fills all rb slots
+        for (int64_t e = 0; e < nu; ++e) {
+          if (t_mask[e] == 0 || !uniform[e] || __builtin_popcount(static_cast<uint32_t>(t_mask[e])) < 2) continue;
+          t_mask[e] = static_cast<int32_t>(static_cast<uint32_t>(t_mask[e]) | kMaskUniform);
+          for (int r = 0; r < rb; ++r) memcpy(t_w + e * rb + r, &wbits[e], 4);
+        }
+        pos += words;
+      }
+    }
+  }
+  *info = in;
+  g_err.clear();
+  return TAL_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 const char* tal_last_error(void) { return g_err.c_str(); }
@@ -925,204 +1481,58 @@ int64_t tal_round_plan_words(int32_t rows, int64_t nnz) {
   return 2 * (static_cast<int64_t>(rows) + 1) + nnz + (rows + 1) + 2 * nnz + rows + 16;
 }
 
+
 int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host,
                              const double* w_host, const int32_t* out_row_host, int32_t c4,
                              int32_t lds_bytes, int32_t dense_rb, int32_t* plan_host,
                              int64_t plan_capacity_words, tal_round_plan_info* info) {
-  if (rows <= 0 || !row_ptr_host || !col_host || !w_host || !out_row_host || !info)
-    return fail(TAL_ERR_INVALID, "tal_round_plan_build: bad arguments");
+  if (!info) return fail(TAL_ERR_INVALID, "tal_round_plan_build: bad arguments");
+  int32_t max_col = 0;
+  int32_t rc = check_csr("tal_round_plan_build", rows, row_ptr_host, col_host, w_host, out_row_host, &max_col);
+  if (rc) return rc;
   if (c4 != 64 && c4 != 128)
     return fail(TAL_ERR_INVALID, "tal_round_plan_build: c4 must be 64 or 128");
   if (dense_rb != 0 && dense_rb != kDenseRb && dense_rb != -1)
     return fail(TAL_ERR_INVALID, "tal_round_plan_build: dense_rb must be 0, 8 or -1");
-  if (row_ptr_host[0] != 0) return fail(TAL_ERR_INVALID, "tal_round_plan_build: row_ptr[0] != 0");
-  for (int r = 0; r < rows; ++r)
-    if (row_ptr_host[r + 1] <= row_ptr_host[r])
-      return fail(TAL_ERR_INVALID, "tal_round_plan_build: every row needs >= 1 operand");
-  const int64_t nnz = row_ptr_host[rows];
-  for (int64_t k = 0; k < nnz; ++k)
-    if (col_host[k] < 0) return fail(TAL_ERR_INVALID, "tal_round_plan_build: negative source row");
-
-  // 1. group consecutive rows while the union of their sources fits the LDS budget
-  //    (both round kernels stage 16*c4 bytes per source; the scalar one also the plan slice)
+  // group consecutive rows while the union of their sources fits the LDS budget (both round
+  // kernels stage 16*c4 bytes per source; the scalar one also the plan slice)
   const int64_t per_src = 16LL * c4;
-  auto need = [&](int64_t ns, int64_t nr, int64_t no) {
-    return ns * per_src + (nr + 1 + 2 * no + ns + nr) * 4;
+  auto fits = [&](int64_t ns, int64_t nr, int64_t no) {
+    return ns * per_src + (nr + 1 + 2 * no + ns + nr) * 4 <= lds_bytes;
   };
+  Groups grp;
+  rc = group_rows(rows, row_ptr_host, col_host, max_col, fits, &grp);
+  if (rc) return rc;
+  return finish_plan(rows, row_ptr_host, col_host, w_host, out_row_host, max_col, grp, c4, dense_rb, 0,
+                     plan_host, plan_capacity_words, info);
+}
+
+int32_t tal_round_plan_build_stream(int32_t rows, const int32_t* row_ptr_host,
+                                    const int32_t* col_host, const double* w_host,
+                                    const int32_t* out_row_host, int32_t max_group_rows,
+                                    int32_t max_group_src, int32_t* plan_host,
+                                    int64_t plan_capacity_words, tal_round_plan_info* info) {
+  if (!info) return fail(TAL_ERR_INVALID, "tal_round_plan_build_stream: bad arguments");
   int32_t max_col = 0;
-  for (int64_t k = 0; k < nnz; ++k) max_col = std::max(max_col, col_host[k]);
-  std::vector<int32_t> seen(static_cast<size_t>(max_col) + 1, -1);  // source -> group id that has it
-  std::vector<int32_t> grp_row_ptr{0};
-  std::vector<std::vector<int32_t>> grp_srcs(1);
-  int64_t cur_nnz = 0;
-  for (int r = 0; r < rows; ++r) {
-    const int g = static_cast<int>(grp_srcs.size()) - 1;
-    std::vector<int32_t> fresh;
-    for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1]; ++k) {
-      const int32_t sr = col_host[k];
-      if (seen[sr] != g && std::find(fresh.begin(), fresh.end(), sr) == fresh.end()) fresh.push_back(sr);
-    }
-    const int64_t row_nnz = row_ptr_host[r + 1] - row_ptr_host[r];
-    const int64_t cur_rows = r - grp_row_ptr.back();
-    if (cur_rows > 0 &&
-        need(static_cast<int64_t>(grp_srcs[g].size() + fresh.size()), cur_rows + 1, cur_nnz + row_nnz) > lds_bytes) {
-      grp_row_ptr.push_back(r);
-      grp_srcs.emplace_back();
-      cur_nnz = 0;
-      const int g2 = static_cast<int>(grp_srcs.size()) - 1;
-      fresh.clear();
-      for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1]; ++k) {
-        const int32_t sr = col_host[k];
-        if (seen[sr] != g2 && std::find(fresh.begin(), fresh.end(), sr) == fresh.end()) fresh.push_back(sr);
-      }
-      if (need(static_cast<int64_t>(fresh.size()), 1, row_nnz) > lds_bytes)
-        return fail(TAL_ERR_CAPACITY, "tal_round_plan_build: row " + std::to_string(r) +
-                                          " has more distinct sources than one LDS tile holds");
-    } else if (need(static_cast<int64_t>(grp_srcs[g].size() + fresh.size()), cur_rows + 1, cur_nnz + row_nnz) >
-               lds_bytes) {
-      return fail(TAL_ERR_CAPACITY, "tal_round_plan_build: row " + std::to_string(r) +
-                                        " has more distinct sources than one LDS tile holds");
-    }
-    const int gg = static_cast<int>(grp_srcs.size()) - 1;
-    for (int32_t sr : fresh) {
-      seen[sr] = gg;
-      grp_srcs[gg].push_back(sr);
-    }
-    cur_nnz += row_nnz;
-  }
-  grp_row_ptr.push_back(rows);
-  const int32_t G = static_cast<int32_t>(grp_srcs.size());
-
-  // 2. staged sources of a group in ascending pool-row order; operand slots
-  std::vector<int32_t> grp_src_ptr{0}, src_row, slot(nnz);
-  std::vector<int32_t> map(static_cast<size_t>(max_col) + 1, -1);
-  int32_t max_src = 0, max_rows = 0, max_nnz = 0;
-  for (int g = 0; g < G; ++g) {
-    std::vector<int32_t>& ss = grp_srcs[g];
-    std::sort(ss.begin(), ss.end());
-    for (size_t i = 0; i < ss.size(); ++i) map[ss[i]] = static_cast<int32_t>(i);
-    for (int r = grp_row_ptr[g]; r < grp_row_ptr[g + 1]; ++r)
-      for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1]; ++k) slot[k] = map[col_host[k]];
-    src_row.insert(src_row.end(), ss.begin(), ss.end());
-    grp_src_ptr.push_back(static_cast<int32_t>(src_row.size()));
-    max_src = std::max<int32_t>(max_src, static_cast<int32_t>(ss.size()));
-    max_rows = std::max<int32_t>(max_rows, grp_row_ptr[g + 1] - grp_row_ptr[g]);
-    max_nnz = std::max<int32_t>(max_nnz, row_ptr_host[grp_row_ptr[g + 1]] - row_ptr_host[grp_row_ptr[g]]);
-  }
-
-  // 3. dense row blocks: valid when every row's operands are strictly ascending sources followed
-  //    by one more (its own model) that does not occur before it
-  bool dense_ok = dense_rb != 0;
-  for (int r = 0; r < rows && dense_ok; ++r) {
-    const int32_t k0 = row_ptr_host[r], k1 = row_ptr_host[r + 1];
-    for (int32_t k = k0 + 1; k < k1 - 1 && dense_ok; ++k) dense_ok = col_host[k] > col_host[k - 1];
-    for (int32_t k = k0; k < k1 - 1 && dense_ok; ++k) dense_ok = col_host[k] != col_host[k1 - 1];
-  }
-  // dense walk: per block of kDenseRb rows, one LDS read per distinct (non-self) source the
-  // block uses plus one per row for its own model
-  std::vector<std::vector<int32_t>> blk_used;  // per block: used slots, ascending
-  int64_t dense_reads = 0;
-  if (dense_ok) {
-    for (int g = 0; g < G; ++g) {
-      for (int r0 = grp_row_ptr[g]; r0 < grp_row_ptr[g + 1]; r0 += kDenseRb) {
-        std::vector<int32_t> used;
-        const int r1 = std::min(r0 + kDenseRb, grp_row_ptr[g + 1]);
-        for (int r = r0; r < r1; ++r)
-          for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1] - 1; ++k) used.push_back(slot[k]);
-        std::sort(used.begin(), used.end());
-        used.erase(std::unique(used.begin(), used.end()), used.end());
-        dense_reads += static_cast<int64_t>(used.size()) + (r1 - r0);
-        blk_used.push_back(std::move(used));
-      }
-    }
-    if (dense_rb == -1) dense_ok = dense_reads * 4 <= nnz * 3;
-  }
-  const int32_t rb = dense_ok ? kDenseRb : 0;
-  std::vector<int32_t> grp_blk_ptr{0};
-  int64_t dense_words = 0;
-  if (rb) {
-    for (int g = 0; g < G; ++g)
-      grp_blk_ptr.push_back(grp_blk_ptr.back() + (grp_row_ptr[g + 1] - grp_row_ptr[g] + rb - 1) / rb);
-    for (const auto& u : blk_used) dense_words += 8 + ((static_cast<int64_t>(u.size()) + 3) / 4 * 4) * (rb + 2);
-  }
-  const int32_t n_blocks = rb ? grp_blk_ptr.back() : 0;
-
-  tal_round_plan_info in;
-  memset(&in, 0, sizeof(in));
-  in.rows = rows;
-  in.nnz = static_cast<int32_t>(nnz);
-  in.n_groups = G;
-  in.total_src = static_cast<int32_t>(src_row.size());
-  in.max_src = max_src;
-  in.max_rows = max_rows;
-  in.max_nnz = max_nnz;
-  in.c4 = c4;
-  in.dense_rb = rb;
-  in.n_blocks = n_blocks;
-  in.dense_reads = static_cast<int32_t>(rb ? dense_reads : nnz);
-  int64_t off = 0;
-  in.off_grp_row_ptr = static_cast<int32_t>(off); off += G + 1;
-  in.off_grp_src_ptr = static_cast<int32_t>(off); off += G + 1;
-  in.off_src_row = static_cast<int32_t>(off); off += in.total_src;
-  in.off_row_ptr = static_cast<int32_t>(off); off += rows + 1;
-  in.off_op_slot = static_cast<int32_t>(off); off += nnz;
-  in.off_op_w = static_cast<int32_t>(off); off += nnz;
-  in.off_out_row = static_cast<int32_t>(off); off += rows;
-  in.off_grp_blk_ptr = static_cast<int32_t>(off); off += rb ? G + 1 : 0;
-  in.off_blk_tab = static_cast<int32_t>(off); off += n_blocks;
-  off = (off + 7) / 8 * 8;  // dense tables 32-B aligned (vector scalar loads)
-  in.off_dense = static_cast<int32_t>(off); off += dense_words;
-  if (off > 0x7fffffff) return fail(TAL_ERR_INVALID, "tal_round_plan_build: plan larger than 2^31 words");
-  in.words = static_cast<int32_t>(off);
-  in.lds_bytes = static_cast<int32_t>(plan_lds_bytes(in, 16 * c4));
-  if (!plan_host || off > plan_capacity_words) {
-    *info = in;
-    return fail(TAL_ERR_CAPACITY, "tal_round_plan_build: plan buffer too small: need " +
-                                      std::to_string(off) + " words");
-  }
-
-  memcpy(plan_host + in.off_grp_row_ptr, grp_row_ptr.data(), 4 * (G + 1));
-  memcpy(plan_host + in.off_grp_src_ptr, grp_src_ptr.data(), 4 * (G + 1));
-  memcpy(plan_host + in.off_src_row, src_row.data(), 4 * src_row.size());
-  memcpy(plan_host + in.off_row_ptr, row_ptr_host, 4 * (static_cast<size_t>(rows) + 1));
-  memcpy(plan_host + in.off_op_slot, slot.data(), 4 * nnz);
-  for (int64_t k = 0; k < nnz; ++k) {
-    const float wf = static_cast<float>(w_host[k]);
-    memcpy(plan_host + in.off_op_w + k, &wf, 4);
-  }
-  memcpy(plan_host + in.off_out_row, out_row_host, 4 * static_cast<size_t>(rows));
-  if (rb) {
-    memcpy(plan_host + in.off_grp_blk_ptr, grp_blk_ptr.data(), 4 * (G + 1));
-    int64_t pos = in.off_dense;
-    int b = 0;
-    for (int g = 0; g < G; ++g) {
-      for (int r0 = grp_row_ptr[g]; r0 < grp_row_ptr[g + 1]; r0 += rb, ++b) {
-        const std::vector<int32_t>& used = blk_used[b];
-        const int64_t nu = (static_cast<int64_t>(used.size()) + 3) / 4 * 4;  // padded (mask-0 entries)
-        plan_host[in.off_blk_tab + b] = static_cast<int32_t>(pos);
-        int32_t* tab = plan_host + pos;
-        const int64_t words = 8 + nu * (rb + 2);  // multiple of 8: the next table stays aligned
-        memset(tab, 0, 4 * static_cast<size_t>(words));
-        tab[0] = static_cast<int32_t>(nu);
-        int32_t* t_slot = tab + 8;
-        int32_t* t_mask = t_slot + nu;
-        int32_t* t_w = t_mask + nu;
-        for (size_t e = 0; e < used.size(); ++e) t_slot[e] = used[e];
-        for (int r = r0; r < std::min(r0 + rb, grp_row_ptr[g + 1]); ++r) {
-          for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1] - 1; ++k) {  // self excluded
-            const int64_t e = std::lower_bound(used.begin(), used.end(), slot[k]) - used.begin();
-            t_mask[e] |= static_cast<int32_t>(1u << (r - r0));
-            const float wf = static_cast<float>(w_host[k]);
-            memcpy(t_w + e * rb + (r - r0), &wf, 4);
-          }
-        }
-        pos += words;
-      }
-    }
-  }
-  *info = in;
-  g_err.clear();
-  return TAL_OK;
+  int32_t rc = check_csr("tal_round_plan_build_stream", rows, row_ptr_host, col_host, w_host, out_row_host,
+                         &max_col);
+  if (rc) return rc;
+  if (max_group_rows < 1 || max_group_rows > kStreamMaxRows || max_group_src < 0)
+    return fail(TAL_ERR_INVALID, "tal_round_plan_build_stream: max_group_rows must be 1.." +
+                                     std::to_string(kStreamMaxRows) + ", max_group_src >= 0");
+  if (!reference_order(rows, row_ptr_host, col_host))
+    return fail(TAL_ERR_INVALID, "tal_round_plan_build_stream: rows must list operands in reference order");
+  auto fits = [&](int64_t ns, int64_t nr, int64_t) {
+    return nr <= max_group_rows && (max_group_src == 0 || ns <= max_group_src || nr == 1);
+  };
+  Groups grp;
+  rc = group_rows(rows, row_ptr_host, col_host, max_col, fits, &grp);
+  if (rc) return rc;
+  int32_t max_rows = 0;
+  for (size_t g = 0; g + 1 < grp.row_ptr.size(); ++g) max_rows = std::max(max_rows, grp.row_ptr[g + 1] - grp.row_ptr[g]);
+  const int32_t cs = max_rows <= 8 * 8 ? 8 : 16;  // one row block per wavefront
+  return finish_plan(rows, row_ptr_host, col_host, w_host, out_row_host, max_col, grp, 64, kDenseRb, cs,
+                     plan_host, plan_capacity_words, info);
 }
 
 int32_t tal_agg_round_f32(const float* pool_in, int64_t ld_in, float* pool_out, int64_t ld_out,
@@ -1144,7 +1554,10 @@ int32_t tal_agg_round_f32(const float* pool_in, int64_t ld_in, float* pool_out, 
   if (vec) {
     const int64_t n4 = n / 4;
     e_vec = n4 * 4;
-    if (n4 > 0) {
+    if (n4 > 0 && info->stream_cs > 0) {
+      rc = launch_round_stream(pool_in, ld_in, pool_out, ld_out, n4, v, *info, exact, s);
+      if (rc) return rc;
+    } else if (n4 > 0) {
       const bool dense = info->dense_rb > 0;
       switch (info->c4 * 4 + (exact ? 2 : 0) + (dense ? 1 : 0)) {
         case 515: rc = launch_round_vec<128, true, true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
@@ -1159,6 +1572,8 @@ int32_t tal_agg_round_f32(const float* pool_in, int64_t ld_in, float* pool_out, 
       if (rc) return rc;
     }
   }
+  if (info->stream_cs > 0)
+    return launch_round_stream_scalar<false>(pool_in, ld_in, pool_out, ld_out, e_vec, n, v, *info, exact, s);
   return launch_round_scalar<false>(pool_in, ld_in, pool_out, ld_out, e_vec, n, v, *info, exact, s);
 }
 
@@ -1174,6 +1589,9 @@ int32_t tal_agg_round_i64(const int64_t* pool_in, int64_t ld_in, int64_t* pool_o
                 "tal_agg_round_i64: in-place round needs a single-group plan (snapshot semantics)");
   if (n == 0) { g_err.clear(); return TAL_OK; }
   const PlanView v = make_view(plan_dev, *info);
+  if (info->stream_cs > 0)
+    return launch_round_stream_scalar<true>(pool_in, ld_in, pool_out, ld_out, 0, n, v, *info, true,
+                                            static_cast<hipStream_t>(stream));
   return launch_round_scalar<true>(pool_in, ld_in, pool_out, ld_out, 0, n, v, *info, true,
                                    static_cast<hipStream_t>(stream));
 }

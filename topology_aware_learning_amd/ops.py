@@ -153,6 +153,45 @@ def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0, dense:
     return best[1]
 
 
+STREAM_GROUPINGS = ((64, 0), (128, 0), (64, 96))  # (max rows, max sources) per streamed group
+
+
+def _csr(row_ptr, col, w, out_row):
+    row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int32)
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    out_row = np.ascontiguousarray(out_row, dtype=np.int32)
+    if len(row_ptr) != len(out_row) + 1 or row_ptr[-1] != len(col) or len(w) != len(col):
+        raise ValueError("inconsistent CSR arrays")
+    return row_ptr, col, w, out_row
+
+
+def build_stream_plan(row_ptr, col, w, out_row, max_group_rows: int = 64, max_group_src: int = 0) -> RoundPlan:
+    """Streamed-form plan (tal_round_plan_build_stream): groups of <= max_group_rows
+    consecutive rows (and <= max_group_src distinct sources if > 0) whose sources stream through
+    an LDS ring, so cliques and other dense neighborhoods of any size run without the LDS bound
+    of build_plan.  Needs every row in reference order (sorted neighbors, then self)."""
+    row_ptr, col, w, out_row = _csr(row_ptr, col, w, out_row)
+    rows = len(out_row)
+    L = _lib.load()
+    P32 = ctypes.POINTER(ctypes.c_int32)
+    size = L.tal_round_plan_words(rows, len(col))
+    info = RoundPlanInfo()
+    for _ in range(2):
+        blob = np.zeros(size, dtype=np.int32)
+        rc = L.tal_round_plan_build_stream(rows, row_ptr.ctypes.data_as(P32), col.ctypes.data_as(P32),
+                                           w.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                           out_row.ctypes.data_as(P32), int(max_group_rows),
+                                           int(max_group_src), blob.ctypes.data_as(P32), size,
+                                           ctypes.byref(info))
+        if rc == _lib.TAL_ERR_CAPACITY and info.words > size:
+            size = int(info.words)
+            continue
+        break
+    check(rc)
+    return RoundPlan(info=info, host=blob[: info.words].copy(), rows=rows, nnz=len(col))
+
+
 def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.Tensor,
               n: Optional[int] = None, reps: int = 2, mode: int = MODE_EXACT) -> RoundPlan:
     """Pick the plan by measurement: every (tile width, LDS budget, sparse/dense) candidate that
@@ -171,9 +210,17 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
                     continue
                 if dense and not p.info.dense_rb:
                     continue
-                key = (p.info.c4, p.info.n_groups, p.info.total_src, p.info.dense_rb, p.info.max_src)
+                key = (p.info.c4, p.info.n_groups, p.info.total_src, p.info.dense_rb, p.info.max_src, 0)
                 if all(key != k for k, _ in cands):
                     cands.append((key, p))
+    for max_rows, max_src in STREAM_GROUPINGS:
+        try:
+            p = build_stream_plan(row_ptr, col, w, out_row, max_rows, max_src)
+        except (_lib.TalError, ValueError):
+            continue
+        key = (p.info.c4, p.info.n_groups, p.info.total_src, p.info.dense_rb, p.info.max_src, p.info.stream_cs)
+        if all(key != k for k, _ in cands):
+            cands.append((key, p))
     if not cands:
         return build_plan(row_ptr, col, w, out_row)
     if len(cands) == 1:
@@ -193,7 +240,7 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
             ts.append(s.elapsed_time(e))
         t = float(np.median(ts))
         timings.append({"c4": key[0], "groups": key[1], "staged": key[2], "dense_rb": key[3],
-                        "max_src": key[4], "ms": round(t, 4)})
+                        "max_src": key[4], "stream_cs": key[5], "ms": round(t, 4)})
         if best_t is None or t < best_t:
             best, best_t = p, t
     best.tuned_ms = best_t
@@ -203,6 +250,8 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
 
 def round_kernel_name(info: RoundPlanInfo) -> str:
     """Which K3 kernel tal_agg_round_f32 launches for this plan (mirrors launch_round_vec)."""
+    if info.stream_cs:
+        return "k_round_stream"
     threads = 1024 if info.c4 == 64 else 512
     j_max = 20 if threads <= 512 else 8
     loads = info.max_src * info.c4
