@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--mode", default="exact", choices=["exact", "fma"])
     p.add_argument("--c4", type=int, default=0)
     p.add_argument("--no-tune", action="store_true", help="use the model-based plan choice instead of timing candidates")
+    p.add_argument("--stream-rows", type=int, default=0,
+                   help="force a streamed plan with groups of at most this many rows (profiling)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU baseline sample")
     p.add_argument("--no-k1", action="store_true", help="skip the per-call K1 side measurement")
@@ -147,7 +149,9 @@ def main():
         fill_pool(pin, 1234)
         row_ptr, col, w = _round_csr(orders, weights)
         out_rows = np.arange(rows, dtype=np.int32)
-        if args.no_tune or args.c4:
+        if args.stream_rows:
+            plan = _ops.build_stream_plan(row_ptr, col, w, out_rows, args.stream_rows).to(dev)
+        elif args.no_tune or args.c4:
             plan = _ops.build_plan(row_ptr, col, w, out_rows, c4=args.c4).to(dev)
         else:  # time every plan candidate on the real pools (a few rounds, once per topology)
             plan = _ops.tune_plan(row_ptr, col, w, out_rows, pin.f32, pout.f32, n=layout.n_f32, mode=mode)
@@ -224,7 +228,8 @@ def main():
         staged = sr.staged_sources
         rows = sr.local_rows
         bytes_round = 4 * layout.n_f32 * (staged + rows)
-        result_extra = dict(kernel="k_round_f32_persistent", halo_rows_in=sr.halo_rows_in,
+        result_extra = dict(kernel=",".join(sorted({ops.round_kernel_name(p.info) for p in sr.plans.values()})),
+                            halo_rows_in=sr.halo_rows_in,
                             halo_bytes_in=sr.halo_rows_in * 4 * layout.ld_f32)
         units = n_dev_total * n_params * args.steps
         parity_ok = parity_dist

@@ -111,13 +111,14 @@ typedef struct tal_round_plan_info {
                              * w[n_used][dense_rb] fp32}; n_used padded to a multiple of 4
                              * with mask-0 entries */
   int32_t dense_reads;      /* LDS operand reads per column in the dense form (sparse: nnz) */
-  /* streamed form (stream_cs > 0, built by tal_round_plan_build_stream): a workgroup of
-   * stream_cs wavefronts owns a group of at most 8*stream_cs rows (one dense row block per
+  /* streamed form (stream_cs > 0, built by tal_round_plan_build_stream): a workgroup of W
+   * wavefronts (W = 8 or 16) owns a group of at most 8*W rows (one dense row block per
    * wavefront) and streams the group's staged sources through a ring of LDS chunks of
-   * stream_cs sources x 64 float4 columns (one global->LDS DMA per wavefront per chunk), so a
-   * group's source count is not bounded by LDS.  Each block's table lists its entries chunk by
-   * chunk, every chunk's run padded to a multiple of 4 with mask-0 entries. */
-  int32_t stream_cs;        /* sources per chunk = wavefronts per workgroup (8 or 16); 0 = LDS-resident groups */
+   * stream_cs = 2*W sources x 64 float4 columns (two 1 KiB global->LDS DMAs per wavefront per
+   * chunk), so a group's source count is not bounded by LDS.  Each block's table lists its
+   * entries chunk by chunk (including the rows' own models, flagged in mask bits 8..15), every
+   * chunk's run padded to a multiple of 4 with mask-0 entries. */
+  int32_t stream_cs;        /* sources per chunk (16 or 32); 0 = LDS-resident groups */
 } tal_round_plan_info;
 
 /* Blob size in int32 words of the sparse form for `rows` rows / `nnz` operands (an upper

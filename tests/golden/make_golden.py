@@ -46,14 +46,17 @@ def import_reference():
     tvd = types.ModuleType("torchvision.datasets")
     tv.transforms, tv.datasets = tvt, tvd
     sys.modules.update({"torchvision": tv, "torchvision.transforms": tvt, "torchvision.datasets": tvd})
-    sys.path.insert(0, str(REF))
+    # the reference's src/ is a namespace package (no __init__.py): a regular `src` package
+    # anywhere on sys.path (this repo's interface mirror) would shadow it, so hide the repo root
+    hidden = [p for p in sys.path if Path(p or ".").resolve() == ROOT]
+    sys.path[:] = [str(REF)] + [p for p in sys.path if p not in hidden]
     import src.decentralized_client as dc  # reference module
     import src.aggregation_scheduler as sch
     from src.models import resnet
     from src import modules
 
-    # this repo also has a `src` package (the interface mirror): make sure the reference's won
     assert str(REF) in dc.__file__, dc.__file__
+    sys.path.extend(hidden)
     return dc, sch, resnet, modules
 
 
@@ -303,15 +306,60 @@ def gen_round(dc, out_npz, out_json):
     print("round: sequential in-place 4-ring")
 
 
-def main():
+GOSSIP_GRAPHS = {
+    "ring16": lambda: nx.cycle_graph(16),
+    "barbell6_2": lambda: nx.barbell_graph(6, 2),
+    "regular4_20": lambda: nx.random_regular_graph(4, 20, seed=1),
+    "ba33_2": lambda: nx.barabasi_albert_graph(33, 2, seed=0),
+    "star9": lambda: nx.star_graph(8),
+    "sbm": lambda: nx.stochastic_block_model([6, 6, 6], [[0.8, 0.1, 0.05], [0.1, 0.8, 0.1], [0.05, 0.1, 0.8]], seed=3),
+}
+
+
+def gen_gossip(out):
+    """Reference gossip matrices (float32 bits), effective neighbors and placement picks
+    (src/effective_neighbors.py) on a few graphs."""
+    import src.effective_neighbors as en  # reference module
+    assert str(REF) in en.__file__, en.__file__
+    res = {}
+    for name, mk in GOSSIP_GRAPHS.items():
+        g = mk()
+        g = nx.convert_node_labels_to_integers(g)
+        W = en.NetworkxTopology(g).gossip_matrix()
+        eff = en.effective_number_of_neighbors(en.Matrix(W), gamma=0.9, t=0, mode="all", start_at=1)
+        eff_mean = en.effective_number_of_neighbors(en.Matrix(W), gamma=0.5, mode="mean")
+        res[name] = dict(
+            edges=[[int(a), int(b)] for a, b in g.edges()],
+            n=g.number_of_nodes(),
+            W_bits=W.numpy().view(np.uint32).tolist(),
+            eff_all_g09=[float(x) for x in eff],
+            eff_mean_g05=float(eff_mean),
+            placement4=en.get_n_placement_locations(g, 0.9, 4),
+        )
+    out.write_text(json.dumps(res))
+    print("gossip:", ", ".join(res))
+
+
+GENERATORS = ("layouts", "tiny", "weights", "schedulers", "round", "big", "gossip")
+
+
+def main(which=GENERATORS):
     dc, sch, resnet, modules = import_reference()
-    gen_layouts(resnet, modules, HERE / "layouts.json")
-    gen_tiny(dc, HERE / "tiny_cases.json", HERE / "tiny_cases.npz")
-    gen_weights(dc, HERE / "weights_onehot.json", HERE / "centrality.json")
-    gen_schedulers(sch, HERE / "schedulers.json")
-    gen_round(dc, HERE / "round_4ring.npz", HERE / "round_4ring.json")
-    gen_big(dc, resnet, HERE / "big_sha256.json")
+    if "layouts" in which:
+        gen_layouts(resnet, modules, HERE / "layouts.json")
+    if "tiny" in which:
+        gen_tiny(dc, HERE / "tiny_cases.json", HERE / "tiny_cases.npz")
+    if "weights" in which:
+        gen_weights(dc, HERE / "weights_onehot.json", HERE / "centrality.json")
+    if "schedulers" in which:
+        gen_schedulers(sch, HERE / "schedulers.json")
+    if "round" in which:
+        gen_round(dc, HERE / "round_4ring.npz", HERE / "round_4ring.json")
+    if "big" in which:
+        gen_big(dc, resnet, HERE / "big_sha256.json")
+    if "gossip" in which:
+        gen_gossip(HERE / "gossip.json")
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]) or GENERATORS)

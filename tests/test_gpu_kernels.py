@@ -184,7 +184,7 @@ def test_round_stream_vs_oracle(cuda, graph, n, grouping):
     pool = np.stack([_rand_f32(rng, n, special=(rows % 3 == 0)) for _ in range(rows)])
     ref = oracle.round_f32(pool, row_ptr, col, w, out_rows)
     plan = ops.build_stream_plan(row_ptr, col, w, out_rows, *grouping)
-    assert plan.info.stream_cs in (8, 16) and ops.round_kernel_name(plan.info) == "k_round_stream"
+    assert plan.info.stream_cs in (16, 32) and ops.round_kernel_name(plan.info) == "k_round_stream"
     pin = torch.from_numpy(pool).to(cuda)
     pout = torch.zeros_like(pin)
     ops.round_f32(pin, pout, plan)
@@ -245,6 +245,27 @@ def test_round_stream_padded_ld_tail_unaligned_i64(cuda):
     ipout = torch.zeros_like(ipin)
     ops.round_i64(ipin, ipout, plan)
     assert np.array_equal(ipout.cpu().numpy(), iref)
+
+
+def test_round_gossip_matrix(cuda):
+    """A reference gossip matrix (Metropolis weights) run as a device round: K3 resident and
+    streamed plans are bitwise the oracle, and the oracle is W . X within fp32 rounding."""
+    from topology_aware_learning_amd import gossip
+    g = nx.barabasi_albert_graph(60, 3, seed=1)
+    W = gossip.gossip_matrix(g).double().numpy()
+    orders, weights = gossip.orders_from_matrix(W)
+    row_ptr, col, w = ra.round_csr(orders, weights)
+    out_rows = np.arange(len(W), dtype=np.int32)
+    rng = np.random.default_rng(21)
+    X = rng.standard_normal((len(W), 10007)).astype(np.float32)
+    ref = oracle.round_f32(X, row_ptr, col, w, out_rows)
+    pin = torch.from_numpy(X).to(cuda)
+    for plan in (ops.build_plan(row_ptr, col, w, out_rows), ops.build_stream_plan(row_ptr, col, w, out_rows)):
+        pout = torch.zeros_like(pin)
+        ops.round_f32(pin, pout, plan)
+        assert _bits_equal(pout.cpu().numpy(), ref)
+    bound = np.abs(W) @ np.abs(X.astype(np.float64)) * 64 * 2.0 ** -24
+    assert np.all(np.abs(ref - W @ X.astype(np.float64)) <= bound)
 
 
 def test_round_f32_padded_ld_and_tail(cuda):

@@ -310,8 +310,8 @@ def test_stream_plan_walk_matches_oracle(graph):
     for max_rows, max_src in ((64, 0), (128, 0), (16, 0), (64, 24)):
         plan = ops.build_stream_plan(row_ptr, col, w, out_rows, max_rows, max_src)
         i = plan.info
-        assert i.stream_cs in (8, 16) and i.c4 == 64 and i.dense_rb == 8
-        assert i.max_rows <= min(max_rows, 8 * i.stream_cs)
+        assert i.stream_cs in (16, 32) and i.c4 == 64 and i.dense_rb == 8
+        assert i.max_rows <= min(max_rows, 4 * i.stream_cs)
         got = _emulate_stream(plan, pool)
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (graph, max_rows, max_src)
 

@@ -34,6 +34,8 @@ constexpr int kAbiVersion = 4;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
+constexpr uint32_t kMaskSelf0 = 0x100u;          // streamed tables: bit 8+r = the entry is row r's own model
+constexpr uint32_t kMaskSelf = 0xff00u;
 constexpr int kMaxGrid = 256 * 8; // 256 CUs x 8 resident 256-thread blocks
 constexpr int kK1Unroll = 2;     // float4 chunks per lane per K1 grid-stride step
 constexpr int kK1Grid = 4096;    // K1 grid cap (16 blocks per CU in flight)
@@ -91,6 +93,12 @@ __device__ __forceinline__ float4 mul4(float w, float4 x) {
 
 __device__ __forceinline__ float4 add4(float4 a, float4 p) {
   return make_float4(__fadd_rn(a.x, p.x), __fadd_rn(a.y, p.y), __fadd_rn(a.z, p.z), __fadd_rn(a.w, p.w));
+}
+
+// by value: a ?: over two float4 lvalues would select between addresses and keep the
+// arrays out of registers
+__device__ __forceinline__ float4 sel4(bool c, float4 a, float4 b) {
+  return make_float4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
 }
 
 // fp32 accumulator -> int64 the way load_state_dict's copy_ does it on x86: truncation toward
@@ -496,6 +504,7 @@ __device__ __forceinline__ void emit_tile_dense(const float4* s_data, const Plan
 
 constexpr int kDenseRb = 8;
 constexpr int kStreamDepth = 3;        // chunks in flight ahead of the one being read
+constexpr int kStreamPerWave = 2;      // sources each wavefront moves per chunk (1 KiB DMA each)
 constexpr int kStreamMaxRows = 128;    // 16 wavefronts x one 8-row block
 constexpr size_t stream_lds_bytes(int cs) { return static_cast<size_t>(kStreamDepth + 1) * cs * 64 * 16; }
 
@@ -672,18 +681,22 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_byte_addr) 
 // s_waitcnt vmcnt(n) lgkmcnt(0) + s_barrier, n wave-uniform (clamped: waiting longer is safe)
 __device__ __forceinline__ void wait_vm_barrier(int n) {
 #define TAL_WB(k) case k: asm volatile("s_waitcnt vmcnt(" #k ") lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
-  switch (n < 0 ? 0 : (n > 15 ? 15 : n)) {
+  switch (n < 0 ? 0 : (n > 31 ? 31 : n)) {
     TAL_WB(0) TAL_WB(1) TAL_WB(2) TAL_WB(3) TAL_WB(4) TAL_WB(5) TAL_WB(6) TAL_WB(7)
     TAL_WB(8) TAL_WB(9) TAL_WB(10) TAL_WB(11) TAL_WB(12) TAL_WB(13) TAL_WB(14) TAL_WB(15)
+    TAL_WB(16) TAL_WB(17) TAL_WB(18) TAL_WB(19) TAL_WB(20) TAL_WB(21) TAL_WB(22) TAL_WB(23)
+    TAL_WB(24) TAL_WB(25) TAL_WB(26) TAL_WB(27) TAL_WB(28) TAL_WB(29) TAL_WB(30) TAL_WB(31)
   }
 #undef TAL_WB
 }
 
 template <int NT, bool EXACT>
-__global__ __launch_bounds__(NT) void k_round_stream(const float* __restrict__ pin, int64_t ld_in4,
+__global__ __launch_bounds__(NT, 2048 / NT) void k_round_stream(const float* __restrict__ pin, int64_t ld_in4,
                                                      float* __restrict__ pout, int64_t ld_out4,
                                                      int64_t n4, PlanView p, int64_t n_tiles) {
-  constexpr int CS = NT / 64;
+  constexpr int NW = NT / 64;
+  constexpr int D = kStreamPerWave;
+  constexpr int CS = NW * D;
   constexpr int P = kStreamDepth;
   constexpr int NBUF = P + 1;
   constexpr int RB = kDenseRb;
@@ -706,17 +719,27 @@ __global__ __launch_bounds__(NT) void k_round_stream(const float* __restrict__ p
   const uint32_t lds0 = static_cast<uint32_t>(
       reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)s_data));
 
-  // DMA cursor: (tile i, chunk k) of step qi
+  // DMA cursor: (tile i, chunk k) of step qi; wavefront w moves sources k*CS + d*NW + w, d < D.
+  // The pool rows of the next issue are fetched one issue ahead (off the critical path).
   int64_t qi = 0, ii = 0;
   int ik = 0;
+  int next_row[D];
+  auto fetch_rows = [&]() {
+#pragma unroll
+    for (int d = 0; d < D; ++d)  // past the last source: a duplicate (an L2 hit)
+      next_row[d] = src_row[s_beg + min(ik * CS + d * NW + wave, ns - 1)];
+  };
+  fetch_rows();
   auto issue = [&]() {
     const int64_t t = bx + ii * gx;
-    const int s = min(ik * CS + wave, ns - 1);  // past the last source: a duplicate (L2 hit)
-    const int64_t row = src_row[s_beg + s];
     const int64_t col = min(t * 64 + lane, n4 - 1);
-    dma16(pin4 + row * ld_in4 + col, lds0 + static_cast<uint32_t>(((qi % NBUF) * CS + wave) * 1024));
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      dma16(pin4 + static_cast<int64_t>(next_row[d]) * ld_in4 + col,
+            lds0 + static_cast<uint32_t>(((qi % NBUF) * CS + d * NW + wave) * 1024));
     ++qi;
     if (++ik == nch) { ik = 0; ++ii; }
+    if (qi < total) fetch_rows();
   };
   for (int d = 0; d < P; ++d)
     if (qi < total) issue();
@@ -731,23 +754,19 @@ __global__ __launch_bounds__(NT) void k_round_stream(const float* __restrict__ p
   const ConstI32x4 slots4 = (ConstI32x4)(tab + 8);
   const ConstI32x4 masks4 = (ConstI32x4)(tab + 8 + n_used);
   const ConstF32x8 wts8 = (ConstF32x8)(tab + 8 + 2 * n_used);
-  int self_slot[RB];
   float self_w[RB];
 #pragma unroll
   for (int r = 0; r < RB; ++r) {
-    self_slot[r] = -1;
     self_w[r] = 0.f;
-    if (r < rows_here) {
-      const int q = ((ConstI32)p.row_ptr)[r_beg + wave * RB + r + 1] - 1;  // own model: last operand
-      self_slot[r] = ((ConstI32)p.op_slot)[q];
-      self_w[r] = ((ConstF32)p.op_w)[q];
-    }
+    if (r < rows_here)  // own model: the row's last operand
+      self_w[r] = ((ConstF32)p.op_w)[((ConstI32)p.row_ptr)[r_beg + wave * RB + r + 1] - 1];
   }
+  const float4 kNeg0 = make_float4(-0.f, -0.f, -0.f, -0.f);  // x + (-0) == x for every x
   float4 acc[RB], self_x[RB];
 #pragma unroll
   for (int r = 0; r < RB; ++r) {
-    acc[r] = make_float4(-0.f, -0.f, -0.f, -0.f);
-    self_x[r] = acc[r];
+    acc[r] = kNeg0;
+    self_x[r] = kNeg0;
   }
 
   int64_t ci = 0;   // compute cursor: tile i, chunk k
@@ -755,16 +774,13 @@ __global__ __launch_bounds__(NT) void k_round_stream(const float* __restrict__ p
   int e = 0;        // table cursor (entries of chunks < ck consumed)
   uint32_t ends = 0;  // bit j: the step j+1 before this one ended a tile (issued stores)
   for (int64_t q = 0; q < total; ++q) {
-    const int younger_dma = static_cast<int>(min<int64_t>(P - 1, total - 1 - q));
+    const int younger_dma = D * static_cast<int>(min<int64_t>(P - 1, total - 1 - q));
     const int younger_st = rows_here * __builtin_popcount(ends & ((1u << P) - 1));
     wait_vm_barrier(younger_dma + younger_st);  // chunk q resident; step q-1's readers done
     if (qi < total) issue();                    // into the slot step q-1 read
     if (has_blk) {
       const float4* buf = s_data + (q % NBUF) * CS * 64 + lane;
       const int lo = ck * CS, hi = lo + CS;
-#pragma unroll
-      for (int r = 0; r < RB; ++r)
-        if (self_slot[r] >= lo && self_slot[r] < hi) self_x[r] = buf[(self_slot[r] - lo) * 64];
       for (; e < n_used; e += 4) {
         const i32x4 sl = slots4[e >> 2];
         if (sl.x >= hi) break;
@@ -774,25 +790,33 @@ __global__ __launch_bounds__(NT) void k_round_stream(const float* __restrict__ p
         for (int u = 0; u < 4; ++u) x[u] = buf[(sl[u] - lo) * 64];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const f32x8 wv = wts8[e + u];
           const uint32_t m = static_cast<uint32_t>(mk[u]);
-          if (EXACT && (m & kMaskUniform)) {  // one product serves every row
-            const float4 pr = x[u] = mul4(wv[0], x[u]);
+          if (m & kMaskSelf) {  // this source is some rows' own model: keep it for the end
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+              if (m & (kMaskSelf0 << r)) self_x[r] = x[u];
+          }
+          const f32x8 wv = wts8[e + u];
+          if ((m & 0xffu) == 0) {
+            // padding or own-model-only entry
+          } else if (EXACT && (m & kMaskUniform)) {  // one product serves every row
+            const float4 pr = mul4(wv[0], x[u]);
             if ((m & 0xffu) == 0xffu) {
 #pragma unroll
               for (int r = 0; r < RB; ++r) acc[r] = add4(acc[r], pr);
-            } else {
+            } else {  // rows without this source add -0: bitwise a no-op, and no branches
 #pragma unroll
-              for (int r = 0; r < RB; ++r)
-                if (m & (1u << r)) acc[r] = add4(acc[r], pr);
+              for (int r = 0; r < RB; ++r) acc[r] = add4(acc[r], sel4((m >> r) & 1u, pr, kNeg0));
             }
-          } else if (m == (1u << RB) - 1) {  // cliques: every row of the block takes this source
+          } else if ((m & 0xffu) == 0xffu) {  // cliques: every row of the block takes this source
 #pragma unroll
             for (int r = 0; r < RB; ++r) acc[r] = next4<EXACT>(acc[r], wv[r], x[u]);
-          } else if (m) {
+          } else {
 #pragma unroll
-            for (int r = 0; r < RB; ++r)
-              if (m & (1u << r)) acc[r] = next4<EXACT>(acc[r], wv[r], x[u]);
+            for (int r = 0; r < RB; ++r) {
+              const float4 t = next4<EXACT>(acc[r], wv[r], x[u]);
+              acc[r] = sel4((m >> r) & 1u, t, acc[r]);
+            }
           }
         }
       }
@@ -899,10 +923,10 @@ int32_t validate_info(const tal_round_plan_info* info) {
     return fail(TAL_ERR_INVALID, "plan c4 must be 64 or 128");
   if (info->dense_rb != 0 && info->dense_rb != kDenseRb)
     return fail(TAL_ERR_INVALID, "plan dense_rb must be 0 or 8");
-  if (info->stream_cs != 0 && (info->stream_cs != 8 && info->stream_cs != 16))
-    return fail(TAL_ERR_INVALID, "plan stream_cs must be 0, 8 or 16");
+  if (info->stream_cs != 0 && info->stream_cs != 8 * kStreamPerWave && info->stream_cs != 16 * kStreamPerWave)
+    return fail(TAL_ERR_INVALID, "plan stream_cs must be 0 or the library's chunk size (8 or 16 wavefronts)");
   if (info->stream_cs != 0 && (info->c4 != 64 || info->dense_rb != kDenseRb ||
-                               info->max_rows > kDenseRb * info->stream_cs))
+                               info->max_rows > kDenseRb * info->stream_cs / kStreamPerWave))
     return fail(TAL_ERR_INVALID, "streamed plan: c4 64, dense row blocks, <= 8 rows per wavefront");
   return TAL_OK;
 }
@@ -951,7 +975,7 @@ template <int NT, bool EXACT>
 int32_t launch_round_stream_nt(const float* pin, int64_t ld_in, float* pout, int64_t ld_out, int64_t n4,
                                const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
   auto k = k_round_stream<NT, EXACT>;
-  const size_t lds = stream_lds_bytes(NT / 64);
+  const size_t lds = stream_lds_bytes(NT / 64 * kStreamPerWave);
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;
   static int per_cu = 0;  // resident workgroups per CU (registers / LDS), asked once
@@ -971,7 +995,7 @@ int32_t launch_round_stream_nt(const float* pin, int64_t ld_in, float* pout, int
 
 int32_t launch_round_stream(const float* pin, int64_t ld_in, float* pout, int64_t ld_out, int64_t n4,
                             const PlanView& v, const tal_round_plan_info& in, bool exact, hipStream_t s) {
-  if (in.stream_cs == 8)
+  if (in.stream_cs == 8 * kStreamPerWave)
     return exact ? launch_round_stream_nt<512, true>(pin, ld_in, pout, ld_out, n4, v, in, s)
                  : launch_round_stream_nt<512, false>(pin, ld_in, pout, ld_out, n4, v, in, s);
   return exact ? launch_round_stream_nt<1024, true>(pin, ld_in, pout, ld_out, n4, v, in, s)
@@ -1276,8 +1300,9 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
       for (int r0 = grp_row_ptr[g]; r0 < grp_row_ptr[g + 1]; r0 += kDenseRb) {
         std::vector<int32_t> used;
         const int r1 = std::min(r0 + kDenseRb, grp_row_ptr[g + 1]);
-        for (int r = r0; r < r1; ++r)
-          for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1] - 1; ++k) used.push_back(slot[k]);
+        for (int r = r0; r < r1; ++r)  // streamed tables also list each row's own model
+          for (int32_t k = row_ptr_host[r]; k < row_ptr_host[r + 1] - (stream_cs > 0 ? 0 : 1); ++k)
+            used.push_back(slot[k]);
         std::sort(used.begin(), used.end());
         used.erase(std::unique(used.begin(), used.end()), used.end());
         std::vector<int32_t> tab;
@@ -1292,7 +1317,7 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
           tab = used;
           while (tab.size() % 4) tab.push_back(-1);
         }
-        dense_reads += static_cast<int64_t>(stream_cs > 0 ? tab.size() : used.size()) + (r1 - r0);
+        dense_reads += stream_cs > 0 ? static_cast<int64_t>(tab.size()) : static_cast<int64_t>(used.size()) + (r1 - r0);
         blk_used.push_back(std::move(tab));
       }
     }
@@ -1404,6 +1429,14 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
           if (t_mask[e] == 0 || !uniform[e] || __builtin_popcount(static_cast<uint32_t>(t_mask[e])) < 2) continue;
           t_mask[e] = static_cast<int32_t>(static_cast<uint32_t>(t_mask[e]) | kMaskUniform);
           for (int r = 0; r < rb; ++r) memcpy(t_w + e * rb + r, &wbits[e], 4);
+        }
+        if (stream_cs > 0) {  // bit 8+r: the entry is row r's own model (captured, added last)
+          for (int r = r0; r < std::min(r0 + rb, grp_row_ptr[g + 1]); ++r) {
+            const int32_t ks = row_ptr_host[r + 1] - 1;
+            const int64_t d = std::lower_bound(distinct.begin(), distinct.end(), slot[ks]) - distinct.begin();
+            t_mask[entry_of[d]] = static_cast<int32_t>(static_cast<uint32_t>(t_mask[entry_of[d]]) |
+                                                       (kMaskSelf0 << (r - r0)));
+          }
         }
         pos += words;
       }
@@ -1530,7 +1563,7 @@ int32_t tal_round_plan_build_stream(int32_t rows, const int32_t* row_ptr_host,
   if (rc) return rc;
   int32_t max_rows = 0;
   for (size_t g = 0; g + 1 < grp.row_ptr.size(); ++g) max_rows = std::max(max_rows, grp.row_ptr[g + 1] - grp.row_ptr[g]);
-  const int32_t cs = max_rows <= 8 * 8 ? 8 : 16;  // one row block per wavefront
+  const int32_t cs = (max_rows <= 8 * 8 ? 8 : 16) * kStreamPerWave;  // one row block per wavefront
   return finish_plan(rows, row_ptr_host, col_host, w_host, out_row_host, max_col, grp, 64, kDenseRb, cs,
                      plan_host, plan_capacity_words, info);
 }

@@ -123,6 +123,10 @@ class ShardedRound:
                 self.plans[name] = (ops.tune_plan(rp, col, w, np.asarray(idx, np.int32), self.pool_a.f32,
                                                   self.pool_b.f32, n=layout.n_f32, mode=mode)
                                     if tune else ops.build_plan(rp, col, w, np.asarray(idx, np.int32)).to(self.device))
+        if exchange is None and dist.is_available() and dist.is_initialized():
+            # a collective over the whole group first: RCCL then builds the communicator with
+            # every rank, so the first batched P2P does not depend on which ranks have halos
+            dist.barrier(group=group)
         self.local_rows = len(self.spec.own)
         self.halo_rows_in = len(self.spec.halo)
         self.staged_sources = sum(p.info.total_src for p in self.plans.values())
