@@ -804,19 +804,18 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_round_stream(const float* __r
             if ((m & 0xffu) == 0xffu) {
 #pragma unroll
               for (int r = 0; r < RB; ++r) acc[r] = add4(acc[r], pr);
-            } else {  // rows without this source add -0: bitwise a no-op, and no branches
+            } else {
 #pragma unroll
-              for (int r = 0; r < RB; ++r) acc[r] = add4(acc[r], sel4((m >> r) & 1u, pr, kNeg0));
+              for (int r = 0; r < RB; ++r)
+                if (m & (1u << r)) acc[r] = add4(acc[r], pr);
             }
           } else if ((m & 0xffu) == 0xffu) {  // cliques: every row of the block takes this source
 #pragma unroll
             for (int r = 0; r < RB; ++r) acc[r] = next4<EXACT>(acc[r], wv[r], x[u]);
           } else {
 #pragma unroll
-            for (int r = 0; r < RB; ++r) {
-              const float4 t = next4<EXACT>(acc[r], wv[r], x[u]);
-              acc[r] = sel4((m >> r) & 1u, t, acc[r]);
-            }
+            for (int r = 0; r < RB; ++r)
+              if (m & (1u << r)) acc[r] = next4<EXACT>(acc[r], wv[r], x[u]);
           }
         }
       }
