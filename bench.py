@@ -243,7 +243,7 @@ def main():
         return
 
     achieved = bytes_round / (k_ms * 1e-3) / 1e9
-    traffic = load_traffic(args.model)
+    traffic = load_traffic(workload_key(args.graph, n_dev_total, args.model))
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(lay, M, args.cpu_seconds)
@@ -288,29 +288,6 @@ def _round_csr(orders, weights):
     from topology_aware_learning_amd.round import csr_from_lists
 
     return csr_from_lists(orders, weights)
-
-
-def bench_copy(pin, pout, bytes_round, dev, reps: int = 5):
-    """Same-device reference: a plain device copy moving the round's compulsory bytes (read
-    every staged source row once, write every output row once) — what a 50/50 read/write
-    stream achieves on this particular GPU (MI355X boards differ by several %)."""
-    import torch
-
-    n = min(pin.f32.numel(), bytes_round // 8)
-    a = pin.f32.view(-1)[:n]
-    b = pout.f32.view(-1)[:n]
-    b.copy_(a)
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ts = []
-    for _ in range(reps):
-        s.record()
-        b.copy_(a)
-        e.record()
-        e.synchronize()
-        ts.append(s.elapsed_time(e))
-    ms = float(np.median(ts))
-    gbps = 8 * n / (ms * 1e-3) / 1e9
-    return dict(GBps=gbps, frac_of_peak=gbps / HBM_PEAK_GBPS, bytes=8 * n, ms=ms, kernel="torch copy_ (D2D)")
 
 
 def bench_k1(layout, pool, orders, weights, mode, dev, reps: int = 20):
@@ -366,14 +343,18 @@ def bench_host_path(lay, m, dev, reps: int = 5):
     return dict(ms=ms, params_per_s=n / (ms * 1e-3), note="includes pack, H2D, kernel, D2H, unpack")
 
 
-def load_traffic(model: str):
-    """HBM bytes per launch of k_round_tiled_f32 from the committed rocprofv3 PMC summary."""
+def workload_key(graph: str, devices: int, model: str) -> str:
+    return f"{graph}-{devices}-{model}"
+
+
+def load_traffic(key: str):
+    """HBM bytes per launch of this workload's round kernel from the committed rocprofv3 PMC
+    summary (tools/summarize_profile.py), or None when that workload was not profiled."""
     f = ROOT / "profiles" / "traffic.json"
     if not f.exists():
         return None
     try:
-        d = json.loads(f.read_text())
-        return d.get(model, {}).get("bytes_per_launch")
+        return json.loads(f.read_text()).get(key, {}).get("bytes_per_launch")
     except Exception:
         return None
 

@@ -18,6 +18,7 @@ import torch
 from src.aggregation_scheduler import BaseScheduler
 from src.decentralized_client import DecentralClient
 from src.types import Result
+from topology_aware_learning_amd.checkpoint import common_pool, load_state_dicts_into_pool, save_pool_checkpoint
 
 DEFAULT_FORMAT = (
     "%(created)f %(asctime)s %(processName)s-%(process)d "
@@ -28,8 +29,14 @@ DEFAULT_FORMAT = (
 
 def save_checkpoint(round_idx: int, clients: list[DecentralClient], client_results: list[Result],
                     ckpt_path: pathlib.Path) -> None:
-    sds = [{k: v.detach().to("cpu").clone() for k, v in c.model.state_dict().items()} for c in clients]
-    torch.save({"client_state_dicts": sds, "round_idx": round_idx, "client_results": client_results}, ckpt_path)
+    """Reference utils.py:19-38.  Models bound to one device ModelPool are written straight
+    from the pool (one D2H per segment, topology_aware_learning_amd.checkpoint)."""
+    pr = common_pool([c.model for c in clients])
+    if pr is not None:
+        save_pool_checkpoint(ckpt_path, round_idx, pr[0], pr[1], client_results)
+    else:
+        sds = [{k: v.detach().to("cpu").clone() for k, v in c.model.state_dict().items()} for c in clients]
+        torch.save({"client_state_dicts": sds, "round_idx": round_idx, "client_results": client_results}, ckpt_path)
     print(f"Saved checkpoint for round: {round_idx}")
 
 
@@ -39,8 +46,12 @@ def load_checkpoint(ckpt_path: pathlib.Path, clients: list[DecentralClient],
     The file is this framework's own (or the reference's) checkpoint; it holds result dicts
     with datetimes, so it is not a weights-only payload."""
     ckpt = torch.load(ckpt_path, map_location=torch.device("cpu"), weights_only=False)
-    for client, sd in zip(clients, ckpt["client_state_dicts"]):
-        client.model.load_state_dict(sd)
+    pr = common_pool([c.model for c in clients])
+    if pr is not None:  # pool-bound models: one H2D per segment into their rows
+        load_state_dicts_into_pool(pr[0], pr[1], ckpt["client_state_dicts"][: len(clients)])
+    else:
+        for client, sd in zip(clients, ckpt["client_state_dicts"]):
+            client.model.load_state_dict(sd)
     for i in range(ckpt["round_idx"]):
         softmax_coeff_scheduler.step(i)
     return ckpt["round_idx"], clients, ckpt["client_results"], softmax_coeff_scheduler

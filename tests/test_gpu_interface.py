@@ -146,3 +146,22 @@ def test_driver_config1_on_gpu(cuda, tmp_path, monkeypatch):
                                   str(tmp_path / "logs"), "--batch_size", "32"])
     _parsl_compat.configure({"threadpool_executor": 2})
     assert rc == 0 and checked == [3] * 16
+
+
+def test_checkpoint_from_device_pool(cuda, tmp_path):
+    """SURVEY §8(f) row 2 on the GPU: the checkpoint is written from the pool rows and reads
+    back (reference loader and pool loader) bit-identically."""
+    import test_checkpoint as tc
+    from src import utils as U
+    from src.aggregation_scheduler import BaseScheduler
+
+    cl, pool = tc._bound([1, 0, 2], seed=3, device=cuda)
+    U.save_checkpoint(2, cl, [], tmp_path / "g.pth")
+    ref = [{k: v.cpu() for k, v in c.model.state_dict().items()} for c in cl]
+    got = torch.load(tmp_path / "g.pth", weights_only=False)["client_state_dicts"]
+    for a, b in zip(got, ref):
+        tc._check_same(a, b)
+    cl2, pool2 = tc._bound([0, 1, 2], seed=8, device=cuda)
+    U.load_checkpoint(tmp_path / "g.pth", cl2, BaseScheduler(1.0))
+    for a, c2 in zip(ref, cl2):
+        tc._check_same(a, c2.model.state_dict())

@@ -21,7 +21,7 @@ def per_kernel(path):
     return {k: sum(v) / len(v) for k, v in by.items()}
 
 
-def main(tag, sub, model="resnet50"):
+def main(tag, sub, key="random-64-resnet50"):
     src = ROOT / "gpurun_out"
     dst = ROOT / "profiles" / sub
     dst.mkdir(parents=True, exist_ok=True)
@@ -36,12 +36,13 @@ def main(tag, sub, model="resnet50"):
                            hbm_bytes_corrected=2 * f_kb * 1024 + w_kb * 1024)
     (dst / "pmc_summary.json").write_text(json.dumps(summ, indent=1))
     stats = {r["Name"]: r for r in csv.DictReader(open(dst / "kernel_stats.csv"))}
-    rk = [k for k in summ if "k_round_f32_persistent" in k]
+    rk = sorted((k for k in summ if "k_round_" in k and "scalar" not in k), key=lambda k: -summ[k]["FETCH_SIZE_kB_raw"])
     if rk:
-        k = rk[0]
+        k = rk[0]  # the round's dominant kernel
         t = ROOT / "profiles" / "traffic.json"
         d = json.loads(t.read_text()) if t.exists() else {}
-        d[model] = dict(kernel=k, bytes_per_launch=summ[k]["hbm_bytes_corrected"],
+        d.pop("resnet50", None)  # round-1 key, superseded by workload keys
+        d[key] = dict(kernel=k, bytes_per_launch=summ[k]["hbm_bytes_corrected"],
                         fetch_kB_raw=summ[k]["FETCH_SIZE_kB_raw"], write_kB=summ[k]["WRITE_SIZE_kB"],
                         correction="FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); units kB=1024 B",
                         rocprof_avg_ns=float(stats[k]["AverageNs"]) if k in stats else None,
