@@ -88,29 +88,50 @@ def fill_pool(pool, seed: int):
 
 
 def cpu_baseline(layout_list, m: int, budget_s: float):
-    """The reference loop (clone/mul/add_/load_state_dict, oracle/torch_path.py) on host cores."""
+    """The reference loop (clone/mul/add_/load_state_dict, oracle/torch_path.py) on host cores:
+    (i) one call at a time for ~budget_s seconds (the reported value), and (ii) the reference's
+    effective configuration, two concurrent calls (Parsl ThreadPoolExecutor(max_threads=2),
+    parsl_setup.py:75-78), for ~budget_s / 2 seconds."""
+    import threading
+
     import torch
 
     from oracle import torch_path
     from topology_aware_learning_amd import synth
 
     sds = [synth.synth_state_dict(layout_list, 100 + i) for i in range(m)]
-    target = synth.synth_state_dict(layout_list, 99)
+    targets = [synth.synth_state_dict(layout_list, 99), synth.synth_state_dict(layout_list, 98)]
     w = [1 / m] * m
-    torch_path.aggregate_call(sds, w, target)  # warm-up
-    n_out = sum(t.numel() for t in target.values())
+    torch_path.aggregate_call(sds, w, targets[0])  # warm-up
+    n_out = sum(t.numel() for t in targets[0].values())
     calls = 0
     t0 = time.perf_counter()
     while True:
-        torch_path.aggregate_call(sds, w, target)
+        torch_path.aggregate_call(sds, w, targets[0])
         calls += 1
         el = time.perf_counter() - t0
-        if el >= budget_s or calls >= 64:
+        if el >= budget_s or calls >= 1024:
             break
+    counts = [0, 0]
+    stop = time.perf_counter() + budget_s / 2
+
+    def worker(k):
+        while time.perf_counter() < stop:
+            torch_path.aggregate_call(sds, w, targets[k])
+            counts[k] += 1
+
+    t1 = time.perf_counter()
+    ths = [threading.Thread(target=worker, args=(k,)) for k in range(2)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    el2 = time.perf_counter() - t1
     return dict(value=calls * n_out / el, unit="params/s", cores=torch.get_num_threads(), kind="port",
                 sample=f"{calls} reference aggregation calls (M={m}, {n_out} params each, state_dicts in host "
-                       f"memory, torch CPU ops clone/mul/add_/copy_) in {el:.2f} s",
-                ms_per_call=1e3 * el / calls)
+                       f"memory, torch CPU ops clone/mul/add_/copy_, one call at a time) in {el:.2f} s",
+                ms_per_call=1e3 * el / calls,
+                two_concurrent_calls=dict(value=sum(counts) * n_out / el2, calls=sum(counts), seconds=round(el2, 2)))
 
 
 def main():
@@ -190,7 +211,8 @@ def main():
                                                   c4=plan.info.c4, dense_rb=plan.info.dense_rb,
                                                   lds_reads_per_column=plan.info.dense_reads,
                                                   tuned_ms=plan.tuned_ms, candidates=plan.candidates),
-            per_call_equivalent_GBps=per_call_bytes / (k_ms * 1e-3) / 1e9, parity_k3_vs_k1_row0=parity_ok)
+            per_call_equivalent_GBps=per_call_bytes / (k_ms * 1e-3) / 1e9, parity_k3_vs_k1_row0=parity_ok,
+            valu=valu_floor(len(col), rows, layout.n_f32, k_ms, mode))
         steps_done = args.steps
         units = rows * n_params * steps_done
         k1 = None
@@ -341,6 +363,21 @@ def bench_host_path(lay, m, dev, reps: int = 5):
     ms = 1e3 * (time.perf_counter() - t0) / reps
     n = sum(v.numel() for v in models[0].state_dict().values())
     return dict(ms=ms, params_per_s=n / (ms * 1e-3), note="includes pack, H2D, kernel, D2H, unpack")
+
+
+VALU_LANE_OPS_PER_S = 256 * 4 * 32 * 2.4e9  # fp32 lane-ops/s: 256 CUs x 4 SIMD-32 x 2.4 GHz
+
+
+def valu_floor(nnz: int, rows: int, n: int, k_ms: float, mode) -> dict:
+    """Vector-ALU floor of the round: the exact mode issues a separate multiply and add per
+    operand element (no FMA; the shared-product form saves some multiplies on uniform-weight
+    cliques), i.e. ~2 lane-ops per operand element.  Dense rounds (cliques) are bound here, not
+    by HBM: compare floor_ms with the HBM floor bytes_per_launch / 8 TB/s."""
+    from topology_aware_learning_amd import ops
+
+    ops_round = (2 if mode == ops.MODE_EXACT else 1) * (nnz - rows) * n + rows * n
+    floor_ms = 1e3 * ops_round / VALU_LANE_OPS_PER_S
+    return dict(lane_ops=ops_round, floor_ms=floor_ms, frac=floor_ms / k_ms)
 
 
 def workload_key(graph: str, devices: int, model: str) -> str:

@@ -14,11 +14,23 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 
 
-def per_kernel(path):
+def per_kernel(path, last=4):
+    """Mean counter value per kernel name over its last `last` dispatches (the bench's timed
+    steps come last; earlier dispatches include tune_plan's candidates)."""
     by = {}
     for r in csv.DictReader(open(path)):
-        by.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in by.items()}
+        by.setdefault(r["Kernel_Name"], []).append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
+    return {k: sum(x for _, x in sorted(v)[-last:]) / len(sorted(v)[-last:]) for k, v in by.items()}
+
+
+def last_round_kernel(path):
+    """Name of the round kernel dispatched last (the plan the bench timed)."""
+    best = (-1, None)
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"]
+        if "k_round_" in k and "scalar" not in k and int(r["Dispatch_Id"]) > best[0]:
+            best = (int(r["Dispatch_Id"]), k)
+    return best[1]
 
 
 def main(tag, sub, key="random-64-resnet50"):
@@ -36,9 +48,8 @@ def main(tag, sub, key="random-64-resnet50"):
                            hbm_bytes_corrected=2 * f_kb * 1024 + w_kb * 1024)
     (dst / "pmc_summary.json").write_text(json.dumps(summ, indent=1))
     stats = {r["Name"]: r for r in csv.DictReader(open(dst / "kernel_stats.csv"))}
-    rk = sorted((k for k in summ if "k_round_" in k and "scalar" not in k), key=lambda k: -summ[k]["FETCH_SIZE_kB_raw"])
-    if rk:
-        k = rk[0]  # the round's dominant kernel
+    k = last_round_kernel(src / f"{tag}_pmc_fetch" / "pmc_counter_collection.csv")
+    if k is not None:
         t = ROOT / "profiles" / "traffic.json"
         d = json.loads(t.read_text()) if t.exists() else {}
         d.pop("resnet50", None)  # round-1 key, superseded by workload keys
