@@ -187,6 +187,32 @@ int32_t tal_cosine_params(const float* const* a_ptrs_host, const float* const* b
                           int32_t n_pairs, const int64_t* plan_dev, int32_t n_chunks,
                           int32_t n_seg, void* scratch, float* out_dev, void* stream);
 
+/* ---- FedProx proximal term ------------------------------------------------
+ * Reference: local_train, tasks.py:277-286: loss += (prox_coeff / 2) * sum_t sum_p
+ * ||w_p - wt_p||_2 over the neighbors t and the parameter tensors p.  Here the parameters are
+ * segments of flat fp32 rows (a device ModelPool row per model).
+ *
+ * seg_host: 2*n_seg int64 {offset, length} of each parameter in the flat row.  The plan
+ * (int64, copied to the device by the caller) cuts them into workgroup chunks.
+ * tal_prox_norms: norms_out[t*n_seg + p] = ||w_p - wt_p||_2 (sums of squares per chunk in
+ * fp32, combined in double in a fixed order: deterministic); scratch >=
+ * tal_prox_scratch_bytes(n_chunks, k).
+ * tal_prox_grad: gw = s * sum_t (w - wt) / ||w - wt||_p and, for each non-null gwt_host[t],
+ * gwt[t] = -s * (w - wt) / ||w - wt||_p, with 0 where a norm is 0 (torch's norm backward);
+ * s = *scale_dev (the upstream gradient, read on the device).  Only the parameter segments
+ * of gw / gwt are written. */
+int64_t tal_prox_plan_words(const int64_t* seg_host, int32_t n_seg);
+int32_t tal_prox_plan_build(const int64_t* seg_host, int32_t n_seg, int64_t* plan_host,
+                            int64_t plan_capacity_words, int32_t* n_chunks);
+int64_t tal_prox_scratch_bytes(int32_t n_chunks, int32_t k);
+int32_t tal_prox_norms(const float* w, const float* const* wt_host, int32_t k,
+                       const int64_t* plan_dev, int32_t n_chunks, int32_t n_seg, void* scratch,
+                       float* norms_out, void* stream);
+int32_t tal_prox_grad(const float* w, const float* const* wt_host, int32_t k,
+                      const int64_t* plan_dev, int32_t n_chunks, int32_t n_seg,
+                      const float* norms, const float* scale_dev, float* gw,
+                      float* const* gwt_host, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

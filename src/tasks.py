@@ -16,6 +16,7 @@ from torch.utils.data import DataLoader
 
 from src._parsl_compat import python_app
 from src.types import DataChoices, Result  # noqa: F401
+from topology_aware_learning_amd.prox import prox_term
 
 
 def _device_of(model) -> torch.device:
@@ -66,10 +67,13 @@ def _train(future, round_idx, epochs, batch_size, lr, momentum, prox_coeff, seed
             loss = F.cross_entropy(client.model(x), y)
             running += loss.item()
             if with_prox and prox_coeff > 0:  # FedProx term (reference tasks.py:277-286)
-                prox = 0.0
-                for nf in neighbor_futures:
-                    for w, wt in zip(client.model.parameters(), nf[1].model.parameters()):
-                        prox = prox + (w - wt.to(device)).norm(2)
+                # pool-bound client + neighbors: one fused pass (topology_aware_learning_amd.prox)
+                prox = prox_term(client.model, [nf[1].model for nf in neighbor_futures])
+                if prox is None:
+                    prox = 0.0
+                    for nf in neighbor_futures:
+                        for w, wt in zip(client.model.parameters(), nf[1].model.parameters()):
+                            prox = prox + (w - wt.to(device)).norm(2)
                 loss = loss + (prox_coeff / 2) * prox
             loss.backward()
             opt.step()

@@ -165,3 +165,36 @@ def test_checkpoint_from_device_pool(cuda, tmp_path):
     U.load_checkpoint(tmp_path / "g.pth", cl2, BaseScheduler(1.0))
     for a, c2 in zip(ref, cl2):
         tc._check_same(a, c2.model.state_dict())
+
+
+@pytest.mark.parametrize("k", [1, 3, 70])
+def test_prox_term_matches_torch_loop(cuda, k):
+    """fused proximal term over pool rows vs the reference's loop
+    (tasks.py:277-286): value and gradients (client and neighbor parameters)."""
+    import test_checkpoint as tc
+    from topology_aware_learning_amd.prox import prox_term
+
+    cl, pool = tc._bound(list(range(k + 1)), seed=k, device=cuda)
+    with torch.no_grad():
+        for c in cl:
+            for p in c.model.parameters():
+                p.add_(torch.randn_like(p) * 0.1)
+        ref_params = dict(cl[0].model.named_parameters())
+        for n, p in cl[1].model.named_parameters():  # an identical pair: norm 0, zero gradient
+            p.copy_(ref_params[n])
+    client, nbs = cl[0].model, [c.model for c in cl[1:]]
+    fused = prox_term(client, nbs)
+    assert fused is not None
+    fused.backward()
+    g_fused = [p.grad.clone() for c in cl for p in c.model.parameters()]
+    for c in cl:
+        c.model.zero_grad()
+    ref = 0.0
+    for m in nbs:
+        for w, wt in zip(client.parameters(), m.parameters()):
+            ref = ref + (w - wt).norm(2)
+    ref.backward()
+    g_ref = [p.grad.clone() for c in cl for p in c.model.parameters()]
+    assert abs(float(fused) - float(ref)) <= 1e-5 * abs(float(ref)) + 1e-6
+    for a, b in zip(g_fused, g_ref):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-6)

@@ -329,3 +329,24 @@ def test_round_plan_capacity_error():
     w = np.full(300, 1 / 300)
     with pytest.raises(Exception, match="LDS"):
         ops.build_plan(row_ptr, col, w, np.zeros(1, np.int32), c4=64, lds_bytes=64 * 1024)
+
+
+def test_prox_plan_covers_parameter_segments():
+    from topology_aware_learning_amd.aggregate import layout_of_module
+    from topology_aware_learning_amd.prox import ProxPlan
+    from _models import TinyNet
+
+    m = TinyNet()
+    lay = layout_of_module(m)
+    names = [n for n, _ in m.named_parameters()]
+    pl = ProxPlan(lay, names, "cpu")
+    h = pl.plan.numpy()
+    ptr = h[: pl.n_seg + 1]
+    ch = h[pl.n_seg + 1:].reshape(-1, 3)
+    assert len(ch) == pl.n_chunks == ptr[-1]
+    for s, name in enumerate(names):
+        e = lay.by_name[name]
+        rows = ch[ptr[s]: ptr[s + 1]]
+        assert np.all(rows[:, 0] == s)
+        assert rows[0, 1] == e.offset and rows[:, 2].sum() == e.numel
+        assert np.all(rows[1:, 1] == rows[:-1, 1] + rows[:-1, 2])  # contiguous chunks

@@ -23,7 +23,7 @@ TAL_ERR_HIP = 2
 TAL_ERR_CAPACITY = 3
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 EXPORTED = (
     "tal_last_error",
@@ -39,6 +39,11 @@ EXPORTED = (
     "tal_cosine_plan_build",
     "tal_cosine_scratch_bytes",
     "tal_cosine_params",
+    "tal_prox_plan_words",
+    "tal_prox_plan_build",
+    "tal_prox_scratch_bytes",
+    "tal_prox_norms",
+    "tal_prox_grad",
 )
 
 
@@ -111,6 +116,11 @@ _SIGS = {
     "tal_cosine_plan_build": (_I32, [_PI64, _I32, _PI64, _I64, _PI32]),
     "tal_cosine_scratch_bytes": (_I64, [_I32, _I32]),
     "tal_cosine_params": (_I32, [_PP, _PP, _I32, _P, _I32, _I32, _P, _P, _P]),
+    "tal_prox_plan_words": (_I64, [_PI64, _I32]),
+    "tal_prox_plan_build": (_I32, [_PI64, _I32, _PI64, _I64, _PI32]),
+    "tal_prox_scratch_bytes": (_I64, [_I32, _I32]),
+    "tal_prox_norms": (_I32, [_P, _PP, _I32, _P, _I32, _I32, _P, _P, _P]),
+    "tal_prox_grad": (_I32, [_P, _PP, _I32, _P, _I32, _I32, _P, _P, _P, _PP, _P]),
 }
 
 _lock = threading.Lock()

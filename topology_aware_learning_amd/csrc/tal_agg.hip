@@ -30,7 +30,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 4;
+constexpr int kAbiVersion = 5;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -1173,6 +1173,99 @@ __global__ void k_cosine_finish(const int64_t* __restrict__ plan, int n_seg, int
   out[pair0 + pair] = static_cast<float>(total / static_cast<double>(n_seg));
 }
 
+// ------------------------------------------------------------------------------------------
+// FedProx proximal term (reference tasks.py:277-286): prox = sum_t sum_p ||w_p - wt_p||_2 over
+// neighbors t and parameter tensors p, and its gradient.  The parameters are segments of the
+// flat fp32 pool rows.  Plan (int64): seg_chunk_ptr[n_seg+1], then per chunk {seg, begin, len}.
+// ------------------------------------------------------------------------------------------
+constexpr int kProxMaxNb = 64;             // neighbors per launch (more: host batches)
+constexpr int64_t kProxChunk = 8192;       // elements per workgroup chunk
+constexpr int kProxTile = 8;               // neighbors accumulated per pass over w
+
+struct ProxPtrs {
+  const float* wt[kProxMaxNb];
+  float* gwt[kProxMaxNb];
+};
+
+__device__ __forceinline__ double block_sum_f64(double v, double* s_red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) s_red[wave] = v;
+  __syncthreads();
+  double tot = 0.0;
+  for (int w = 0; w < kBlock / 64; ++w) tot += s_red[w];  // fixed order: deterministic
+  return tot;
+}
+
+__global__ __launch_bounds__(kBlock) void k_prox_sumsq(const float* __restrict__ w, ProxPtrs pp, int k,
+                                                       const int64_t* __restrict__ plan, int n_seg,
+                                                       int n_chunks, double* __restrict__ partial) {
+  __shared__ double s_red[kBlock / 64];
+  const int c = blockIdx.x;
+  const int64_t* ch = plan + (n_seg + 1) + 3 * static_cast<int64_t>(c);
+  const int64_t beg = ch[1], len = ch[2];
+  for (int t0 = 0; t0 < k; t0 += kProxTile) {
+    const int nt = min(kProxTile, k - t0);
+    float acc[kProxTile];
+#pragma unroll
+    for (int j = 0; j < kProxTile; ++j) acc[j] = 0.f;
+    for (int64_t e = threadIdx.x; e < len; e += kBlock) {
+      const float wv = w[beg + e];
+#pragma unroll
+      for (int j = 0; j < kProxTile; ++j) {
+        if (j < nt) {
+          const float d = wv - pp.wt[t0 + j][beg + e];
+          acc[j] = fmaf(d, d, acc[j]);
+        }
+      }
+    }
+    for (int j = 0; j < nt; ++j) {
+      const double tot = block_sum_f64(static_cast<double>(acc[j]), s_red);
+      if (threadIdx.x == 0) partial[static_cast<int64_t>(t0 + j) * n_chunks + c] = tot;
+    }
+  }
+}
+
+__global__ void k_prox_finish(const int64_t* __restrict__ plan, int n_seg, int n_chunks, int k,
+                              const double* __restrict__ partial, float* __restrict__ norms) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= static_cast<int64_t>(k) * n_seg) return;
+  const int t = static_cast<int>(i / n_seg), sg = static_cast<int>(i % n_seg);
+  double ss = 0.0;
+  for (int64_t c = plan[sg]; c < plan[sg + 1]; ++c) ss += partial[static_cast<int64_t>(t) * n_chunks + c];
+  norms[i] = static_cast<float>(sqrt(ss));
+}
+
+// g_w = s * sum_t (w - wt) / ||w - wt||,  g_wt = -s * (w - wt) / ||w - wt||  (0 where the
+// norm is 0, as torch's norm backward); s = *scale (the upstream gradient, on the device).
+__global__ __launch_bounds__(kBlock) void k_prox_grad(const float* __restrict__ w, ProxPtrs pp, int k,
+                                                      const int64_t* __restrict__ plan, int n_seg,
+                                                      const float* __restrict__ norms,
+                                                      const float* __restrict__ scale,
+                                                      float* __restrict__ gw, int accumulate) {
+  __shared__ float s_c[kProxMaxNb];
+  const int c = blockIdx.x;
+  const int64_t* ch = plan + (n_seg + 1) + 3 * static_cast<int64_t>(c);
+  const int64_t sg = ch[0], beg = ch[1], len = ch[2];
+  if (threadIdx.x < k) {
+    const float nrm = norms[static_cast<int64_t>(threadIdx.x) * n_seg + sg];
+    s_c[threadIdx.x] = nrm > 0.f ? *scale / nrm : 0.f;
+  }
+  __syncthreads();
+  for (int64_t e = threadIdx.x; e < len; e += kBlock) {
+    const float wv = w[beg + e];
+    float g = accumulate ? gw[beg + e] : 0.f;
+    for (int t = 0; t < k; ++t) {
+      const float d = (wv - pp.wt[t][beg + e]) * s_c[t];
+      g += d;
+      if (pp.gwt[t]) pp.gwt[t][beg + e] = -d;
+    }
+    gw[beg + e] = g;
+  }
+}
+
 }  // namespace
 
 // ==========================================================================================
@@ -1694,6 +1787,93 @@ int32_t tal_cosine_params(const float* const* a_ptrs_host, const float* const* b
     k_cosine_finish<<<cnt, 64, 0, s>>>(plan_dev, n_seg, n_chunks, part, out_dev, base);
   }
   return check_launch("tal_cosine_params");
+}
+
+
+int64_t tal_prox_plan_words(const int64_t* seg_host, int32_t n_seg) {
+  if (!seg_host || n_seg <= 0) return -1;
+  int64_t chunks = 0;
+  for (int s = 0; s < n_seg; ++s) {
+    if (seg_host[2 * s] < 0 || seg_host[2 * s + 1] <= 0) return -1;
+    chunks += (seg_host[2 * s + 1] + kProxChunk - 1) / kProxChunk;
+  }
+  return (n_seg + 1) + 3 * chunks;
+}
+
+int32_t tal_prox_plan_build(const int64_t* seg_host, int32_t n_seg, int64_t* plan_host,
+                            int64_t plan_capacity_words, int32_t* n_chunks) {
+  const int64_t words = tal_prox_plan_words(seg_host, n_seg);
+  if (words < 0 || !n_chunks) return fail(TAL_ERR_INVALID, "tal_prox_plan_build: bad segments");
+  if (!plan_host || words > plan_capacity_words)
+    return fail(TAL_ERR_CAPACITY, "tal_prox_plan_build: plan buffer too small: need " + std::to_string(words));
+  const int64_t nc = (words - (n_seg + 1)) / 3;
+  if (nc > 0x7fffffff) return fail(TAL_ERR_INVALID, "tal_prox_plan_build: too many chunks");
+  int64_t c = 0;
+  int64_t* ch = plan_host + (n_seg + 1);
+  for (int s = 0; s < n_seg; ++s) {
+    plan_host[s] = c;
+    for (int64_t b = 0; b < seg_host[2 * s + 1]; b += kProxChunk, ++c) {
+      ch[3 * c] = s;
+      ch[3 * c + 1] = seg_host[2 * s] + b;
+      ch[3 * c + 2] = std::min<int64_t>(kProxChunk, seg_host[2 * s + 1] - b);
+    }
+  }
+  plan_host[n_seg] = c;
+  *n_chunks = static_cast<int32_t>(nc);
+  g_err.clear();
+  return TAL_OK;
+}
+
+int64_t tal_prox_scratch_bytes(int32_t n_chunks, int32_t k) {
+  return static_cast<int64_t>(sizeof(double)) * n_chunks * std::min<int32_t>(k, kProxMaxNb);
+}
+
+int32_t tal_prox_norms(const float* w, const float* const* wt_host, int32_t k, const int64_t* plan_dev,
+                       int32_t n_chunks, int32_t n_seg, void* scratch, float* norms_out, void* stream) {
+  if (!w || !wt_host || k <= 0 || !plan_dev || n_chunks <= 0 || n_seg <= 0 || !scratch || !norms_out)
+    return fail(TAL_ERR_INVALID, "tal_prox_norms: bad arguments");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  for (int base = 0; base < k; base += kProxMaxNb) {
+    const int cnt = std::min(kProxMaxNb, k - base);
+    ProxPtrs pp{};
+    for (int j = 0; j < cnt; ++j) {
+      if (!wt_host[base + j]) return fail(TAL_ERR_INVALID, "tal_prox_norms: null neighbor pointer");
+      pp.wt[j] = wt_host[base + j];
+    }
+    double* part = static_cast<double*>(scratch);
+    k_prox_sumsq<<<n_chunks, kBlock, 0, s>>>(w, pp, cnt, plan_dev, n_seg, n_chunks, part);
+    const int64_t outs = static_cast<int64_t>(cnt) * n_seg;
+    k_prox_finish<<<static_cast<unsigned>((outs + 255) / 256), 256, 0, s>>>(
+        plan_dev, n_seg, n_chunks, cnt, part, norms_out + static_cast<int64_t>(base) * n_seg);
+    int32_t rc = check_launch("prox norms");
+    if (rc) return rc;
+  }
+  g_err.clear();
+  return TAL_OK;
+}
+
+int32_t tal_prox_grad(const float* w, const float* const* wt_host, int32_t k, const int64_t* plan_dev,
+                      int32_t n_chunks, int32_t n_seg, const float* norms, const float* scale_dev,
+                      float* gw, float* const* gwt_host, void* stream) {
+  if (!w || !wt_host || k <= 0 || !plan_dev || n_chunks <= 0 || n_seg <= 0 || !norms || !scale_dev || !gw)
+    return fail(TAL_ERR_INVALID, "tal_prox_grad: bad arguments");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  for (int base = 0; base < k; base += kProxMaxNb) {
+    const int cnt = std::min(kProxMaxNb, k - base);
+    ProxPtrs pp{};
+    for (int j = 0; j < cnt; ++j) {
+      if (!wt_host[base + j]) return fail(TAL_ERR_INVALID, "tal_prox_grad: null neighbor pointer");
+      pp.wt[j] = wt_host[base + j];
+      pp.gwt[j] = gwt_host ? gwt_host[base + j] : nullptr;
+    }
+    k_prox_grad<<<n_chunks, kBlock, 0, s>>>(w, pp, cnt, plan_dev, n_seg,
+                                           norms + static_cast<int64_t>(base) * n_seg, scale_dev, gw,
+                                           base > 0 ? 1 : 0);
+    int32_t rc = check_launch("prox grad");
+    if (rc) return rc;
+  }
+  g_err.clear();
+  return TAL_OK;
 }
 
 }  // extern "C"
