@@ -7,7 +7,7 @@ TAG=${1:-full}
 OUT=$GRAFT_REPO_ROOT/gpurun_out
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -x -q -m gpu > $OUT/${TAG}_tests.log 2>&1 && \
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $OUT/${TAG}_tests.log 2>&1 && \
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/${TAG}_smoke.log 2>&1 && \
 timeout -k 10 300 python bench.py > $OUT/${TAG}_bench.log 2>&1 && \
 cd /tmp && \

@@ -893,6 +893,64 @@ __global__ __launch_bounds__(kBlock) void k_round_stream_scalar(const void* __re
   }
 }
 
+// Few columns (the fp32 n mod 4 tail after a float4 kernel, the int64 segment): one thread per
+// (row, column), the row's operands read straight from the pool (L2-served, no staging), eight
+// loads in flight ahead of the ordered accumulate.  Out of place only: threads of different
+// workgroups would otherwise read rows others are writing.  Serves sparse, dense and streamed
+// plans alike (src_row / op_slot mean the same in every form).
+constexpr int64_t kDirectMaxCols = 256;
+
+template <bool IS_I64, bool EXACT>
+__global__ __launch_bounds__(kBlock) void k_round_direct(const void* __restrict__ pin_v, int64_t ld_in,
+                                                         void* __restrict__ pout_v, int64_t ld_out,
+                                                         int64_t e0, int cols, int rows, int n_groups,
+                                                         PlanView p) {
+  const int k = blockIdx.x * kBlock + threadIdx.x;
+  if (k >= rows * cols) return;
+  const int r = k / cols;
+  const int64_t e = e0 + k % cols;
+  int g = 0;
+  while (g + 1 < n_groups && p.grp_row_ptr[g + 1] <= r) ++g;
+  const int s_beg = p.grp_src_ptr[g];
+  const int q0 = p.row_ptr[r], q1 = p.row_ptr[r + 1];
+  auto load = [&](int q) -> float {
+    const int64_t row = p.src_row[s_beg + p.op_slot[q]];
+    if constexpr (IS_I64) return static_cast<float>(static_cast<const int64_t*>(pin_v)[row * ld_in + e]);
+    else return static_cast<const float*>(pin_v)[row * ld_in + e];
+  };
+  constexpr bool kExact = EXACT || IS_I64;
+  float acc = first_term<kExact>(p.op_w[q0], load(q0));
+  int q = q0 + 1;
+  for (; q + 8 <= q1; q += 8) {
+    float x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = load(q + u);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = next_term<kExact>(acc, p.op_w[q + u], x[u]);
+  }
+  for (; q < q1; ++q) acc = next_term<kExact>(acc, p.op_w[q], load(q));
+  const int64_t orow = p.out_row[r];
+  if constexpr (IS_I64) static_cast<int64_t*>(pout_v)[orow * ld_out + e] = trunc_i64(acc);
+  else static_cast<float*>(pout_v)[orow * ld_out + e] = acc;
+}
+
+template <bool IS_I64>
+int32_t launch_round_direct(const void* pin, int64_t ld_in, void* pout, int64_t ld_out, int64_t e0,
+                            int64_t n, const PlanView& v, const tal_round_plan_info& in, bool exact,
+                            hipStream_t s) {
+  const int cols = static_cast<int>(n - e0);
+  const int64_t threads = static_cast<int64_t>(cols) * in.rows;
+  const unsigned blocks = static_cast<unsigned>((threads + kBlock - 1) / kBlock);
+  auto k = (IS_I64 || exact) ? k_round_direct<IS_I64, true> : k_round_direct<IS_I64, false>;
+  k<<<blocks, kBlock, 0, s>>>(pin, ld_in, pout, ld_out, e0, cols, in.rows, in.n_groups, v);
+  return check_launch("round direct kernel");
+}
+
+// the direct kernel serves the call: few columns, out of place
+inline bool use_direct(const void* pin, const void* pout, int64_t e0, int64_t n) {
+  return pin != pout && n > e0 && n - e0 <= kDirectMaxCols;
+}
+
 size_t plan_lds_bytes(const tal_round_plan_info& in, int tile_bytes_per_src) {
   return static_cast<size_t>(in.max_src) * tile_bytes_per_src +
          static_cast<size_t>(in.max_rows + 1 + 2 * in.max_nnz + in.max_src + in.max_rows) * 4;
@@ -1697,6 +1755,9 @@ int32_t tal_agg_round_f32(const float* pool_in, int64_t ld_in, float* pool_out, 
       if (rc) return rc;
     }
   }
+  if (n <= e_vec) return TAL_OK;
+  if (use_direct(pool_in, pool_out, e_vec, n))
+    return launch_round_direct<false>(pool_in, ld_in, pool_out, ld_out, e_vec, n, v, *info, exact, s);
   if (info->stream_cs > 0)
     return launch_round_stream_scalar<false>(pool_in, ld_in, pool_out, ld_out, e_vec, n, v, *info, exact, s);
   return launch_round_scalar<false>(pool_in, ld_in, pool_out, ld_out, e_vec, n, v, *info, exact, s);
@@ -1714,6 +1775,9 @@ int32_t tal_agg_round_i64(const int64_t* pool_in, int64_t ld_in, int64_t* pool_o
                 "tal_agg_round_i64: in-place round needs a single-group plan (snapshot semantics)");
   if (n == 0) { g_err.clear(); return TAL_OK; }
   const PlanView v = make_view(plan_dev, *info);
+  if (use_direct(pool_in, pool_out, 0, n))
+    return launch_round_direct<true>(pool_in, ld_in, pool_out, ld_out, 0, n, v, *info, true,
+                                     static_cast<hipStream_t>(stream));
   if (info->stream_cs > 0)
     return launch_round_stream_scalar<true>(pool_in, ld_in, pool_out, ld_out, 0, n, v, *info, true,
                                             static_cast<hipStream_t>(stream));
