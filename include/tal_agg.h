@@ -83,7 +83,7 @@ typedef struct tal_round_plan_info {
   int32_t max_src;       /* largest group source count (sizes the LDS tile) */
   int32_t max_rows;      /* largest group row count */
   int32_t max_nnz;       /* largest group operand count */
-  int32_t c4;            /* float4 columns per staged source row per tile (64 or 128) */
+  int32_t c4;            /* float4 columns per staged source row per tile (16, 32, 64 or 128) */
   int32_t lds_bytes;     /* LDS per workgroup the round kernel will request */
   /* offsets (in int32 words) of the plan's arrays inside the blob */
   int32_t off_grp_row_ptr;  /* [n_groups+1] */
@@ -119,15 +119,25 @@ typedef struct tal_round_plan_info {
    * entries chunk by chunk (including the rows' own models, flagged in mask bits 8..15), every
    * chunk's run padded to a multiple of 4 with mask-0 entries. */
   int32_t stream_cs;        /* sources per chunk (16 or 32); 0 = LDS-resident groups */
+  /* narrow form (c4 16 / 32): each row's operands as (slot * c4, fp32 weight bits) pairs - its
+   * first operand, then the rest padded to a multiple of 4 with (max_src * c4, 1.0f) pairs that
+   * read a tile of -0.0 the kernel keeps in LDS slot max_src: fl(1 * -0) = -0 and x + -0 == x
+   * for every x, so padding is an exact identity.  Rows of a group are ordered by operand count
+   * (descending) so that the 64 / c4 rows a wavefront computes together have similar counts. */
+  int32_t off_nrow_ptr;     /* [rows+1] pair offset of each row */
+  int32_t off_npairs;       /* [npairs][2] int32 */
+  int32_t npairs;           /* pairs over all rows (padded) */
+  int32_t max_npairs;       /* largest group pair count */
 } tal_round_plan_info;
 
-/* Blob size in int32 words of the sparse form for `rows` rows / `nnz` operands (an upper
+/* Blob size in int32 words of the sparse or narrow form for `rows` rows / `nnz` operands (an upper
  * bound); the dense tables come on top — tal_round_plan_build reports the exact need. */
 int64_t tal_round_plan_words(int32_t rows, int64_t nnz);
 
 /* Build the plan on the host.  row_ptr_host[rows+1], col_host[nnz], w_host[nnz] (float64),
- * out_row_host[rows].  c4 in {64,128}; lds_bytes = LDS budget per workgroup (staged tile
- * 16*c4 B per source plus the scalar kernels' plan slice).  Rows keep their order; consecutive rows
+ * out_row_host[rows].  c4 in {16,32,64,128} (16 / 32: narrow tiles, a wavefront computes 64/c4
+ * rows at once, sparse form only); lds_bytes = LDS budget per workgroup (staged tile
+ * 16*c4 B per source plus the plan slice the narrow and scalar kernels stage).  Rows keep their order; consecutive rows
  * share a group while the union of their sources fits; a group's staged sources are in
  * ascending pool row order.  dense_rb: 0 = sparse form, 8 = dense row blocks of 8 (falls back
  * to sparse if a row is not in reference order), -1 = dense when it cuts the LDS operand reads

@@ -161,6 +161,71 @@ def test_round_f32_vs_oracle(cuda, graph, n, c4, lds, dense):
         assert _bits_equal(pin.cpu().numpy(), ref)
 
 
+_NARROW_GRAPHS = {
+    "ring": lambda: nx.cycle_graph(16),
+    "regular": lambda: nx.random_regular_graph(8, 64, seed=0),
+    "sbm": lambda: nx.stochastic_block_model([32] * 4, [[0.45 if a == b else 0.01 for b in range(4)] for a in range(4)], seed=0),
+    "barbell": lambda: nx.barbell_graph(12, 4),
+    "complete": lambda: nx.complete_graph(40),
+    "gnp": lambda: nx.gnp_random_graph(150, 0.08, seed=2),
+}
+
+
+@pytest.mark.parametrize("c4,lds", [(16, 160 * 1024), (32, 160 * 1024), (16, 80 * 1024), (32, 24 * 1024)])
+@pytest.mark.parametrize("n", [4099, 70001])
+@pytest.mark.parametrize("graph", list(_NARROW_GRAPHS))
+def test_round_narrow_vs_oracle(cuda, graph, n, c4, lds):
+    """Narrow-tile kernel (c4 16 / 32: 64/c4 rows per wavefront, per-lane plan from LDS)."""
+    g = _NARROW_GRAPHS[graph]()
+    orders, ws = _graph_csr(g, "softmax" if graph in ("regular", "gnp", "sbm") else "unweighted")
+    rows = len(orders)
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    out_rows = np.random.default_rng(rows).permutation(rows).astype(np.int32)
+    rng = np.random.default_rng(rows + n + c4)
+    pool = np.stack([_rand_f32(rng, n, special=(rows % 3 == 0)) for _ in range(rows)])
+    ref = oracle.round_f32(pool, row_ptr, col, w, out_rows)
+    try:
+        plan = ops.build_plan(row_ptr, col, w, out_rows, c4=c4, lds_bytes=lds)
+    except ops._lib.TalError:  # a row alone does not fit this budget
+        assert lds < 64 * 1024
+        return
+    assert plan.info.c4 == c4 and plan.info.dense_rb == 0
+    assert ops.round_kernel_name(plan.info) == "k_round_f32_narrow"
+    pin = torch.from_numpy(pool).to(cuda)
+    pout = torch.zeros_like(pin)
+    ops.round_f32(pin, pout, plan)
+    assert _bits_equal(pout.cpu().numpy(), ref)
+    ops.round_f32(pin, pout, plan, mode=ops.MODE_FMA)
+    m = max(len(o) for o in orders)
+    fin = np.isfinite(ref)
+    tol = m * 2.0 ** -24 * np.abs(np.where(np.isfinite(pool), pool, 0)).max() + 1e-30
+    got = pout.cpu().numpy()
+    assert np.max(np.abs(got[fin] - ref[fin])) <= tol
+    if plan.single_group:
+        ops.round_f32(pin, pin, plan)
+        assert _bits_equal(pin.cpu().numpy(), ref)
+
+
+def test_round_narrow_sbm256_one_group(cuda):
+    """BASELINE config 5's topology (256-device SBM) fits one narrow group: each source read once."""
+    sizes = [32] * 8
+    p = [[14 / 31 if a == b else 2 / 224 for b in range(8)] for a in range(8)]
+    g = nx.stochastic_block_model(sizes, p, seed=0)
+    orders, ws = _graph_csr(g)
+    rows = len(orders)
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    out_rows = np.arange(rows, dtype=np.int32)
+    plan = ops.build_plan(row_ptr, col, w, out_rows, c4=16, lds_bytes=160 * 1024)
+    assert plan.info.n_groups == 1 and plan.info.total_src == rows
+    n = 8195
+    rng = np.random.default_rng(5)
+    pool = rng.standard_normal((rows, n)).astype(np.float32)
+    pin = torch.from_numpy(pool).to(cuda)
+    pout = torch.zeros_like(pin)
+    ops.round_f32(pin, pout, plan)
+    assert _bits_equal(pout.cpu().numpy(), oracle.round_f32(pool, row_ptr, col, w, out_rows))
+
+
 _STREAM_GRAPHS = {
     "ring": lambda: nx.cycle_graph(16),
     "regular": lambda: nx.random_regular_graph(8, 64, seed=0),

@@ -172,6 +172,39 @@ def test_cosine_segments_reproduce_reference_semantics():
             assert abs(got - ref) < 1e-5
 
 
+def test_narrow_plan_orders_rows_by_operand_count():
+    """Narrow plans (c4 16 / 32) reorder each group's rows by operand count (descending, stable);
+    every row keeps its operands, weights and output row."""
+    g = nx.stochastic_block_model([32] * 4, [[0.45 if a == b else 0.02 for b in range(4)] for a in range(4)], seed=1)
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(g.number_of_nodes())]
+    ws = [W.unweighted(len(o)) for o in orders]
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    rows = len(orders)
+    out_rows = np.random.default_rng(0).permutation(rows).astype(np.int32)
+    want = {int(out_rows[r]): (col[row_ptr[r]:row_ptr[r + 1]].tolist(), w[row_ptr[r]:row_ptr[r + 1]].astype(np.float32).tolist())
+            for r in range(rows)}
+    for c4, budget in ((16, 160 * 1024), (32, 40 * 1024)):
+        plan = ops.build_plan(row_ptr, col, w, out_rows, c4=c4, lds_bytes=budget)
+        i, h = plan.info, plan.host
+        grp_row = h[i.off_grp_row_ptr: i.off_grp_row_ptr + i.n_groups + 1]
+        grp_src = h[i.off_grp_src_ptr: i.off_grp_src_ptr + i.n_groups + 1]
+        src_row = h[i.off_src_row: i.off_src_row + i.total_src]
+        rp = h[i.off_row_ptr: i.off_row_ptr + i.rows + 1]
+        slot = h[i.off_op_slot: i.off_op_slot + i.nnz]
+        wf = h[i.off_op_w: i.off_op_w + i.nnz].view(np.float32)
+        orow = h[i.off_out_row: i.off_out_row + i.rows]
+        assert sorted(orow.tolist()) == list(range(rows))
+        got = {}
+        for gi in range(i.n_groups):
+            srcs = src_row[grp_src[gi]: grp_src[gi + 1]]
+            counts = np.diff(rp[grp_row[gi]: grp_row[gi + 1] + 1])
+            assert np.all(np.diff(counts) <= 0)  # descending operand counts within the group
+            for r in range(grp_row[gi], grp_row[gi + 1]):
+                got[int(orow[r])] = ([int(srcs[slot[k]]) for k in range(rp[r], rp[r + 1])],
+                                     [float(x) for x in wf[rp[r]: rp[r + 1]]])
+        assert got == want
+
+
 def test_round_plan_reconstructs_csr():
     g = nx.random_regular_graph(8, 64, seed=0)
     orders = [sorted(g.neighbors(i)) + [i] for i in range(64)]
@@ -179,7 +212,8 @@ def test_round_plan_reconstructs_csr():
     row_ptr, col, w = ra.round_csr(orders, ws)
     out_rows = np.arange(64, dtype=np.int32)[::-1].copy()
     for c4, budget, dense in ((64, ops.LDS_BUDGET, 0), (64, 20 * 1024, 0), (128, 40 * 1024, 0),
-                              (64, ops.LDS_BUDGET, 8), (128, 40 * 1024, 8)):
+                              (64, ops.LDS_BUDGET, 8), (128, 40 * 1024, 8), (16, ops.LDS_BUDGET, 0),
+                              (32, 12 * 1024, 0), (16, 160 * 1024, 8)):
         plan = ops.build_plan(row_ptr, col, w, out_rows, c4=c4, lds_bytes=budget, dense=dense)
         i, h = plan.info, plan.host
         grp_row = h[i.off_grp_row_ptr: i.off_grp_row_ptr + i.n_groups + 1]
@@ -200,8 +234,8 @@ def test_round_plan_reconstructs_csr():
                 for k in range(rp[r], rp[r + 1]):
                     rec[k] = srcs[slot[k]]
         assert np.array_equal(rec, col)
-        assert i.dense_rb == dense
-        if dense:
+        assert i.dense_rb == (dense if c4 >= 64 else 0)  # narrow tiles are sparse only
+        if i.dense_rb:
             blk_ptr = h[i.off_grp_blk_ptr: i.off_grp_blk_ptr + i.n_groups + 1]
             tabs = h[i.off_blk_tab: i.off_blk_tab + i.n_blocks]
             reads = 0

@@ -104,9 +104,11 @@ __global__ __launch_bounds__(NT) void k_tilecopy1(const v4f* __restrict__ pin, v
 }
 
 static int ld_sweep(int argc, char** argv);
+static int rows_sweep(int argc, char** argv);
 
 int main(int argc, char** argv) {
   if (argc > 1 && strcmp(argv[1], "ld") == 0) return ld_sweep(argc, argv);
+  if (argc > 1 && strcmp(argv[1], "rows") == 0) return rows_sweep(argc, argv);
   const int R = 64, deg = 8;
   const long n = 23573962L, ld = (n + 63) / 64 * 64, n4 = n / 4, ld4 = ld / 4;
   v4f *pin, *pout; float* sink;
@@ -208,5 +210,32 @@ static int ld_sweep(int argc, char** argv) {
     const long tiles2 = (n4 + 127) / 128;
     timeit("tilecopy persistent c4=128 nt=1024 bpc2", 2.0 * 16 * n4 * R, [&]{ k_tilecopy<128, 1024, 8, true, true><<<std::min<long>(tiles2, ncu * 2), 1024>>>(pin, pout, ld4, n4, R, tiles2); });
   }
+  return 0;
+}
+
+// many rows, small pieces: the tile walk over R rows at C4 float4 per row per tile
+static int rows_sweep(int argc, char** argv) {
+  const long n = 23573962L, ld = (n + 63) / 64 * 64, n4 = n / 4, ld4 = ld / 4;
+  const int RMAX = 256;
+  int ncu = 0; CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  v4f *pin, *pout;
+  CK(hipMalloc(&pin, (size_t)RMAX * ld * 4)); CK(hipMalloc(&pout, (size_t)RMAX * ld * 4));
+  k_fill<<<4096, 256>>>(pin, (long)RMAX * ld / 4, 12345u); CK(hipDeviceSynchronize());
+  auto timeit = [&](const char* name, int R, double bytes, auto launch) {
+    for (int i = 0; i < 2; ++i) launch();
+    CK(hipDeviceSynchronize()); CK(hipGetLastError());
+    const int reps = 8; float sum = 0;
+    for (int i = 0; i < reps; ++i) { CK(hipEventRecord(e0)); launch(); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); float ms; CK(hipEventElapsedTime(&ms, e0, e1)); sum += ms; }
+    printf("R=%3d %-44s avg %.3f ms  %6.0f GB/s\n", R, name, sum / reps, bytes / (sum / reps * 1e-3) / 1e9);
+    fflush(stdout);
+  };
+#define TR(R_, C4_, NT_, J_, BPC) { const long tiles = (n4 + C4_ - 1) / C4_; char nm[96]; snprintf(nm, sizeof nm, "tilecopy c4=%d nt=%d J=%d wg/cu=%d", C4_, NT_, J_, BPC); \
+    timeit(nm, R_, 2.0 * 16 * n4 * R_, [&]{ k_tilecopy<C4_, NT_, J_, true, true><<<std::min<long>(tiles, (long)ncu * BPC), NT_>>>(pin, pout, ld4, n4, R_, tiles); }); }
+  TR(64, 64, 1024, 4, 2) TR(128, 32, 1024, 4, 2) TR(256, 16, 1024, 4, 2) TR(256, 32, 1024, 8, 1) TR(256, 16, 512, 8, 2) TR(256, 8, 1024, 2, 2)
+  TR(128, 64, 1024, 8, 1) TR(256, 16, 1024, 4, 1) TR(256, 16, 1024, 4, 3)
+#define TR1(R_, C4_, NT_, J_) { const long tiles = (n4 + C4_ - 1) / C4_; char nm[96]; snprintf(nm, sizeof nm, "tilecopy1 c4=%d nt=%d J=%d", C4_, NT_, J_); \
+    timeit(nm, R_, 2.0 * 16 * n4 * R_, [&]{ k_tilecopy1<C4_, NT_, J_, true, true><<<tiles, NT_>>>(pin, pout, ld4, n4, R_); }); }
+  TR1(256, 16, 1024, 4) TR1(128, 32, 1024, 4)
   return 0;
 }

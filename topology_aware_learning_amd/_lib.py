@@ -23,7 +23,7 @@ TAL_ERR_HIP = 2
 TAL_ERR_CAPACITY = 3
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 EXPORTED = (
     "tal_last_error",
@@ -85,6 +85,10 @@ class RoundPlanInfo(ctypes.Structure):
         ("off_dense", ctypes.c_int32),
         ("dense_reads", ctypes.c_int32),
         ("stream_cs", ctypes.c_int32),
+        ("off_nrow_ptr", ctypes.c_int32),
+        ("off_npairs", ctypes.c_int32),
+        ("npairs", ctypes.c_int32),
+        ("max_npairs", ctypes.c_int32),
     ]
 
 

@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/tal_agg.h"
@@ -30,7 +31,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 5;
+constexpr int kAbiVersion = 6;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -295,6 +296,8 @@ struct PlanView {
   const int32_t* grp_blk_ptr;  // dense form only
   const int32_t* blk_tab;
   const int32_t* base;         // the blob (dense tables are addressed from it)
+  const int32_t* nrow_ptr;     // narrow form only
+  const int32_t* npairs;
 };
 
 PlanView make_view(const int32_t* plan, const tal_round_plan_info& in) {
@@ -309,6 +312,8 @@ PlanView make_view(const int32_t* plan, const tal_round_plan_info& in) {
   v.grp_blk_ptr = plan + in.off_grp_blk_ptr;
   v.blk_tab = plan + in.off_blk_tab;
   v.base = plan;
+  v.nrow_ptr = plan + in.off_nrow_ptr;
+  v.npairs = plan + in.off_npairs;
   return v;
 }
 
@@ -555,6 +560,175 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const float* __rest
       emit_tile_dense<C4, NT, kDenseRb, EXACT>(s_data, p, g, r_beg, nr, ns, pout, ld_out4, t * C4, n4);
     else
       emit_tile<C4, NT, EXACT>(s_data, p, r_beg, nr, pout, ld_out4, t * C4, n4);
+  }
+}
+
+// Narrow-tile persistent form (C4 = 16 or 32 float4 = 256 or 512 B per source per tile): groups
+// of up to 256 (C4 = 16) or 128 (C4 = 32) sources fit one LDS tile, so a whole community graph
+// is one group and every source is read from HBM once per round.  A wavefront computes
+// 64 / C4 rows at once (lanes [k*C4, (k+1)*C4) own row k of the set); the rows' operand counts
+// differ, so the plan is per lane: the group's (slot, weight) pairs and row extents are staged in
+// LDS once per workgroup, after the data tile and a tile of -0.0 in slot max_src that the
+// padding pairs read (see tal_round_plan_info: every row's operands after the first come in
+// whole batches of four).  Each wavefront computes the same rows for every tile, so its first
+// kNarrowPasses row sets (extents, output rows) live in registers; within a row the next
+// batch's pairs are read while the current batch's data reads are in flight.
+constexpr int kNarrowPasses = 4;
+
+struct NarrowLds {
+  const int32_t* rowptr;  // [nr + 1], group-relative pair index
+  const int2* pairs;      // [group pairs + 4 read-ahead] (slot * C4, fp32 weight bits)
+  const int32_t* out;     // [nr] pool_out row
+  int nr;
+};
+
+__host__ __device__ constexpr size_t narrow_lds_bytes(int64_t max_src, int64_t max_rows, int64_t max_pairs,
+                                                      int c4) {
+  return static_cast<size_t>((max_src + 1) * c4 * 16 + (2 * max_rows + 2 + 2 * (max_pairs + 4)) * 4 + 16);
+}
+
+template <int C4>
+__device__ __forceinline__ NarrowLds stage_narrow(const PlanView& p, int g, float4* s_data, int max_src,
+                                                  int nthreads) {
+  NarrowLds L;
+  const int r_beg = p.grp_row_ptr[g];
+  L.nr = p.grp_row_ptr[g + 1] - r_beg;
+  const int32_t* nrp = p.nrow_ptr;
+  const int32_t* np = p.npairs;
+  const int e_beg = nrp[r_beg];
+  const int ne = nrp[r_beg + L.nr] - e_beg;
+  int32_t* rowptr = reinterpret_cast<int32_t*>(s_data + static_cast<size_t>(max_src + 1) * C4);
+  int2* pairs = reinterpret_cast<int2*>(rowptr + ((L.nr + 2) & ~1));
+  int32_t* out = reinterpret_cast<int32_t*>(pairs + ne + 4);
+  for (int k = threadIdx.x; k < C4; k += nthreads)  // the padding pairs' tile of -0.0
+    s_data[static_cast<size_t>(max_src) * C4 + k] = make_float4(-0.f, -0.f, -0.f, -0.f);
+  for (int k = threadIdx.x; k <= L.nr; k += nthreads) rowptr[k] = nrp[r_beg + k] - e_beg;
+  for (int k = threadIdx.x; k < ne + 4; k += nthreads)  // + 4 read-ahead pairs (never used)
+    pairs[k] = k < ne ? make_int2(np[2 * (e_beg + k)], np[2 * (e_beg + k) + 1]) : make_int2(0, 0);
+  for (int k = threadIdx.x; k < L.nr; k += nthreads) out[k] = p.out_row[r_beg + k];
+  L.rowptr = rowptr;
+  L.pairs = pairs;
+  L.out = out;
+  return L;
+}
+
+// One row (pairs q0 .. q1-1, q1 - q0 - 1 a multiple of 4) for this lane's column.  PIPE: the
+// next batch's pairs are read while this batch's data reads are in flight (8 more VGPRs).
+template <bool EXACT, bool PIPE>
+__device__ __forceinline__ float4 narrow_row(const float4* s_data, const int2* pairs, int q0, int q1, int cl) {
+  const int2 f = pairs[q0];
+  float4 acc = first4<EXACT>(__int_as_float(f.y), s_data[f.x + cl]);
+  int q = q0 + 1;
+  if constexpr (!PIPE) {
+    for (; q < q1; q += 4) {
+      int2 e[4];
+      float4 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) e[u] = pairs[q + u];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = s_data[e[u].x + cl];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = next4<EXACT>(acc, __int_as_float(e[u].y), x[u]);
+    }
+    return acc;
+  }
+  if (q < q1) {
+    int2 e[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) e[u] = pairs[q + u];
+    do {
+      float4 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = s_data[e[u].x + cl];
+      int2 en[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) en[u] = pairs[q + 4 + u];  // next batch (or the read-ahead pad)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = next4<EXACT>(acc, __int_as_float(e[u].y), x[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) e[u] = en[u];
+      q += 4;
+    } while (q < q1);
+  }
+  return acc;
+}
+
+// Row set of pass p for wavefront `wave`: snake order over the passes, so that with rows sorted
+// by operand count no wavefront takes the longest set of every pass.
+__device__ __forceinline__ int narrow_set(int p, int wave, int nwaves) {
+  return p * nwaves + ((p & 1) ? nwaves - 1 - wave : wave);
+}
+
+// NP = row sets held in registers: kNarrowPasses for one resident workgroup per CU (128 VGPRs),
+// 0 for two (64 VGPRs: the extents are then read from LDS each pass).
+template <int C4, int NT, int J, int NP, bool EXACT>
+__global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round_f32_narrow(
+    const float* __restrict__ pin, int64_t ld_in4, float* __restrict__ pout, int64_t ld_out4, int64_t n4,
+    PlanView p, int64_t n_tiles, int max_src) {
+  static_assert(C4 == 16 || C4 == 32, "narrow tiles are 16 or 32 float4 wide");
+  static_assert(NT % C4 == 0, "a block stages whole source tiles");
+  constexpr int kRpw = 64 / C4;
+  constexpr int kW = NT / 64;
+  extern __shared__ float4 s_data[];
+  const int g = blockIdx.y;
+  const NarrowLds L = stage_narrow<C4>(p, g, s_data, max_src, NT);
+  const int s_beg = p.grp_src_ptr[g];
+  const int ns = p.grp_src_ptr[g + 1] - s_beg;
+  const int c = threadIdx.x % C4;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int sub = lane / C4;
+  const int cl = lane % C4;
+  int srow[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int src = (j * NT + threadIdx.x) / C4;
+    srow[j] = src < ns ? p.src_row[s_beg + src] : -1;
+  }
+  __syncthreads();  // plan slice staged
+  constexpr int kNP = NP > 0 ? NP : 1;
+  int rq0[kNP], rq1[kNP], rout[kNP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int r = narrow_set(k, wave, kW) * kRpw + sub;
+    rq0[k] = r < L.nr ? L.rowptr[r] : 0;
+    rq1[k] = r < L.nr ? L.rowptr[r + 1] : 0;
+    rout[k] = r < L.nr ? L.out[r] : 0;
+  }
+  const int n_sets = (L.nr + kRpw - 1) / kRpw;
+  float4 v[J];
+  auto load_tile = [&](int64_t tt) {
+    const int64_t col = tt * C4 + c;
+    if (col < n4) {
+#pragma unroll
+      for (int j = 0; j < J; ++j)
+        if (srow[j] >= 0) v[j] = ld_stream(pin, static_cast<int64_t>(srow[j]) * ld_in4 + col);
+    }
+  };
+  int64_t t = blockIdx.x;
+  if (t < n_tiles) load_tile(t);
+  for (; t < n_tiles; t += gridDim.x) {
+    __syncthreads();  // the previous tile's readers are done with s_data
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+      if (srow[j] >= 0) s_data[j * NT + threadIdx.x] = v[j];
+    __syncthreads();
+    if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
+    const int64_t col = t * C4 + cl;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      if (rq1[k] > rq0[k]) {
+        const float4 acc = narrow_row<EXACT, (NP > 0)>(s_data, L.pairs, rq0[k], rq1[k], cl);
+        if (col < n4) st_stream(pout, static_cast<int64_t>(rout[k]) * ld_out4 + col, acc);
+      }
+    }
+    for (int k = NP; k * kW < n_sets; ++k) {  // row sets beyond the register-held ones
+      const int r = narrow_set(k, wave, kW) * kRpw + sub;
+      if (r < L.nr) {
+        const float4 acc = narrow_row<EXACT, (NP > 0)>(s_data, L.pairs, L.rowptr[r], L.rowptr[r + 1], cl);
+        if (col < n4) st_stream(pout, static_cast<int64_t>(L.out[r]) * ld_out4 + col, acc);
+      }
+    }
   }
 }
 
@@ -976,8 +1150,10 @@ int32_t validate_info(const tal_round_plan_info* info) {
   if (!info) return fail(TAL_ERR_INVALID, "null plan info");
   if (info->rows <= 0 || info->n_groups <= 0 || info->max_src <= 0)
     return fail(TAL_ERR_INVALID, "empty round plan");
-  if (info->c4 != 64 && info->c4 != 128)
-    return fail(TAL_ERR_INVALID, "plan c4 must be 64 or 128");
+  if (info->c4 != 16 && info->c4 != 32 && info->c4 != 64 && info->c4 != 128)
+    return fail(TAL_ERR_INVALID, "plan c4 must be 16, 32, 64 or 128");
+  if (info->c4 < 64 && info->dense_rb != 0)
+    return fail(TAL_ERR_INVALID, "narrow plans (c4 16 / 32) are sparse");
   if (info->dense_rb != 0 && info->dense_rb != kDenseRb)
     return fail(TAL_ERR_INVALID, "plan dense_rb must be 0 or 8");
   if (info->stream_cs != 0 && info->stream_cs != 8 * kStreamPerWave && info->stream_cs != 16 * kStreamPerWave)
@@ -1026,6 +1202,58 @@ int32_t launch_round_persistent(const float* pin, int64_t ld_in, float* pout, in
   const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(in.n_groups));
   k<<<grid, kRoundThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles);
   return check_launch("round kernel (persistent)");
+}
+
+constexpr int kNarrowThreads = 1024;
+
+// Workgroups of `kernel` resident per CU with `lds` bytes of dynamic LDS (registers and LDS both
+// count), asked from the runtime once per (kernel, lds) - a persistent grid larger than what is
+// resident would run a second, straggling wave of workgroups.
+std::mutex g_occ_mu;
+std::vector<std::tuple<const void*, size_t, int>> g_occ;
+
+int resident_per_cu(const void* kernel, int threads, size_t lds) {
+  std::lock_guard<std::mutex> lk(g_occ_mu);
+  for (const auto& e : g_occ)
+    if (std::get<0>(e) == kernel && std::get<1>(e) == lds) return std::get<2>(e);
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, threads, lds) != hipSuccess) nb = 1;
+  nb = std::max(1, nb);
+  g_occ.emplace_back(kernel, lds, nb);
+  return nb;
+}
+
+template <int C4, int J, bool EXACT>
+int32_t launch_round_narrow_j(const float* pin, int64_t ld_in, float* pout, int64_t ld_out, int64_t n4,
+                              const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
+  const size_t lds = static_cast<size_t>(in.lds_bytes);
+  // two workgroups per CU when their LDS allows it (registers capped at 64), else one with the
+  // row extents in registers
+  constexpr int kNP = J >= 12 ? kNarrowPasses / 2 : kNarrowPasses;  // J = 12: VGPRs for the staging
+  auto k = k_round_f32_narrow<C4, kNarrowThreads, J, kNP, EXACT>;
+  if constexpr (J <= 4)
+    if (2 * lds <= 160 * 1024) k = k_round_f32_narrow<C4, kNarrowThreads, J, 0, EXACT>;
+  int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
+  if (rc) return rc;
+  const int64_t tiles = (n4 + C4 - 1) / C4;
+  const int64_t per_cu = resident_per_cu(reinterpret_cast<const void*>(k), kNarrowThreads, lds);
+  int64_t gx = std::max<int64_t>(1, 256 * per_cu / in.n_groups);
+  gx = std::min<int64_t>(gx, tiles);
+  const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(in.n_groups));
+  k<<<grid, kNarrowThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles, in.max_src);
+  return check_launch("round kernel (narrow tiles)");
+}
+
+template <int C4, bool EXACT>
+int32_t launch_round_narrow(const float* pin, int64_t ld_in, float* pout, int64_t ld_out, int64_t n4,
+                            const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
+  const int64_t loads = static_cast<int64_t>(in.max_src) * C4;  // float4 staging loads per tile
+  if (loads <= 1LL * kNarrowThreads) return launch_round_narrow_j<C4, 1, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  if (loads <= 2LL * kNarrowThreads) return launch_round_narrow_j<C4, 2, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  if (loads <= 4LL * kNarrowThreads) return launch_round_narrow_j<C4, 4, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  if (loads <= 8LL * kNarrowThreads) return launch_round_narrow_j<C4, 8, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  if (loads <= 12LL * kNarrowThreads) return launch_round_narrow_j<C4, 12, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  return fail(TAL_ERR_CAPACITY, "narrow round plan: group tile larger than 160 KiB");
 }
 
 template <int NT, bool EXACT>
@@ -1485,6 +1713,36 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
   }
   const int32_t n_blocks = rb ? grp_blk_ptr.back() : 0;
 
+  // narrow form: (slot * c4, weight) pairs, each row's operands after the first padded to whole
+  // batches of 4 with (max_src * c4, 1.0f): the kernel's -0.0 tile makes them exact identities
+  std::vector<int32_t> nrp, npr;
+  int64_t max_np = 0;
+  if (c4 < 64) {
+    nrp.assign(static_cast<size_t>(rows) + 1, 0);
+    const float one = 1.0f;
+    int32_t one_bits;
+    memcpy(&one_bits, &one, 4);
+    for (int g = 0; g < G; ++g) {
+      const int64_t g0 = static_cast<int64_t>(npr.size()) / 2;
+      for (int r = grp_row_ptr[g]; r < grp_row_ptr[g + 1]; ++r) {
+        const int32_t k0 = row_ptr_host[r], k1 = row_ptr_host[r + 1];
+        for (int32_t k = k0; k < k1; ++k) {
+          const float wf = static_cast<float>(w_host[k]);
+          int32_t wb;
+          memcpy(&wb, &wf, 4);
+          npr.push_back(slot[k] * c4);
+          npr.push_back(wb);
+        }
+        for (int32_t pad = (4 - (k1 - k0 - 1) % 4) % 4; pad > 0; --pad) {
+          npr.push_back(max_src * c4);
+          npr.push_back(one_bits);
+        }
+        nrp[r + 1] = static_cast<int32_t>(npr.size() / 2);
+      }
+      max_np = std::max<int64_t>(max_np, static_cast<int64_t>(npr.size()) / 2 - g0);
+    }
+  }
+
   tal_round_plan_info in;
   memset(&in, 0, sizeof(in));
   in.rows = rows;
@@ -1511,9 +1769,16 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
   in.off_blk_tab = static_cast<int32_t>(off); off += n_blocks;
   off = (off + 7) / 8 * 8;  // dense tables 32-B aligned (vector scalar loads)
   in.off_dense = static_cast<int32_t>(off); off += dense_words;
+  in.off_nrow_ptr = static_cast<int32_t>(off); off += static_cast<int64_t>(nrp.size());
+  in.off_npairs = static_cast<int32_t>(off); off += static_cast<int64_t>(npr.size());
+  in.npairs = static_cast<int32_t>(npr.size() / 2);
+  in.max_npairs = static_cast<int32_t>(max_np);
   if (off > 0x7fffffff) return fail(TAL_ERR_INVALID, "tal_round_plan_build: plan larger than 2^31 words");
   in.words = static_cast<int32_t>(off);
   in.lds_bytes = static_cast<int32_t>(stream_cs > 0 ? stream_lds_bytes(stream_cs) : plan_lds_bytes(in, 16 * c4));
+  if (c4 < 64)  // the narrow kernel's carve (the scalar tail kernel's fits in the same budget)
+    in.lds_bytes = static_cast<int32_t>(std::max<size_t>(narrow_lds_bytes(max_src, max_rows, max_np, c4),
+                                                         plan_lds_bytes(in, 16 * c4)));
   if (!plan_host || off > plan_capacity_words) {
     *info = in;
     return fail(TAL_ERR_CAPACITY, "tal_round_plan_build: plan buffer too small: need " +
@@ -1530,6 +1795,10 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
     memcpy(plan_host + in.off_op_w + k, &wf, 4);
   }
   memcpy(plan_host + in.off_out_row, out_row_host, 4 * static_cast<size_t>(rows));
+  if (!nrp.empty()) {
+    memcpy(plan_host + in.off_nrow_ptr, nrp.data(), 4 * nrp.size());
+    memcpy(plan_host + in.off_npairs, npr.data(), 4 * npr.size());
+  }
   if (rb) {
     memcpy(plan_host + in.off_grp_blk_ptr, grp_blk_ptr.data(), 4 * (G + 1));
     int64_t pos = in.off_dense;
@@ -1661,7 +1930,9 @@ int32_t tal_agg_i64(const int64_t* const* x_host, const double* w_host, int32_t 
 int64_t tal_round_plan_words(int32_t rows, int64_t nnz) {
   if (rows < 0 || nnz < 0) return -1;
   // grp_row_ptr + grp_src_ptr (<= rows+1 each) + src_row (<= nnz) + row_ptr + slot + w + out_row
-  return 2 * (static_cast<int64_t>(rows) + 1) + nnz + (rows + 1) + 2 * nnz + rows + 16;
+  // + the narrow form's row pointers and padded pairs
+  return 2 * (static_cast<int64_t>(rows) + 1) + nnz + (rows + 1) + 2 * nnz + rows + 16 +
+         (rows + 1) + 2 * (nnz + 3LL * rows);
 }
 
 
@@ -1673,20 +1944,49 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
   int32_t max_col = 0;
   int32_t rc = check_csr("tal_round_plan_build", rows, row_ptr_host, col_host, w_host, out_row_host, &max_col);
   if (rc) return rc;
-  if (c4 != 64 && c4 != 128)
-    return fail(TAL_ERR_INVALID, "tal_round_plan_build: c4 must be 64 or 128");
+  if (c4 != 16 && c4 != 32 && c4 != 64 && c4 != 128)
+    return fail(TAL_ERR_INVALID, "tal_round_plan_build: c4 must be 16, 32, 64 or 128");
+  if (c4 < 64) dense_rb = 0;  // narrow tiles: sparse form (a wavefront covers 64 / c4 rows)
   if (dense_rb != 0 && dense_rb != kDenseRb && dense_rb != -1)
     return fail(TAL_ERR_INVALID, "tal_round_plan_build: dense_rb must be 0, 8 or -1");
   // group consecutive rows while the union of their sources fits the LDS budget (both round
   // kernels stage 16*c4 bytes per source; the scalar one also the plan slice)
   const int64_t per_src = 16LL * c4;
   auto fits = [&](int64_t ns, int64_t nr, int64_t no) {
-    return ns * per_src + (nr + 1 + 2 * no + ns + nr) * 4 <= lds_bytes;
+    const int64_t sliced = ns * per_src + (nr + 1 + 2 * no + ns + nr) * 4;
+    if (c4 >= 64) return sliced <= lds_bytes;
+    // narrow kernel: + the -0.0 tile, pairs padded (<= 3 per row) and read-ahead
+    return std::max<int64_t>(sliced, static_cast<int64_t>(narrow_lds_bytes(ns, nr, no + 3 * nr, c4))) <= lds_bytes;
   };
   Groups grp;
   rc = group_rows(rows, row_ptr_host, col_host, max_col, fits, &grp);
   if (rc) return rc;
-  return finish_plan(rows, row_ptr_host, col_host, w_host, out_row_host, max_col, grp, c4, dense_rb, 0,
+  if (c4 >= 64)
+    return finish_plan(rows, row_ptr_host, col_host, w_host, out_row_host, max_col, grp, c4, dense_rb, 0,
+                       plan_host, plan_capacity_words, info);
+  // Narrow tiles: a wavefront pass computes 64 / c4 consecutive plan rows in lock step, so the
+  // rows of each group are ordered by operand count (descending, stable): rows of a pass then
+  // have similar counts and few lanes idle.  Rows are independent and each names its output
+  // row, so the order is free.
+  std::vector<int32_t> perm(rows);
+  for (int g = 0; g + 1 < static_cast<int>(grp.row_ptr.size()); ++g) {
+    const int r0 = grp.row_ptr[g], r1 = grp.row_ptr[g + 1];
+    for (int r = r0; r < r1; ++r) perm[r] = r;
+    std::stable_sort(perm.begin() + r0, perm.begin() + r1, [&](int32_t a, int32_t b) {
+      return row_ptr_host[a + 1] - row_ptr_host[a] > row_ptr_host[b + 1] - row_ptr_host[b];
+    });
+  }
+  const int64_t nnz = row_ptr_host[rows];
+  std::vector<int32_t> rp(static_cast<size_t>(rows) + 1, 0), cl(nnz), orow(rows);
+  std::vector<double> wv(nnz);
+  for (int r = 0; r < rows; ++r) {
+    const int32_t src = perm[r], k0 = row_ptr_host[src], k1 = row_ptr_host[src + 1];
+    rp[r + 1] = rp[r] + (k1 - k0);
+    std::copy(col_host + k0, col_host + k1, cl.begin() + rp[r]);
+    std::copy(w_host + k0, w_host + k1, wv.begin() + rp[r]);
+    orow[r] = out_row_host[src];
+  }
+  return finish_plan(rows, rp.data(), cl.data(), wv.data(), orow.data(), max_col, grp, c4, 0, 0,
                      plan_host, plan_capacity_words, info);
 }
 
@@ -1739,6 +2039,14 @@ int32_t tal_agg_round_f32(const float* pool_in, int64_t ld_in, float* pool_out, 
     e_vec = n4 * 4;
     if (n4 > 0 && info->stream_cs > 0) {
       rc = launch_round_stream(pool_in, ld_in, pool_out, ld_out, n4, v, *info, exact, s);
+      if (rc) return rc;
+    } else if (n4 > 0 && info->c4 < 64) {
+      if (info->c4 == 16)
+        rc = exact ? launch_round_narrow<16, true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s)
+                   : launch_round_narrow<16, false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s);
+      else
+        rc = exact ? launch_round_narrow<32, true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s)
+                   : launch_round_narrow<32, false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s);
       if (rc) return rc;
     } else if (n4 > 0) {
       const bool dense = info->dense_rb > 0;

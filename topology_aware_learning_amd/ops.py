@@ -78,6 +78,7 @@ def agg_i64(xs: Sequence[torch.Tensor], weights: Sequence[float], out: torch.Ten
 # ------------------------------------------------------------------------------------------
 LDS_BUDGET = 80 * 1024  # two workgroups per CU overlap one's HBM staging with the other's math
 LDS_BUDGETS = (80 * 1024, 160 * 1024)  # candidates: 2 workgroups / CU, or 1 with bigger groups
+TILE_WIDTHS = (64, 128, 32, 16)  # float4 per staged source per tile (ties keep the earlier)
 
 
 @dataclass
@@ -107,8 +108,9 @@ def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0, dense:
     """Tile plan for a round given as CSR (row r: operands col[row_ptr[r]:row_ptr[r+1]] with
     float64 weights w, written to pool row out_row[r]).
 
-    c4 = 0 / lds_bytes = 0 search the float4 tile width (64 or 128 float4 per source) and the
-    LDS budget (LDS_BUDGETS) for the plan with the lowest estimated time per element:
+    c4 = 0 / lds_bytes = 0 search the float4 tile width (16, 32, 64 or 128 float4 per source;
+    16 / 32 are the narrow-tile kernel: up to 256 / 128 sources in one group, sparse form) and
+    the LDS budget (LDS_BUDGETS) for the plan with the lowest estimated time per element:
       HBM  = 4 B x (staged sources + rows)                     at ~5.5 TB/s
       LDS  = 4 B x operands (one LDS read per operand)         at ~150 TB/s x eff(workgroups/CU)
     (eff = 0.33 / 0.6 / 0.8 for 1 / 2 / >= 3 resident workgroups, halved at c4 = 64; fitted to
@@ -126,7 +128,7 @@ def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0, dense:
     cap = L.tal_round_plan_words(rows, len(col))
     best = None
     last_err = None
-    cands = [(c, b) for b in ([lds_bytes] if lds_bytes else LDS_BUDGETS) for c in ([c4] if c4 else [64, 128])]
+    cands = [(c, b) for b in ([lds_bytes] if lds_bytes else LDS_BUDGETS) for c in ([c4] if c4 else TILE_WIDTHS)]
     for cand, budget in cands:
         info = RoundPlanInfo()
         P32 = ctypes.POINTER(ctypes.c_int32)
@@ -201,9 +203,9 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
     if pool_in.data_ptr() == pool_out.data_ptr():
         raise ValueError("tune_plan needs distinct input / output pools")
     cands = []
-    for c4 in (64, 128):
+    for c4 in TILE_WIDTHS:
         for budget in LDS_BUDGETS:
-            for dense in (0, 8):
+            for dense in ((0,) if c4 < 64 else (0, 8)):
                 try:
                     p = build_plan(row_ptr, col, w, out_row, c4=c4, lds_bytes=budget, dense=dense)
                 except _lib.TalError:
@@ -252,6 +254,8 @@ def round_kernel_name(info: RoundPlanInfo) -> str:
     """Which K3 kernel tal_agg_round_f32 launches for this plan (mirrors launch_round_vec)."""
     if info.stream_cs:
         return "k_round_stream"
+    if info.c4 < 64:
+        return "k_round_f32_narrow"
     threads = 1024 if info.c4 == 64 else 512
     j_max = 20 if threads <= 512 else 8
     loads = info.max_src * info.c4
@@ -259,6 +263,8 @@ def round_kernel_name(info: RoundPlanInfo) -> str:
 
 
 def _blocks_per_cu(info: RoundPlanInfo) -> int:
+    if info.c4 < 64:  # narrow kernel: 1024 threads, data tile + plan slice
+        return max(1, min(2, (160 * 1024) // max(1, info.lds_bytes)))
     lds = max(1, info.max_src * info.c4 * 16)
     return max(1, min(4, (160 * 1024) // lds))
 
@@ -266,7 +272,7 @@ def _blocks_per_cu(info: RoundPlanInfo) -> int:
 def _plan_cost(info: RoundPlanInfo) -> float:
     """Estimated seconds per element column of the round (see build_plan)."""
     eff = {1: 0.33, 2: 0.6}.get(_blocks_per_cu(info), 0.8)
-    if info.c4 == 64:
+    if info.c4 <= 64:
         eff *= 0.5  # one float4 column per lane: half the LDS reads in flight of the c4=128 form
     hbm = 4.0 * (info.total_src + info.rows) / 5.5e12
     lds = 4.0 * info.dense_reads / (150e12 * eff)
