@@ -67,6 +67,15 @@ int32_t tal_agg_f32(const float* const* x_host, const double* w_host, int32_t m,
 int32_t tal_agg_i64(const int64_t* const* x_host, const double* w_host, int32_t m,
                     int64_t* out, int64_t n, void* stream);
 
+/* bf16 buffers (uint16_t bit patterns; bf16 models).  mode TAL_MODE_EXACT: the reference's
+ * own ops on bf16 tensors (decentralized_client.py:407-411 - `w * clone(v)` and `+=` each
+ * round their fp32 result to bf16, nearest even), bit-identical to it; TAL_MODE_FMA: fp32
+ * fused accumulation rounded to bf16 once (|error| <= 2^-8 |result| + M 2^-24 sum|w x|).  NaN
+ * results are stored as 0xFFFF (torch's vectorized conversion).  m <= 256; out may alias
+ * any x[i]. */
+int32_t tal_agg_bf16(const uint16_t* const* x_host, const double* w_host, int32_t m,
+                     uint16_t* out, int64_t n, int32_t mode, void* stream);
+
 /* ---- K3: one whole aggregation round over a device-resident model pool -----------------
  * Row r of the round computes pool_out[out_row[r]][e] = sum_k fp32(w[k]) * pool_in[col[k]][e]
  * over k = row_ptr[r] .. row_ptr[r+1]-1 in that (reference) order, for e < n.  All rows read
@@ -173,6 +182,13 @@ int32_t tal_agg_round_f32(const float* pool_in, int64_t ld_in, float* pool_out, 
 int32_t tal_agg_round_i64(const int64_t* pool_in, int64_t ld_in, int64_t* pool_out,
                           int64_t ld_out, int64_t n, const int32_t* plan_dev,
                           const tal_round_plan_info* info, void* stream);
+
+/* The same round on bf16 pools (arithmetic as tal_agg_bf16, per mode).  Takes sparse plans
+ * (c4 64 / 128, dense_rb 0) and narrow plans (c4 16 / 32); TAL_ERR_INVALID for dense or
+ * streamed plans.  A staged tile holds the sources' values as fp32 (c4 float4 per source). */
+int32_t tal_agg_round_bf16(const uint16_t* pool_in, int64_t ld_in, uint16_t* pool_out,
+                           int64_t ld_out, int64_t n, const int32_t* plan_dev,
+                           const tal_round_plan_info* info, int32_t mode, void* stream);
 
 /* ---- K2: cosine similarity of two models' parameters --------------------------------------
  * Reference: cosine_similarity, decentralized_client.py:661-681: for each parameter tensor

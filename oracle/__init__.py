@@ -7,7 +7,8 @@ src/) never imports it and has no CPU fallback.
 Contents
   agg_oracle.c / Makefile  plain-C restatement of the reference arithmetic
                            (src/decentralized_client.py:399-413) — `agg_f32`, `agg_i64`,
-                           `round_f32`, `round_i64` below are its numpy wrappers
+                           `round_f32`, `round_i64`, and for bf16 tensors `agg_bf16`,
+                           `round_bf16` (uint16 bit patterns) below are its numpy wrappers
   reference_alg.py         numpy restatement of the host-side logic on the path: weight
                            vectors of every app, cosine similarity, round semantics
   torch_path.py            the reference loop restated with the same torch CPU ops
@@ -49,6 +50,9 @@ def lib() -> ctypes.CDLL:
         rargs = [P, ctypes.c_int64, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, P, P, P, P]
         L.oracle_round_f32.argtypes = rargs
         L.oracle_round_i64.argtypes = rargs
+        L.oracle_agg_bf16.argtypes = [P, P, ctypes.c_int32, P, ctypes.c_int64, ctypes.c_int32]
+        L.oracle_round_bf16.argtypes = rargs + [ctypes.c_int32]
+        L.oracle_f32_to_bf16.argtypes = [P, P, ctypes.c_int64]
         _lib = L
     return _lib
 
@@ -101,3 +105,41 @@ def round_i64(pool_in, row_ptr, col, w, out_row, pool_out=None) -> np.ndarray:
     if pool_out is None:
         pool_out = pool_in.copy()
     return _round(lib().oracle_round_i64, pool_in, row_ptr, col, w, out_row, pool_out)
+
+
+# ---- bf16 (numpy has no bf16: arrays of uint16 bit patterns) -------------------------------
+def f32_to_bf16(x) -> np.ndarray:
+    """fp32 -> bf16 bits, round to nearest even, NaN -> 0xFFFF (torch's vectorized conversion)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty(x.shape, dtype=np.uint16)
+    lib().oracle_f32_to_bf16(x.ctypes.data, out.ctypes.data, x.size)
+    return out
+
+
+def bf16_to_f32(b) -> np.ndarray:
+    b = np.ascontiguousarray(b, dtype=np.uint16)
+    return (b.astype(np.uint32) << np.uint32(16)).view(np.float32)
+
+
+def agg_bf16(xs, w, exact: bool = True) -> np.ndarray:
+    """One call on bf16 operands.  exact: the reference's torch ops on bf16 tensors (every
+    product and partial sum rounded to bf16); else fp32 fused accumulation, one rounding."""
+    xs = [np.ascontiguousarray(x, dtype=np.uint16).reshape(-1) for x in xs]
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    out = np.empty_like(xs[0])
+    lib().oracle_agg_bf16(_ptrs(xs), w.ctypes.data, len(xs), out.ctypes.data, out.size, int(bool(exact)))
+    return out
+
+
+def round_bf16(pool_in, row_ptr, col, w, out_row, pool_out=None, exact: bool = True) -> np.ndarray:
+    pool_in = np.ascontiguousarray(pool_in, dtype=np.uint16)
+    if pool_out is None:
+        pool_out = pool_in.copy()
+    row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int32)
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    out_row = np.ascontiguousarray(out_row, dtype=np.int32)
+    lib().oracle_round_bf16(pool_in.ctypes.data, pool_in.shape[1], pool_out.ctypes.data, pool_out.shape[1],
+                            pool_in.shape[1], len(out_row), row_ptr.ctypes.data, col.ctypes.data, w.ctypes.data,
+                            out_row.ctypes.data, int(bool(exact)))
+    return pool_out

@@ -340,7 +340,54 @@ def gen_gossip(out):
     print("gossip:", ", ".join(res))
 
 
-GENERATORS = ("layouts", "tiny", "weights", "schedulers", "round", "big", "gossip")
+def gen_bf16(dc, out_json, out_npz):
+    """Every weight-building app on bf16 models (TinyNet.to(torch.bfloat16): fp32 entries become
+    bf16, num_batches_tracked stays int64) through the reference's own loop: inputs and outputs
+    as uint16 bit patterns (numpy has no bf16)."""
+    torch.manual_seed(0)
+    layout = synth.layout_of(TinyNet().state_dict())
+    g = nx.barabasi_albert_graph(20, 2, seed=0)
+    cent = dc.create_centrality_dict(nx.to_numpy_array(g), np.random.default_rng(0))
+    rng = np.random.default_rng(1)
+    specs = []
+    for M in (1, 2, 3, 9, 17):
+        specs += [("unweighted_module_avg", M, {}), ("weighted_module_avg", M, {}), ("scale_agg", M, {}),
+                  ("centrality_module_avg", M, dict(centrality_metric="degree", softmax=True, softmax_coeff=10.0)),
+                  ("centrality_module_avg", M, dict(centrality_metric="betweenness", softmax=False, softmax_coeff=10.0))]
+    cases, arrays = [], {}
+
+    def bits(t):
+        t = t.detach().cpu()
+        return t.view(torch.int16).numpy().view(np.uint16).copy() if t.dtype == torch.bfloat16 else t.numpy().copy()
+
+    for ci, (fn_name, M, kw) in enumerate(specs):
+        order = sorted(rng.choice(20, size=M, replace=False).tolist())
+        lens = [int(x) for x in rng.integers(1, 500, size=M)]
+        clients = []
+        for oi, idx in enumerate(order):
+            m = TinyNet()
+            m.load_state_dict(tiny_inputs(layout, 9000 + 1000 * ci + oi, ci, oi, M))
+            m = m.to(torch.bfloat16)
+            clients.append((["r"], make_client(dc, idx, m, n_train=lens[oi])))
+            for k, v in m.state_dict().items():
+                arrays[f"c{ci}_in{oi}_{k}"] = bits(v)
+        kwargs = dict(centrality_metric=kw.get("centrality_metric"), centrality_dict=cent,
+                      softmax=kw.get("softmax", False), softmax_coeff=kw.get("softmax_coeff", 10.0))
+        res = getattr(dc, fn_name)(clients[-1], 0, *clients, **kwargs)
+        for k, v in res[1].model.state_dict().items():
+            arrays[f"c{ci}_out_{k}"] = bits(v)
+        cases.append(dict(case=ci, fn=fn_name, M=M, order=order, data_lens=lens,
+                          centrality_metric=kw.get("centrality_metric"), softmax=kw.get("softmax", False),
+                          softmax_coeff=kw.get("softmax_coeff", 10.0)))
+    bf_layout = [(n, s, "bfloat16" if d == "float32" else d) for n, s, d in layout]
+    out_json.write_text(json.dumps(dict(layout=bf_layout, graph="barabasi_albert_graph(20, 2, seed=0)",
+                                        centrality={k: {str(i): float(v) for i, v in d.items()} for k, d in cent.items()},
+                                        cases=cases), indent=1))
+    np.savez_compressed(out_npz, **arrays)
+    print(f"bf16: {len(cases)} cases")
+
+
+GENERATORS = ("layouts", "tiny", "weights", "schedulers", "round", "big", "gossip", "bf16")
 
 
 def main(which=GENERATORS):
@@ -359,6 +406,8 @@ def main(which=GENERATORS):
         gen_big(dc, resnet, HERE / "big_sha256.json")
     if "gossip" in which:
         gen_gossip(HERE / "gossip.json")
+    if "bf16" in which:
+        gen_bf16(dc, HERE / "bf16_cases.json", HERE / "bf16_cases.npz")
 
 
 if __name__ == "__main__":

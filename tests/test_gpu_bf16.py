@@ -1,0 +1,233 @@
+"""bf16 storage (BASELINE config 5's bf16 run): K1 and K3 on bf16 buffers through the C-ABI,
+and bf16 models through the reference interface.
+
+Two modes, both checked bit for bit against the C oracle (oracle/agg_oracle.c):
+  EXACT  the reference's own torch ops on bf16 tensors (decentralized_client.py:407-411): every
+         product and every partial sum rounded to bf16 (the oracle is pinned to the reference by
+         tests/golden/bf16_cases.*, test_oracle_golden.py)
+  FMA    fp32 accumulation, fused, rounded to bf16 once; also against the fp32 reference on the
+         same (bf16-valued) inputs within |d| <= 2^-8 |ref| + M 2^-24 sum|w x|
+"""
+import json
+
+import networkx as nx
+import numpy as np
+import pytest
+import torch
+from torch.utils.data import Subset, TensorDataset
+
+import oracle
+from oracle import reference_alg as ra
+from topology_aware_learning_amd import ops
+from topology_aware_learning_amd.arena import ModelPool, StateLayout
+from topology_aware_learning_amd.round import RoundExecutor
+
+from _models import TinyNet
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf16_bits(rng, n, special=False):
+    x = (rng.standard_normal(n) * 3.0).astype(np.float32)
+    if special and n > 12:
+        x[:12] = [1e-40, -0.0, 3.3e38, -1e-45, 65504.0, 1.17e-38, -3.3e38, 2.0 ** -133, 0.0, 1.0, -1.0, 3.0e38]
+    return oracle.f32_to_bf16(x)
+
+
+def _as_torch(bits, dev):
+    return torch.from_numpy(np.ascontiguousarray(bits).view(np.int16)).view(torch.bfloat16).to(dev)
+
+
+def _bits(t):
+    return t.cpu().view(torch.int16).numpy().view(np.uint16)
+
+
+def _tol_ok(got_bits, xs_bits, w):
+    """FMA mode vs the fp32 reference on the same inputs."""
+    xs = [oracle.bf16_to_f32(x) for x in xs_bits]
+    ref = oracle.agg_f32(xs, w)
+    got = oracle.bf16_to_f32(got_bits)
+    mag = sum(abs(np.float32(wi)) * np.abs(x) for wi, x in zip(w, xs))
+    fin = np.isfinite(ref) & np.isfinite(got) & np.isfinite(mag)
+    bound = 2.0 ** -8 * np.abs(ref) + len(xs) * 2.0 ** -24 * mag
+    return bool(np.all(np.abs(got[fin] - ref[fin]) <= bound[fin]))
+
+
+@pytest.mark.parametrize("mode", [ops.MODE_EXACT, ops.MODE_FMA])
+@pytest.mark.parametrize("m", [1, 2, 3, 9, 17, 40])
+@pytest.mark.parametrize("n", [1, 7, 4096, 100003])
+def test_agg_bf16_vs_oracle(cuda, m, n, mode):
+    rng = np.random.default_rng(m * 1000 + n)
+    xs = [_bf16_bits(rng, n, special=(i == 0)) for i in range(m)]
+    w = ra.unweighted_weights(m) if m % 2 else list(rng.uniform(0.01, 1.0, m))
+    ref = oracle.agg_bf16(xs, w, exact=(mode == ops.MODE_EXACT))
+    dx = [_as_torch(x, cuda) for x in xs]
+    out = torch.empty(n, dtype=torch.bfloat16, device=cuda)
+    ops.agg_bf16(dx, w, out, mode=mode)
+    assert np.array_equal(_bits(out), ref)
+    if mode == ops.MODE_FMA:
+        assert _tol_ok(ref, xs, w)
+
+
+def test_agg_bf16_nan_aliasing_unaligned(cuda):
+    rng = np.random.default_rng(3)
+    n = 1030
+    xs = [_bf16_bits(rng, n) for _ in range(5)]
+    xs[2][7] = 0x7FC1  # a NaN with payload: stored as 0xFFFF (torch's vectorized conversion)
+    w = ra.unweighted_weights(5)
+    for mode in (ops.MODE_EXACT, ops.MODE_FMA):
+        ref = oracle.agg_bf16(xs, w, exact=(mode == ops.MODE_EXACT))
+        assert ref[7] == 0xFFFF
+        dx = [_as_torch(x, cuda) for x in xs]
+        ops.agg_bf16(dx, w, dx[-1], mode=mode)  # out = the own model (the reference writes in place)
+        assert np.array_equal(_bits(dx[-1]), ref)
+        # operands at a 2-byte offset: the scalar kernel
+        big = [_as_torch(np.concatenate([np.zeros(1, np.uint16), x]), cuda) for x in xs]
+        out = torch.empty(n + 1, dtype=torch.bfloat16, device=cuda)
+        ops.agg_bf16([b[1:] for b in big], w, out[1:], mode=mode)
+        assert np.array_equal(_bits(out[1:]), ref)
+
+
+_GRAPHS = {
+    "ring": lambda: nx.cycle_graph(16),
+    "regular": lambda: nx.random_regular_graph(8, 64, seed=0),
+    "sbm": lambda: nx.stochastic_block_model([32] * 4, [[0.45 if a == b else 0.01 for b in range(4)] for a in range(4)], seed=0),
+    "barbell": lambda: nx.barbell_graph(12, 4),
+}
+
+
+@pytest.mark.parametrize("mode", [ops.MODE_EXACT, ops.MODE_FMA])
+@pytest.mark.parametrize("c4,lds", [(64, 80 * 1024), (128, 160 * 1024), (64, 24 * 1024), (16, 160 * 1024), (32, 40 * 1024)])
+@pytest.mark.parametrize("graph", list(_GRAPHS))
+def test_round_bf16_vs_oracle(cuda, graph, c4, lds, mode):
+    g = _GRAPHS[graph]()
+    orders = [sorted(g.neighbors(i)) + [i] for i in sorted(g.nodes)]
+    cent = nx.degree_centrality(g)
+    ws = [ra.centrality_weights(o, cent, True, 10.0) if graph == "sbm" else ra.unweighted_weights(len(o))
+          for o in orders]
+    rows = len(orders)
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    out_rows = np.random.default_rng(rows).permutation(rows).astype(np.int32)
+    n = 20003
+    rng = np.random.default_rng(rows + c4)
+    pool = np.stack([_bf16_bits(rng, n, special=(r == 0)) for r in range(rows)])
+    ref = oracle.round_bf16(pool, row_ptr, col, w, out_rows, exact=(mode == ops.MODE_EXACT))
+    try:
+        plan = ops.build_plan(row_ptr, col, w, out_rows, c4=c4, lds_bytes=lds, dense=0)
+    except ops._lib.TalError:  # a row alone does not fit this budget
+        assert lds < 64 * 1024
+        return
+    pin = _as_torch(pool, cuda)
+    pout = torch.zeros_like(pin)
+    ops.round_bf16(pin, pout, plan, mode=mode)
+    assert np.array_equal(_bits(pout), ref)
+    if plan.single_group:  # in place: snapshot-safe with one group (the tail by the staged kernel)
+        ops.round_bf16(pin, pin, plan, mode=mode)
+        assert np.array_equal(_bits(pin), ref)
+
+
+def test_round_bf16_padded_rows(cuda):
+    """Rows padded past n (the ModelPool layout): results in [0, n), padding left untouched."""
+    g = nx.random_regular_graph(4, 20, seed=1)
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(20)]
+    ws = [ra.unweighted_weights(len(o)) for o in orders]
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    n, ld = 1001, 1024
+    rng = np.random.default_rng(9)
+    pool = np.full((20, ld), 0x1234, np.uint16)
+    pool[:, :n] = np.stack([_bf16_bits(rng, n) for _ in range(20)])
+    ref = oracle.round_bf16(np.ascontiguousarray(pool[:, :n]), row_ptr, col, w, np.arange(20, dtype=np.int32),
+                            exact=True)
+    plan = ops.build_plan(row_ptr, col, w, np.arange(20, dtype=np.int32), c4=64, lds_bytes=80 * 1024, dense=0)
+    assert plan.single_group
+    for in_place in (False, True):
+        pin = _as_torch(pool, cuda)
+        pout = pin if in_place else torch.full_like(pin, 0.5)
+        pad = _bits(pout)[:, n:].copy()
+        ops.round_bf16(pin, pout, plan, n=n)
+        got = _bits(pout)
+        assert np.array_equal(got[:, :n], ref)
+        assert np.array_equal(got[:, n:], pad)
+
+
+def test_round_bf16_rejects_dense_plans(cuda):
+    g = nx.complete_graph(20)
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(20)]
+    row_ptr, col, w = ra.round_csr(orders, [ra.unweighted_weights(len(o)) for o in orders])
+    plan = ops.build_plan(row_ptr, col, w, np.arange(20, dtype=np.int32), c4=64, lds_bytes=80 * 1024, dense=8)
+    assert plan.info.dense_rb == 8
+    pin = torch.zeros((20, 256), dtype=torch.bfloat16, device=cuda)
+    with pytest.raises(ops._lib.TalError, match="bf16"):
+        ops.round_bf16(pin, torch.zeros_like(pin), plan)
+
+
+# ---- bf16 models through the reference interface ---------------------------------------------
+BF16 = json.loads((GOLDEN / "bf16_cases.json").read_text())
+BF16Z = np.load(GOLDEN / "bf16_cases.npz")
+BF16_CENT = {k: {int(i): v for i, v in d.items()} for k, d in BF16["centrality"].items()}
+DUMMY = TensorDataset(torch.zeros(4, 1), torch.zeros(4, dtype=torch.long))
+
+
+def _client(idx, model, n_train):
+    from src.decentralized_client import DecentralClient
+
+    data = TensorDataset(torch.zeros(n_train, 1), torch.zeros(n_train, dtype=torch.long))
+    return DecentralClient(idx=idx, prox_coeff=0.0, model=model, train_data=Subset(data, list(range(n_train))),
+                           test_data=None, valid_data=None, global_test_data=DUMMY,
+                           global_backdoor_test_data=None, neighbors=[], neighbor_probs=[])
+
+
+def _load_bf16(model, ci, oi):
+    sd = {}
+    for name, _, dt in BF16["layout"]:
+        a = BF16Z[f"c{ci}_in{oi}_{name}"]
+        sd[name] = torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16) if dt == "bfloat16" \
+            else torch.from_numpy(a.copy())
+    model.load_state_dict(sd)
+
+
+@pytest.mark.parametrize("placement", ["cpu", "gpu", "pool"])
+def test_every_app_bit_exact_bf16_models(cuda, placement):
+    """bf16 models (reference apps on bf16 state_dicts) reproduce the reference's outputs."""
+    import src.decentralized_client as dc
+
+    layout = StateLayout.from_layout([(n, tuple(s), d) for n, s, d in BF16["layout"]])
+    assert layout.n_b16 > 0 and layout.n_f32 == 0
+    for case in BF16["cases"]:
+        ci, M = case["case"], case["M"]
+        pool = ModelPool(layout, M, cuda) if placement == "pool" else None
+        clients = []
+        for oi, idx in enumerate(case["order"]):
+            m = TinyNet().to(torch.bfloat16)
+            _load_bf16(m, ci, oi)
+            if placement != "cpu":
+                m = m.to(cuda)
+            if pool is not None:
+                pool.bind(m, oi)
+            clients.append((["r"], _client(idx, m, case["data_lens"][oi])))
+        res = getattr(dc, case["fn"])(clients[-1], 0, *clients, centrality_metric=case["centrality_metric"],
+                                      centrality_dict=BF16_CENT, softmax=case["softmax"],
+                                      softmax_coeff=case["softmax_coeff"]).result()
+        sd = res[1].model.state_dict()
+        for name, _, dt in BF16["layout"]:
+            t = sd[name].detach().cpu()
+            got = t.view(torch.int16).numpy().view(np.uint16) if dt == "bfloat16" else t.numpy()
+            assert np.array_equal(got, BF16Z[f"c{ci}_out_{name}"]), (ci, case["fn"], name)
+
+
+def test_round_executor_bf16_pool(cuda):
+    """A bf16 pool through RoundExecutor (K3 bf16, snapshot) == per-row K1 bf16 on the snapshot."""
+    layout = StateLayout.from_layout([(n, tuple(s), d) for n, s, d in BF16["layout"]])
+    g = nx.random_regular_graph(3, 12, seed=2)
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(12)]
+    ws = [ra.unweighted_weights(len(o)) for o in orders]
+    pool = ModelPool(layout, 12, cuda)
+    rng = np.random.default_rng(4)
+    pool.b16[:, : layout.n_b16].copy_(_as_torch(np.stack([_bf16_bits(rng, layout.n_b16) for _ in range(12)]), cuda))
+    pool.i64[:, : layout.n_i64].random_(0, 1000)
+    before = pool.b16.clone()
+    RoundExecutor(pool).run(orders, ws)
+    for i in range(12):
+        ref = oracle.agg_bf16([_bits(before[j, : layout.n_b16]) for j in orders[i]], ws[i], exact=True)
+        assert np.array_equal(_bits(pool.row_b16(i)), ref), i

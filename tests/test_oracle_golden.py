@@ -67,6 +67,52 @@ def test_c_oracle_matches_reference_apps(case):
         assert bits_equal(got.reshape(ref.shape), ref), (name, case["fn"])
 
 
+BF16 = json.loads((GOLDEN / "bf16_cases.json").read_text())
+BF16Z = np.load(GOLDEN / "bf16_cases.npz")
+BF16_CENT = {k: {int(i): v for i, v in d.items()} for k, d in BF16["centrality"].items()}
+
+
+def bf16_case_weights(case):
+    order, M, fn = case["order"], case["M"], case["fn"]
+    if fn == "unweighted_module_avg":
+        return ra.unweighted_weights(M)
+    if fn == "weighted_module_avg":
+        return ra.weighted_weights(case["data_lens"])
+    if fn == "scale_agg":
+        return [1 / M]
+    return ra.centrality_weights(order, BF16_CENT[case["centrality_metric"]], case["softmax"], case["softmax_coeff"])
+
+
+@pytest.mark.parametrize("case", BF16["cases"], ids=lambda c: f"{c['case']}-{c['fn']}-M{c['M']}")
+def test_c_oracle_bf16_matches_reference_apps(case):
+    """bf16 models through the reference's own loop (tests/golden/bf16_cases.*, generated from
+    the reference): the exact-mode bf16 restatement reproduces every output bit."""
+    ci, M = case["case"], case["M"]
+    w = bf16_case_weights(case)
+    for name, _, dt in BF16["layout"]:
+        ins = [BF16Z[f"c{ci}_in{i}_{name}"] for i in range(M)]
+        ref = BF16Z[f"c{ci}_out_{name}"]
+        xs = [ins[-1]] if case["fn"] == "scale_agg" else ins
+        if dt == "bfloat16":
+            got = oracle.agg_bf16([x.reshape(-1) for x in xs], w, exact=True)
+        else:
+            got = oracle.agg_i64([x.reshape(-1) for x in xs], w)
+        assert np.array_equal(got.reshape(ref.shape), ref), (name, case["fn"])
+
+
+def test_bf16_fixture_covers_rounding_cases():
+    """The fixture exercises bf16 rounding: results differ from fp32-accumulate-then-round."""
+    differs = 0
+    for case in BF16["cases"]:
+        if case["fn"] != "unweighted_module_avg" or case["M"] < 9:
+            continue
+        ci, M = case["case"], case["M"]
+        w = bf16_case_weights(case)
+        ins = [BF16Z[f"c{ci}_in{i}_fc.weight"].reshape(-1) for i in range(M)]
+        differs += int(np.sum(oracle.agg_bf16(ins, w, exact=True) != oracle.agg_bf16(ins, w, exact=False)))
+    assert differs > 0
+
+
 @pytest.mark.parametrize("case", [c for c in TINY["cases"] if c["fn"] != "test_agg"][::3],
                          ids=lambda c: f"{c['case']}-{c['fn']}")
 def test_torch_port_matches_reference_apps(case):

@@ -23,18 +23,20 @@ TAL_ERR_HIP = 2
 TAL_ERR_CAPACITY = 3
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 EXPORTED = (
     "tal_last_error",
     "tal_abi_version",
     "tal_agg_f32",
     "tal_agg_i64",
+    "tal_agg_bf16",
     "tal_round_plan_words",
     "tal_round_plan_build",
     "tal_round_plan_build_stream",
     "tal_agg_round_f32",
     "tal_agg_round_i64",
+    "tal_agg_round_bf16",
     "tal_cosine_plan_words",
     "tal_cosine_plan_build",
     "tal_cosine_scratch_bytes",
@@ -105,6 +107,7 @@ _SIGS = {
     "tal_abi_version": (_I32, []),
     "tal_agg_f32": (_I32, [_PP, _PD, _I32, _P, _I64, _I32, _P]),
     "tal_agg_i64": (_I32, [_PP, _PD, _I32, _P, _I64, _P]),
+    "tal_agg_bf16": (_I32, [_PP, _PD, _I32, _P, _I64, _I32, _P]),
     "tal_round_plan_words": (_I64, [_I32, _I64]),
     "tal_round_plan_build": (
         _I32,
@@ -116,6 +119,7 @@ _SIGS = {
     ),
     "tal_agg_round_f32": (_I32, [_P, _I64, _P, _I64, _I64, _P, ctypes.POINTER(RoundPlanInfo), _I32, _P]),
     "tal_agg_round_i64": (_I32, [_P, _I64, _P, _I64, _I64, _P, ctypes.POINTER(RoundPlanInfo), _P]),
+    "tal_agg_round_bf16": (_I32, [_P, _I64, _P, _I64, _I64, _P, ctypes.POINTER(RoundPlanInfo), _I32, _P]),
     "tal_cosine_plan_words": (_I64, [_PI64, _I32]),
     "tal_cosine_plan_build": (_I32, [_PI64, _I32, _PI64, _I64, _PI32]),
     "tal_cosine_scratch_bytes": (_I64, [_I32, _I32]),

@@ -1,7 +1,8 @@
 """One aggregation call on the GPU: the body the reference's apps share
 (src/decentralized_client.py:399-413), i.e.
 
-    avg = sum_i w_i * state_dict(model_i)      (fp32 mul + fp32 add per operand, in order)
+    avg = sum_i w_i * state_dict(model_i)      (fp32 mul + fp32 add per operand, in order;
+                                                bf16 entries rounded to bf16 after each op)
     target.load_state_dict(avg)                (int64 buffers truncated)
 
 Operands and target may be
@@ -74,15 +75,21 @@ def _mark_used(tag: str, device) -> None:
     _tls.events[tag] = ev
 
 
-def _stage(models: Sequence[nn.Module], layout: StateLayout, device) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Pack non-bound models' f32 / i64 segments into [k, n] device tensors.
+_SEG_DTYPE = {"f32": torch.float32, "b16": torch.bfloat16, "i64": torch.int64}
+
+
+def _seg_sizes(layout: StateLayout):
+    return {"f32": layout.n_f32, "b16": layout.n_b16, "i64": layout.n_i64}
+
+
+def _stage(models: Sequence[nn.Module], layout: StateLayout, device) -> dict:
+    """Pack non-bound models' segments into [k, n] device tensors (one per non-empty segment).
 
     Models already on `device` are packed there; the others go through one pinned host buffer
     and a single H2D copy per segment (the host-memory path of the reference's CPU models)."""
     k = len(models)
-    nf, ni = layout.n_f32, layout.n_i64
-    df = torch.empty(k, nf, dtype=torch.float32, device=device)
-    di = torch.empty(k, max(ni, 1), dtype=torch.int64, device=device)
+    sizes = {g: n for g, n in _seg_sizes(layout).items() if n}
+    dev = {g: torch.empty(k, n, dtype=_SEG_DTYPE[g], device=device) for g, n in sizes.items()}
     host_rows = []
     sds = []
     for j, m in enumerate(models):
@@ -90,99 +97,97 @@ def _stage(models: Sequence[nn.Module], layout: StateLayout, device) -> Tuple[to
         layout.check_compatible(sd, f"operand {j}")
         sds.append(sd)
         if all(t.device == device for t in sd.values()):
-            fl = layout.flatten_cat(sd, "f32")
-            if fl:
-                torch.cat(fl, out=df[j])
-            il = layout.flatten_cat(sd, "i64")
-            if il:
-                torch.cat(il, out=di[j, :ni])
+            for g in sizes:
+                torch.cat(layout.flatten_cat(sd, g), out=dev[g][j])
         else:
             host_rows.append(j)
     if host_rows:
         h = len(host_rows)
-        hf = _pinned(4 * h * max(nf, 1), "in_f32").view(torch.float32).view(h, max(nf, 1))
-        hi = _pinned(8 * h * max(ni, 1), "in_i64").view(torch.int64).view(h, max(ni, 1))
-        for q, j in enumerate(host_rows):
-            fl = layout.flatten_cat(sds[j], "f32")
-            if fl:
-                torch.cat([t.detach().to("cpu") for t in fl], out=hf[q, :nf])
-            il = layout.flatten_cat(sds[j], "i64")
-            if il:
-                torch.cat([t.detach().to("cpu") for t in il], out=hi[q, :ni])
         idx = torch.tensor(host_rows, dtype=torch.long, device=device)
-        if nf:
-            df.index_copy_(0, idx, hf[:, :nf].to(device, non_blocking=True))
-        if ni:
-            di.index_copy_(0, idx, hi.to(device, non_blocking=True))
-        _mark_used("in_f32", device)
-        _mark_used("in_i64", device)
-    return df, di
+        for g, n in sizes.items():
+            esz = torch.empty((), dtype=_SEG_DTYPE[g]).element_size()
+            hb = _pinned(esz * h * n, "in_" + g).view(_SEG_DTYPE[g]).view(h, n)
+            for q, j in enumerate(host_rows):
+                torch.cat([t.detach().to("cpu") for t in layout.flatten_cat(sds[j], g)], out=hb[q])
+            dev[g].index_copy_(0, idx, hb.to(device, non_blocking=True))
+            _mark_used("in_" + g, device)
+    return dev
+
+
+_AGG = {"f32": lambda xs, w, out, mode: ops.agg_f32(xs, w, out, mode=mode),
+        "b16": lambda xs, w, out, mode: ops.agg_bf16(xs, w, out, mode=mode),
+        "i64": lambda xs, w, out, mode: ops.agg_i64(xs, w, out)}
 
 
 def aggregate_models(operands: Sequence[nn.Module], weights: Sequence[float], target: nn.Module,
                      mode: int = ops.MODE_EXACT) -> nn.Module:
-    """target <- sum_i weights[i] * operands[i] (state_dict-wise), reference semantics."""
+    """target <- sum_i weights[i] * operands[i] (state_dict-wise), reference semantics (bf16
+    entries: the reference's ops on bf16 tensors in MODE_EXACT)."""
     if len(operands) == 0:
         raise ValueError("no operands")
     if len(weights) != len(operands):
         raise ValueError("one weight per operand is required")
     layout = layout_of_module(target)
     device = _device_for(list(operands) + [target])
+    sizes = {g: n for g, n in _seg_sizes(layout).items() if n}
 
-    f32_ptrs: List[Optional[torch.Tensor]] = [None] * len(operands)
-    i64_ptrs: List[Optional[torch.Tensor]] = [None] * len(operands)
+    ptrs: dict = {g: [None] * len(operands) for g in sizes}
     unbound = []
     for j, m in enumerate(operands):
         b = bound_row(m)
         if b is not None and b[0].device == device and b[0].layout == layout:
             pool, r = b
-            f32_ptrs[j] = pool.row_f32(r)
-            i64_ptrs[j] = pool.row_i64(r)
+            rows = {"f32": pool.row_f32, "b16": pool.row_b16, "i64": pool.row_i64}
+            for g in sizes:
+                ptrs[g][j] = rows[g](r)
         else:
             unbound.append(j)
     if unbound:
-        df, di = _stage([operands[j] for j in unbound], layout, device)
+        staged = _stage([operands[j] for j in unbound], layout, device)
         for k, j in enumerate(unbound):
-            f32_ptrs[j] = df[k]
-            i64_ptrs[j] = di[k, : layout.n_i64]
+            for g in sizes:
+                ptrs[g][j] = staged[g][k]
 
     tb = bound_row(target)
     if tb is not None and tb[0].device == device and tb[0].layout == layout:
-        out_f = tb[0].row_f32(tb[1])
-        out_i = tb[0].row_i64(tb[1])
+        rows = {"f32": tb[0].row_f32, "b16": tb[0].row_b16, "i64": tb[0].row_i64}
+        outs = {g: rows[g](tb[1]) for g in sizes}
         in_place = True
     else:
-        out_f = torch.empty(layout.n_f32, dtype=torch.float32, device=device)
-        out_i = torch.empty(layout.n_i64, dtype=torch.int64, device=device)
+        outs = {g: torch.empty(n, dtype=_SEG_DTYPE[g], device=device) for g, n in sizes.items()}
         in_place = False
 
     w = [float(x) for x in weights]
-    if layout.n_f32:
-        ops.agg_f32(f32_ptrs, w, out_f, mode=mode)
-    if layout.n_i64:
-        ops.agg_i64(i64_ptrs, w, out_i)
+    for g in sizes:
+        _AGG[g](ptrs[g], w, outs[g], mode)
 
     if not in_place:
-        _write_back(target, layout, out_f, out_i)
+        _write_back(target, layout, outs)
     return target
 
 
-def _write_back(target: nn.Module, layout: StateLayout, out_f: torch.Tensor, out_i: torch.Tensor) -> None:
+def _write_back(target: nn.Module, layout: StateLayout, outs: dict) -> None:
     """load_state_dict(avg) equivalent: copy_ into the target's existing tensors."""
     sd = target.state_dict()
+    empty = {g: torch.empty(0, dtype=_SEG_DTYPE[g]) for g in _SEG_DTYPE}
     on_gpu = [t.device.type == "cuda" for t in sd.values()]
     if all(on_gpu):
-        views = layout.views(out_f, out_i)
+        segs = {g: outs.get(g, empty[g]) for g in _SEG_DTYPE}
+        views = layout.views(segs["f32"], segs["i64"], segs["b16"])
         with torch.no_grad():
             for name, t in sd.items():
                 t.copy_(views[name])
         return
-    hf = _pinned(4 * max(layout.n_f32, 1), "out_f32").view(torch.float32)[: layout.n_f32]
-    hi = _pinned(8 * max(layout.n_i64, 1), "out_i64").view(torch.int64)[: layout.n_i64]
-    hf.copy_(out_f, non_blocking=True)
-    hi.copy_(out_i, non_blocking=True)
-    torch.cuda.current_stream(out_f.device).synchronize()  # host reads hf / hi next
-    views = layout.views(hf, hi)
+    host = dict(empty)
+    dev = None
+    for g, o in outs.items():
+        esz = o.element_size()
+        host[g] = _pinned(esz * max(o.numel(), 1), "out_" + g).view(o.dtype)[: o.numel()]
+        host[g].copy_(o, non_blocking=True)
+        dev = o.device
+    if dev is not None:
+        torch.cuda.current_stream(dev).synchronize()  # host reads the buffers next
+    views = layout.views(host["f32"], host["i64"], host["b16"])
     with torch.no_grad():
         for name, t in sd.items():
             t.copy_(views[name])

@@ -1,9 +1,10 @@
 """Flattened state_dict layout and the device-resident model pool.
 
-A model's state_dict is split into two flat segments: every fp32 entry back to back (the
-"f32 segment", where the kernels stream) and every int64 entry (the "i64 segment",
-num_batches_tracked counters).  A ``ModelPool`` holds many models of one layout as rows of two
-2-D device tensors ``f32[rows, ld_f32]`` / ``i64[rows, ld_i64]`` (rows 256-B aligned), and can
+A model's state_dict is split into flat segments: every fp32 entry back to back (the "f32
+segment", where the kernels stream), every bf16 entry (the "b16 segment", bf16 models) and every
+int64 entry (the "i64 segment", num_batches_tracked counters).  A ``ModelPool`` holds many
+models of one layout as rows of 2-D device tensors ``f32[rows, ld_f32]`` / ``b16[rows, ld_b16]``
+/ ``i64[rows, ld_i64]`` (fp32 rows 256-B aligned, bf16 rows 128-B aligned), and can
 rebind an ``nn.Module``'s parameters and buffers to views of a row — so training, optimizers and
 the aggregation kernels all work on the same HBM bytes, with no pack/unpack per call
 (SURVEY §7 "state_dict flattening without re-packing every call", §8(f) rank 1).
@@ -17,8 +18,8 @@ from typing import Dict, List, Mapping, Optional, Sequence, Tuple
 import torch
 import torch.nn as nn
 
-SUPPORTED = {torch.float32: "f32", torch.int64: "i64"}
-ROW_ALIGN = 64  # elements: 256 B for fp32 rows
+SUPPORTED = {torch.float32: "f32", torch.int64: "i64", torch.bfloat16: "b16"}
+ROW_ALIGN = 64  # elements: 256 B for fp32 rows, 128 B for bf16 rows
 
 
 def _round_up(x: int, a: int) -> int:
@@ -30,7 +31,7 @@ class Entry:
     name: str
     shape: Tuple[int, ...]
     dtype: torch.dtype
-    seg: str          # "f32" | "i64"
+    seg: str          # "f32" | "b16" | "i64"
     offset: int       # element offset inside its segment
     numel: int
     alias_of: Optional[str] = None  # tied entry (same storage as an earlier key)
@@ -44,8 +45,10 @@ class StateLayout:
         self.by_name: Dict[str, Entry] = {e.name: e for e in self.entries}
         self.n_f32 = sum(e.numel for e in self.entries if e.seg == "f32" and e.alias_of is None)
         self.n_i64 = sum(e.numel for e in self.entries if e.seg == "i64" and e.alias_of is None)
+        self.n_b16 = sum(e.numel for e in self.entries if e.seg == "b16" and e.alias_of is None)
         self.ld_f32 = max(_round_up(self.n_f32, ROW_ALIGN), ROW_ALIGN)
         self.ld_i64 = max(_round_up(self.n_i64, 8), 8)
+        self.ld_b16 = max(_round_up(self.n_b16, ROW_ALIGN), ROW_ALIGN)
         self.key = tuple((e.name, e.shape, str(e.dtype), e.alias_of) for e in self.entries)
 
     def __eq__(self, other) -> bool:
@@ -57,13 +60,13 @@ class StateLayout:
     @classmethod
     def from_state_dict(cls, sd: Mapping[str, torch.Tensor]) -> "StateLayout":
         entries: List[Entry] = []
-        off = {"f32": 0, "i64": 0}
+        off = {"f32": 0, "i64": 0, "b16": 0}
         seen: Dict[Tuple[int, int, Tuple[int, ...]], str] = {}
         for name, t in sd.items():
             if t.dtype not in SUPPORTED:
                 raise NotImplementedError(
                     f"state_dict entry {name!r} has dtype {t.dtype}; the aggregation kernels handle "
-                    "float32 and int64 entries (all the reference models have)")
+                    "float32, bfloat16 and int64 entries")
             seg = SUPPORTED[t.dtype]
             key = (t.data_ptr(), t.storage_offset(), tuple(t.shape)) if t.numel() else None
             if key is not None and key in seen and t.is_contiguous():
@@ -78,10 +81,10 @@ class StateLayout:
 
     @classmethod
     def from_layout(cls, layout: Sequence[Tuple[str, Sequence[int], str]]) -> "StateLayout":
-        dt = {"float32": torch.float32, "int64": torch.int64}
+        dt = {"float32": torch.float32, "int64": torch.int64, "bfloat16": torch.bfloat16}
         sd = OrderedDict((n, torch.empty(tuple(s), dtype=dt[d], device="meta")) for n, s, d in layout)
         entries: List[Entry] = []
-        off = {"f32": 0, "i64": 0}
+        off = {"f32": 0, "i64": 0, "b16": 0}
         for name, t in sd.items():
             seg = SUPPORTED[t.dtype]
             n = 1
@@ -102,21 +105,22 @@ class StateLayout:
                                    f"{e.name!r} {e.shape} {e.dtype}")
 
     # ---------------------------------------------------------------------------------------
-    def views(self, f32: torch.Tensor, i64: torch.Tensor) -> "OrderedDict[str, torch.Tensor]":
+    def views(self, f32: torch.Tensor, i64: torch.Tensor,
+              b16: Optional[torch.Tensor] = None) -> "OrderedDict[str, torch.Tensor]":
         out: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+        segs = {"f32": f32, "i64": i64, "b16": b16}
         for e in self.entries:
-            base = f32 if e.seg == "f32" else i64
-            out[e.name] = base[e.offset: e.offset + e.numel].view(e.shape)
+            out[e.name] = segs[e.seg][e.offset: e.offset + e.numel].view(e.shape)
         return out
 
     def flatten_into(self, sd: Mapping[str, torch.Tensor], f32: torch.Tensor, i64: torch.Tensor,
-                     non_blocking: bool = False) -> None:
+                     non_blocking: bool = False, b16: Optional[torch.Tensor] = None) -> None:
         """Copy a state_dict's values into flat segment tensors (any devices)."""
+        segs = {"f32": f32, "i64": i64, "b16": b16}
         for e in self.entries:
             if e.alias_of is not None:
                 continue
-            base = f32 if e.seg == "f32" else i64
-            base[e.offset: e.offset + e.numel].copy_(sd[e.name].reshape(-1), non_blocking=non_blocking)
+            segs[e.seg][e.offset: e.offset + e.numel].copy_(sd[e.name].reshape(-1), non_blocking=non_blocking)
 
     def flatten_cat(self, sd: Mapping[str, torch.Tensor], seg: str) -> List[torch.Tensor]:
         return [sd[e.name].reshape(-1) for e in self.entries if e.seg == seg and e.alias_of is None]
@@ -157,15 +161,16 @@ def _resolve(module: nn.Module, name: str) -> Tuple[nn.Module, str]:
 
 
 class ModelPool:
-    """Rows of flat model state on one GPU: f32[rows, ld_f32], i64[rows, ld_i64]."""
+    """Rows of flat model state on one GPU: f32[rows, ld_f32], b16[rows, ld_b16], i64[rows, ld_i64]."""
 
     def __init__(self, layout: StateLayout, rows: int, device, f32: Optional[torch.Tensor] = None,
-                 i64: Optional[torch.Tensor] = None):
+                 i64: Optional[torch.Tensor] = None, b16: Optional[torch.Tensor] = None):
         self.layout = layout
         self.rows = rows
         self.device = torch.device(device)
         self.f32 = f32 if f32 is not None else torch.zeros(rows, layout.ld_f32, dtype=torch.float32, device=self.device)
         self.i64 = i64 if i64 is not None else torch.zeros(rows, layout.ld_i64, dtype=torch.int64, device=self.device)
+        self.b16 = b16 if b16 is not None else torch.zeros(rows, layout.ld_b16, dtype=torch.bfloat16, device=self.device)
         self._bound: Dict[int, int] = {}  # id(module) -> row
 
     def row_f32(self, r: int) -> torch.Tensor:
@@ -174,12 +179,21 @@ class ModelPool:
     def row_i64(self, r: int) -> torch.Tensor:
         return self.i64[r, : self.layout.n_i64]
 
+    def row_b16(self, r: int) -> torch.Tensor:
+        return self.b16[r, : self.layout.n_b16]
+
+    def segments(self):
+        """(name, pool tensor, elements per row) of the layout's non-empty segments."""
+        lay = self.layout
+        return [(k, t, n) for k, t, n in (("f32", self.f32, lay.n_f32), ("b16", self.b16, lay.n_b16),
+                                          ("i64", self.i64, lay.n_i64)) if n]
+
     def load_row(self, r: int, sd: Mapping[str, torch.Tensor]) -> None:
         self.layout.check_compatible(sd)
-        self.layout.flatten_into(sd, self.f32[r], self.i64[r])
+        self.layout.flatten_into(sd, self.f32[r], self.i64[r], b16=self.b16[r])
 
     def state_dict(self, r: int) -> "OrderedDict[str, torch.Tensor]":
-        return self.layout.views(self.f32[r], self.i64[r])
+        return self.layout.views(self.f32[r], self.i64[r], self.b16[r])
 
     def bind(self, module: nn.Module, r: int) -> nn.Module:
         """Copy `module`'s state into row r and make its parameters / buffers views of that row.
@@ -189,7 +203,7 @@ class ModelPool:
         sd = module.state_dict()
         self.layout.check_compatible(sd, "module")
         with torch.no_grad():
-            self.layout.flatten_into(sd, self.f32[r], self.i64[r])
+            self.layout.flatten_into(sd, self.f32[r], self.i64[r], b16=self.b16[r])
         views = self.state_dict(r)
         for e in self.layout.entries:
             if e.alias_of is not None:

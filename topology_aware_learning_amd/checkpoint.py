@@ -21,18 +21,20 @@ from .arena import ModelPool
 
 def pool_state_dicts_host(pool: ModelPool, rows: Sequence[int]) -> List["OrderedDict[str, torch.Tensor]"]:
     """State dicts of pool rows `rows` (in that order) as CPU tensors, copied with one D2H per
-    segment (fp32, int64) through pinned memory."""
+    segment (fp32, bf16, int64) through pinned memory."""
     rows = [int(r) for r in rows]
     lay = pool.layout
     pin = pool.device.type == "cuda"
-    f32 = torch.empty((len(rows), lay.ld_f32), dtype=torch.float32, pin_memory=pin)
-    i64 = torch.empty((len(rows), lay.ld_i64), dtype=torch.int64, pin_memory=pin)
-    for dst, src in ((f32, pool.f32), (i64, pool.i64)):
+    host = {id(t): torch.empty((len(rows), t.shape[1]), dtype=t.dtype, pin_memory=pin)
+            for t in (pool.f32, pool.i64, pool.b16)}
+    for _, src, _ in pool.segments():
+        dst = host[id(src)]
         for a, b, r0 in _runs(rows):  # consecutive pool rows move as one copy (no device temp)
             dst[a:b].copy_(src[r0: r0 + b - a], non_blocking=pin)
     if pin:
         torch.cuda.current_stream(pool.device).synchronize()
-    return [lay.views(f32[k], i64[k]) for k in range(len(rows))]
+    f32, i64, b16 = host[id(pool.f32)], host[id(pool.i64)], host[id(pool.b16)]
+    return [lay.views(f32[k], i64[k], b16[k]) for k in range(len(rows))]
 
 
 def _runs(rows):
@@ -58,13 +60,15 @@ def load_state_dicts_into_pool(pool: ModelPool, rows: Sequence[int], state_dicts
     one H2D per segment."""
     lay = pool.layout
     pin = pool.device.type == "cuda"
-    f32 = torch.zeros((len(rows), lay.ld_f32), dtype=torch.float32, pin_memory=pin)
-    i64 = torch.zeros((len(rows), lay.ld_i64), dtype=torch.int64, pin_memory=pin)
+    host = {id(t): torch.zeros((len(rows), t.shape[1]), dtype=t.dtype, pin_memory=pin)
+            for t in (pool.f32, pool.i64, pool.b16)}
+    f32, i64, b16 = host[id(pool.f32)], host[id(pool.i64)], host[id(pool.b16)]
     for k, sd in enumerate(state_dicts):
         lay.check_compatible(sd, "checkpoint state_dict")
-        lay.flatten_into(sd, f32[k], i64[k])
+        lay.flatten_into(sd, f32[k], i64[k], b16=b16[k])
     rows = [int(r) for r in rows]
-    for src, dst in ((f32, pool.f32), (i64, pool.i64)):
+    for _, dst, _ in pool.segments():
+        src = host[id(dst)]
         for a, b, r0 in _runs(rows):
             dst[r0: r0 + b - a].copy_(src[a:b], non_blocking=pin)
     if pin:  # the pinned staging buffers must outlive the copies

@@ -23,6 +23,7 @@
 #include <mutex>
 #include <string>
 #include <tuple>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/tal_agg.h"
@@ -31,7 +32,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 6;
+constexpr int kAbiVersion = 7;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -58,6 +59,7 @@ int32_t check_launch(const char* what) {
 }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+inline bool aligned8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }
 
 // ------------------------------------------------------------------------------------------
 // element arithmetic
@@ -358,6 +360,146 @@ __device__ __forceinline__ void st_stream(float* base, int64_t i, float4 v) {
   __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(base) + i);
 }
 
+// ------------------------------------------------------------------------------------------
+// Storage types: fp32 (float) and bf16 (uint16_t bit patterns).  Kernels index pools in chunks
+// of 4 elements (16 B fp32, 8 B bf16) and always compute in fp32.  Element k of a 32-bit bf16
+// word is its low half for k = 0 (little endian).
+// ------------------------------------------------------------------------------------------
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+
+// fp32 pair -> bf16 pair, round to nearest even (v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t cvt_bf16x2(float a, float b) {
+  bf16x2_t r;
+  r.x = static_cast<__bf16>(a);
+  r.y = static_cast<__bf16>(b);
+  return __builtin_bit_cast(uint32_t, r);
+}
+
+// The stored form: NaN becomes 0xFFFF, as torch's vectorized CPU fp32 -> bf16 conversion writes
+// it (the reference aggregates tensors, never single elements); NaN inputs stay NaN through the
+// intermediate roundings, so only the store canonicalises.
+__device__ __forceinline__ uint32_t store_bf16x2(float a, float b) {
+  uint32_t u = cvt_bf16x2(a, b);
+  if (a != a) u |= 0x0000ffffu;
+  if (b != b) u |= 0xffff0000u;
+  return u;
+}
+
+__device__ __forceinline__ float round_bf16(float a) { return bf16_lo(cvt_bf16x2(a, 0.f)); }
+
+__device__ __forceinline__ float4 round_bf16x4(float4 v) {
+  const uint32_t p = cvt_bf16x2(v.x, v.y), q = cvt_bf16x2(v.z, v.w);
+  return make_float4(bf16_lo(p), bf16_hi(p), bf16_lo(q), bf16_hi(q));
+}
+
+template <typename T>
+struct Io;
+
+template <>
+struct Io<float> {
+  static __device__ __forceinline__ float4 ld(const float* b, int64_t i4) { return ld_stream(b, i4); }
+  static __device__ __forceinline__ void st(float* b, int64_t i4, float4 v) { st_stream(b, i4, v); }
+  static __device__ __forceinline__ float ld1(const float* b, int64_t e) { return b[e]; }
+  static __device__ __forceinline__ void st1(float* b, int64_t e, float v) { b[e] = v; }
+};
+
+template <>
+struct Io<uint16_t> {
+  static __device__ __forceinline__ float4 ld(const uint16_t* b, int64_t i4) {
+    const u32x2 q = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(b) + i4);
+    return make_float4(bf16_lo(q.x), bf16_hi(q.x), bf16_lo(q.y), bf16_hi(q.y));
+  }
+  static __device__ __forceinline__ void st(uint16_t* b, int64_t i4, float4 v) {
+    const u32x2 q = {store_bf16x2(v.x, v.y), store_bf16x2(v.z, v.w)};
+    __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(b) + i4);
+  }
+  static __device__ __forceinline__ float ld1(const uint16_t* b, int64_t e) {
+    return __uint_as_float(static_cast<uint32_t>(b[e]) << 16);
+  }
+  static __device__ __forceinline__ void st1(uint16_t* b, int64_t e, float v) {
+    b[e] = static_cast<uint16_t>(store_bf16x2(v, 0.f) & 0xffffu);
+  }
+};
+
+template <typename T>
+constexpr bool kIsBf16 = std::is_same<T, uint16_t>::value;
+
+// Arithmetic per storage type.  fp32: first4 / next4.  bf16 EXACT: the reference's own ops on
+// bf16 tensors (decentralized_client.py:407-411: `w * clone(v)` and `+=` each round their fp32
+// result to bf16).  bf16 FMA: fp32 accumulation (fused), rounded once by the store.
+template <typename T, bool EXACT>
+__device__ __forceinline__ float4 first4t(float w, float4 x) {
+  if constexpr (kIsBf16<T> && EXACT) return round_bf16x4(mul4(w, x));
+  else return first4<EXACT>(w, x);
+}
+
+template <typename T, bool EXACT>
+__device__ __forceinline__ float4 next4t(float4 a, float w, float4 x) {
+  if constexpr (kIsBf16<T> && EXACT) return round_bf16x4(add4(a, round_bf16x4(mul4(w, x))));
+  else return next4<EXACT>(a, w, x);
+}
+
+template <typename T, bool EXACT>
+__device__ __forceinline__ float first1t(float w, float x) {
+  if constexpr (kIsBf16<T> && EXACT) return round_bf16(__fmul_rn(w, x));
+  else return first_term<EXACT>(w, x);
+}
+
+template <typename T, bool EXACT>
+__device__ __forceinline__ float next1t(float a, float w, float x) {
+  if constexpr (kIsBf16<T> && EXACT) return round_bf16(__fadd_rn(a, round_bf16(__fmul_rn(w, x))));
+  else return next_term<EXACT>(a, w, x);
+}
+
+// K1 on bf16 buffers: one call, chunks of 4 elements (8 B) per lane, operand loads in batches of
+// 8 ahead of the ordered accumulate.  All m <= kMaxOps operands are in the table (one pass), so
+// `out` may alias any of them.
+struct OpTableB16 {
+  const uint16_t* x[kMaxOps];
+  float w[kMaxOps];
+};
+
+template <bool EXACT>
+__global__ __launch_bounds__(kBlock) void k_agg_b16_vec(OpTableB16 t, int m, uint16_t* out, int64_t n4) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock * kK1Unroll;
+  for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * kBlock * kK1Unroll + threadIdx.x; i0 < n4;
+       i0 += stride) {
+#pragma unroll
+    for (int u = 0; u < kK1Unroll; ++u) {
+      const int64_t i = i0 + u * kBlock;
+      if (i >= n4) break;
+      float4 acc = first4t<uint16_t, EXACT>(t.w[0], Io<uint16_t>::ld(t.x[0], i));
+      for (int k = 1; k < m; k += 8) {
+        float4 v[8];
+        const int kn = min(8, m - k);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j < kn) v[j] = Io<uint16_t>::ld(t.x[k + j], i);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j < kn) acc = next4t<uint16_t, EXACT>(acc, t.w[k + j], v[j]);
+      }
+      Io<uint16_t>::st(out, i, acc);
+    }
+  }
+}
+
+// unaligned operands and the n % 4 tail
+template <bool EXACT>
+__global__ __launch_bounds__(kBlock) void k_agg_b16_scalar(OpTableB16 t, int m, uint16_t* out, int64_t e0,
+                                                           int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t e = e0 + static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n; e += stride) {
+    float acc = first1t<uint16_t, EXACT>(t.w[0], Io<uint16_t>::ld1(t.x[0], e));
+    for (int k = 1; k < m; ++k) acc = next1t<uint16_t, EXACT>(acc, t.w[k], Io<uint16_t>::ld1(t.x[k], e));
+    Io<uint16_t>::st1(out, e, acc);
+  }
+}
+
 // Compute one column tile from LDS.  A wavefront owns whole rows (row index wave-uniform, so
 // the plan entries — row extent, operand slots and weights — are scalar loads from the plan in
 // global memory, served by the scalar cache); each lane owns C4/64 float4 columns.  Operands are
@@ -371,9 +513,9 @@ typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(4))) const i32x4* ConstI32x4;
 typedef __attribute__((address_space(4))) const f32x8* ConstF32x8;
 
-template <int C4, int NT, bool EXACT>
+template <int C4, int NT, bool EXACT, typename T = float>
 __device__ __forceinline__ void emit_tile(const float4* s_data, const PlanView& p, int r_beg, int nr,
-                                          float* pout, int64_t ld_out4, int64_t c0, int64_t n4) {
+                                          T* pout, int64_t ld_out4, int64_t c0, int64_t n4) {
   constexpr int kB = C4 >= 128 ? 8 : 4;  // operands per batch (LDS reads in flight per lane)
   static_assert(C4 % 64 == 0, "a wavefront covers 64 float4 columns");
   constexpr int kWaves = NT / 64;
@@ -394,7 +536,7 @@ __device__ __forceinline__ void emit_tile(const float4* s_data, const PlanView& 
       const float w = op_w[q0];
       const int sl = op_slot[q0] * C4 + lane;
 #pragma unroll
-      for (int j = 0; j < kCpl; ++j) acc[j] = first4<EXACT>(w, s_data[sl + 64 * j]);
+      for (int j = 0; j < kCpl; ++j) acc[j] = first4t<T, EXACT>(w, s_data[sl + 64 * j]);
     }
     int q = q0 + 1;
     for (; q + kB <= q1; q += kB) {
@@ -413,18 +555,18 @@ __device__ __forceinline__ void emit_tile(const float4* s_data, const PlanView& 
 #pragma unroll
       for (int u = 0; u < kB; ++u)
 #pragma unroll
-        for (int j = 0; j < kCpl; ++j) acc[j] = next4<EXACT>(acc[j], w[u], x[u][j]);
+        for (int j = 0; j < kCpl; ++j) acc[j] = next4t<T, EXACT>(acc[j], w[u], x[u][j]);
     }
     for (; q < q1; ++q) {
       const float w = op_w[q];
       const int sl = op_slot[q] * C4 + lane;
 #pragma unroll
-      for (int j = 0; j < kCpl; ++j) acc[j] = next4<EXACT>(acc[j], w, s_data[sl + 64 * j]);
+      for (int j = 0; j < kCpl; ++j) acc[j] = next4t<T, EXACT>(acc[j], w, s_data[sl + 64 * j]);
     }
 #pragma unroll
     for (int j = 0; j < kCpl; ++j) {
       const int64_t col = c0 + lane + 64 * j;
-      if (col < n4) st_stream(pout, orow * ld_out4 + col, acc[j]);
+      if (col < n4) Io<T>::st(pout, orow * ld_out4 + col, acc[j]);
     }
   }
 }
@@ -516,10 +658,10 @@ constexpr size_t stream_lds_bytes(int cs) { return static_cast<size_t>(kStreamDe
 // Persistent form (the fast path): each workgroup walks column tiles t, t+gridDim.x, ...;
 // every lane owns J fixed staging slots (source, column) and keeps the next tile's J float4
 // loads in flight in registers while the workgroup computes the current tile from LDS.
-template <int C4, int NT, int J, bool EXACT, bool DENSE>
-__global__ __launch_bounds__(NT) void k_round_f32_persistent(const float* __restrict__ pin,
+template <int C4, int NT, int J, bool EXACT, bool DENSE, typename T = float>
+__global__ __launch_bounds__(NT) void k_round_f32_persistent(const T* __restrict__ pin,
                                                              int64_t ld_in4,
-                                                             float* __restrict__ pout,
+                                                             T* __restrict__ pout,
                                                              int64_t ld_out4, int64_t n4,
                                                              PlanView p, int64_t n_tiles) {
   extern __shared__ float4 s_data[];
@@ -544,7 +686,7 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const float* __rest
     if (col < n4) {
 #pragma unroll
       for (int j = 0; j < J; ++j)
-        if (srow[j] >= 0) v[j] = ld_stream(pin, static_cast<int64_t>(srow[j]) * ld_in4 + col);
+        if (srow[j] >= 0) v[j] = Io<T>::ld(pin, static_cast<int64_t>(srow[j]) * ld_in4 + col);
     }
   };
   int64_t t = blockIdx.x;
@@ -559,7 +701,7 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const float* __rest
     if constexpr (DENSE)
       emit_tile_dense<C4, NT, kDenseRb, EXACT>(s_data, p, g, r_beg, nr, ns, pout, ld_out4, t * C4, n4);
     else
-      emit_tile<C4, NT, EXACT>(s_data, p, r_beg, nr, pout, ld_out4, t * C4, n4);
+      emit_tile<C4, NT, EXACT, T>(s_data, p, r_beg, nr, pout, ld_out4, t * C4, n4);
   }
 }
 
@@ -588,8 +730,7 @@ __host__ __device__ constexpr size_t narrow_lds_bytes(int64_t max_src, int64_t m
 }
 
 template <int C4>
-__device__ __forceinline__ NarrowLds stage_narrow(const PlanView& p, int g, float4* s_data, int max_src,
-                                                  int nthreads) {
+__device__ __forceinline__ NarrowLds stage_narrow(const PlanView& p, int g, float4* s_data, int nthreads) {
   NarrowLds L;
   const int r_beg = p.grp_row_ptr[g];
   L.nr = p.grp_row_ptr[g + 1] - r_beg;
@@ -597,11 +738,12 @@ __device__ __forceinline__ NarrowLds stage_narrow(const PlanView& p, int g, floa
   const int32_t* np = p.npairs;
   const int e_beg = nrp[r_beg];
   const int ne = nrp[r_beg + L.nr] - e_beg;
-  int32_t* rowptr = reinterpret_cast<int32_t*>(s_data + static_cast<size_t>(max_src + 1) * C4);
+  const int ns = p.grp_src_ptr[g + 1] - p.grp_src_ptr[g];  // the -0.0 tile is slot ns
+  int32_t* rowptr = reinterpret_cast<int32_t*>(s_data + static_cast<size_t>(ns + 1) * C4);
   int2* pairs = reinterpret_cast<int2*>(rowptr + ((L.nr + 2) & ~1));
   int32_t* out = reinterpret_cast<int32_t*>(pairs + ne + 4);
   for (int k = threadIdx.x; k < C4; k += nthreads)  // the padding pairs' tile of -0.0
-    s_data[static_cast<size_t>(max_src) * C4 + k] = make_float4(-0.f, -0.f, -0.f, -0.f);
+    s_data[static_cast<size_t>(ns) * C4 + k] = make_float4(-0.f, -0.f, -0.f, -0.f);
   for (int k = threadIdx.x; k <= L.nr; k += nthreads) rowptr[k] = nrp[r_beg + k] - e_beg;
   for (int k = threadIdx.x; k < ne + 4; k += nthreads)  // + 4 read-ahead pairs (never used)
     pairs[k] = k < ne ? make_int2(np[2 * (e_beg + k)], np[2 * (e_beg + k) + 1]) : make_int2(0, 0);
@@ -614,10 +756,10 @@ __device__ __forceinline__ NarrowLds stage_narrow(const PlanView& p, int g, floa
 
 // One row (pairs q0 .. q1-1, q1 - q0 - 1 a multiple of 4) for this lane's column.  PIPE: the
 // next batch's pairs are read while this batch's data reads are in flight (8 more VGPRs).
-template <bool EXACT, bool PIPE>
+template <typename T, bool EXACT, bool PIPE>
 __device__ __forceinline__ float4 narrow_row(const float4* s_data, const int2* pairs, int q0, int q1, int cl) {
   const int2 f = pairs[q0];
-  float4 acc = first4<EXACT>(__int_as_float(f.y), s_data[f.x + cl]);
+  float4 acc = first4t<T, EXACT>(__int_as_float(f.y), s_data[f.x + cl]);
   int q = q0 + 1;
   if constexpr (!PIPE) {
     for (; q < q1; q += 4) {
@@ -628,7 +770,7 @@ __device__ __forceinline__ float4 narrow_row(const float4* s_data, const int2* p
 #pragma unroll
       for (int u = 0; u < 4; ++u) x[u] = s_data[e[u].x + cl];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc = next4<EXACT>(acc, __int_as_float(e[u].y), x[u]);
+      for (int u = 0; u < 4; ++u) acc = next4t<T, EXACT>(acc, __int_as_float(e[u].y), x[u]);
     }
     return acc;
   }
@@ -644,7 +786,7 @@ __device__ __forceinline__ float4 narrow_row(const float4* s_data, const int2* p
 #pragma unroll
       for (int u = 0; u < 4; ++u) en[u] = pairs[q + 4 + u];  // next batch (or the read-ahead pad)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc = next4<EXACT>(acc, __int_as_float(e[u].y), x[u]);
+      for (int u = 0; u < 4; ++u) acc = next4t<T, EXACT>(acc, __int_as_float(e[u].y), x[u]);
 #pragma unroll
       for (int u = 0; u < 4; ++u) e[u] = en[u];
       q += 4;
@@ -661,17 +803,17 @@ __device__ __forceinline__ int narrow_set(int p, int wave, int nwaves) {
 
 // NP = row sets held in registers: kNarrowPasses for one resident workgroup per CU (128 VGPRs),
 // 0 for two (64 VGPRs: the extents are then read from LDS each pass).
-template <int C4, int NT, int J, int NP, bool EXACT>
+template <int C4, int NT, int J, int NP, bool EXACT, typename T = float>
 __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round_f32_narrow(
-    const float* __restrict__ pin, int64_t ld_in4, float* __restrict__ pout, int64_t ld_out4, int64_t n4,
-    PlanView p, int64_t n_tiles, int max_src) {
+    const T* __restrict__ pin, int64_t ld_in4, T* __restrict__ pout, int64_t ld_out4, int64_t n4,
+    PlanView p, int64_t n_tiles) {
   static_assert(C4 == 16 || C4 == 32, "narrow tiles are 16 or 32 float4 wide");
   static_assert(NT % C4 == 0, "a block stages whole source tiles");
   constexpr int kRpw = 64 / C4;
   constexpr int kW = NT / 64;
   extern __shared__ float4 s_data[];
   const int g = blockIdx.y;
-  const NarrowLds L = stage_narrow<C4>(p, g, s_data, max_src, NT);
+  const NarrowLds L = stage_narrow<C4>(p, g, s_data, NT);
   const int s_beg = p.grp_src_ptr[g];
   const int ns = p.grp_src_ptr[g + 1] - s_beg;
   const int c = threadIdx.x % C4;
@@ -702,7 +844,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
     if (col < n4) {
 #pragma unroll
       for (int j = 0; j < J; ++j)
-        if (srow[j] >= 0) v[j] = ld_stream(pin, static_cast<int64_t>(srow[j]) * ld_in4 + col);
+        if (srow[j] >= 0) v[j] = Io<T>::ld(pin, static_cast<int64_t>(srow[j]) * ld_in4 + col);
     }
   };
   int64_t t = blockIdx.x;
@@ -718,15 +860,15 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       if (rq1[k] > rq0[k]) {
-        const float4 acc = narrow_row<EXACT, (NP > 0)>(s_data, L.pairs, rq0[k], rq1[k], cl);
-        if (col < n4) st_stream(pout, static_cast<int64_t>(rout[k]) * ld_out4 + col, acc);
+        const float4 acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, rq0[k], rq1[k], cl);
+        if (col < n4) Io<T>::st(pout, static_cast<int64_t>(rout[k]) * ld_out4 + col, acc);
       }
     }
     for (int k = NP; k * kW < n_sets; ++k) {  // row sets beyond the register-held ones
       const int r = narrow_set(k, wave, kW) * kRpw + sub;
       if (r < L.nr) {
-        const float4 acc = narrow_row<EXACT, (NP > 0)>(s_data, L.pairs, L.rowptr[r], L.rowptr[r + 1], cl);
-        if (col < n4) st_stream(pout, static_cast<int64_t>(L.out[r]) * ld_out4 + col, acc);
+        const float4 acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, L.rowptr[r], L.rowptr[r + 1], cl);
+        if (col < n4) Io<T>::st(pout, static_cast<int64_t>(L.out[r]) * ld_out4 + col, acc);
       }
     }
   }
@@ -734,9 +876,9 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
 
 // General form (groups whose staging needs more than 8 loads per lane): one tile per
 // workgroup, staging in batches of 4 independent loads per lane.
-template <int C4, int NT, bool EXACT, bool DENSE>
-__global__ __launch_bounds__(NT) void k_round_f32_tiled(const float* __restrict__ pin,
-                                                        int64_t ld_in4, float* __restrict__ pout,
+template <int C4, int NT, bool EXACT, bool DENSE, typename T = float>
+__global__ __launch_bounds__(NT) void k_round_f32_tiled(const T* __restrict__ pin,
+                                                        int64_t ld_in4, T* __restrict__ pout,
                                                         int64_t ld_out4, int64_t n4, PlanView p) {
   extern __shared__ float4 s_data[];
   const int g = blockIdx.y;
@@ -755,7 +897,7 @@ __global__ __launch_bounds__(NT) void k_round_f32_tiled(const float* __restrict_
       const int c = k % C4;
       v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (k < total && c0 + c < n4)
-        v[u] = ld_stream(pin, static_cast<int64_t>(p.src_row[s_beg + k / C4]) * ld_in4 + c0 + c);
+        v[u] = Io<T>::ld(pin, static_cast<int64_t>(p.src_row[s_beg + k / C4]) * ld_in4 + c0 + c);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -767,21 +909,21 @@ __global__ __launch_bounds__(NT) void k_round_f32_tiled(const float* __restrict_
   if constexpr (DENSE)
     emit_tile_dense<C4, NT, kDenseRb, EXACT>(s_data, p, g, r_beg, nr, ns, pout, ld_out4, c0, n4);
   else
-    emit_tile<C4, NT, EXACT>(s_data, p, r_beg, nr, pout, ld_out4, c0, n4);
+    emit_tile<C4, NT, EXACT, T>(s_data, p, r_beg, nr, pout, ld_out4, c0, n4);
 }
 
 // Scalar tiled round: the fp32 tail (elements e0..n-1 when the float4 path ran) or whole
 // unaligned pools, and the int64 segment (IS_I64: fp32 accumulate, truncation).  The tile is
 // 4*c4 elements so one staged source costs the same 16*c4 LDS bytes as in the float4 kernel.
-template <bool IS_I64, bool EXACT>
-__global__ __launch_bounds__(kBlock) void k_round_tiled_scalar(const void* __restrict__ pin_v,
-                                                               int64_t ld_in,
-                                                               void* __restrict__ pout_v,
-                                                               int64_t ld_out, int64_t e0,
-                                                               int64_t n, PlanView p,
-                                                               int max_src, int tile) {
+template <typename T, bool EXACT>
+__global__ __launch_bounds__(kBlock) void k_round_tiled_scalar(const T* __restrict__ pin, int64_t ld_in,
+                                                               T* __restrict__ pout, int64_t ld_out,
+                                                               int64_t e0, int64_t n, PlanView p,
+                                                               int tile) {
+  constexpr bool kI64 = std::is_same<T, int64_t>::value;
   extern __shared__ float s_f[];
-  const GroupLds L = stage_group(p, blockIdx.y, s_f + static_cast<size_t>(max_src) * tile, tile, kBlock);
+  const int ns = p.grp_src_ptr[blockIdx.y + 1] - p.grp_src_ptr[blockIdx.y];
+  const GroupLds L = stage_group(p, blockIdx.y, s_f + static_cast<size_t>(ns) * tile, tile, kBlock);
   __syncthreads();
   const int64_t t0 = e0 + static_cast<int64_t>(blockIdx.x) * tile;
   const int64_t cols = min(static_cast<int64_t>(tile), n - t0);
@@ -791,11 +933,8 @@ __global__ __launch_bounds__(kBlock) void k_round_tiled_scalar(const void* __res
     float v = 0.f;
     if (c < cols) {
       const int64_t row = L.src[s];
-      if constexpr (IS_I64) {
-        v = static_cast<float>(static_cast<const int64_t*>(pin_v)[row * ld_in + t0 + c]);
-      } else {
-        v = static_cast<const float*>(pin_v)[row * ld_in + t0 + c];
-      }
+      if constexpr (kI64) v = static_cast<float>(pin[row * ld_in + t0 + c]);
+      else v = Io<T>::ld1(pin, row * ld_in + t0 + c);
     }
     s_f[k] = v;
   }
@@ -805,21 +944,11 @@ __global__ __launch_bounds__(kBlock) void k_round_tiled_scalar(const void* __res
     for (int r = 0; r < L.nr; ++r) {
       const int q0 = L.rowptr[r];
       const int q1 = L.rowptr[r + 1];
-      float acc;
-      if constexpr (IS_I64) {
-        acc = __fmul_rn(L.w[q0], s_f[L.slot[q0] + c]);
-        for (int q = q0 + 1; q < q1; ++q)
-          acc = __fadd_rn(acc, __fmul_rn(L.w[q], s_f[L.slot[q] + c]));
-      } else {
-        acc = first_term<EXACT>(L.w[q0], s_f[L.slot[q0] + c]);
-        for (int q = q0 + 1; q < q1; ++q) acc = next_term<EXACT>(acc, L.w[q], s_f[L.slot[q] + c]);
-      }
+      float acc = first1t<T, EXACT || kI64>(L.w[q0], s_f[L.slot[q0] + c]);
+      for (int q = q0 + 1; q < q1; ++q) acc = next1t<T, EXACT || kI64>(acc, L.w[q], s_f[L.slot[q] + c]);
       const int64_t orow = L.out[r];
-      if constexpr (IS_I64) {
-        static_cast<int64_t*>(pout_v)[orow * ld_out + t0 + c] = trunc_i64(acc);
-      } else {
-        static_cast<float*>(pout_v)[orow * ld_out + t0 + c] = acc;
-      }
+      if constexpr (kI64) pout[orow * ld_out + t0 + c] = trunc_i64(acc);
+      else Io<T>::st1(pout, orow * ld_out + t0 + c, acc);
     }
   }
 }
@@ -1074,11 +1203,12 @@ __global__ __launch_bounds__(kBlock) void k_round_stream_scalar(const void* __re
 // plans alike (src_row / op_slot mean the same in every form).
 constexpr int64_t kDirectMaxCols = 256;
 
-template <bool IS_I64, bool EXACT>
-__global__ __launch_bounds__(kBlock) void k_round_direct(const void* __restrict__ pin_v, int64_t ld_in,
-                                                         void* __restrict__ pout_v, int64_t ld_out,
+template <typename T, bool EXACT>
+__global__ __launch_bounds__(kBlock) void k_round_direct(const T* __restrict__ pin, int64_t ld_in,
+                                                         T* __restrict__ pout, int64_t ld_out,
                                                          int64_t e0, int cols, int rows, int n_groups,
                                                          PlanView p) {
+  constexpr bool kI64 = std::is_same<T, int64_t>::value;
   const int k = blockIdx.x * kBlock + threadIdx.x;
   if (k >= rows * cols) return;
   const int r = k / cols;
@@ -1089,34 +1219,34 @@ __global__ __launch_bounds__(kBlock) void k_round_direct(const void* __restrict_
   const int q0 = p.row_ptr[r], q1 = p.row_ptr[r + 1];
   auto load = [&](int q) -> float {
     const int64_t row = p.src_row[s_beg + p.op_slot[q]];
-    if constexpr (IS_I64) return static_cast<float>(static_cast<const int64_t*>(pin_v)[row * ld_in + e]);
-    else return static_cast<const float*>(pin_v)[row * ld_in + e];
+    if constexpr (kI64) return static_cast<float>(pin[row * ld_in + e]);
+    else return Io<T>::ld1(pin, row * ld_in + e);
   };
-  constexpr bool kExact = EXACT || IS_I64;
-  float acc = first_term<kExact>(p.op_w[q0], load(q0));
+  float acc = first1t<T, EXACT>(p.op_w[q0], load(q0));
   int q = q0 + 1;
   for (; q + 8 <= q1; q += 8) {
     float x[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) x[u] = load(q + u);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc = next_term<kExact>(acc, p.op_w[q + u], x[u]);
+    for (int u = 0; u < 8; ++u) acc = next1t<T, EXACT>(acc, p.op_w[q + u], x[u]);
   }
-  for (; q < q1; ++q) acc = next_term<kExact>(acc, p.op_w[q], load(q));
+  for (; q < q1; ++q) acc = next1t<T, EXACT>(acc, p.op_w[q], load(q));
   const int64_t orow = p.out_row[r];
-  if constexpr (IS_I64) static_cast<int64_t*>(pout_v)[orow * ld_out + e] = trunc_i64(acc);
-  else static_cast<float*>(pout_v)[orow * ld_out + e] = acc;
+  if constexpr (kI64) pout[orow * ld_out + e] = trunc_i64(acc);
+  else Io<T>::st1(pout, orow * ld_out + e, acc);
 }
 
-template <bool IS_I64>
-int32_t launch_round_direct(const void* pin, int64_t ld_in, void* pout, int64_t ld_out, int64_t e0,
+template <typename T>
+int32_t launch_round_direct(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t e0,
                             int64_t n, const PlanView& v, const tal_round_plan_info& in, bool exact,
                             hipStream_t s) {
-  const int cols = static_cast<int>(n - e0);
-  const int64_t threads = static_cast<int64_t>(cols) * in.rows;
+  const int64_t cols = n - e0;
+  const int64_t threads = cols * in.rows;
+  if (threads > 0x7fffffffLL) return fail(TAL_ERR_INVALID, "round direct kernel: too many elements");
   const unsigned blocks = static_cast<unsigned>((threads + kBlock - 1) / kBlock);
-  auto k = (IS_I64 || exact) ? k_round_direct<IS_I64, true> : k_round_direct<IS_I64, false>;
-  k<<<blocks, kBlock, 0, s>>>(pin, ld_in, pout, ld_out, e0, cols, in.rows, in.n_groups, v);
+  auto k = (std::is_same<T, int64_t>::value || exact) ? k_round_direct<T, true> : k_round_direct<T, false>;
+  k<<<blocks, kBlock, 0, s>>>(pin, ld_in, pout, ld_out, e0, static_cast<int>(cols), in.rows, in.n_groups, v);
   return check_launch("round direct kernel");
 }
 
@@ -1125,9 +1255,10 @@ inline bool use_direct(const void* pin, const void* pout, int64_t e0, int64_t n)
   return pin != pout && n > e0 && n - e0 <= kDirectMaxCols;
 }
 
-size_t plan_lds_bytes(const tal_round_plan_info& in, int tile_bytes_per_src) {
-  return static_cast<size_t>(in.max_src) * tile_bytes_per_src +
-         static_cast<size_t>(in.max_rows + 1 + 2 * in.max_nnz + in.max_src + in.max_rows) * 4;
+// LDS of one group in the staged scalar kernel (and the float4 kernels' tile): its sources'
+// tile (16 * c4 B each) plus its plan slice [row_ptr (nr+1)][slot (no)][w (no)][src (ns)][out (nr)]
+constexpr int64_t group_lds_bytes(int64_t ns, int64_t nr, int64_t no, int c4) {
+  return ns * 16 * c4 + (nr + 1 + 2 * no + ns + nr) * 4;
 }
 
 std::mutex g_lds_mu;
@@ -1164,20 +1295,20 @@ int32_t validate_info(const tal_round_plan_info* info) {
   return TAL_OK;
 }
 
-template <bool IS_I64>
-int32_t launch_round_scalar(const void* pin, int64_t ld_in, void* pout, int64_t ld_out,
+template <typename T>
+int32_t launch_round_scalar(const T* pin, int64_t ld_in, T* pout, int64_t ld_out,
                             int64_t e0, int64_t n, const PlanView& v,
                             const tal_round_plan_info& in, bool exact, hipStream_t s) {
   if (n <= e0) return TAL_OK;
   const int tile = 4 * in.c4;
-  const size_t lds = plan_lds_bytes(in, tile * 4);
+  const size_t lds = static_cast<size_t>(in.lds_bytes);  // the largest group's tile + plan slice
   const int64_t tiles = (n - e0 + tile - 1) / tile;
   if (tiles > 0x7fffffff) return fail(TAL_ERR_INVALID, "too many tiles");
   const dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(in.n_groups));
-  auto k = (IS_I64 || exact) ? k_round_tiled_scalar<IS_I64, true> : k_round_tiled_scalar<IS_I64, false>;
+  auto k = (std::is_same<T, int64_t>::value || exact) ? k_round_tiled_scalar<T, true> : k_round_tiled_scalar<T, false>;
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;
-  k<<<grid, kBlock, lds, s>>>(pin, ld_in, pout, ld_out, e0, n, v, in.max_src, tile);
+  k<<<grid, kBlock, lds, s>>>(pin, ld_in, pout, ld_out, e0, n, v, tile);
   return check_launch("round scalar kernel");
 }
 
@@ -1187,12 +1318,12 @@ int32_t launch_round_scalar(const void* pin, int64_t ld_in, void* pout, int64_t 
 template <int C4>
 constexpr int round_threads() { return C4 >= 128 ? 512 : 1024; }
 
-template <int C4, int J, bool EXACT, bool DENSE>
-int32_t launch_round_persistent(const float* pin, int64_t ld_in, float* pout, int64_t ld_out,
+template <int C4, int J, bool EXACT, bool DENSE, typename T = float>
+int32_t launch_round_persistent(const T* pin, int64_t ld_in, T* pout, int64_t ld_out,
                                 int64_t n4, const PlanView& v, const tal_round_plan_info& in,
                                 size_t lds, hipStream_t s) {
   constexpr int kRoundThreads = round_threads<C4>();
-  auto k = k_round_f32_persistent<C4, kRoundThreads, J, EXACT, DENSE>;
+  auto k = k_round_f32_persistent<C4, kRoundThreads, J, EXACT, DENSE, T>;
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;
   const int64_t tiles = (n4 + C4 - 1) / C4;
@@ -1223,16 +1354,16 @@ int resident_per_cu(const void* kernel, int threads, size_t lds) {
   return nb;
 }
 
-template <int C4, int J, bool EXACT>
-int32_t launch_round_narrow_j(const float* pin, int64_t ld_in, float* pout, int64_t ld_out, int64_t n4,
+template <int C4, int J, bool EXACT, typename T = float>
+int32_t launch_round_narrow_j(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
                               const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
   const size_t lds = static_cast<size_t>(in.lds_bytes);
   // two workgroups per CU when their LDS allows it (registers capped at 64), else one with the
   // row extents in registers
   constexpr int kNP = J >= 12 ? kNarrowPasses / 2 : kNarrowPasses;  // J = 12: VGPRs for the staging
-  auto k = k_round_f32_narrow<C4, kNarrowThreads, J, kNP, EXACT>;
+  auto k = k_round_f32_narrow<C4, kNarrowThreads, J, kNP, EXACT, T>;
   if constexpr (J <= 4)
-    if (2 * lds <= 160 * 1024) k = k_round_f32_narrow<C4, kNarrowThreads, J, 0, EXACT>;
+    if (2 * lds <= 160 * 1024) k = k_round_f32_narrow<C4, kNarrowThreads, J, 0, EXACT, T>;
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;
   const int64_t tiles = (n4 + C4 - 1) / C4;
@@ -1240,19 +1371,19 @@ int32_t launch_round_narrow_j(const float* pin, int64_t ld_in, float* pout, int6
   int64_t gx = std::max<int64_t>(1, 256 * per_cu / in.n_groups);
   gx = std::min<int64_t>(gx, tiles);
   const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(in.n_groups));
-  k<<<grid, kNarrowThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles, in.max_src);
+  k<<<grid, kNarrowThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles);
   return check_launch("round kernel (narrow tiles)");
 }
 
-template <int C4, bool EXACT>
-int32_t launch_round_narrow(const float* pin, int64_t ld_in, float* pout, int64_t ld_out, int64_t n4,
+template <int C4, bool EXACT, typename T = float>
+int32_t launch_round_narrow(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
                             const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
   const int64_t loads = static_cast<int64_t>(in.max_src) * C4;  // float4 staging loads per tile
-  if (loads <= 1LL * kNarrowThreads) return launch_round_narrow_j<C4, 1, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, s);
-  if (loads <= 2LL * kNarrowThreads) return launch_round_narrow_j<C4, 2, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, s);
-  if (loads <= 4LL * kNarrowThreads) return launch_round_narrow_j<C4, 4, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, s);
-  if (loads <= 8LL * kNarrowThreads) return launch_round_narrow_j<C4, 8, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, s);
-  if (loads <= 12LL * kNarrowThreads) return launch_round_narrow_j<C4, 12, EXACT>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  if (loads <= 1LL * kNarrowThreads) return launch_round_narrow_j<C4, 1, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  if (loads <= 2LL * kNarrowThreads) return launch_round_narrow_j<C4, 2, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  if (loads <= 4LL * kNarrowThreads) return launch_round_narrow_j<C4, 4, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  if (loads <= 8LL * kNarrowThreads) return launch_round_narrow_j<C4, 8, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  if (loads <= 12LL * kNarrowThreads) return launch_round_narrow_j<C4, 12, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
   return fail(TAL_ERR_CAPACITY, "narrow round plan: group tile larger than 160 KiB");
 }
 
@@ -1305,21 +1436,21 @@ int32_t launch_round_stream_scalar(const void* pin, int64_t ld_in, void* pout, i
   return check_launch("round scalar kernel (streamed plan)");
 }
 
-template <int C4, bool EXACT, bool DENSE>
-int32_t launch_round_vec(const float* pin, int64_t ld_in, float* pout, int64_t ld_out, int64_t n4,
+template <int C4, bool EXACT, bool DENSE, typename T = float>
+int32_t launch_round_vec(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
                          const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
   constexpr int kRoundThreads = round_threads<C4>();
   const size_t lds = static_cast<size_t>(in.max_src) * C4 * 16;
   const int64_t loads = static_cast<int64_t>(in.max_src) * C4;  // float4 staging loads per tile
-  if (loads <= 1LL * kRoundThreads) return launch_round_persistent<C4, 1, EXACT, DENSE>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
-  if (loads <= 2LL * kRoundThreads) return launch_round_persistent<C4, 2, EXACT, DENSE>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
-  if (loads <= 4LL * kRoundThreads) return launch_round_persistent<C4, 4, EXACT, DENSE>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
-  if (loads <= 8LL * kRoundThreads) return launch_round_persistent<C4, 8, EXACT, DENSE>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+  if (loads <= 1LL * kRoundThreads) return launch_round_persistent<C4, 1, EXACT, DENSE, T>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+  if (loads <= 2LL * kRoundThreads) return launch_round_persistent<C4, 2, EXACT, DENSE, T>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+  if (loads <= 4LL * kRoundThreads) return launch_round_persistent<C4, 4, EXACT, DENSE, T>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+  if (loads <= 8LL * kRoundThreads) return launch_round_persistent<C4, 8, EXACT, DENSE, T>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
   if constexpr (kRoundThreads <= 512) {  // 16-20 float4 in flight per lane: 512-thread blocks only (VGPRs)
-    if (loads <= 16LL * kRoundThreads) return launch_round_persistent<C4, 16, EXACT, DENSE>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
-    if (loads <= 20LL * kRoundThreads) return launch_round_persistent<C4, 20, EXACT, DENSE>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+    if (loads <= 16LL * kRoundThreads) return launch_round_persistent<C4, 16, EXACT, DENSE, T>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
+    if (loads <= 20LL * kRoundThreads) return launch_round_persistent<C4, 20, EXACT, DENSE, T>(pin, ld_in, pout, ld_out, n4, v, in, lds, s);
   }
-  auto k = k_round_f32_tiled<C4, kRoundThreads, EXACT, DENSE>;
+  auto k = k_round_f32_tiled<C4, kRoundThreads, EXACT, DENSE, T>;
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;
   const int64_t tiles = (n4 + C4 - 1) / C4;
@@ -1717,6 +1848,12 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
   // batches of 4 with (max_src * c4, 1.0f): the kernel's -0.0 tile makes them exact identities
   std::vector<int32_t> nrp, npr;
   int64_t max_np = 0;
+  int64_t lds_need = 0;  // the largest group's LDS (exact, per group: what the kernels carve)
+  for (int g = 0; g < G; ++g) {
+    const int64_t nr = grp_row_ptr[g + 1] - grp_row_ptr[g];
+    const int64_t no = row_ptr_host[grp_row_ptr[g + 1]] - row_ptr_host[grp_row_ptr[g]];
+    lds_need = std::max(lds_need, group_lds_bytes(grp_src_ptr[g + 1] - grp_src_ptr[g], nr, no, c4));
+  }
   if (c4 < 64) {
     nrp.assign(static_cast<size_t>(rows) + 1, 0);
     const float one = 1.0f;
@@ -1734,12 +1871,15 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
           npr.push_back(wb);
         }
         for (int32_t pad = (4 - (k1 - k0 - 1) % 4) % 4; pad > 0; --pad) {
-          npr.push_back(max_src * c4);
+          npr.push_back((grp_src_ptr[g + 1] - grp_src_ptr[g]) * c4);  // the group's -0.0 tile
           npr.push_back(one_bits);
         }
         nrp[r + 1] = static_cast<int32_t>(npr.size() / 2);
       }
-      max_np = std::max<int64_t>(max_np, static_cast<int64_t>(npr.size()) / 2 - g0);
+      const int64_t gp = static_cast<int64_t>(npr.size()) / 2 - g0;
+      max_np = std::max<int64_t>(max_np, gp);
+      lds_need = std::max<int64_t>(lds_need, static_cast<int64_t>(narrow_lds_bytes(
+          grp_src_ptr[g + 1] - grp_src_ptr[g], grp_row_ptr[g + 1] - grp_row_ptr[g], gp, c4)));
     }
   }
 
@@ -1775,10 +1915,7 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
   in.max_npairs = static_cast<int32_t>(max_np);
   if (off > 0x7fffffff) return fail(TAL_ERR_INVALID, "tal_round_plan_build: plan larger than 2^31 words");
   in.words = static_cast<int32_t>(off);
-  in.lds_bytes = static_cast<int32_t>(stream_cs > 0 ? stream_lds_bytes(stream_cs) : plan_lds_bytes(in, 16 * c4));
-  if (c4 < 64)  // the narrow kernel's carve (the scalar tail kernel's fits in the same budget)
-    in.lds_bytes = static_cast<int32_t>(std::max<size_t>(narrow_lds_bytes(max_src, max_rows, max_np, c4),
-                                                         plan_lds_bytes(in, 16 * c4)));
+  in.lds_bytes = static_cast<int32_t>(stream_cs > 0 ? stream_lds_bytes(stream_cs) : lds_need);
   if (!plan_host || off > plan_capacity_words) {
     *info = in;
     return fail(TAL_ERR_CAPACITY, "tal_round_plan_build: plan buffer too small: need " +
@@ -1951,9 +2088,8 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
     return fail(TAL_ERR_INVALID, "tal_round_plan_build: dense_rb must be 0, 8 or -1");
   // group consecutive rows while the union of their sources fits the LDS budget (both round
   // kernels stage 16*c4 bytes per source; the scalar one also the plan slice)
-  const int64_t per_src = 16LL * c4;
   auto fits = [&](int64_t ns, int64_t nr, int64_t no) {
-    const int64_t sliced = ns * per_src + (nr + 1 + 2 * no + ns + nr) * 4;
+    const int64_t sliced = group_lds_bytes(ns, nr, no, c4);
     if (c4 >= 64) return sliced <= lds_bytes;
     // narrow kernel: + the -0.0 tile, pairs padded (<= 3 per row) and read-ahead
     return std::max<int64_t>(sliced, static_cast<int64_t>(narrow_lds_bytes(ns, nr, no + 3 * nr, c4))) <= lds_bytes;
@@ -2065,10 +2201,10 @@ int32_t tal_agg_round_f32(const float* pool_in, int64_t ld_in, float* pool_out, 
   }
   if (n <= e_vec) return TAL_OK;
   if (use_direct(pool_in, pool_out, e_vec, n))
-    return launch_round_direct<false>(pool_in, ld_in, pool_out, ld_out, e_vec, n, v, *info, exact, s);
+    return launch_round_direct<float>(pool_in, ld_in, pool_out, ld_out, e_vec, n, v, *info, exact, s);
   if (info->stream_cs > 0)
     return launch_round_stream_scalar<false>(pool_in, ld_in, pool_out, ld_out, e_vec, n, v, *info, exact, s);
-  return launch_round_scalar<false>(pool_in, ld_in, pool_out, ld_out, e_vec, n, v, *info, exact, s);
+  return launch_round_scalar<float>(pool_in, ld_in, pool_out, ld_out, e_vec, n, v, *info, exact, s);
 }
 
 int32_t tal_agg_round_i64(const int64_t* pool_in, int64_t ld_in, int64_t* pool_out, int64_t ld_out,
@@ -2084,13 +2220,88 @@ int32_t tal_agg_round_i64(const int64_t* pool_in, int64_t ld_in, int64_t* pool_o
   if (n == 0) { g_err.clear(); return TAL_OK; }
   const PlanView v = make_view(plan_dev, *info);
   if (use_direct(pool_in, pool_out, 0, n))
-    return launch_round_direct<true>(pool_in, ld_in, pool_out, ld_out, 0, n, v, *info, true,
+    return launch_round_direct<int64_t>(pool_in, ld_in, pool_out, ld_out, 0, n, v, *info, true,
                                      static_cast<hipStream_t>(stream));
   if (info->stream_cs > 0)
     return launch_round_stream_scalar<true>(pool_in, ld_in, pool_out, ld_out, 0, n, v, *info, true,
                                             static_cast<hipStream_t>(stream));
-  return launch_round_scalar<true>(pool_in, ld_in, pool_out, ld_out, 0, n, v, *info, true,
+  return launch_round_scalar<int64_t>(pool_in, ld_in, pool_out, ld_out, 0, n, v, *info, true,
                                    static_cast<hipStream_t>(stream));
+}
+
+int32_t tal_agg_bf16(const uint16_t* const* x_host, const double* w_host, int32_t m, uint16_t* out,
+                     int64_t n, int32_t mode, void* stream) {
+  if (m <= 0) return fail(TAL_ERR_INVALID, "tal_agg_bf16: m must be >= 1");
+  if (m > kMaxOps)
+    return fail(TAL_ERR_INVALID, "tal_agg_bf16: more than 256 operands: use tal_agg_round_bf16");
+  if (n < 0) return fail(TAL_ERR_INVALID, "tal_agg_bf16: n < 0");
+  if (!x_host || !w_host || (n > 0 && !out)) return fail(TAL_ERR_INVALID, "tal_agg_bf16: null pointer");
+  if (n == 0) { g_err.clear(); return TAL_OK; }
+  OpTableB16 t;
+  bool vec = aligned8(out);
+  for (int i = 0; i < m; ++i) {
+    if (!x_host[i]) return fail(TAL_ERR_INVALID, "tal_agg_bf16: null operand pointer");
+    t.x[i] = x_host[i];
+    t.w[i] = static_cast<float>(w_host[i]);
+    vec = vec && aligned8(x_host[i]);
+  }
+  for (int i = m; i < kMaxOps; ++i) { t.x[i] = nullptr; t.w[i] = 0.f; }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool exact = mode == TAL_MODE_EXACT;
+  const int64_t n4 = vec ? n / 4 : 0;
+  if (n4) {
+    int64_t nb = (n4 + kBlock * kK1Unroll - 1) / (kBlock * kK1Unroll);
+    nb = std::max<int64_t>(1, std::min<int64_t>(nb, kK1Grid));
+    if (exact) k_agg_b16_vec<true><<<static_cast<unsigned>(nb), kBlock, 0, s>>>(t, m, out, n4);
+    else k_agg_b16_vec<false><<<static_cast<unsigned>(nb), kBlock, 0, s>>>(t, m, out, n4);
+  }
+  if (n > 4 * n4) {
+    if (exact) k_agg_b16_scalar<true><<<grid_for(n - 4 * n4), kBlock, 0, s>>>(t, m, out, 4 * n4, n);
+    else k_agg_b16_scalar<false><<<grid_for(n - 4 * n4), kBlock, 0, s>>>(t, m, out, 4 * n4, n);
+  }
+  return check_launch("tal_agg_bf16");
+}
+
+int32_t tal_agg_round_bf16(const uint16_t* pool_in, int64_t ld_in, uint16_t* pool_out, int64_t ld_out,
+                           int64_t n, const int32_t* plan_dev, const tal_round_plan_info* info,
+                           int32_t mode, void* stream) {
+  int32_t rc = validate_info(info);
+  if (rc) return rc;
+  if (info->dense_rb != 0 || info->stream_cs != 0)
+    return fail(TAL_ERR_INVALID, "tal_agg_round_bf16: bf16 rounds take sparse or narrow plans "
+                                 "(dense_rb 0, stream_cs 0)");
+  if (!pool_in || !pool_out || !plan_dev) return fail(TAL_ERR_INVALID, "tal_agg_round_bf16: null pointer");
+  if (n < 0 || ld_in < n || ld_out < n) return fail(TAL_ERR_INVALID, "tal_agg_round_bf16: bad n / ld");
+  if (pool_in == pool_out && info->n_groups > 1)
+    return fail(TAL_ERR_INVALID,
+                "tal_agg_round_bf16: in-place round needs a single-group plan (snapshot semantics)");
+  if (n == 0) { g_err.clear(); return TAL_OK; }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const PlanView v = make_view(plan_dev, *info);
+  const bool exact = mode == TAL_MODE_EXACT;
+  const bool vec = aligned8(pool_in) && aligned8(pool_out) && ld_in % 4 == 0 && ld_out % 4 == 0;
+  int64_t e_vec = 0;
+  if (vec) {
+    const int64_t n4 = n / 4;
+    e_vec = n4 * 4;
+    if (n4 > 0) {
+      switch (info->c4 * 2 + (exact ? 1 : 0)) {
+        case 33: rc = launch_round_narrow<16, true, uint16_t>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        case 32: rc = launch_round_narrow<16, false, uint16_t>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        case 65: rc = launch_round_narrow<32, true, uint16_t>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        case 64: rc = launch_round_narrow<32, false, uint16_t>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        case 129: rc = launch_round_vec<64, true, false, uint16_t>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        case 128: rc = launch_round_vec<64, false, false, uint16_t>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        case 257: rc = launch_round_vec<128, true, false, uint16_t>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+        default: rc = launch_round_vec<128, false, false, uint16_t>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
+      }
+      if (rc) return rc;
+    }
+  }
+  if (n <= e_vec) return TAL_OK;
+  if (use_direct(pool_in, pool_out, e_vec, n))
+    return launch_round_direct<uint16_t>(pool_in, ld_in, pool_out, ld_out, e_vec, n, v, *info, exact, s);
+  return launch_round_scalar<uint16_t>(pool_in, ld_in, pool_out, ld_out, e_vec, n, v, *info, exact, s);
 }
 
 int64_t tal_cosine_plan_words(const int64_t* seg_host, int32_t n_seg) {

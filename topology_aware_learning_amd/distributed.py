@@ -105,6 +105,9 @@ class ShardedRound:
     def __init__(self, layout: StateLayout, orders, weights, rank: int, world: int, device,
                  mode: int = ops.MODE_EXACT, owner: Optional[np.ndarray] = None, group=None,
                  exchange: Optional[Callable[["ShardedRound"], list]] = None, tune: bool = False):
+        if layout.n_b16:
+            raise NotImplementedError("sharded rounds move fp32 / int64 pools; bf16 layouts run on one GPU "
+                                      "(RoundExecutor) in this version")
         self.layout = layout
         self.device = torch.device(device)
         self.mode = mode

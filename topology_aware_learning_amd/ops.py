@@ -73,6 +73,20 @@ def agg_i64(xs: Sequence[torch.Tensor], weights: Sequence[float], out: torch.Ten
     return out
 
 
+def agg_bf16(xs: Sequence[torch.Tensor], weights: Sequence[float], out: torch.Tensor,
+             mode: int = MODE_EXACT, stream=None) -> torch.Tensor:
+    """K1 on bf16 buffers.  MODE_EXACT: the reference's torch ops on bf16 tensors (every product
+    and partial sum rounded to bf16; decentralized_client.py:407-411); MODE_FMA: fp32 fused
+    accumulation rounded once."""
+    _require_gpu(out, "out", torch.bfloat16)
+    n = out.numel()
+    P, W = _ptrs_and_weights(xs, weights, n, torch.bfloat16, out)
+    L = _lib.load()
+    check(L.tal_agg_bf16(P, W, len(xs), ctypes.c_void_p(out.data_ptr()), n, int(mode),
+                         _stream(out.device, stream)))
+    return out
+
+
 # ------------------------------------------------------------------------------------------
 # K3 round plans
 # ------------------------------------------------------------------------------------------
@@ -290,6 +304,16 @@ def round_i64(pool_in: torch.Tensor, pool_out: torch.Tensor, plan: RoundPlan, n:
     return _round(pool_in, pool_out, plan, n, torch.int64, MODE_EXACT, stream)
 
 
+def round_bf16(pool_in: torch.Tensor, pool_out: torch.Tensor, plan: RoundPlan, n: Optional[int] = None,
+               mode: int = MODE_EXACT, stream=None) -> torch.Tensor:
+    """K3 on [models, ld] bf16 pools (sparse or narrow plans; modes as agg_bf16)."""
+    return _round(pool_in, pool_out, plan, n, torch.bfloat16, mode, stream)
+
+
+_ROUND_FN = {torch.float32: "tal_agg_round_f32", torch.int64: "tal_agg_round_i64",
+             torch.bfloat16: "tal_agg_round_bf16"}
+
+
 def _round(pool_in, pool_out, plan, n, dtype, mode, stream):
     _require_gpu(pool_in, "pool_in", dtype)
     _require_gpu(pool_out, "pool_out", dtype)
@@ -309,10 +333,10 @@ def _round(pool_in, pool_out, plan, n, dtype, mode, stream):
     if h[i.off_out_row: i.off_out_row + i.rows].max(initial=-1) >= rows_out:
         raise ValueError("plan writes a pool row beyond pool_out")
     L = _lib.load()
-    fn = L.tal_agg_round_f32 if dtype == torch.float32 else L.tal_agg_round_i64
+    fn = getattr(L, _ROUND_FN[dtype])
     args = [ctypes.c_void_p(pool_in.data_ptr()), pool_in.stride(0), ctypes.c_void_p(pool_out.data_ptr()),
             pool_out.stride(0), n, ctypes.c_void_p(plan.device.data_ptr()), ctypes.byref(plan.info)]
-    if dtype == torch.float32:
+    if dtype != torch.int64:
         args.append(int(mode))
     args.append(_stream(pool_in.device, stream))
     check(fn(*args))

@@ -49,7 +49,8 @@ class RoundExecutor:
         p = self._plans.get(key)
         if p is None:
             row_ptr, col, w = csr_from_lists(orders, weights)
-            p = ops.build_plan(row_ptr, col, w, np.asarray(out_rows, np.int32)).to(self.pool.device)
+            dense = 0 if self.pool.layout.n_b16 else -1  # bf16 rounds take sparse / narrow plans
+            p = ops.build_plan(row_ptr, col, w, np.asarray(out_rows, np.int32), dense=dense).to(self.pool.device)
             if len(self._plans) > 64:
                 self._plans.clear()
             self._plans[key] = p
@@ -67,23 +68,27 @@ class RoundExecutor:
             for r, o, w in zip(out_rows, orders, weights):
                 if lay.n_f32:
                     ops.agg_f32([self.pool.row_f32(j) for j in o], w, self.pool.row_f32(r), mode=self.mode)
+                if lay.n_b16:
+                    ops.agg_bf16([self.pool.row_b16(j) for j in o], w, self.pool.row_b16(r), mode=self.mode)
                 if lay.n_i64:
                     ops.agg_i64([self.pool.row_i64(j) for j in o], w, self.pool.row_i64(r))
             return
         plan = self.plan(orders, weights, out_rows)
-        if plan.single_group:
-            # every workgroup stages all sources of its tile before writing: in place is safe
-            if lay.n_f32:
-                ops.round_f32(self.pool.f32, self.pool.f32, plan, n=lay.n_f32, mode=self.mode)
-            if lay.n_i64:
-                ops.round_i64(self.pool.i64, self.pool.i64, plan, n=lay.n_i64)
-            return
-        if self.scratch is None:
+        # every workgroup stages all sources of its tile before writing: with one group in place
+        # is safe; otherwise the round goes through the scratch pool
+        if not plan.single_group and self.scratch is None:
             self.scratch = ModelPool(lay, self.pool.rows, self.pool.device)
+        dst = self.pool if plan.single_group else self.scratch
         if lay.n_f32:
-            ops.round_f32(self.pool.f32, self.scratch.f32, plan, n=lay.n_f32, mode=self.mode)
+            ops.round_f32(self.pool.f32, dst.f32, plan, n=lay.n_f32, mode=self.mode)
+        if lay.n_b16:
+            ops.round_bf16(self.pool.b16, dst.b16, plan, n=lay.n_b16, mode=self.mode)
         if lay.n_i64:
-            ops.round_i64(self.pool.i64, self.scratch.i64, plan, n=lay.n_i64)
+            ops.round_i64(self.pool.i64, dst.i64, plan, n=lay.n_i64)
+        if dst is self.pool:
+            return
         idx = torch.as_tensor(list(out_rows), dtype=torch.long, device=self.pool.device)
-        self.pool.f32.index_copy_(0, idx, self.scratch.f32.index_select(0, idx))
-        self.pool.i64.index_copy_(0, idx, self.scratch.i64.index_select(0, idx))
+        for _, t, _ in self.pool.segments():
+            src = {id(self.pool.f32): self.scratch.f32, id(self.pool.b16): self.scratch.b16,
+                   id(self.pool.i64): self.scratch.i64}[id(t)]
+            t.index_copy_(0, idx, src.index_select(0, idx))

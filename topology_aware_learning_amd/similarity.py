@@ -35,7 +35,7 @@ def _flat(models: Sequence[nn.Module], layout, device) -> List[torch.Tensor]:
         else:
             rest.append(j)
     if rest:
-        df, _ = _stage([models[j] for j in rest], layout, device)
+        df = _stage([models[j] for j in rest], layout, device)["f32"]
         for k, j in enumerate(rest):
             out[j] = df[k]
     return out
