@@ -43,7 +43,10 @@ def parse():
                         "ring: cycle (config 2); barbell: nx.barbell_graph(60, 8) (config 4); "
                         "sbm: 8 blocks of 32, p_in=14/31, p_out=2/224 (config 5)")
     p.add_argument("--devices", type=int, default=0, help="total devices (overrides devices-per-gpu x N)")
-    p.add_argument("--mode", default="exact", choices=["exact", "fma"])
+    p.add_argument("--mode", default=None, choices=["exact", "fma"],
+                   help="default: exact for f32 (bitwise the reference), fma for bf16 (fp32 accumulation)")
+    p.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
+                   help="model storage: f32 (the reference) or bf16 (BASELINE config 5's bf16 tolerance run)")
     p.add_argument("--c4", type=int, default=0)
     p.add_argument("--no-tune", action="store_true", help="use the model-based plan choice instead of timing candidates")
     p.add_argument("--stream-rows", type=int, default=0,
@@ -84,6 +87,7 @@ def fill_pool(pool, seed: int):
     g = torch.Generator(device=pool.device)
     g.manual_seed(seed)
     pool.f32.normal_(generator=g)
+    pool.b16.normal_(generator=g)
     pool.i64.random_(0, 1_000_000, generator=g)
 
 
@@ -153,9 +157,16 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     lay = synth.get_layout(args.model)
+    if args.dtype == "bf16":
+        lay = synth.as_bf16(lay)
     layout = StateLayout.from_layout(lay)
-    n_params = layout.n_f32 + layout.n_i64
+    n_params = layout.n_f32 + layout.n_b16 + layout.n_i64
+    if args.mode is None:
+        args.mode = "exact" if args.dtype == "f32" else "fma"
     mode = ops.MODE_EXACT if args.mode == "exact" else ops.MODE_FMA
+    bf16 = args.dtype == "bf16"
+    n_float = layout.n_b16 if bf16 else layout.n_f32  # the streamed segment
+    esize = 2 if bf16 else 4
     n_dev_total = args.devices or args.devices_per_gpu * world
     orders, weights = round_spec(n_dev_total, args.degree, kind=args.graph)
     n_dev_total = len(orders)
@@ -170,22 +181,28 @@ def main():
         fill_pool(pin, 1234)
         row_ptr, col, w = _round_csr(orders, weights)
         out_rows = np.arange(rows, dtype=np.int32)
+        seg = (lambda p: p.b16) if bf16 else (lambda p: p.f32)
+        row = (lambda p, r: p.row_b16(r)) if bf16 else (lambda p, r: p.row_f32(r))
+        round_fn = _ops.round_bf16 if bf16 else _ops.round_f32
+        agg_fn = _ops.agg_bf16 if bf16 else _ops.agg_f32
         if args.stream_rows:
             plan = _ops.build_stream_plan(row_ptr, col, w, out_rows, args.stream_rows).to(dev)
         elif args.no_tune or args.c4:
-            plan = _ops.build_plan(row_ptr, col, w, out_rows, c4=args.c4).to(dev)
+            plan = _ops.build_plan(row_ptr, col, w, out_rows, c4=args.c4, dense=0 if bf16 else -1).to(dev)
         else:  # time every plan candidate on the real pools (a few rounds, once per topology)
-            plan = _ops.tune_plan(row_ptr, col, w, out_rows, pin.f32, pout.f32, n=layout.n_f32, mode=mode)
+            plan = _ops.tune_plan(row_ptr, col, w, out_rows, seg(pin), seg(pout), n=n_float, mode=mode)
 
         def step(a, b):
-            _ops.round_f32(a.f32, b.f32, plan, n=layout.n_f32, mode=mode)
+            round_fn(seg(a), seg(b), plan, n=n_float, mode=mode)
             _ops.round_i64(a.i64, b.i64, plan, n=layout.n_i64)
 
         # correctness spot check at full size: K3 row 0 == K1 on the same operands (bitwise)
         step(pin, pout)
-        chk = torch.empty(layout.n_f32, dtype=torch.float32, device=dev)
-        _ops.agg_f32([pin.row_f32(j) for j in orders[0]], weights[0], chk, mode=mode)
-        parity_ok = bool(torch.equal(chk.view(torch.int32), pout.row_f32(0).view(torch.int32)))
+        chk = torch.empty(n_float, dtype=seg(pin).dtype, device=dev)
+        agg_fn([row(pin, j) for j in orders[0]], weights[0], chk, mode=mode)
+        parity_ok = bool(torch.equal(chk.view(torch.int16 if bf16 else torch.int32),
+                                     row(pout, 0).view(torch.int16 if bf16 else torch.int32)))
+        tol = bf16_tolerance(pin, pout, orders[0], weights[0], n_float, dev) if bf16 else None
 
         pools = [pin, pout]
         for i in range(args.warmup):
@@ -197,26 +214,28 @@ def main():
         for i in range(args.steps):
             a, b = pools[i % 2], pools[(i + 1) % 2]
             ev[i][0].record(stream)
-            _ops.round_f32(a.f32, b.f32, plan, n=layout.n_f32, mode=mode)
+            round_fn(seg(a), seg(b), plan, n=n_float, mode=mode)
             ev[i][1].record(stream)
             _ops.round_i64(a.i64, b.i64, plan, n=layout.n_i64)
         torch.cuda.synchronize(dev)
         el = time.perf_counter() - t0
         k_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
         staged = plan.info.total_src
-        bytes_round = 4 * layout.n_f32 * (staged + rows)  # compulsory: each staged source read once, each output written once
-        per_call_bytes = 4 * layout.n_f32 * (len(col) + rows)  # SURVEY §8(d) B summed over the round's calls
+        bytes_round = esize * n_float * (staged + rows)  # compulsory: each staged source read once, each output written once
+        per_call_bytes = esize * n_float * (len(col) + rows)  # SURVEY §8(d) B summed over the round's calls
         result_extra = dict(
             kernel=_ops.round_kernel_name(plan.info), plan=dict(groups=plan.info.n_groups, staged_sources=staged,
                                                   c4=plan.info.c4, dense_rb=plan.info.dense_rb,
                                                   lds_reads_per_column=plan.info.dense_reads,
                                                   tuned_ms=plan.tuned_ms, candidates=plan.candidates),
             per_call_equivalent_GBps=per_call_bytes / (k_ms * 1e-3) / 1e9, parity_k3_vs_k1_row0=parity_ok,
-            valu=valu_floor(len(col), rows, layout.n_f32, k_ms, mode))
+            valu=valu_floor(len(col), rows, n_float, k_ms, mode))
+        if tol is not None:
+            result_extra["bf16_vs_fp32_reference_row0"] = tol
         steps_done = args.steps
         units = rows * n_params * steps_done
         k1 = None
-        if not args.no_k1:
+        if not args.no_k1 and not bf16:
             k1 = bench_k1(layout, pin, orders, weights, mode, dev)
         hostp = bench_host_path(lay, M, dev) if args.host_path else None
     else:
@@ -268,7 +287,7 @@ def main():
     traffic = load_traffic(workload_key(args.graph, n_dev_total, args.model))
     cpu = None
     if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(lay, M, args.cpu_seconds)
+        cpu = cpu_baseline(lay, M, args.cpu_seconds)  # bf16 layouts: the reference's loop on bf16 tensors
     value = units / el
     out = {
         "metric": "device-resident aggregated params/s at K=8 neighbors",
@@ -281,8 +300,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32" if args.mode == "exact" else "f32-fma",
-        "data": "synthetic (random fp32 / int64 state_dicts of the reference layout in HBM)",
+        "dtype": ("bf16" if bf16 else "f32") + ("" if args.mode == "exact" else "-fma"),
+        "data": f"synthetic (random {'bf16' if bf16 else 'fp32'} / int64 state_dicts of the reference layout in HBM)",
         "config": {"workload": f"{n_dev_total}-device {args.graph} graph"
                                + (f" ({args.degree}-regular, seed 0)" if args.graph == "random" else "")
                                + f", {args.model} state_dicts, max M={M} (self last), unweighted, "
@@ -310,6 +329,26 @@ def _round_csr(orders, weights):
     from topology_aware_learning_amd.round import csr_from_lists
 
     return csr_from_lists(orders, weights)
+
+
+def bf16_tolerance(pin, pout, order, weights, n, dev) -> dict:
+    """Row 0 of a bf16 round against the fp32 reference (K1 in exact fp32 on the same operands
+    upcast): max |d| / (2^-8 |ref| + M 2^-24 sum|w x|) over the row, the SURVEY §8(a) bf16 bound."""
+    import torch
+
+    from topology_aware_learning_amd import ops
+
+    xs = [pin.row_b16(j).float() for j in order]
+    ref = torch.empty(n, dtype=torch.float32, device=dev)
+    ops.agg_f32(xs, weights, ref, mode=ops.MODE_EXACT)
+    mag = torch.zeros_like(ref)
+    for x, w in zip(xs, weights):
+        mag.add_(x.abs(), alpha=abs(float(np.float32(w))))
+    bound = 2.0 ** -8 * ref.abs() + len(xs) * 2.0 ** -24 * mag
+    err = (pout.row_b16(0).float() - ref).abs()
+    ratio = float((err / bound.clamp_min(1e-38)).max().item())
+    return dict(max_err_over_bound=ratio, within_tolerance=ratio <= 1.0,
+                bound="|d| <= 2^-8 |ref| + M 2^-24 sum|w x| (SURVEY §8(a) bf16 run)")
 
 
 def bench_k1(layout, pool, orders, weights, mode, dev, reps: int = 20):

@@ -216,10 +216,12 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
     the fallback when only one candidate builds."""
     if pool_in.data_ptr() == pool_out.data_ptr():
         raise ValueError("tune_plan needs distinct input / output pools")
+    bf16 = pool_in.dtype == torch.bfloat16  # bf16 rounds: sparse and narrow plans only
+    run = round_bf16 if bf16 else round_f32
     cands = []
     for c4 in TILE_WIDTHS:
         for budget in LDS_BUDGETS:
-            for dense in ((0,) if c4 < 64 else (0, 8)):
+            for dense in ((0,) if c4 < 64 or bf16 else (0, 8)):
                 try:
                     p = build_plan(row_ptr, col, w, out_row, c4=c4, lds_bytes=budget, dense=dense)
                 except _lib.TalError:
@@ -229,7 +231,7 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
                 key = (p.info.c4, p.info.n_groups, p.info.total_src, p.info.dense_rb, p.info.max_src, 0)
                 if all(key != k for k, _ in cands):
                     cands.append((key, p))
-    for max_rows, max_src in STREAM_GROUPINGS:
+    for max_rows, max_src in (() if bf16 else STREAM_GROUPINGS):
         try:
             p = build_stream_plan(row_ptr, col, w, out_row, max_rows, max_src)
         except (_lib.TalError, ValueError):
@@ -238,7 +240,7 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
         if all(key != k for k, _ in cands):
             cands.append((key, p))
     if not cands:
-        return build_plan(row_ptr, col, w, out_row)
+        return build_plan(row_ptr, col, w, out_row, dense=0 if bf16 else -1)
     if len(cands) == 1:
         return cands[0][1].to(pool_in.device)
     best, best_t = None, None
@@ -246,11 +248,11 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for key, p in cands:
         p.to(pool_in.device)
-        round_f32(pool_in, pool_out, p, n=n, mode=mode)  # warm (LDS attribute, code load)
+        run(pool_in, pool_out, p, n=n, mode=mode)  # warm (LDS attribute, code load)
         ts = []
         for _ in range(reps):
             s.record()
-            round_f32(pool_in, pool_out, p, n=n, mode=mode)
+            run(pool_in, pool_out, p, n=n, mode=mode)
             e.record()
             e.synchronize()
             ts.append(s.elapsed_time(e))

@@ -18,7 +18,7 @@ from typing import Iterable, List, Sequence, Tuple
 import numpy as np
 import torch
 
-Layout = List[Tuple[str, Tuple[int, ...], str]]  # dtype in {"float32", "int64"}
+Layout = List[Tuple[str, Tuple[int, ...], str]]  # dtype in {"float32", "bfloat16", "int64"}
 
 _M1 = np.uint64(0x9E3779B97F4A7C15)
 _M2 = np.uint64(0xBF58476D1CE4E5B9)
@@ -67,6 +67,11 @@ def numel(shape: Sequence[int]) -> int:
     return n
 
 
+def as_bf16(layout: Layout) -> Layout:
+    """The layout of `model.to(torch.bfloat16)`: fp32 entries become bf16, int64 buffers stay."""
+    return [(n, s, "bfloat16" if d == "float32" else d) for n, s, d in layout]
+
+
 def layout_counts(layout: Layout) -> Tuple[int, int]:
     nf = sum(numel(s) for _, s, d in layout if d == "float32")
     ni = sum(numel(s) for _, s, d in layout if d == "int64")
@@ -85,6 +90,10 @@ def synth_state_dict(layout: Layout, seed: int) -> "OrderedDict[str, torch.Tenso
                 a = np.abs(a) + np.float32(0.5)
         elif dt == "int64":
             a = counter_i64(seed, pos, n)
+        elif dt == "bfloat16":
+            sd[name] = torch.from_numpy(counter_f32(seed, pos, n).reshape(shape).copy()).to(torch.bfloat16)
+            pos += n
+            continue
         else:
             raise ValueError(f"unsupported dtype {dt} for {name}")
         sd[name] = torch.from_numpy(a.reshape(shape).copy())
