@@ -49,6 +49,7 @@ def parse():
                    help="model storage: f32 (the reference) or bf16 (BASELINE config 5's bf16 tolerance run)")
     p.add_argument("--c4", type=int, default=0)
     p.add_argument("--no-tune", action="store_true", help="use the model-based plan choice instead of timing candidates")
+    p.add_argument("--plan", default="", help="JSON plan spec (a previous run's plan.spec): build it, no tuning")
     p.add_argument("--stream-rows", type=int, default=0,
                    help="force a streamed plan with groups of at most this many rows (profiling)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -185,7 +186,9 @@ def main():
         row = (lambda p, r: p.row_b16(r)) if bf16 else (lambda p, r: p.row_f32(r))
         round_fn = _ops.round_bf16 if bf16 else _ops.round_f32
         agg_fn = _ops.agg_bf16 if bf16 else _ops.agg_f32
-        if args.stream_rows:
+        if args.plan:
+            plan = _ops.plan_from_spec(row_ptr, col, w, out_rows, json.loads(args.plan)).to(dev)
+        elif args.stream_rows:
             plan = _ops.build_stream_plan(row_ptr, col, w, out_rows, args.stream_rows).to(dev)
         elif args.no_tune or args.c4:
             plan = _ops.build_plan(row_ptr, col, w, out_rows, c4=args.c4, dense=0 if bf16 else -1).to(dev)
@@ -227,7 +230,8 @@ def main():
             kernel=_ops.round_kernel_name(plan.info), plan=dict(groups=plan.info.n_groups, staged_sources=staged,
                                                   c4=plan.info.c4, dense_rb=plan.info.dense_rb,
                                                   lds_reads_per_column=plan.info.dense_reads,
-                                                  tuned_ms=plan.tuned_ms, candidates=plan.candidates),
+                                                  tuned_ms=plan.tuned_ms, candidates=plan.candidates,
+                                                  spec=plan.spec),
             per_call_equivalent_GBps=per_call_bytes / (k_ms * 1e-3) / 1e9, parity_k3_vs_k1_row0=parity_ok,
             valu=valu_floor(len(col), rows, n_float, k_ms, mode))
         if tol is not None:

@@ -28,7 +28,7 @@ def last_round_kernel(path):
     best = (-1, None)
     for r in csv.DictReader(open(path)):
         k = r["Kernel_Name"]
-        if "k_round_" in k and "scalar" not in k and int(r["Dispatch_Id"]) > best[0]:
+        if "k_round_" in k and "scalar" not in k and "direct" not in k and int(r["Dispatch_Id"]) > best[0]:
             best = (int(r["Dispatch_Id"]), k)
     return best[1]
 

@@ -104,6 +104,7 @@ class RoundPlan:
     nnz: int = 0
     tuned_ms: Optional[float] = None
     candidates: Optional[list] = None  # tune_plan's measured candidates
+    spec: Optional[dict] = None        # how it was built (plan_from_spec rebuilds it)
 
     @property
     def single_group(self) -> bool:
@@ -230,6 +231,7 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
                     continue
                 key = (p.info.c4, p.info.n_groups, p.info.total_src, p.info.dense_rb, p.info.max_src, 0)
                 if all(key != k for k, _ in cands):
+                    p.spec = dict(c4=c4, lds=budget, dense=dense)
                     cands.append((key, p))
     for max_rows, max_src in (() if bf16 else STREAM_GROUPINGS):
         try:
@@ -238,6 +240,7 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
             continue
         key = (p.info.c4, p.info.n_groups, p.info.total_src, p.info.dense_rb, p.info.max_src, p.info.stream_cs)
         if all(key != k for k, _ in cands):
+            p.spec = dict(stream_rows=max_rows, stream_src=max_src)
             cands.append((key, p))
     if not cands:
         return build_plan(row_ptr, col, w, out_row, dense=0 if bf16 else -1)
@@ -258,12 +261,24 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
             ts.append(s.elapsed_time(e))
         t = float(np.median(ts))
         timings.append({"c4": key[0], "groups": key[1], "staged": key[2], "dense_rb": key[3],
-                        "max_src": key[4], "stream_cs": key[5], "ms": round(t, 4)})
+                        "max_src": key[4], "stream_cs": key[5], "ms": round(t, 4), "spec": p.spec})
         if best_t is None or t < best_t:
             best, best_t = p, t
     best.tuned_ms = best_t
     best.candidates = timings
     return best
+
+
+def plan_from_spec(row_ptr, col, w, out_row, spec: dict) -> RoundPlan:
+    """Rebuild a plan tune_plan chose (its `spec`): profiling runs then time the same plan
+    without re-tuning."""
+    if "stream_rows" in spec:
+        p = build_stream_plan(row_ptr, col, w, out_row, int(spec["stream_rows"]), int(spec["stream_src"]))
+    else:
+        p = build_plan(row_ptr, col, w, out_row, c4=int(spec["c4"]), lds_bytes=int(spec["lds"]),
+                       dense=int(spec["dense"]))
+    p.spec = dict(spec)
+    return p
 
 
 def round_kernel_name(info: RoundPlanInfo) -> str:
