@@ -137,6 +137,15 @@ typedef struct tal_round_plan_info {
   int32_t off_npairs;       /* [npairs][2] int32 */
   int32_t npairs;           /* pairs over all rows (padded) */
   int32_t max_npairs;       /* largest group pair count */
+  /* narrow_roww = 1 when every row's operands share one fp32 weight (the unweighted strategy,
+   * scale_agg): the pairs are replaced by 16-bit slots (slot * c4, two per int32 word), each
+   * row's run padded to a multiple of 4 with a zero-tile slot (slot ns: a -0.0 tile for a
+   * row weight with the sign bit clear, slot ns + 1: +0.0 otherwise, so fl(w * 0) = -0 exactly),
+   * the accumulator starts at -0.0 (-0 + y == y for every y), and the row weights are in
+   * off_nrow_w.  off_nrow_ptr then counts slots; npairs counts slots. */
+  int32_t narrow_roww;
+  int32_t off_nrow_w;       /* [rows] fp32 weight bits (narrow_roww) */
+  int32_t scalar_lds_bytes; /* LDS of the staged scalar tail kernel (the largest group) */
 } tal_round_plan_info;
 
 /* Blob size in int32 words of the sparse or narrow form for `rows` rows / `nnz` operands (an upper

@@ -206,6 +206,39 @@ def test_round_narrow_vs_oracle(cuda, graph, n, c4, lds):
         assert _bits_equal(pin.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("sign", [1.0, -1.0])
+def test_round_narrow_row_uniform_weights_signed_zero(cuda, sign):
+    """ROWW encoding (one weight per row): padding reads a zero tile chosen by the weight's sign
+    so fl(w * 0) == -0 and -0 results survive (rows of all-zero and -0.0 inputs)."""
+    g = nx.random_regular_graph(6, 40, seed=3)
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(40)]
+    ws = [[sign / len(o)] * len(o) for o in orders]
+    rows = len(orders)
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    out_rows = np.arange(rows, dtype=np.int32)
+    n = 4099
+    rng = np.random.default_rng(7)
+    pool = rng.standard_normal((rows, n)).astype(np.float32)
+    pool[:, :4] = np.float32(-0.0)
+    pool[::2, 4:8] = np.float32(0.0)
+    pool[1::2, 4:8] = np.float32(-0.0)
+    pool[:, 8] = np.float32(1e-45)
+    ref = oracle.round_f32(pool, row_ptr, col, w, out_rows)
+    for c4 in (16, 32):
+        plan = ops.build_plan(row_ptr, col, w, out_rows, c4=c4, lds_bytes=80 * 1024)
+        assert plan.info.narrow_roww == 1
+        pin = torch.from_numpy(pool).to(cuda)
+        pout = torch.zeros_like(pin)
+        ops.round_f32(pin, pout, plan)
+        assert _bits_equal(pout.cpu().numpy(), ref), c4
+        bits = oracle.f32_to_bf16(pool)
+        refb = oracle.round_bf16(bits, row_ptr, col, w, out_rows, exact=True)
+        pb = torch.from_numpy(bits.view(np.int16)).view(torch.bfloat16).to(cuda)
+        ob = torch.zeros_like(pb)
+        ops.round_bf16(pb, ob, plan)
+        assert np.array_equal(ob.cpu().view(torch.int16).numpy().view(np.uint16), refb), c4
+
+
 def test_round_narrow_sbm256_one_group(cuda):
     """BASELINE config 5's topology (256-device SBM) fits one narrow group: each source read once."""
     sizes = [32] * 8

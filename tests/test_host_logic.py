@@ -205,6 +205,37 @@ def test_narrow_plan_orders_rows_by_operand_count():
         assert got == want
 
 
+def test_narrow_roww_encoding():
+    """Row-uniform weights: 16-bit slots in batches of 4 padded with the zero tile that keeps
+    -0 (slot ns for a weight with the sign bit clear, ns + 1 otherwise), one weight per row."""
+    g = nx.random_regular_graph(4, 24, seed=5)
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(24)]
+    for sign in (1.0, -1.0):
+        ws = [[sign / len(o)] * len(o) for o in orders]
+        row_ptr, col, w = ra.round_csr(orders, ws)
+        plan = ops.build_plan(row_ptr, col, w, np.arange(24, dtype=np.int32), c4=16, lds_bytes=80 * 1024)
+        i, h = plan.info, plan.host
+        assert i.narrow_roww == 1 and i.n_groups == 1
+        rp = h[i.off_nrow_ptr: i.off_nrow_ptr + i.rows + 1]
+        slots = h[i.off_npairs: i.off_npairs + (i.npairs + 1) // 2].view(np.uint16)[: i.npairs]
+        rw = h[i.off_nrow_w: i.off_nrow_w + i.rows].view(np.float32)
+        src = h[i.off_src_row: i.off_src_row + i.total_src]
+        ns = i.total_src
+        orow = h[i.off_out_row: i.off_out_row + i.rows]
+        for r in range(i.rows):
+            assert rp[r] % 4 == 0 and rp[r + 1] % 4 == 0
+            run = slots[rp[r]: rp[r + 1]] // 16
+            o = orders[orow[r]]
+            assert [int(src[x]) for x in run[: len(o)]] == o
+            assert np.all(run[len(o):] == (ns if sign > 0 else ns + 1)) and len(run) - len(o) < 4
+            assert rw[r] == np.float32(sign / len(o))
+    ws = [ra.unweighted_weights(len(o)) for o in orders]
+    ws[3] = list(np.linspace(0.1, 0.2, len(orders[3])))  # one non-uniform row: pairs
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    plan = ops.build_plan(row_ptr, col, w, np.arange(24, dtype=np.int32), c4=16, lds_bytes=80 * 1024)
+    assert plan.info.narrow_roww == 0
+
+
 def test_round_plan_reconstructs_csr():
     g = nx.random_regular_graph(8, 64, seed=0)
     orders = [sorted(g.neighbors(i)) + [i] for i in range(64)]

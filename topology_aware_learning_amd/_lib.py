@@ -23,7 +23,7 @@ TAL_ERR_HIP = 2
 TAL_ERR_CAPACITY = 3
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 EXPORTED = (
     "tal_last_error",
@@ -91,6 +91,9 @@ class RoundPlanInfo(ctypes.Structure):
         ("off_npairs", ctypes.c_int32),
         ("npairs", ctypes.c_int32),
         ("max_npairs", ctypes.c_int32),
+        ("narrow_roww", ctypes.c_int32),
+        ("off_nrow_w", ctypes.c_int32),
+        ("scalar_lds_bytes", ctypes.c_int32),
     ]
 
 

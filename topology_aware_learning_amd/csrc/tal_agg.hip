@@ -20,6 +20,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <mutex>
 #include <string>
 #include <tuple>
@@ -32,7 +33,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 7;
+constexpr int kAbiVersion = 8;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -300,6 +301,7 @@ struct PlanView {
   const int32_t* base;         // the blob (dense tables are addressed from it)
   const int32_t* nrow_ptr;     // narrow form only
   const int32_t* npairs;
+  const int32_t* nrow_w;       // narrow_roww only
 };
 
 PlanView make_view(const int32_t* plan, const tal_round_plan_info& in) {
@@ -316,6 +318,7 @@ PlanView make_view(const int32_t* plan, const tal_round_plan_info& in) {
   v.base = plan;
   v.nrow_ptr = plan + in.off_nrow_ptr;
   v.npairs = plan + in.off_npairs;
+  v.nrow_w = plan + in.off_nrow_w;
   return v;
 }
 
@@ -718,8 +721,10 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const T* __restrict
 constexpr int kNarrowPasses = 4;
 
 struct NarrowLds {
-  const int32_t* rowptr;  // [nr + 1], group-relative pair index
+  const int32_t* rowptr;  // [nr + 1], group-relative pair (ROWW: slot) index
   const int2* pairs;      // [group pairs + 4 read-ahead] (slot * C4, fp32 weight bits)
+  const uint16_t* slots;  // ROWW: [group slots + 8 read-ahead] slot * C4
+  const float* rw;        // ROWW: [nr] row weights
   const int32_t* out;     // [nr] pool_out row
   int nr;
 };
@@ -727,6 +732,68 @@ struct NarrowLds {
 __host__ __device__ constexpr size_t narrow_lds_bytes(int64_t max_src, int64_t max_rows, int64_t max_pairs,
                                                       int c4) {
   return static_cast<size_t>((max_src + 1) * c4 * 16 + (2 * max_rows + 2 + 2 * (max_pairs + 4)) * 4 + 16);
+}
+
+// ROWW carve: [ns + 2 tiles (-0.0, +0.0)][rowptr nr+1][w nr][out nr][pad to 8 B][slots + 8]
+__host__ __device__ constexpr size_t narrow_roww_lds_bytes(int64_t ns, int64_t nr, int64_t nslots, int c4) {
+  return static_cast<size_t>((ns + 2) * c4 * 16 + (3 * nr + 2) * 4 + (nslots + 8) * 2 + 16);
+}
+
+template <int C4>
+__device__ __forceinline__ NarrowLds stage_narrow_roww(const PlanView& p, int g, float4* s_data, int nthreads) {
+  NarrowLds L;
+  const int r_beg = p.grp_row_ptr[g];
+  L.nr = p.grp_row_ptr[g + 1] - r_beg;
+  const int e_beg = p.nrow_ptr[r_beg];  // a multiple of 4 (every run is)
+  const int ne = p.nrow_ptr[r_beg + L.nr] - e_beg;
+  const int ns = p.grp_src_ptr[g + 1] - p.grp_src_ptr[g];
+  // offsets in 32-bit words from s_data (index arithmetic keeps the LDS address space: a
+  // pointer rebuilt from an integer would become a generic one and every read a flat load)
+  int32_t* base32 = reinterpret_cast<int32_t*>(s_data);
+  const int o_rowptr = (ns + 2) * C4 * 4;
+  int32_t* rowptr = base32 + o_rowptr;
+  float* rw = reinterpret_cast<float*>(rowptr + L.nr + 1);
+  int32_t* out = reinterpret_cast<int32_t*>(rw + L.nr);
+  uint32_t* slots = reinterpret_cast<uint32_t*>(base32 + ((o_rowptr + 3 * L.nr + 2) & ~1));  // 8-B aligned
+  for (int k = threadIdx.x; k < 2 * C4; k += nthreads)  // zero tiles: slot ns = -0.0, ns + 1 = +0.0
+    s_data[static_cast<size_t>(ns) * C4 + k] = k < C4 ? make_float4(-0.f, -0.f, -0.f, -0.f)
+                                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k = threadIdx.x; k <= L.nr; k += nthreads) rowptr[k] = p.nrow_ptr[r_beg + k] - e_beg;
+  for (int k = threadIdx.x; k < L.nr; k += nthreads) {
+    rw[k] = __int_as_float(p.nrow_w[r_beg + k]);
+    out[k] = p.out_row[r_beg + k];
+  }
+  const int nw = ne / 2;  // ne is a multiple of 4: whole words
+  for (int k = threadIdx.x; k < nw + 4; k += nthreads)  // + 4 read-ahead words (never used)
+    slots[k] = k < nw ? static_cast<uint32_t>(p.npairs[e_beg / 2 + k]) : 0u;
+  L.rowptr = rowptr;
+  L.pairs = nullptr;
+  L.slots = reinterpret_cast<const uint16_t*>(slots);
+  L.rw = rw;
+  L.out = out;
+  return L;
+}
+
+// One ROWW row: the accumulator starts at -0.0, every batch of four slots is one 8-B LDS read
+// (the next batch's read is issued ahead of this batch's data reads).
+template <typename T, bool EXACT>
+__device__ __forceinline__ float4 narrow_row_roww(const float4* s_data, const NarrowLds& L, int r, int cl) {
+  const uint32_t b0 = static_cast<uint32_t>(L.rowptr[r]) >> 2, b1 = static_cast<uint32_t>(L.rowptr[r + 1]) >> 2;
+  const float w = L.rw[r];
+  float4 acc = make_float4(-0.f, -0.f, -0.f, -0.f);
+  const uint2* s4 = reinterpret_cast<const uint2*>(L.slots);
+  uint2 e = s4[b0];
+  for (uint32_t b = b0; b < b1; ++b) {
+    float4 x[4];
+    x[0] = s_data[(e.x & 0xffffu) + cl];
+    x[1] = s_data[(e.x >> 16) + cl];
+    x[2] = s_data[(e.y & 0xffffu) + cl];
+    x[3] = s_data[(e.y >> 16) + cl];
+    e = s4[b + 1];  // next batch (or the read-ahead pad), in flight with this batch's data reads
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = next4t<T, EXACT>(acc, w, x[u]);
+  }
+  return acc;
 }
 
 template <int C4>
@@ -803,7 +870,7 @@ __device__ __forceinline__ int narrow_set(int p, int wave, int nwaves) {
 
 // NP = row sets held in registers: kNarrowPasses for one resident workgroup per CU (128 VGPRs),
 // 0 for two (64 VGPRs: the extents are then read from LDS each pass).
-template <int C4, int NT, int J, int NP, bool EXACT, typename T = float>
+template <int C4, int NT, int J, int NP, bool EXACT, typename T = float, bool ROWW = false>
 __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round_f32_narrow(
     const T* __restrict__ pin, int64_t ld_in4, T* __restrict__ pout, int64_t ld_out4, int64_t n4,
     PlanView p, int64_t n_tiles) {
@@ -813,7 +880,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   constexpr int kW = NT / 64;
   extern __shared__ float4 s_data[];
   const int g = blockIdx.y;
-  const NarrowLds L = stage_narrow<C4>(p, g, s_data, NT);
+  const NarrowLds L = ROWW ? stage_narrow_roww<C4>(p, g, s_data, NT) : stage_narrow<C4>(p, g, s_data, NT);
   const int s_beg = p.grp_src_ptr[g];
   const int ns = p.grp_src_ptr[g + 1] - s_beg;
   const int c = threadIdx.x % C4;
@@ -860,14 +927,22 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       if (rq1[k] > rq0[k]) {
-        const float4 acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, rq0[k], rq1[k], cl);
+        float4 acc;
+        if constexpr (ROWW)
+          acc = narrow_row_roww<T, EXACT>(s_data, L, narrow_set(k, wave, kW) * kRpw + sub, cl);
+        else
+          acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, rq0[k], rq1[k], cl);
         if (col < n4) Io<T>::st(pout, static_cast<int64_t>(rout[k]) * ld_out4 + col, acc);
       }
     }
     for (int k = NP; k * kW < n_sets; ++k) {  // row sets beyond the register-held ones
       const int r = narrow_set(k, wave, kW) * kRpw + sub;
       if (r < L.nr) {
-        const float4 acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, L.rowptr[r], L.rowptr[r + 1], cl);
+        float4 acc;
+        if constexpr (ROWW)
+          acc = narrow_row_roww<T, EXACT>(s_data, L, r, cl);
+        else
+          acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, L.rowptr[r], L.rowptr[r + 1], cl);
         if (col < n4) Io<T>::st(pout, static_cast<int64_t>(L.out[r]) * ld_out4 + col, acc);
       }
     }
@@ -1301,7 +1376,7 @@ int32_t launch_round_scalar(const T* pin, int64_t ld_in, T* pout, int64_t ld_out
                             const tal_round_plan_info& in, bool exact, hipStream_t s) {
   if (n <= e0) return TAL_OK;
   const int tile = 4 * in.c4;
-  const size_t lds = static_cast<size_t>(in.lds_bytes);  // the largest group's tile + plan slice
+  const size_t lds = static_cast<size_t>(in.scalar_lds_bytes);  // the largest group's tile + plan slice
   const int64_t tiles = (n - e0 + tile - 1) / tile;
   if (tiles > 0x7fffffff) return fail(TAL_ERR_INVALID, "too many tiles");
   const dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(in.n_groups));
@@ -1354,16 +1429,16 @@ int resident_per_cu(const void* kernel, int threads, size_t lds) {
   return nb;
 }
 
-template <int C4, int J, bool EXACT, typename T = float>
-int32_t launch_round_narrow_j(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
-                              const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
+template <int C4, int J, bool EXACT, typename T = float, bool ROWW = false>
+int32_t launch_round_narrow_jr(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
+                               const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
   const size_t lds = static_cast<size_t>(in.lds_bytes);
   // two workgroups per CU when their LDS allows it (registers capped at 64), else one with the
   // row extents in registers
   constexpr int kNP = J >= 12 ? kNarrowPasses / 2 : kNarrowPasses;  // J = 12: VGPRs for the staging
-  auto k = k_round_f32_narrow<C4, kNarrowThreads, J, kNP, EXACT, T>;
+  auto k = k_round_f32_narrow<C4, kNarrowThreads, J, kNP, EXACT, T, ROWW>;
   if constexpr (J <= 4)
-    if (2 * lds <= 160 * 1024) k = k_round_f32_narrow<C4, kNarrowThreads, J, 0, EXACT, T>;
+    if (2 * lds <= 160 * 1024) k = k_round_f32_narrow<C4, kNarrowThreads, J, 0, EXACT, T, ROWW>;
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;
   const int64_t tiles = (n4 + C4 - 1) / C4;
@@ -1373,6 +1448,13 @@ int32_t launch_round_narrow_j(const T* pin, int64_t ld_in, T* pout, int64_t ld_o
   const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(in.n_groups));
   k<<<grid, kNarrowThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles);
   return check_launch("round kernel (narrow tiles)");
+}
+
+template <int C4, int J, bool EXACT, typename T = float>
+int32_t launch_round_narrow_j(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
+                              const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
+  return in.narrow_roww ? launch_round_narrow_jr<C4, J, EXACT, T, true>(pin, ld_in, pout, ld_out, n4, v, in, s)
+                        : launch_round_narrow_jr<C4, J, EXACT, T, false>(pin, ld_in, pout, ld_out, n4, v, in, s);
 }
 
 template <int C4, bool EXACT, typename T = float>
@@ -1727,6 +1809,18 @@ bool reference_order(int32_t rows, const int32_t* row_ptr_host, const int32_t* c
   return true;
 }
 
+// Every row's operands carry one fp32 weight (bitwise): the narrow ROWW encoding applies.
+bool rows_uniform_weights(int32_t rows, const int32_t* row_ptr_host, const double* w_host) {
+  for (int r = 0; r < rows; ++r) {
+    const float w0 = static_cast<float>(w_host[row_ptr_host[r]]);
+    for (int32_t k = row_ptr_host[r] + 1; k < row_ptr_host[r + 1]; ++k) {
+      const float wk = static_cast<float>(w_host[k]);
+      if (memcmp(&wk, &w0, 4) != 0) return false;
+    }
+  }
+  return true;
+}
+
 // Greedy grouping: a row joins the current group unless that breaks `fits(n_src, n_rows, n_ops)`.
 template <class Fits>
 int32_t group_rows(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host, int32_t max_col,
@@ -1854,15 +1948,32 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
     const int64_t no = row_ptr_host[grp_row_ptr[g + 1]] - row_ptr_host[grp_row_ptr[g]];
     lds_need = std::max(lds_need, group_lds_bytes(grp_src_ptr[g + 1] - grp_src_ptr[g], nr, no, c4));
   }
+  const int64_t scalar_need = lds_need;
+  const bool roww = c4 < 64 && rows_uniform_weights(rows, row_ptr_host, w_host);
+  std::vector<uint16_t> nsl;   // ROWW slots
+  std::vector<int32_t> nrw;    // ROWW row weights
   if (c4 < 64) {
+    lds_need = 0;  // the narrow kernel's carve replaces the staged one
     nrp.assign(static_cast<size_t>(rows) + 1, 0);
     const float one = 1.0f;
     int32_t one_bits;
     memcpy(&one_bits, &one, 4);
     for (int g = 0; g < G; ++g) {
-      const int64_t g0 = static_cast<int64_t>(npr.size()) / 2;
+      const int32_t ns = grp_src_ptr[g + 1] - grp_src_ptr[g];
+      const int64_t g0 = roww ? static_cast<int64_t>(nsl.size()) : static_cast<int64_t>(npr.size()) / 2;
       for (int r = grp_row_ptr[g]; r < grp_row_ptr[g + 1]; ++r) {
         const int32_t k0 = row_ptr_host[r], k1 = row_ptr_host[r + 1];
+        if (roww) {  // slots only, whole batches of 4; the pad reads the zero tile that keeps -0
+          const float wf = static_cast<float>(w_host[k0]);
+          int32_t wb;
+          memcpy(&wb, &wf, 4);
+          nrw.push_back(wb);
+          for (int32_t k = k0; k < k1; ++k) nsl.push_back(static_cast<uint16_t>(slot[k] * c4));
+          const uint16_t zero = static_cast<uint16_t>((std::signbit(wf) ? ns + 1 : ns) * c4);
+          while (nsl.size() % 4) nsl.push_back(zero);
+          nrp[r + 1] = static_cast<int32_t>(nsl.size());
+          continue;
+        }
         for (int32_t k = k0; k < k1; ++k) {
           const float wf = static_cast<float>(w_host[k]);
           int32_t wb;
@@ -1871,15 +1982,20 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
           npr.push_back(wb);
         }
         for (int32_t pad = (4 - (k1 - k0 - 1) % 4) % 4; pad > 0; --pad) {
-          npr.push_back((grp_src_ptr[g + 1] - grp_src_ptr[g]) * c4);  // the group's -0.0 tile
+          npr.push_back(ns * c4);  // the group's -0.0 tile
           npr.push_back(one_bits);
         }
         nrp[r + 1] = static_cast<int32_t>(npr.size() / 2);
       }
-      const int64_t gp = static_cast<int64_t>(npr.size()) / 2 - g0;
+      const int64_t gp = (roww ? static_cast<int64_t>(nsl.size()) : static_cast<int64_t>(npr.size()) / 2) - g0;
       max_np = std::max<int64_t>(max_np, gp);
-      lds_need = std::max<int64_t>(lds_need, static_cast<int64_t>(narrow_lds_bytes(
-          grp_src_ptr[g + 1] - grp_src_ptr[g], grp_row_ptr[g + 1] - grp_row_ptr[g], gp, c4)));
+      const int64_t nr = grp_row_ptr[g + 1] - grp_row_ptr[g];
+      lds_need = std::max<int64_t>(lds_need, static_cast<int64_t>(
+          roww ? narrow_roww_lds_bytes(ns, nr, gp, c4) : narrow_lds_bytes(ns, nr, gp, c4)));
+    }
+    if (roww) {  // two slots per int32 word
+      npr.assign((nsl.size() + 1) / 2, 0);
+      memcpy(npr.data(), nsl.data(), 2 * nsl.size());
     }
   }
 
@@ -1911,8 +2027,11 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
   in.off_dense = static_cast<int32_t>(off); off += dense_words;
   in.off_nrow_ptr = static_cast<int32_t>(off); off += static_cast<int64_t>(nrp.size());
   in.off_npairs = static_cast<int32_t>(off); off += static_cast<int64_t>(npr.size());
-  in.npairs = static_cast<int32_t>(npr.size() / 2);
+  in.npairs = static_cast<int32_t>(roww ? nsl.size() : npr.size() / 2);
   in.max_npairs = static_cast<int32_t>(max_np);
+  in.narrow_roww = roww ? 1 : 0;
+  in.off_nrow_w = static_cast<int32_t>(off); off += static_cast<int64_t>(nrw.size());
+  in.scalar_lds_bytes = static_cast<int32_t>(scalar_need);
   if (off > 0x7fffffff) return fail(TAL_ERR_INVALID, "tal_round_plan_build: plan larger than 2^31 words");
   in.words = static_cast<int32_t>(off);
   in.lds_bytes = static_cast<int32_t>(stream_cs > 0 ? stream_lds_bytes(stream_cs) : lds_need);
@@ -1936,6 +2055,7 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
     memcpy(plan_host + in.off_nrow_ptr, nrp.data(), 4 * nrp.size());
     memcpy(plan_host + in.off_npairs, npr.data(), 4 * npr.size());
   }
+  if (!nrw.empty()) memcpy(plan_host + in.off_nrow_w, nrw.data(), 4 * nrw.size());
   if (rb) {
     memcpy(plan_host + in.off_grp_blk_ptr, grp_blk_ptr.data(), 4 * (G + 1));
     int64_t pos = in.off_dense;
@@ -2069,7 +2189,7 @@ int64_t tal_round_plan_words(int32_t rows, int64_t nnz) {
   // grp_row_ptr + grp_src_ptr (<= rows+1 each) + src_row (<= nnz) + row_ptr + slot + w + out_row
   // + the narrow form's row pointers and padded pairs
   return 2 * (static_cast<int64_t>(rows) + 1) + nnz + (rows + 1) + 2 * nnz + rows + 16 +
-         (rows + 1) + 2 * (nnz + 3LL * rows);
+         (rows + 1) + 2 * (nnz + 3LL * rows) + rows;
 }
 
 
@@ -2088,11 +2208,15 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
     return fail(TAL_ERR_INVALID, "tal_round_plan_build: dense_rb must be 0, 8 or -1");
   // group consecutive rows while the union of their sources fits the LDS budget (both round
   // kernels stage 16*c4 bytes per source; the scalar one also the plan slice)
+  const bool roww = c4 < 64 && rows_uniform_weights(rows, row_ptr_host, w_host);
   auto fits = [&](int64_t ns, int64_t nr, int64_t no) {
     const int64_t sliced = group_lds_bytes(ns, nr, no, c4);
     if (c4 >= 64) return sliced <= lds_bytes;
-    // narrow kernel: + the -0.0 tile, pairs padded (<= 3 per row) and read-ahead
-    return std::max<int64_t>(sliced, static_cast<int64_t>(narrow_lds_bytes(ns, nr, no + 3 * nr, c4))) <= lds_bytes;
+    // narrow kernel: its own carve (padding <= 3 per row, read-ahead) within the budget; the
+    // staged scalar tail kernel within the hardware's 160 KiB
+    const int64_t narrow = static_cast<int64_t>(roww ? narrow_roww_lds_bytes(ns, nr, no + 3 * nr, c4)
+                                                     : narrow_lds_bytes(ns, nr, no + 3 * nr, c4));
+    return narrow <= lds_bytes && sliced <= 160 * 1024;
   };
   Groups grp;
   rc = group_rows(rows, row_ptr_host, col_host, max_col, fits, &grp);
