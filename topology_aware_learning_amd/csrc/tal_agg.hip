@@ -40,8 +40,10 @@ constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one we
 constexpr uint32_t kMaskSelf0 = 0x100u;          // streamed tables: bit 8+r = the entry is row r's own model
 constexpr uint32_t kMaskSelf = 0xff00u;
 constexpr int kMaxGrid = 256 * 8; // 256 CUs x 8 resident 256-thread blocks
-constexpr int kK1Unroll = 2;     // float4 chunks per lane per K1 grid-stride step
-constexpr int kK1Grid = 4096;    // K1 grid cap (16 blocks per CU in flight)
+constexpr int kK1Unroll = 1;     // float4 chunks per lane per K1 grid-stride step
+constexpr int kK1Grid = 1 << 24; // K1 grid cap: in practice one chunk per lane and no second pass
+                                 // (measured 5.98 vs 5.63 TB/s for a 4096-block grid-stride launch,
+                                 // tools/tune/k1_probe.hip, ResNet-50 M = 9)
 
 typedef float v4f __attribute__((ext_vector_type(4)));
 
@@ -134,7 +136,7 @@ __device__ __forceinline__ float4 ld_stream(const float* base, int64_t i) {
 }
 
 // K1 vector kernel.  Each lane owns kK1Unroll float4 chunks per grid-stride step and issues the
-// loads of every operand of both chunks before the ordered accumulate: M * kK1Unroll 16-B loads
+// loads of every operand of its chunks before the ordered accumulate: M * kK1Unroll 16-B loads
 // in flight per lane.
 // M_STATIC > 0: operand count known at compile time; 0: runtime count, loads in batches of 8.
 // CONT: accumulate onto `out` (passes after the first when M > kMaxOps; keeps the exact order).
