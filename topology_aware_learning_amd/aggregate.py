@@ -76,6 +76,7 @@ def _mark_used(tag: str, device) -> None:
 
 
 _SEG_DTYPE = {"f32": torch.float32, "b16": torch.bfloat16, "i64": torch.int64}
+_D2H_CHUNK = 16 << 20  # bytes per write-back chunk
 
 
 def _seg_sizes(layout: StateLayout):
@@ -85,8 +86,9 @@ def _seg_sizes(layout: StateLayout):
 def _stage(models: Sequence[nn.Module], layout: StateLayout, device) -> dict:
     """Pack non-bound models' segments into [k, n] device tensors (one per non-empty segment).
 
-    Models already on `device` are packed there; the others go through one pinned host buffer
-    and a single H2D copy per segment (the host-memory path of the reference's CPU models)."""
+    Models already on `device` are packed there; the others are packed into one pinned host
+    buffer per segment, each operand's H2D copy issued as soon as that operand is packed so the
+    copy overlaps packing the next one (the host-memory path of the reference's CPU models)."""
     k = len(models)
     sizes = {g: n for g, n in _seg_sizes(layout).items() if n}
     dev = {g: torch.empty(k, n, dtype=_SEG_DTYPE[g], device=device) for g, n in sizes.items()}
@@ -103,13 +105,12 @@ def _stage(models: Sequence[nn.Module], layout: StateLayout, device) -> dict:
             host_rows.append(j)
     if host_rows:
         h = len(host_rows)
-        idx = torch.tensor(host_rows, dtype=torch.long, device=device)
         for g, n in sizes.items():
             esz = torch.empty((), dtype=_SEG_DTYPE[g]).element_size()
             hb = _pinned(esz * h * n, "in_" + g).view(_SEG_DTYPE[g]).view(h, n)
             for q, j in enumerate(host_rows):
                 torch.cat([t.detach().to("cpu") for t in layout.flatten_cat(sds[j], g)], out=hb[q])
-            dev[g].index_copy_(0, idx, hb.to(device, non_blocking=True))
+                dev[g][j].copy_(hb[q], non_blocking=True)  # in flight while the next one packs
             _mark_used("in_" + g, device)
     return dev
 
@@ -178,16 +179,31 @@ def _write_back(target: nn.Module, layout: StateLayout, outs: dict) -> None:
             for name, t in sd.items():
                 t.copy_(views[name])
         return
+    # D2H in chunks of whole entries (~_D2H_CHUNK bytes), each with its own event: the host
+    # copies a chunk's entries into the model while later chunks are still in flight
     host = dict(empty)
-    dev = None
+    pending = []  # (event, entry names)
     for g, o in outs.items():
         esz = o.element_size()
         host[g] = _pinned(esz * max(o.numel(), 1), "out_" + g).view(o.dtype)[: o.numel()]
-        host[g].copy_(o, non_blocking=True)
-        dev = o.device
-    if dev is not None:
-        torch.cuda.current_stream(dev).synchronize()  # host reads the buffers next
+        stream = torch.cuda.current_stream(o.device)
+        ents = [e for e in layout.entries if e.seg == g and e.alias_of is None]
+        names, start = [], 0
+        for k, e in enumerate(ents):
+            names.append(e.name)
+            end = e.offset + e.numel
+            if (end - start) * esz >= _D2H_CHUNK or k == len(ents) - 1:
+                host[g][start:end].copy_(o[start:end], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                pending.append((ev, names))
+                names, start = [], end
     views = layout.views(host["f32"], host["i64"], host["b16"])
     with torch.no_grad():
-        for name, t in sd.items():
-            t.copy_(views[name])
+        for ev, names in pending:
+            ev.synchronize()
+            for name in names:
+                sd[name].copy_(views[name])
+        for e in layout.entries:  # tied keys share storage; copy_ as load_state_dict would
+            if e.alias_of is not None:
+                sd[e.name].copy_(views[e.name])
