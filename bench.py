@@ -8,8 +8,10 @@ one whole aggregation round (64 aggregation calls) executed by the K3 round kern
 device-resident pool, inputs already in HBM, snapshot semantics, exact reference numerics.
 
 With --gpus N > 1 (launched by torch.distributed.run, one rank per GPU) the graph has 64*N
-devices (weak scaling: 64 per GPU, contiguous blocks); neighbor models owned by other GPUs
-arrive by RCCL send/recv over xGMI, overlapped with the interior rows' reduction.
+devices (weak scaling: 64 per GPU, contiguous blocks).  The exchange moves the fewer link
+bytes: neighbor models owned by other GPUs by RCCL send/recv over xGMI, overlapped with the
+interior rows (halo), or every model's column blocks by two RCCL all-to-alls around the local
+round (transpose; random expanders at 4+ GPUs) — topology_aware_learning_amd/transposed.py.
 
 Prints ONE JSON line (rank 0).  See DESIGN.md for the byte accounting.
 """
@@ -56,6 +58,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU baseline sample")
     p.add_argument("--no-k1", action="store_true", help="skip the per-call K1 side measurement")
     p.add_argument("--host-path", action="store_true", help="also time the H2D+K1+D2H per-call path")
+    p.add_argument("--exchange", default="auto", choices=["auto", "halo", "transpose"],
+                   help="N > 1: neighbor models by RCCL P2P (halo) or column blocks by all-to-all "
+                        "(transpose); auto = fewer link bytes (transposed.choose_exchange)")
     return p.parse_args()
 
 
@@ -243,16 +248,15 @@ def main():
             k1 = bench_k1(layout, pin, orders, weights, mode, dev)
         hostp = bench_host_path(lay, M, dev) if args.host_path else None
     else:
-        from topology_aware_learning_amd.distributed import ShardedRound
+        from topology_aware_learning_amd.transposed import make_round
 
-        sr = ShardedRound(layout, orders, weights, rank, world, dev, mode=mode, tune=not args.no_tune)
+        sr = make_round(layout, orders, weights, rank, world, dev, exchange=args.exchange, mode=mode,
+                        tune=not args.no_tune)
         fill_pool(sr.pool_a, 1234 + rank)
         sr.step()
-        # spot check: one (boundary if any) row of this rank == K1 on its operands as received
-        k = (sr.spec.boundary or sr.spec.interior)[0]
-        chk = torch.empty(layout.n_f32, dtype=torch.float32, device=dev)
-        ops.agg_f32([sr.pool_b.row_f32(j) for j in sr.spec.orders_local[k]], sr.spec.weights[k], chk, mode=mode)
-        ok = torch.tensor([int(torch.equal(chk.view(torch.int32), sr.pool_a.row_f32(k).view(torch.int32)))], device=dev)
+        # spot check: one output row (halo) / row block (transpose) of this rank == K1 on its
+        # operands as received, bitwise
+        ok = torch.tensor([int(sr.spot_check())], device=dev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         parity_dist = bool(ok.item())
         for _ in range(args.warmup):
@@ -270,12 +274,10 @@ def main():
         el = float(t.item())
         torch.cuda.synchronize(dev)
         k_ms = float(np.mean(sr.kernel_ms()))
-        staged = sr.staged_sources
-        rows = sr.local_rows
-        bytes_round = 4 * layout.n_f32 * (staged + rows)
+        bytes_round = sr.kernel_bytes
         result_extra = dict(kernel=",".join(sorted({ops.round_kernel_name(p.info) for p in sr.plans.values()})),
-                            halo_rows_in=sr.halo_rows_in,
-                            halo_bytes_in=sr.halo_rows_in * 4 * layout.ld_f32)
+                            exchange=sr.exchange_kind, link_bytes_in_per_round=sr.link_bytes,
+                            link_GBps_in=sr.link_bytes / (el / args.steps) / 1e9)
         units = n_dev_total * n_params * args.steps
         parity_ok = parity_dist
         k1 = None
@@ -311,7 +313,7 @@ def main():
                                + f", {args.model} state_dicts, max M={M} (self last), unweighted, "
                                "one full aggregation round per step, snapshot semantics",
                    "model_layout": args.model, "devices": n_dev_total, "devices_per_gpu": args.devices_per_gpu,
-                   "params_per_model": n_params, "parallelism": f"row-sharded x{world}" if world > 1 else "1 GPU"},
+                   "params_per_model": n_params, "parallelism": f"{result_extra.get('exchange', '')}-sharded x{world}" if world > 1 else "1 GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                      "bytes_per_launch": bytes_round, "kernel_ms": k_ms},

@@ -84,3 +84,95 @@ def test_gloo_exchange_matches_global_round(tmp_path, world):
     igot = np.concatenate([np.load(tmp_path / f"i{r}.npy") for r in range(world)])
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     assert np.array_equal(igot, iref)
+
+
+# ------------------------------------------------------------------------------------------
+# transposed exchange (transposed.py): column blocks by all-to-all instead of halo rows
+
+from topology_aware_learning_amd.transposed import (choose_exchange, column_blocks, exchange_bytes,  # noqa: E402
+                                                    pack_columns, positions, unpack_columns)
+
+
+@pytest.mark.parametrize("n,world", [(203, 1), (203, 2), (203, 3), (5, 4), (1, 3), (4096, 8)])
+def test_column_blocks_pack_round_trip(n, world):
+    b, blocks = column_blocks(n, world)
+    assert b % 4 == 0 and sum(w for _, w in blocks) == n
+    assert all(c0 == p * b and w <= b for p, (c0, w) in enumerate(blocks))
+    rows, ld = 5, n + 7
+    pool = torch.randn(rows, ld)
+    send = torch.zeros(world * rows * b)
+    pack_columns(pool, rows, blocks, b, send)
+    back = torch.zeros(rows, ld)
+    unpack_columns(send, rows, blocks, b, back)
+    assert torch.equal(back[:, :n], pool[:, :n]) and not back[:, n:].any()
+
+
+def test_exchange_choice_follows_link_bytes():
+    import networkx as nx
+
+    def orders_of(g):
+        return [sorted(g.neighbors(i)) + [i] for i in range(g.number_of_nodes())]
+
+    n_f, n_i = 23_573_962, 53
+    reg = orders_of(nx.random_regular_graph(8, 512, seed=0))
+    own8 = partition_contiguous(512, 8)
+    b = exchange_bytes(reg, own8, 8, n_f, n_i)
+    assert b["transpose"] == 2 * 64 * (4 * n_f + 8 * n_i) * 7 // 8
+    assert b["halo"] > 2.5 * b["transpose"]  # ~280 of 448 remote models per rank
+    assert choose_exchange(reg, own8, 8, n_f, n_i) == "transpose"
+    reg2 = orders_of(nx.random_regular_graph(8, 128, seed=0))
+    assert choose_exchange(reg2, partition_contiguous(128, 2), 2, n_f, n_i) == "halo"  # equal bytes
+    ring = orders_of(nx.cycle_graph(64))
+    assert choose_exchange(ring, partition_contiguous(64, 8), 8, n_f, n_i) == "halo"
+    assert choose_exchange(ring, partition_contiguous(64, 1), 1, n_f, n_i) == "halo"
+
+
+def _worker_transposed(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    orders, ws, pool, ipool = problem()
+    n_dev = len(orders)
+    owner = np.array([(i * 7) % world for i in range(n_dev)], np.int32)  # not contiguous
+    own_by_rank, base, pos = positions(owner, world)
+    own = own_by_rank[rank]
+    inv = np.empty(n_dev, np.int64)
+    inv[pos] = np.arange(n_dev)
+    outs = {}
+    for name, data, dt in (("f", pool, torch.float32), ("i", ipool, torch.int64)):
+        n = data.shape[1]
+        b, blocks = column_blocks(n, world)
+        mine = torch.zeros(len(own), n + 3, dtype=dt)
+        mine[:, :n] = torch.from_numpy(data[own])
+        send = torch.zeros(world * len(own) * b, dtype=dt)
+        pack_columns(mine, len(own), blocks, b, send)
+        work_in = torch.zeros(n_dev, b, dtype=dt)
+        dist.all_to_all_single(work_in.view(-1), send, [len(o) * b for o in own_by_rank], [len(own) * b] * world)
+        assert np.array_equal(work_in[:, : blocks[rank][1]].numpy(),
+                              data[inv][:, blocks[rank][0]: blocks[rank][0] + blocks[rank][1]])
+        # the round on this rank's column block, rows in rank-major order (the GPU test runs K3)
+        rp, col, w = ra.round_csr([[int(pos[j]) for j in orders[int(inv[q])]] for q in range(n_dev)],
+                                  [ws[int(inv[q])] for q in range(n_dev)])
+        fn = oracle.round_f32 if dt == torch.float32 else oracle.round_i64
+        work_out = torch.from_numpy(np.ascontiguousarray(fn(work_in.numpy(), rp, col, w, np.arange(n_dev))))
+        back = torch.zeros(world * len(own) * b, dtype=dt)
+        dist.all_to_all_single(back, work_out.view(-1), [len(own) * b] * world, [len(o) * b for o in own_by_rank])
+        unpack_columns(back, len(own), blocks, b, mine)
+        outs[name] = mine[:, :n].numpy()
+    np.save(os.path.join(out_dir, f"tr{rank}.npy"), outs["f"])
+    np.save(os.path.join(out_dir, f"ti{rank}.npy"), outs["i"])
+    np.save(os.path.join(out_dir, f"town{rank}.npy"), np.asarray(own))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_transposed_exchange_matches_global_round(tmp_path, world):
+    mp.spawn(_worker_transposed, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    orders, ws, pool, ipool = problem()
+    rp, col, w = ra.round_csr(orders, ws)
+    ref = oracle.round_f32(pool, rp, col, w, np.arange(len(orders)))
+    iref = oracle.round_i64(ipool, rp, col, w, np.arange(len(orders)))
+    for r in range(world):
+        own = np.load(tmp_path / f"town{r}.npy")
+        assert np.array_equal(np.load(tmp_path / f"tr{r}.npy").view(np.uint32), ref[own].view(np.uint32))
+        assert np.array_equal(np.load(tmp_path / f"ti{r}.npy"), iref[own])

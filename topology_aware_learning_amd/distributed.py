@@ -174,3 +174,22 @@ class ShardedRound:
     def own_rows(self) -> ModelPool:
         """Pool whose rows [0, local_rows) hold this rank's current models."""
         return self.pool_a
+
+    @property
+    def kernel_bytes(self) -> int:
+        """Algorithmic HBM bytes of one round's local kernels (staged sources + written rows)."""
+        return 4 * self.layout.n_f32 * (self.staged_sources + self.local_rows)
+
+    @property
+    def link_bytes(self) -> int:
+        """Bytes this rank receives over the links per round."""
+        return self.halo_rows_in * (4 * self.layout.n_f32 + 8 * self.layout.n_i64)
+
+    def spot_check(self) -> bool:
+        """After a step: one (boundary if any) row == K1 on its operands as they were received
+        (bitwise; the operands are the previous buffer, now pool_b)."""
+        k = (self.spec.boundary or self.spec.interior)[0]
+        chk = torch.empty(self.layout.n_f32, dtype=torch.float32, device=self.device)
+        ops.agg_f32([self.pool_b.row_f32(j) for j in self.spec.orders_local[k]], self.spec.weights[k], chk,
+                    mode=self.mode)
+        return bool(torch.equal(chk.view(torch.int32), self.pool_a.row_f32(k).view(torch.int32)))
