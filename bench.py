@@ -228,11 +228,11 @@ def main():
         torch.cuda.synchronize(dev)
         el = time.perf_counter() - t0
         k_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
-        staged = plan.info.total_src
+        staged = plan.staged_rows()
         bytes_round = esize * n_float * (staged + rows)  # compulsory: each staged source read once, each output written once
         per_call_bytes = esize * n_float * (len(col) + rows)  # SURVEY §8(d) B summed over the round's calls
         result_extra = dict(
-            kernel=_ops.round_kernel_name(plan.info), plan=dict(groups=plan.info.n_groups, staged_sources=staged,
+            kernel=_ops.round_kernel_name(plan), plan=dict(groups=plan.info.n_groups, staged_sources=staged,
                                                   c4=plan.info.c4, dense_rb=plan.info.dense_rb,
                                                   lds_reads_per_column=plan.info.dense_reads,
                                                   tuned_ms=plan.tuned_ms, candidates=plan.candidates,
@@ -275,7 +275,7 @@ def main():
         torch.cuda.synchronize(dev)
         k_ms = float(np.mean(sr.kernel_ms()))
         bytes_round = sr.kernel_bytes
-        result_extra = dict(kernel=",".join(sorted({ops.round_kernel_name(p.info) for p in sr.plans.values()})),
+        result_extra = dict(kernel=",".join(sorted({ops.round_kernel_name(p) for p in sr.plans.values()})),
                             exchange=sr.exchange_kind, link_bytes_in_per_round=sr.link_bytes,
                             link_GBps_in=sr.link_bytes / (el / args.steps) / 1e9)
         units = n_dev_total * n_params * args.steps

@@ -192,6 +192,21 @@ int32_t tal_agg_round_i64(const int64_t* pool_in, int64_t ld_in, int64_t* pool_o
                           int64_t ld_out, int64_t n, const int32_t* plan_dev,
                           const tal_round_plan_info* info, void* stream);
 
+/* Clique rounds (K3c).  Rows of a round that form uniform-weight cliques — m <= 64 sources
+ * s_0 < ... < s_{m-1} (pool rows) with one fp32 weight w, and for member i an output row whose
+ * operands are, in reference order (decentralized_app.py:625), every other member ascending and
+ * then s_i — are computed from one read of each source: the products are shared and each row's
+ * in-order chain extends the shared prefix (bitwise the reference in EXACT mode; FMA mode as
+ * tal_agg_f32's).  table_dev: n_cliques records of TAL_CLIQUE_WORDS int32
+ *   {m, bits of w, 0, 0, src_row[64], out_row[64]}  (out_row -1: member without an output row)
+ * copied to the device.  The other rows of the round run through a regular plan (a second
+ * call).  Out of place only; pools 8-B aligned with even ld.  mmax = the largest m (16, 32 or
+ * 64 registers of products per lane). */
+#define TAL_CLIQUE_WORDS 132
+int32_t tal_agg_round_clique_f32(const float* pool_in, int64_t ld_in, float* pool_out, int64_t ld_out,
+                                 int64_t n, const int32_t* table_dev, int32_t n_cliques, int32_t mmax,
+                                 int32_t mode, void* stream);
+
 /* The same round on bf16 pools (arithmetic as tal_agg_bf16, per mode).  Takes sparse plans
  * (c4 64 / 128, dense_rb 0) and narrow plans (c4 16 / 32); TAL_ERR_INVALID for dense or
  * streamed plans.  A staged tile holds the sources' values as fp32 (c4 float4 per source). */

@@ -470,3 +470,75 @@ def test_cosine_kernel_vs_numpy(cuda):
     for j, b in enumerate(bs):
         ref = ra.cosine_similarity([a[n].numpy() for n in names], [b[n].numpy() for n in names])
         assert abs(got[j] - ref) < 2e-5, (j, got[j], ref)
+
+
+_CLIQUE_GRAPHS = {
+    "barbell60": lambda: nx.barbell_graph(60, 8),   # BASELINE config 4's topology (m = 60)
+    "barbell20": lambda: nx.barbell_graph(20, 3),   # m = 20: the 32-register kernel
+    "complete64": lambda: nx.complete_graph(64),    # m = 64: the largest block
+    "complete9": lambda: nx.complete_graph(9),      # m = 9: the 16-register kernel
+    "mixed": lambda: nx.disjoint_union(nx.complete_graph(12), nx.random_regular_graph(4, 30, seed=1)),
+}
+
+
+@pytest.mark.parametrize("n", [1, 7, 4098, 70001])
+@pytest.mark.parametrize("graph", list(_CLIQUE_GRAPHS))
+def test_round_clique_vs_oracle(cuda, graph, n):
+    """K3c (shared products, prefix-extended chains): bitwise the oracle round in EXACT mode and
+    bitwise K1-FMA in FMA mode, signed weights, fp32 specials, odd n (scalar tail), permuted and
+    padded output rows, the rest rows through their regular plan."""
+    g = _CLIQUE_GRAPHS[graph]()
+    orders = [sorted(g.neighbors(i)) + [i] for i in sorted(g.nodes)]
+    rows = len(orders)
+    sign = -1.0 if n % 2 else 1.0
+    ws = [[sign / len(o)] * len(o) for o in orders]
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    out_rows = (np.random.default_rng(rows).permutation(rows) + 2).astype(np.int32)
+    plan = ops.build_clique_plan(row_ptr, col, w, out_rows)
+    assert plan is not None and plan.n_cliques >= 1
+    rng = np.random.default_rng(rows + n)
+    pool = np.stack([_rand_f32(rng, n, special=True) for _ in range(rows)])
+    if n > 8:
+        pool[:, 5] = np.float32(-0.0)
+        pool[::3, 6] = np.float32(np.inf)
+    ld = n + (3 if n % 2 else 2)  # even, padded stride
+    pin = torch.zeros(rows, ld, device=cuda)
+    pin[:, :n] = torch.from_numpy(pool).to(cuda)
+    pout = torch.full((rows + 2, ld), 7.0, device=cuda)
+    got = pout
+    ops.round_f32(pin, got, plan, n=n)
+    full = oracle.round_f32(pool, row_ptr, col, w, out_rows - 2)
+    assert _bits_equal(got[2:, :n].cpu().numpy(), full)
+    assert torch.all(got[:2] == 7.0) and torch.all(got[:, n:] == 7.0)  # nothing else written
+    # FMA mode: the same chains fused, bitwise K1 in FMA mode on the same operands
+    ops.round_f32(pin, got, plan, n=n, mode=ops.MODE_FMA)
+    chk = torch.empty(n, device=cuda)
+    for r in (0, rows // 2, rows - 1):
+        ops.agg_f32([pin[j, :n] for j in orders[r]], ws[r], chk, mode=ops.MODE_FMA)
+        assert torch.equal(chk.view(torch.int32), got[out_rows[r], :n].contiguous().view(torch.int32))
+    with pytest.raises(ValueError):
+        ops.round_f32(pin, pin, plan, n=n)
+
+
+def test_round_clique_through_tuner_and_i64(cuda):
+    """tune_plan offers the clique plan for a barbell round; the int64 segment of a clique plan
+    runs through its full regular plan."""
+    g = nx.barbell_graph(24, 4)
+    orders = [sorted(g.neighbors(i)) + [i] for i in sorted(g.nodes)]
+    rows = len(orders)
+    ws = [ra.unweighted_weights(len(o)) for o in orders]
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    out_rows = np.arange(rows, dtype=np.int32)
+    rng = np.random.default_rng(3)
+    pool = rng.standard_normal((rows, 20001)).astype(np.float32)
+    pin = torch.from_numpy(pool).to(cuda)
+    pout = torch.zeros_like(pin)
+    plan = ops.tune_plan(row_ptr, col, w, out_rows, pin, pout)
+    assert any(c["spec"] == {"clique": 1} for c in plan.candidates)
+    cp = ops.plan_from_spec(row_ptr, col, w, out_rows, {"clique": 1}).to(cuda)
+    ops.round_f32(pin, pout, cp)
+    assert _bits_equal(pout.cpu().numpy(), oracle.round_f32(pool, row_ptr, col, w, out_rows))
+    ip = rng.integers(0, 10 ** 6, size=(rows, 5)).astype(np.int64)
+    ipo = torch.zeros(rows, 5, dtype=torch.int64, device=cuda)
+    ops.round_i64(torch.from_numpy(ip).to(cuda), ipo, cp)
+    assert np.array_equal(ipo.cpu().numpy(), oracle.round_i64(ip, row_ptr, col, w, out_rows))

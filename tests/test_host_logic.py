@@ -415,3 +415,69 @@ def test_prox_plan_covers_parameter_segments():
         assert np.all(rows[:, 0] == s)
         assert rows[0, 1] == e.offset and rows[:, 2].sum() == e.numel
         assert np.all(rows[1:, 1] == rows[:-1, 1] + rows[:-1, 2])  # contiguous chunks
+
+
+def _orders_of(g):
+    return [sorted(g.neighbors(i)) + [i] for i in sorted(g.nodes)]
+
+
+def test_find_cliques_barbell_complete_and_rejections():
+    import networkx as nx
+
+    from oracle import reference_alg as ra
+    from topology_aware_learning_amd import ops
+
+    g = nx.barbell_graph(12, 4)  # cliques 0..11 and 16..27, path 12..15
+    orders = _orders_of(g)
+    ws = [ra.unweighted_weights(len(o)) for o in orders]
+    rp, col, w = ra.round_csr(orders, ws)
+    out = np.arange(len(orders), dtype=np.int32)[::-1].copy()
+    cliques, rest = ops.find_cliques(rp, col, w, out)
+    assert len(cliques) == 2
+    for srcs, w32, outs in cliques:
+        assert len(srcs) == 12 and len(outs) == 11  # the bridge node has one more neighbor
+        assert w32 == np.float32(1 / 12)
+        for i, o in outs.items():  # member i's row: every other member ascending, then itself
+            r = int(np.flatnonzero(out == o)[0])
+            assert list(col[rp[r]: rp[r + 1]]) == [s for s in srcs if s != srcs[i]] + [srcs[i]]
+    assert sorted(rest) == [11, 12, 13, 14, 15, 16]
+    # a complete graph is one block; a ring has none
+    oc = _orders_of(nx.complete_graph(20))
+    rp, col, w = ra.round_csr(oc, [ra.unweighted_weights(20)] * 20)
+    cl, rest = ops.find_cliques(rp, col, w, np.arange(20))
+    assert len(cl) == 1 and len(cl[0][2]) == 20 and rest == []
+    orr = _orders_of(nx.cycle_graph(16))
+    rp, col, w = ra.round_csr(orr, [ra.unweighted_weights(3)] * 16)
+    assert ops.find_cliques(rp, col, w, np.arange(16))[0] == []
+    # per-operand weights (centrality) and self not last are not cliques
+    cent = nx.degree_centrality(nx.complete_graph(20))
+    wc = [ra.centrality_weights(o, cent, True, 10.0) for o in oc]
+    wc[0] = [0.5] + [0.5 / 19] * 19
+    rp, col, w = ra.round_csr(oc, wc)
+    assert all(len(c[2]) < 20 for c in ops.find_cliques(rp, col, w, np.arange(20), min_rows=2)[0])
+    shuffled = [o[-1:] + o[:-1] for o in oc]
+    rp, col, w = ra.round_csr(shuffled, [ra.unweighted_weights(20)] * 20)
+    assert ops.find_cliques(rp, col, w, np.arange(20))[0] == []
+
+
+def test_clique_plan_table_and_spec():
+    import networkx as nx
+
+    from oracle import reference_alg as ra
+    from topology_aware_learning_amd import ops
+
+    orders = _orders_of(nx.barbell_graph(60, 8))
+    rp, col, w = ra.round_csr(orders, [ra.unweighted_weights(len(o)) for o in orders])
+    out = np.arange(len(orders), dtype=np.int32)
+    p = ops.build_clique_plan(rp, col, w, out)
+    assert p.n_cliques == 2 and p.mmax == 60 and p.clique_rows == 118
+    t = p.table.reshape(p.n_cliques, ops.CLIQUE_WORDS)
+    assert list(t[:, 0]) == [60, 60] and (t[:, 1].view(np.float32) == np.float32(1 / 60)).all()
+    assert p.rest is not None and p.rest.rows == 10 and p.full.rows == 128
+    assert p.staged_rows() == 120 + p.rest.staged_rows()
+    q = ops.plan_from_spec(rp, col, w, out, {"clique": 1})
+    assert np.array_equal(q.table, p.table)
+    assert ops.round_kernel_name(p) == "k_round_clique"
+    ring = _orders_of(nx.cycle_graph(16))
+    rp, col, w = ra.round_csr(ring, [ra.unweighted_weights(3)] * 16)
+    assert ops.build_clique_plan(rp, col, w, np.arange(16)) is None

@@ -23,7 +23,7 @@ TAL_ERR_HIP = 2
 TAL_ERR_CAPACITY = 3
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 EXPORTED = (
     "tal_last_error",
@@ -37,6 +37,7 @@ EXPORTED = (
     "tal_agg_round_f32",
     "tal_agg_round_i64",
     "tal_agg_round_bf16",
+    "tal_agg_round_clique_f32",
     "tal_cosine_plan_words",
     "tal_cosine_plan_build",
     "tal_cosine_scratch_bytes",
@@ -123,6 +124,7 @@ _SIGS = {
     "tal_agg_round_f32": (_I32, [_P, _I64, _P, _I64, _I64, _P, ctypes.POINTER(RoundPlanInfo), _I32, _P]),
     "tal_agg_round_i64": (_I32, [_P, _I64, _P, _I64, _I64, _P, ctypes.POINTER(RoundPlanInfo), _P]),
     "tal_agg_round_bf16": (_I32, [_P, _I64, _P, _I64, _I64, _P, ctypes.POINTER(RoundPlanInfo), _I32, _P]),
+    "tal_agg_round_clique_f32": (_I32, [_P, _I64, _P, _I64, _I64, _P, _I32, _I32, _I32, _P]),
     "tal_cosine_plan_words": (_I64, [_PI64, _I32]),
     "tal_cosine_plan_build": (_I32, [_PI64, _I32, _PI64, _I64, _PI32]),
     "tal_cosine_scratch_bytes": (_I64, [_I32, _I32]),

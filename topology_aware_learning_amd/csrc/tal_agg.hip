@@ -33,7 +33,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 8;
+constexpr int kAbiVersion = 9;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -1471,6 +1471,124 @@ int32_t launch_round_narrow(const T* pin, int64_t ld_in, T* pout, int64_t ld_out
   return fail(TAL_ERR_CAPACITY, "narrow round plan: group tile larger than 160 KiB");
 }
 
+// ------------------------------------------------------------------------------------------
+// K3c: uniform-weight cliques.  A clique block is m <= 64 sources s_0 < ... < s_{m-1} sharing
+// one fp32 weight w, with output rows for (some of) its members, member i's operands being, in
+// reference order, every other member ascending and then s_i itself (a complete graph's or a
+// barbell's clique rows under the unweighted strategy).  The products fl(w * x_j) are the same
+// for every row, and row i = ((S_i + p_{i+1}) + ... + p_{m-1}) + p_i with S_i the in-order
+// prefix p_0 + ... + p_{i-1}, which all later rows extend: one thread keeps p_0..p_{m-1} of its
+// two columns in registers, reads each source once from HBM, and emits every row with
+// ~m^2/2 adds instead of m^2 multiply-adds.  Bitwise the reference: each row's additions are
+// its own left-to-right chain (the prefix is shared, not reassociated); padding terms are -0.0
+// (x + -0.0 == x for every x), S_0 = -0.0 (-0.0 + p == p).  FMA mode keeps x_j and fuses
+// fma(w, x_j, acc); its padding is the zero whose product with w is -0.0.
+// ------------------------------------------------------------------------------------------
+constexpr int kCliqueMax = 64;
+
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+template <bool EXACT>
+__device__ __forceinline__ v2f clique_term(v2f acc, float w, v2f p) {
+  if constexpr (EXACT) return v2f{__fadd_rn(acc.x, p.x), __fadd_rn(acc.y, p.y)};
+  else return v2f{__builtin_fmaf(w, p.x, acc.x), __builtin_fmaf(w, p.y, acc.y)};
+}
+
+// A zero the compiler cannot see through: table reads indexed with it stay where they are
+// instead of being hoisted to the top of the kernel, where 128 live row indices would spill
+// the scalar register file.
+__device__ __forceinline__ int opaque_zero() {
+  int z;
+  asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+  return z;
+}
+
+// Columns e and e + 1 of every row of clique block `t`.
+template <int MMAX, bool EXACT>
+__global__ __launch_bounds__(kBlock) void k_round_clique(const float* __restrict__ pin, int64_t ld_in,
+                                                         float* __restrict__ pout, int64_t ld_out,
+                                                         int64_t n2, const int32_t* __restrict__ table) {
+  const int32_t* t = table + static_cast<int64_t>(blockIdx.y) * TAL_CLIQUE_WORDS;
+  const int64_t c2 = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (c2 >= n2) return;
+  const int64_t e = 2 * c2;
+  const int m = t[0];
+  const float w = __int_as_float(t[1]);
+  const float pad = EXACT ? -0.f : (__float_as_uint(w) >> 31 ? 0.f : -0.f);
+  // every load is issued unconditionally (a padding slot re-reads member 0, an L2 hit) so all
+  // MMAX loads are in flight before the first use; the padding value is selected afterwards
+  v2f p[MMAX];
+#pragma unroll
+  for (int j = 0; j < MMAX; ++j) {
+    const float* src = pin + static_cast<int64_t>(t[4 + (j < m ? j : 0) + opaque_zero()]) * ld_in + e;
+    p[j] = __builtin_nontemporal_load(reinterpret_cast<const v2f*>(src));
+    // batches of 8: the scheduler would otherwise compute all row addresses first
+    if (j % 8 == 7) __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int j = 0; j < MMAX; ++j) {
+    if constexpr (EXACT) p[j] = v2f{__fmul_rn(w, p[j].x), __fmul_rn(w, p[j].y)};
+    if (j >= m) p[j] = v2f{pad, pad};
+  }
+  v2f s = v2f{-0.f, -0.f};
+#pragma unroll
+  for (int i = 0; i < MMAX; ++i) {
+    const int orow = i < m ? t[4 + kCliqueMax + i + opaque_zero()] : -1;  // wave-uniform
+    if (orow >= 0) {
+      v2f acc = s;
+#pragma unroll
+      for (int j = i + 1; j < MMAX; ++j) acc = clique_term<EXACT>(acc, w, p[j]);
+      acc = clique_term<EXACT>(acc, w, p[i]);
+      __builtin_nontemporal_store(acc, reinterpret_cast<v2f*>(pout + static_cast<int64_t>(orow) * ld_out + e));
+    }
+    s = clique_term<EXACT>(s, w, p[i]);
+  }
+}
+
+// The last column of an odd-width round: one thread per member row, its chain in reference
+// order (every other member ascending, then itself).
+template <bool EXACT>
+__global__ __launch_bounds__(kCliqueMax) void k_round_clique_tail(const float* __restrict__ pin, int64_t ld_in,
+                                                                  float* __restrict__ pout, int64_t ld_out,
+                                                                  int64_t e, const int32_t* __restrict__ table) {
+  const int32_t* t = table + static_cast<int64_t>(blockIdx.x) * TAL_CLIQUE_WORDS;
+  const int m = t[0];
+  const int i = threadIdx.x;
+  if (i >= m) return;
+  const int orow = t[4 + kCliqueMax + i];
+  if (orow < 0) return;
+  const float w = __int_as_float(t[1]);
+  float acc = -0.f;
+  for (int j = 0; j <= m; ++j) {
+    if (j == i) continue;
+    const int k = j < m ? j : i;
+    const float x = pin[static_cast<int64_t>(t[4 + k]) * ld_in + e];
+    acc = EXACT ? __fadd_rn(acc, __fmul_rn(w, x)) : __builtin_fmaf(w, x, acc);
+  }
+  pout[static_cast<int64_t>(orow) * ld_out + e] = acc;
+}
+
+template <bool EXACT>
+int32_t launch_round_clique(const float* pin, int64_t ld_in, float* pout, int64_t ld_out, int64_t n,
+                            const int32_t* table, int32_t n_cliques, int32_t mmax, hipStream_t s) {
+  const int64_t n2 = n / 2;
+  const int64_t blocks = (n2 + kBlock - 1) / kBlock;
+  if (blocks > 0x7fffffffLL || n_cliques > 65535) return fail(TAL_ERR_INVALID, "clique round: grid too large");
+  if (n2 > 0) {
+    const dim3 grid(static_cast<unsigned>(blocks), static_cast<unsigned>(n_cliques));
+    if (mmax <= 16) k_round_clique<16, EXACT><<<grid, kBlock, 0, s>>>(pin, ld_in, pout, ld_out, n2, table);
+    else if (mmax <= 32) k_round_clique<32, EXACT><<<grid, kBlock, 0, s>>>(pin, ld_in, pout, ld_out, n2, table);
+    else k_round_clique<64, EXACT><<<grid, kBlock, 0, s>>>(pin, ld_in, pout, ld_out, n2, table);
+    int32_t rc = check_launch("clique round kernel");
+    if (rc) return rc;
+  }
+  if (n % 2) {
+    k_round_clique_tail<EXACT><<<n_cliques, kCliqueMax, 0, s>>>(pin, ld_in, pout, ld_out, n - 1, table);
+    return check_launch("clique round tail kernel");
+  }
+  return TAL_OK;
+}
+
 template <int NT, bool EXACT>
 int32_t launch_round_stream_nt(const float* pin, int64_t ld_in, float* pout, int64_t ld_out, int64_t n4,
                                const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
@@ -2353,6 +2471,25 @@ int32_t tal_agg_round_i64(const int64_t* pool_in, int64_t ld_in, int64_t* pool_o
                                             static_cast<hipStream_t>(stream));
   return launch_round_scalar<int64_t>(pool_in, ld_in, pool_out, ld_out, 0, n, v, *info, true,
                                    static_cast<hipStream_t>(stream));
+}
+
+int32_t tal_agg_round_clique_f32(const float* pool_in, int64_t ld_in, float* pool_out, int64_t ld_out,
+                                 int64_t n, const int32_t* table_dev, int32_t n_cliques, int32_t mmax,
+                                 int32_t mode, void* stream) {
+  if (!pool_in || !pool_out || !table_dev)
+    return fail(TAL_ERR_INVALID, "tal_agg_round_clique_f32: null pointer");
+  if (pool_in == pool_out)
+    return fail(TAL_ERR_INVALID, "tal_agg_round_clique_f32: the clique round runs out of place");
+  if (n < 0 || ld_in < n || ld_out < n) return fail(TAL_ERR_INVALID, "tal_agg_round_clique_f32: bad n / ld");
+  if (n_cliques < 0 || mmax < 1 || mmax > kCliqueMax)
+    return fail(TAL_ERR_INVALID, "tal_agg_round_clique_f32: n_cliques >= 0, 1 <= mmax <= 64");
+  if (!aligned8(pool_in) || !aligned8(pool_out) || ld_in % 2 || ld_out % 2)
+    return fail(TAL_ERR_INVALID, "tal_agg_round_clique_f32: pools must be 8-B aligned with even ld");
+  if (n == 0 || n_cliques == 0) { g_err.clear(); return TAL_OK; }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  return mode == TAL_MODE_EXACT
+             ? launch_round_clique<true>(pool_in, ld_in, pool_out, ld_out, n, table_dev, n_cliques, mmax, s)
+             : launch_round_clique<false>(pool_in, ld_in, pool_out, ld_out, n, table_dev, n_cliques, mmax, s);
 }
 
 int32_t tal_agg_bf16(const uint16_t* const* x_host, const double* w_host, int32_t m, uint16_t* out,

@@ -132,7 +132,7 @@ class ShardedRound:
             dist.barrier(group=group)
         self.local_rows = len(self.spec.own)
         self.halo_rows_in = len(self.spec.halo)
-        self.staged_sources = sum(p.info.total_src for p in self.plans.values())
+        self.staged_sources = sum(p.staged_rows() for p in self.plans.values())
         self._events: list = []
 
     def _run(self, name: str, a: ModelPool, b: ModelPool) -> None:

@@ -170,6 +170,115 @@ def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0, dense:
     return best[1]
 
 
+CLIQUE_MAX = 64
+CLIQUE_WORDS = 132        # TAL_CLIQUE_WORDS: {m, w bits, 0, 0, src[64], out[64]}
+CLIQUE_MIN_ROWS = 8       # smaller blocks stay in the regular plan
+
+
+def find_cliques(row_ptr, col, w, out_row, min_rows: int = CLIQUE_MIN_ROWS):
+    """Uniform-weight clique blocks of a round (the K3c kernel's rows, tal_agg.h): rows whose
+    operands are strictly ascending sources and then their own model (not among them), all with
+    one finite fp32 weight, grouped by (operand set, weight); a group of >= min_rows rows with
+    distinct own models and <= 64 sources is a clique block.  Returns (cliques, rest): cliques =
+    [(sources ascending, fp32 weight, {member index: out_row})], rest = the other row indices."""
+    row_ptr, col, w, out_row = _csr(row_ptr, col, w, out_row)
+    groups: dict = {}
+    for r in range(len(out_row)):
+        ops_ = col[row_ptr[r]: row_ptr[r + 1]]
+        m = len(ops_)
+        if m < 2 or m > CLIQUE_MAX:
+            continue
+        w32 = w[row_ptr[r]: row_ptr[r + 1]].astype(np.float32)
+        if not np.isfinite(w32[0]) or np.any(w32.view(np.uint32) != w32[:1].view(np.uint32)):
+            continue
+        rest, own = ops_[:-1], int(ops_[-1])
+        if np.any(np.diff(rest) <= 0) or own in rest:
+            continue
+        groups.setdefault((tuple(sorted(ops_.tolist())), int(w32[:1].view(np.uint32)[0])), []).append(r)
+    cliques, used = [], set()
+    for (srcs, wbits), rows in groups.items():
+        owns = [int(col[row_ptr[r + 1] - 1]) for r in rows]
+        if len(rows) < min_rows or len(set(owns)) != len(rows):
+            continue
+        idx = {s: i for i, s in enumerate(srcs)}
+        cliques.append((list(srcs), np.array([wbits], np.uint32).view(np.float32)[0],
+                        {idx[o]: int(out_row[r]) for o, r in zip(owns, rows)}))
+        used.update(rows)
+    return cliques, [r for r in range(len(out_row)) if r not in used]
+
+
+@dataclass
+class CliquePlan:
+    """A round split into clique blocks (K3c, one launch) and the remaining rows (a regular
+    RoundPlan, None if there are none).  `full` is a sparse plan over all rows, used for the
+    int64 and bf16 segments (the clique kernel is fp32)."""
+    table: np.ndarray
+    n_cliques: int
+    mmax: int
+    clique_sources: int
+    clique_rows: int
+    rest: Optional[RoundPlan]
+    full: RoundPlan
+    rows: int
+    rest_rows: Optional[list] = None
+    device: Optional[torch.Tensor] = None
+    tuned_ms: Optional[float] = None
+    candidates: Optional[list] = None
+    spec: Optional[dict] = None
+
+    @property
+    def info(self) -> RoundPlanInfo:
+        return self.full.info
+
+    @property
+    def single_group(self) -> bool:
+        return False  # clique blocks read other blocks' sources: never in place
+
+    def staged_rows(self) -> int:
+        """Source rows read from HBM per column (clique sources + the rest plan's)."""
+        return self.clique_sources + (self.rest.staged_rows() if self.rest is not None else 0)
+
+    def to(self, device) -> "CliquePlan":
+        self.device = torch.from_numpy(self.table).to(device)
+        if self.rest is not None:
+            self.rest.to(device)
+        self.full.to(device)
+        return self
+
+
+def build_clique_plan(row_ptr, col, w, out_row, min_rows: int = CLIQUE_MIN_ROWS,
+                      rest_spec: Optional[dict] = None) -> Optional[CliquePlan]:
+    """CliquePlan of a round, or None when it has no clique block (find_cliques)."""
+    row_ptr, col, w, out_row = _csr(row_ptr, col, w, out_row)
+    cliques, rest = find_cliques(row_ptr, col, w, out_row, min_rows)
+    if not cliques:
+        return None
+    table = np.zeros((len(cliques), CLIQUE_WORDS), np.int32)
+    for k, (srcs, w32, outs) in enumerate(cliques):
+        table[k, 0] = len(srcs)
+        table[k, 1] = np.array([w32], np.float32).view(np.int32)[0]
+        table[k, 4: 4 + len(srcs)] = srcs
+        table[k, 4 + CLIQUE_MAX: 4 + 2 * CLIQUE_MAX] = -1
+        for i, o in outs.items():
+            table[k, 4 + CLIQUE_MAX + i] = o
+    rest_plan = None
+    if rest:
+        sub = _sub_csr(row_ptr, col, w, out_row, rest)
+        rest_plan = plan_from_spec(*sub, rest_spec) if rest_spec else build_plan(*sub)
+    mmax = max(len(c[0]) for c in cliques)
+    return CliquePlan(table=table.reshape(-1), n_cliques=len(cliques), mmax=mmax,
+                      clique_sources=sum(len(c[0]) for c in cliques),
+                      clique_rows=sum(len(c[2]) for c in cliques), rest=rest_plan,
+                      full=build_plan(row_ptr, col, w, out_row, dense=0), rows=len(out_row), rest_rows=rest)
+
+
+def _sub_csr(row_ptr, col, w, out_row, rows):
+    """The CSR of a subset of a round's rows."""
+    rp = np.concatenate([[0], np.cumsum([row_ptr[r + 1] - row_ptr[r] for r in rows])]).astype(np.int32)
+    sel = np.concatenate([np.arange(row_ptr[r], row_ptr[r + 1]) for r in rows])
+    return rp, col[sel], w[sel], np.asarray(out_row)[rows]
+
+
 STREAM_GROUPINGS = ((64, 0), (128, 0), (64, 96))  # (max rows, max sources) per streamed group
 
 
@@ -242,6 +351,15 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
         if all(key != k for k, _ in cands):
             p.spec = dict(stream_rows=max_rows, stream_src=max_src)
             cands.append((key, p))
+    if not bf16:
+        cp = build_clique_plan(row_ptr, col, w, out_row)
+        if cp is not None:
+            cp.spec = dict(clique=1)
+            if cp.rest is not None:  # the rows outside the cliques get their own tuned plan
+                r_rp, r_col, r_w, r_out = _sub_csr(row_ptr, col, w, out_row, cp.rest_rows)
+                cp.rest = tune_plan(r_rp, r_col, r_w, r_out, pool_in, pool_out, n=n, reps=reps, mode=mode)
+                cp.spec["rest"] = cp.rest.spec
+            cands.append((("clique", cp.n_cliques, cp.staged_rows(), 0, cp.mmax, 0), cp))
     if not cands:
         return build_plan(row_ptr, col, w, out_row, dense=0 if bf16 else -1)
     if len(cands) == 1:
@@ -272,6 +390,12 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
 def plan_from_spec(row_ptr, col, w, out_row, spec: dict) -> RoundPlan:
     """Rebuild a plan tune_plan chose (its `spec`): profiling runs then time the same plan
     without re-tuning."""
+    if spec.get("clique"):
+        p = build_clique_plan(row_ptr, col, w, out_row, rest_spec=spec.get("rest"))
+        if p is None:
+            raise ValueError("plan spec asks for clique blocks but the round has none")
+        p.spec = dict(spec)
+        return p
     if "stream_rows" in spec:
         p = build_stream_plan(row_ptr, col, w, out_row, int(spec["stream_rows"]), int(spec["stream_src"]))
     else:
@@ -281,8 +405,12 @@ def plan_from_spec(row_ptr, col, w, out_row, spec: dict) -> RoundPlan:
     return p
 
 
-def round_kernel_name(info: RoundPlanInfo) -> str:
-    """Which K3 kernel tal_agg_round_f32 launches for this plan (mirrors launch_round_vec)."""
+def round_kernel_name(plan) -> str:
+    """Which K3 kernel tal_agg_round_f32 launches for this plan or plan info (mirrors
+    launch_round_vec); clique plans name the K3c kernel (their rest rows run a second one)."""
+    if isinstance(plan, CliquePlan):
+        return "k_round_clique"
+    info = plan.info if isinstance(plan, RoundPlan) else plan
     if info.stream_cs:
         return "k_round_stream"
     if info.c4 < 64:
@@ -310,20 +438,57 @@ def _plan_cost(info: RoundPlanInfo) -> float:
     return max(hbm, lds)
 
 
-def round_f32(pool_in: torch.Tensor, pool_out: torch.Tensor, plan: RoundPlan, n: Optional[int] = None,
+def round_f32(pool_in: torch.Tensor, pool_out: torch.Tensor, plan, n: Optional[int] = None,
               mode: int = MODE_EXACT, stream=None) -> torch.Tensor:
-    """K3 on [models, ld] fp32 pools (snapshot semantics; see tal_agg.h)."""
+    """K3 on [models, ld] fp32 pools (snapshot semantics; see tal_agg.h).  A CliquePlan runs
+    its clique blocks with K3c and its other rows with their regular plan (out of place)."""
+    if isinstance(plan, CliquePlan):
+        return _round_clique(pool_in, pool_out, plan, n, mode, stream)
     return _round(pool_in, pool_out, plan, n, torch.float32, mode, stream)
+
+
+def _round_clique(pool_in, pool_out, plan: CliquePlan, n, mode, stream):
+    _require_gpu(pool_in, "pool_in", torch.float32)
+    _require_gpu(pool_out, "pool_out", torch.float32)
+    if pool_in.dim() != 2 or pool_out.dim() != 2:
+        raise ValueError("pools must be 2-D [models, ld]")
+    if pool_in.device != pool_out.device:
+        raise ValueError("pools on different devices")
+    if pool_in.data_ptr() == pool_out.data_ptr():
+        raise ValueError("a clique round runs out of place (snapshot semantics)")
+    if plan.device is None or plan.device.device != pool_in.device:
+        plan.to(pool_in.device)
+    n = pool_in.shape[1] if n is None else int(n)
+    if (pool_in.stride(0) | pool_out.stride(0)) % 2 or (pool_in.data_ptr() | pool_out.data_ptr()) % 8:
+        # K3c reads and writes 8-B column pairs: rows that are not 8-B aligned take the full plan
+        return _round(pool_in, pool_out, plan.full, n, torch.float32, mode, stream)
+    t = plan.table.reshape(plan.n_cliques, CLIQUE_WORDS)
+    if t[:, 4: 4 + CLIQUE_MAX].max() >= pool_in.shape[0]:
+        raise ValueError("plan reads a pool row beyond pool_in")
+    if t[:, 4 + CLIQUE_MAX:].max() >= pool_out.shape[0]:
+        raise ValueError("plan writes a pool row beyond pool_out")
+    L = _lib.load()
+    check(L.tal_agg_round_clique_f32(ctypes.c_void_p(pool_in.data_ptr()), pool_in.stride(0),
+                                     ctypes.c_void_p(pool_out.data_ptr()), pool_out.stride(0), n,
+                                     ctypes.c_void_p(plan.device.data_ptr()), plan.n_cliques, plan.mmax,
+                                     int(mode), _stream(pool_in.device, stream)))
+    if plan.rest is not None:
+        _round(pool_in, pool_out, plan.rest, n, torch.float32, mode, stream)
+    return pool_out
 
 
 def round_i64(pool_in: torch.Tensor, pool_out: torch.Tensor, plan: RoundPlan, n: Optional[int] = None,
               stream=None) -> torch.Tensor:
+    if isinstance(plan, CliquePlan):
+        plan = plan.full
     return _round(pool_in, pool_out, plan, n, torch.int64, MODE_EXACT, stream)
 
 
 def round_bf16(pool_in: torch.Tensor, pool_out: torch.Tensor, plan: RoundPlan, n: Optional[int] = None,
                mode: int = MODE_EXACT, stream=None) -> torch.Tensor:
     """K3 on [models, ld] bf16 pools (sparse or narrow plans; modes as agg_bf16)."""
+    if isinstance(plan, CliquePlan):
+        plan = plan.full
     return _round(pool_in, pool_out, plan, n, torch.bfloat16, mode, stream)
 
 

@@ -156,7 +156,7 @@ class TransposedRound:
         else:
             self.plan = ops.build_plan(rp, col, w, out_rows).to(self.device)
         self.plans = {"round": self.plan}
-        self.staged_sources = self.plan.info.total_src
+        self.staged_sources = self.plan.staged_rows()
         self.exchange_kind = "transpose"
         self._events: list = []
         if dist.is_available() and dist.is_initialized():
