@@ -198,11 +198,15 @@ int32_t tal_agg_round_i64(const int64_t* pool_in, int64_t ld_in, int64_t* pool_o
  * then s_i — are computed from one read of each source: the products are shared and each row's
  * in-order chain extends the shared prefix (bitwise the reference in EXACT mode; FMA mode as
  * tal_agg_f32's).  table_dev: n_cliques records of TAL_CLIQUE_WORDS int32
- *   {m, bits of w, 0, 0, src_row[64], out_row[64]}  (out_row -1: member without an output row)
- * copied to the device.  The other rows of the round run through a regular plan (a second
- * call).  Out of place only; pools 8-B aligned with even ld.  mmax = the largest m (16, 32 or
+ *   {m, bits of w, n_att, 0, src_row[64], out_row[64], attached[4][12]}
+ * (out_row -1: member without an output row) copied to the device.  An attached row (a
+ * barbell's bridge node) has its own weight v and operands = members selected by a 64-bit
+ * mask + at most two other rows + its own model, in reference order:
+ *   {out_row, bits of v, mask lo, mask hi, self member index or -1, self pool row or -1,
+ *    n_ext, ext_row[2], ext_pos[2] (members with a smaller pool row), 0}.
+ * The other rows of the round run through a regular plan (a second call).  Out of place only; pools 8-B aligned with even ld.  mmax = the largest m (16, 32 or
  * 64 registers of products per lane). */
-#define TAL_CLIQUE_WORDS 132
+#define TAL_CLIQUE_WORDS 180
 int32_t tal_agg_round_clique_f32(const float* pool_in, int64_t ld_in, float* pool_out, int64_t ld_out,
                                  int64_t n, const int32_t* table_dev, int32_t n_cliques, int32_t mmax,
                                  int32_t mode, void* stream);

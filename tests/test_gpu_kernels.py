@@ -542,3 +542,38 @@ def test_round_clique_through_tuner_and_i64(cuda):
     ipo = torch.zeros(rows, 5, dtype=torch.int64, device=cuda)
     ops.round_i64(torch.from_numpy(ip).to(cuda), ipo, cp)
     assert np.array_equal(ipo.cpu().numpy(), oracle.round_i64(ip, row_ptr, col, w, out_rows))
+
+
+@pytest.mark.parametrize("n", [5, 4097])
+def test_round_clique_attached_rows_general(cuda, n):
+    """Attached rows with two non-member neighbors interleaved among the members, a member or a
+    non-member as own model, and their own weights: bitwise the oracle (EXACT) and K1 (FMA)."""
+    members = list(range(0, 40, 2))  # 20 members: even pool rows 0..38
+    orders, ws = [], []
+    for i in members:  # the clique rows, weight 1/20
+        orders.append([j for j in members if j != i] + [i])
+        ws.append([1 / 20] * 20)
+    # attached: member self, externals 5 and 31 (interleaved), weight -0.3
+    orders.append([j for j in members if j not in (10,)] [:12] + [5, 31])
+    orders[-1] = sorted(orders[-1]) + [10]
+    ws.append([-0.3] * len(orders[-1]))
+    # attached: non-member self (41), one external below every member? (none) and one above (45)
+    orders.append(sorted(members[3:15] + [45]) + [41])
+    ws.append([0.07] * len(orders[-1]))
+    rows = len(orders)
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    out_rows = np.arange(rows, dtype=np.int32)
+    cliques, rest = ops.find_cliques(row_ptr, col, w, out_rows)
+    assert len(cliques) == 1 and len(cliques[0][3]) == 2 and rest == []
+    plan = ops.build_clique_plan(row_ptr, col, w, out_rows)
+    pool = np.random.default_rng(n).standard_normal((48, n)).astype(np.float32)
+    pin = torch.from_numpy(pool).to(cuda)
+    pout = torch.zeros(rows, n, device=cuda)
+    ops.round_f32(pin, pout, plan)
+    ref = oracle.round_f32(pool, row_ptr, col, w, out_rows, pool_out=np.zeros((rows, n), np.float32))
+    assert _bits_equal(pout.cpu().numpy(), ref)
+    ops.round_f32(pin, pout, plan, mode=ops.MODE_FMA)
+    chk = torch.empty(n, device=cuda)
+    for r in (rows - 2, rows - 1, 3):
+        ops.agg_f32([pin[j] for j in orders[r]], ws[r], chk, mode=ops.MODE_FMA)
+        assert torch.equal(chk.view(torch.int32), pout[r].view(torch.int32))

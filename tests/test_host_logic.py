@@ -434,13 +434,15 @@ def test_find_cliques_barbell_complete_and_rejections():
     out = np.arange(len(orders), dtype=np.int32)[::-1].copy()
     cliques, rest = ops.find_cliques(rp, col, w, out)
     assert len(cliques) == 2
-    for srcs, w32, outs in cliques:
+    for srcs, w32, outs, _ in cliques:
         assert len(srcs) == 12 and len(outs) == 11  # the bridge node has one more neighbor
         assert w32 == np.float32(1 / 12)
         for i, o in outs.items():  # member i's row: every other member ascending, then itself
             r = int(np.flatnonzero(out == o)[0])
             assert list(col[rp[r]: rp[r + 1]]) == [s for s in srcs if s != srcs[i]] + [srcs[i]]
-    assert sorted(rest) == [11, 12, 13, 14, 15, 16]
+    assert sorted(rest) == [12, 13, 14, 15]  # the path; the bridge rows 11 and 16 are attached
+    for srcs, w32, outs, att in cliques:
+        assert len(att) == 1 and bin(att[0]["mask"]).count("1") == 11 and len(att[0]["ext"]) == 1
     # a complete graph is one block; a ring has none
     oc = _orders_of(nx.complete_graph(20))
     rp, col, w = ra.round_csr(oc, [ra.unweighted_weights(20)] * 20)
@@ -470,11 +472,11 @@ def test_clique_plan_table_and_spec():
     rp, col, w = ra.round_csr(orders, [ra.unweighted_weights(len(o)) for o in orders])
     out = np.arange(len(orders), dtype=np.int32)
     p = ops.build_clique_plan(rp, col, w, out)
-    assert p.n_cliques == 2 and p.mmax == 60 and p.clique_rows == 118
+    assert p.n_cliques == 2 and p.mmax == 60 and p.clique_rows == 120  # + the two bridge rows
     t = p.table.reshape(p.n_cliques, ops.CLIQUE_WORDS)
     assert list(t[:, 0]) == [60, 60] and (t[:, 1].view(np.float32) == np.float32(1 / 60)).all()
-    assert p.rest is not None and p.rest.rows == 10 and p.full.rows == 128
-    assert p.staged_rows() == 120 + p.rest.staged_rows()
+    assert p.rest is not None and p.rest.rows == 8 and p.full.rows == 128
+    assert p.staged_rows() == 120 + 2 + p.rest.staged_rows()  # + each bridge's path neighbor
     q = ops.plan_from_spec(rp, col, w, out, {"clique": 1})
     assert np.array_equal(q.table, p.table)
     assert ops.round_kernel_name(p) == "k_round_clique"

@@ -33,7 +33,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 9;
+constexpr int kAbiVersion = 10;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -1485,6 +1485,10 @@ int32_t launch_round_narrow(const T* pin, int64_t ld_in, T* pout, int64_t ld_out
 // fma(w, x_j, acc); its padding is the zero whose product with w is -0.0.
 // ------------------------------------------------------------------------------------------
 constexpr int kCliqueMax = 64;
+constexpr int kCliqueExtra = 4;        // attached rows per clique block
+constexpr int kCliqueExtraWords = 12;  // {out, v bits, mask lo, mask hi, self member, self row,
+                                       //  n_ext, ext row 0, ext row 1, ext pos 0, ext pos 1, 0}
+static_assert(4 + 2 * kCliqueMax + kCliqueExtra * kCliqueExtraWords == TAL_CLIQUE_WORDS, "table layout");
 
 typedef float v2f __attribute__((ext_vector_type(2)));
 
@@ -1504,6 +1508,13 @@ __device__ __forceinline__ int opaque_zero() {
 }
 
 // Columns e and e + 1 of every row of clique block `t`.
+// acc (+)= fl(v * x) for an attached row's operand (raw value x)
+template <bool EXACT>
+__device__ __forceinline__ v2f clique_xterm(v2f acc, float v, v2f x) {
+  if constexpr (EXACT) return v2f{__fadd_rn(acc.x, __fmul_rn(v, x.x)), __fadd_rn(acc.y, __fmul_rn(v, x.y))};
+  else return v2f{__builtin_fmaf(v, x.x, acc.x), __builtin_fmaf(v, x.y, acc.y)};
+}
+
 template <int MMAX, bool EXACT>
 __global__ __launch_bounds__(kBlock) void k_round_clique(const float* __restrict__ pin, int64_t ld_in,
                                                          float* __restrict__ pout, int64_t ld_out,
@@ -1524,6 +1535,35 @@ __global__ __launch_bounds__(kBlock) void k_round_clique(const float* __restrict
     p[j] = __builtin_nontemporal_load(reinterpret_cast<const v2f*>(src));
     // batches of 8: the scheduler would otherwise compute all row addresses first
     if (j % 8 == 7) __builtin_amdgcn_sched_barrier(0);
+  }
+  // attached rows (a barbell's bridge nodes): most operands are members, read from the raw
+  // values in registers before they become products; at most two other neighbors and an
+  // optional non-member self are loaded here.  Each is its own in-order chain with its weight.
+  const int n_extra = t[2];
+  for (int q = 0; q < n_extra; ++q) {
+    const int32_t* xr = t + 4 + 2 * kCliqueMax + q * kCliqueExtraWords + opaque_zero();
+    const float v = __int_as_float(xr[1]);
+    const uint32_t lo = static_cast<uint32_t>(xr[2]), hi = static_cast<uint32_t>(xr[3]);
+    const int self_m = xr[4], self_e = xr[5], n_ext = xr[6];
+    const int pos0 = n_ext > 0 ? xr[9] : -1, pos1 = n_ext > 1 ? xr[10] : -1;
+    auto ld_row = [&](int r) {
+      return __builtin_nontemporal_load(reinterpret_cast<const v2f*>(pin + static_cast<int64_t>(r) * ld_in + e));
+    };
+    const v2f e0 = n_ext > 0 ? ld_row(xr[7]) : v2f{0.f, 0.f};
+    const v2f e1 = n_ext > 1 ? ld_row(xr[8]) : v2f{0.f, 0.f};
+    v2f xs = self_e >= 0 ? ld_row(self_e) : v2f{0.f, 0.f};
+    v2f acc = v2f{-0.f, -0.f};
+#pragma unroll
+    for (int j = 0; j <= MMAX; ++j) {
+      if (pos0 == j) acc = clique_xterm<EXACT>(acc, v, e0);
+      if (pos1 == j) acc = clique_xterm<EXACT>(acc, v, e1);
+      if (j < MMAX) {
+        if (((j < 32 ? lo >> j : hi >> (j - 32)) & 1u) != 0u) acc = clique_xterm<EXACT>(acc, v, p[j]);
+        if (self_m == j) xs = p[j];
+      }
+    }
+    acc = clique_xterm<EXACT>(acc, v, xs);
+    __builtin_nontemporal_store(acc, reinterpret_cast<v2f*>(pout + static_cast<int64_t>(xr[0]) * ld_out + e));
   }
 #pragma unroll
   for (int j = 0; j < MMAX; ++j) {
@@ -1568,6 +1608,31 @@ __global__ __launch_bounds__(kCliqueMax) void k_round_clique_tail(const float* _
   pout[static_cast<int64_t>(orow) * ld_out + e] = acc;
 }
 
+// The last column for a block's attached rows: one thread per attached row.
+template <bool EXACT>
+__global__ __launch_bounds__(kCliqueExtra) void k_round_clique_tail_extra(const float* __restrict__ pin,
+                                                                          int64_t ld_in, float* __restrict__ pout,
+                                                                          int64_t ld_out, int64_t e,
+                                                                          const int32_t* __restrict__ table) {
+  const int32_t* t = table + static_cast<int64_t>(blockIdx.x) * TAL_CLIQUE_WORDS;
+  const int q = threadIdx.x;
+  if (q >= t[2]) return;
+  const int32_t* xr = t + 4 + 2 * kCliqueMax + q * kCliqueExtraWords;
+  const float v = __int_as_float(xr[1]);
+  const uint32_t lo = static_cast<uint32_t>(xr[2]), hi = static_cast<uint32_t>(xr[3]);
+  const int n_ext = xr[6];
+  auto x_of = [&](int r) { return pin[static_cast<int64_t>(r) * ld_in + e]; };
+  auto term = [&](float a, float x) { return EXACT ? __fadd_rn(a, __fmul_rn(v, x)) : __builtin_fmaf(v, x, a); };
+  float acc = -0.f;
+  for (int j = 0; j <= kCliqueMax; ++j) {
+    for (int k = 0; k < n_ext; ++k)
+      if (xr[9 + k] == j) acc = term(acc, x_of(xr[7 + k]));
+    if (j < kCliqueMax && (((j < 32 ? lo >> j : hi >> (j - 32)) & 1u) != 0u)) acc = term(acc, x_of(t[4 + j]));
+  }
+  acc = term(acc, x_of(xr[4] >= 0 ? t[4 + xr[4]] : xr[5]));
+  pout[static_cast<int64_t>(xr[0]) * ld_out + e] = acc;
+}
+
 template <bool EXACT>
 int32_t launch_round_clique(const float* pin, int64_t ld_in, float* pout, int64_t ld_out, int64_t n,
                             const int32_t* table, int32_t n_cliques, int32_t mmax, hipStream_t s) {
@@ -1584,7 +1649,10 @@ int32_t launch_round_clique(const float* pin, int64_t ld_in, float* pout, int64_
   }
   if (n % 2) {
     k_round_clique_tail<EXACT><<<n_cliques, kCliqueMax, 0, s>>>(pin, ld_in, pout, ld_out, n - 1, table);
-    return check_launch("clique round tail kernel");
+    int32_t rc = check_launch("clique round tail kernel");
+    if (rc) return rc;
+    k_round_clique_tail_extra<EXACT><<<n_cliques, kCliqueExtra, 0, s>>>(pin, ld_in, pout, ld_out, n - 1, table);
+    return check_launch("clique round tail kernel (attached rows)");
   }
   return TAL_OK;
 }

@@ -171,16 +171,21 @@ def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0, dense:
 
 
 CLIQUE_MAX = 64
-CLIQUE_WORDS = 132        # TAL_CLIQUE_WORDS: {m, w bits, 0, 0, src[64], out[64]}
+CLIQUE_EXTRA = 4          # attached rows per clique block
+CLIQUE_EXTRA_WORDS = 12
+CLIQUE_WORDS = 4 + 2 * CLIQUE_MAX + CLIQUE_EXTRA * CLIQUE_EXTRA_WORDS  # TAL_CLIQUE_WORDS (180)
 CLIQUE_MIN_ROWS = 8       # smaller blocks stay in the regular plan
+CLIQUE_MIN_SHARED = 8     # an attached row takes at least this many operands from the block
 
 
 def find_cliques(row_ptr, col, w, out_row, min_rows: int = CLIQUE_MIN_ROWS):
     """Uniform-weight clique blocks of a round (the K3c kernel's rows, tal_agg.h): rows whose
     operands are strictly ascending sources and then their own model (not among them), all with
     one finite fp32 weight, grouped by (operand set, weight); a group of >= min_rows rows with
-    distinct own models and <= 64 sources is a clique block.  Returns (cliques, rest): cliques =
-    [(sources ascending, fp32 weight, {member index: out_row})], rest = the other row indices."""
+    distinct own models and <= 64 sources is a clique block.  Other such rows that take at
+    least CLIQUE_MIN_SHARED neighbors from a block and have at most two more are attached to it
+    (up to CLIQUE_EXTRA per block).  Returns (cliques, rest): cliques = [(sources ascending, fp32
+    weight, {member index: out_row}, [attached row records])], rest = the other row indices."""
     row_ptr, col, w, out_row = _csr(row_ptr, col, w, out_row)
     groups: dict = {}
     for r in range(len(out_row)):
@@ -202,8 +207,34 @@ def find_cliques(row_ptr, col, w, out_row, min_rows: int = CLIQUE_MIN_ROWS):
             continue
         idx = {s: i for i, s in enumerate(srcs)}
         cliques.append((list(srcs), np.array([wbits], np.uint32).view(np.float32)[0],
-                        {idx[o]: int(out_row[r]) for o, r in zip(owns, rows)}))
+                        {idx[o]: int(out_row[r]) for o, r in zip(owns, rows)}, []))
         used.update(rows)
+    # attached rows: uniform-weight rows in reference order that take most operands from one
+    # block (a barbell's bridge nodes) - at most two other neighbors, own model anywhere
+    for r in range(len(out_row)):
+        if r in used or not cliques:
+            continue
+        ops_ = col[row_ptr[r]: row_ptr[r + 1]]
+        w32 = w[row_ptr[r]: row_ptr[r + 1]].astype(np.float32)
+        if len(ops_) < 2 or not np.isfinite(w32[0]) or np.any(w32.view(np.uint32) != w32[:1].view(np.uint32)):
+            continue
+        nb, own = ops_[:-1], int(ops_[-1])
+        if np.any(np.diff(nb) <= 0) or own in nb:
+            continue
+        best = max(range(len(cliques)), key=lambda c: len(set(cliques[c][0]).intersection(nb.tolist())))
+        srcs, _, _, att = cliques[best]
+        idx = {s: i for i, s in enumerate(srcs)}
+        mem = [int(x) for x in nb if int(x) in idx]
+        ext = [int(x) for x in nb if int(x) not in idx]
+        if len(mem) < CLIQUE_MIN_SHARED or len(ext) > 2 or len(att) >= CLIQUE_EXTRA:
+            continue
+        mask = 0
+        for x in mem:
+            mask |= 1 << idx[x]
+        att.append(dict(out=int(out_row[r]), w=w32[0], mask=mask, self_member=idx.get(own, -1),
+                        self_row=-1 if own in idx else own,
+                        ext=[(x, sum(1 for s_ in srcs if s_ < x)) for x in ext]))
+        used.add(r)
     return cliques, [r for r in range(len(out_row)) if r not in used]
 
 
@@ -254,21 +285,32 @@ def build_clique_plan(row_ptr, col, w, out_row, min_rows: int = CLIQUE_MIN_ROWS,
     if not cliques:
         return None
     table = np.zeros((len(cliques), CLIQUE_WORDS), np.int32)
-    for k, (srcs, w32, outs) in enumerate(cliques):
+    n_ext_loads = 0
+    for k, (srcs, w32, outs, att) in enumerate(cliques):
         table[k, 0] = len(srcs)
         table[k, 1] = np.array([w32], np.float32).view(np.int32)[0]
+        table[k, 2] = len(att)
         table[k, 4: 4 + len(srcs)] = srcs
         table[k, 4 + CLIQUE_MAX: 4 + 2 * CLIQUE_MAX] = -1
         for i, o in outs.items():
             table[k, 4 + CLIQUE_MAX + i] = o
+        for q, a in enumerate(att):
+            rec = table[k, 4 + 2 * CLIQUE_MAX + q * CLIQUE_EXTRA_WORDS:][:CLIQUE_EXTRA_WORDS]
+            rec[0] = a["out"]
+            rec[1] = np.array([a["w"]], np.float32).view(np.int32)[0]
+            rec[2:4] = np.array([a["mask"] & 0xFFFFFFFF, a["mask"] >> 32], np.uint32).view(np.int32)
+            rec[4], rec[5], rec[6] = a["self_member"], a["self_row"], len(a["ext"])
+            for e_, (row, pos) in enumerate(a["ext"]):
+                rec[7 + e_], rec[9 + e_] = row, pos
+            n_ext_loads += len(a["ext"]) + (a["self_row"] >= 0)
     rest_plan = None
     if rest:
         sub = _sub_csr(row_ptr, col, w, out_row, rest)
         rest_plan = plan_from_spec(*sub, rest_spec) if rest_spec else build_plan(*sub)
     mmax = max(len(c[0]) for c in cliques)
     return CliquePlan(table=table.reshape(-1), n_cliques=len(cliques), mmax=mmax,
-                      clique_sources=sum(len(c[0]) for c in cliques),
-                      clique_rows=sum(len(c[2]) for c in cliques), rest=rest_plan,
+                      clique_sources=sum(len(c[0]) for c in cliques) + n_ext_loads,
+                      clique_rows=sum(len(c[2]) + len(c[3]) for c in cliques), rest=rest_plan,
                       full=build_plan(row_ptr, col, w, out_row, dense=0), rows=len(out_row), rest_rows=rest)
 
 
@@ -463,9 +505,11 @@ def _round_clique(pool_in, pool_out, plan: CliquePlan, n, mode, stream):
         # K3c reads and writes 8-B column pairs: rows that are not 8-B aligned take the full plan
         return _round(pool_in, pool_out, plan.full, n, torch.float32, mode, stream)
     t = plan.table.reshape(plan.n_cliques, CLIQUE_WORDS)
-    if t[:, 4: 4 + CLIQUE_MAX].max() >= pool_in.shape[0]:
+    att = t[:, 4 + 2 * CLIQUE_MAX:].reshape(plan.n_cliques, CLIQUE_EXTRA, CLIQUE_EXTRA_WORDS)
+    used = np.arange(CLIQUE_EXTRA)[None, :] < t[:, 2:3]  # attached records in use
+    if max(t[:, 4: 4 + CLIQUE_MAX].max(), att[used][:, [5, 7, 8]].max(initial=-1)) >= pool_in.shape[0]:
         raise ValueError("plan reads a pool row beyond pool_in")
-    if t[:, 4 + CLIQUE_MAX:].max() >= pool_out.shape[0]:
+    if max(t[:, 4 + CLIQUE_MAX: 4 + 2 * CLIQUE_MAX].max(), att[used][:, 0].max(initial=-1)) >= pool_out.shape[0]:
         raise ValueError("plan writes a pool row beyond pool_out")
     L = _lib.load()
     check(L.tal_agg_round_clique_f32(ctypes.c_void_p(pool_in.data_ptr()), pool_in.stride(0),
