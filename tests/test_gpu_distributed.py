@@ -15,32 +15,62 @@ from topology_aware_learning_amd.distributed import ShardedRound, partition_cont
 pytestmark = pytest.mark.gpu
 
 
+def _seg_setup(dtype, n_dev, seed):
+    """Layout + pool of one test: fp32 or bf16 weights (bf16 kept as uint16 bit patterns)."""
+    dt = "float32" if dtype == "f32" else "bfloat16"
+    layout = StateLayout.from_layout([("w", (1001,), dt), ("b", (7,), dt), ("nbt", (), "int64")])
+    rng = np.random.default_rng(seed)
+    pool = rng.standard_normal((n_dev, 1008)).astype(np.float32)
+    if dtype == "bf16":
+        pool = oracle.f32_to_bf16(pool)
+    ipool = rng.integers(0, 10 ** 6, size=(n_dev, 1)).astype(np.int64)
+    return layout, pool, ipool
+
+
+def _put_row(pool_obj, k, dtype, row, irow, cuda):
+    if dtype == "f32":
+        pool_obj.f32[k, :1008] = torch.from_numpy(row).to(cuda)
+    else:
+        pool_obj.b16[k, :1008] = torch.from_numpy(row.view(np.int16)).to(cuda).view(torch.bfloat16)
+    pool_obj.i64[k, :1] = torch.from_numpy(irow).to(cuda)
+
+
+def _get_rows(pool_obj, rows, dtype):
+    if dtype == "f32":
+        return pool_obj.f32[:rows, :1008].cpu().numpy().view(np.uint32)
+    return pool_obj.b16[:rows, :1008].cpu().view(torch.int16).numpy().view(np.uint16)
+
+
+def _oracle_round(dtype, pool, rp, col, w, n):
+    if dtype == "f32":
+        return oracle.round_f32(pool, rp, col, w, np.arange(n))
+    return oracle.round_bf16(pool, rp, col, w, np.arange(n), exact=True)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("graph,world", [("regular", 4), ("barbell", 8), ("ring", 2)])
-def test_virtual_ranks_two_rounds(cuda, graph, world):
+def test_virtual_ranks_two_rounds(cuda, graph, world, dtype):
     g = {"regular": nx.random_regular_graph(8, 48, seed=0), "barbell": nx.barbell_graph(20, 8),
          "ring": nx.cycle_graph(12)}[graph]
     n = g.number_of_nodes()
     orders = [sorted(g.neighbors(i)) + [i] for i in range(n)]
     ws = [ra.unweighted_weights(len(o)) for o in orders]
-    lay = [("w", (1001,), "float32"), ("b", (7,), "float32"), ("nbt", (), "int64")]
-    layout = StateLayout.from_layout(lay)
-    rng = np.random.default_rng(1)
-    pool = rng.standard_normal((n, layout.n_f32)).astype(np.float32)
-    ipool = rng.integers(0, 10 ** 6, size=(n, 1)).astype(np.int64)
+    layout, pool, ipool = _seg_setup(dtype, n, 1)
     owner = partition_contiguous(n, world)
     srs = [ShardedRound(layout, orders, ws, r, world, cuda, exchange=lambda sr: []) for r in range(world)]
     for sr in srs:
         for k, gid in enumerate(sr.spec.own):
-            sr.pool_a.f32[k, : layout.n_f32] = torch.from_numpy(pool[gid]).to(cuda)
-            sr.pool_a.i64[k, :1] = torch.from_numpy(ipool[gid]).to(cuda)
+            _put_row(sr.pool_a, k, dtype, pool[gid], ipool[gid], cuda)
 
     def exchange_all():
         for sr in srs:
             base = len(sr.spec.own)
             for k, gid in enumerate(sr.spec.halo):
                 src = srs[owner[gid]]
-                sr.pool_a.f32[base + k].copy_(src.pool_a.f32[src.spec.local_of[gid]])
-                sr.pool_a.i64[base + k].copy_(src.pool_a.i64[src.spec.local_of[gid]])
+                for _, t, _ in sr.pool_a.segments():
+                    st = {id(sr.pool_a.f32): src.pool_a.f32, id(sr.pool_a.b16): src.pool_a.b16,
+                          id(sr.pool_a.i64): src.pool_a.i64}[id(t)]
+                    t[base + k].copy_(st[src.spec.local_of[gid]])
 
     rp, col, w = ra.round_csr(orders, ws)
     ref, iref = pool, ipool
@@ -48,17 +78,19 @@ def test_virtual_ranks_two_rounds(cuda, graph, world):
         exchange_all()
         for sr in srs:
             sr.step()
-        ref = oracle.round_f32(ref, rp, col, w, np.arange(n))
+        ref = _oracle_round(dtype, ref, rp, col, w, n)
         iref = oracle.round_i64(iref, rp, col, w, np.arange(n))
     torch.cuda.synchronize()
     for sr in srs:
-        got = sr.own_rows().f32[: len(sr.spec.own), : layout.n_f32].cpu().numpy()
-        assert np.array_equal(got.view(np.uint32), ref[sr.spec.own].view(np.uint32))
+        assert sr.spot_check()
+        got = _get_rows(sr.own_rows(), len(sr.spec.own), dtype)
+        assert np.array_equal(got, ref[sr.spec.own].view(got.dtype))
         assert np.array_equal(sr.own_rows().i64[: len(sr.spec.own), :1].cpu().numpy(), iref[sr.spec.own])
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("graph,world", [("regular", 4), ("barbell", 8), ("ring", 3)])
-def test_virtual_ranks_transposed_two_rounds(cuda, graph, world):
+def test_virtual_ranks_transposed_two_rounds(cuda, graph, world, dtype):
     """TransposedRound (column blocks by all-to-all) with the two all-to-alls done by in-process
     copies between virtual ranks: K3 on each rank's column block, bitwise the oracle round."""
     from topology_aware_learning_amd.transposed import TransposedRound
@@ -68,17 +100,12 @@ def test_virtual_ranks_transposed_two_rounds(cuda, graph, world):
     n = g.number_of_nodes()
     orders = [sorted(g.neighbors(i)) + [i] for i in range(n)]
     ws = [ra.unweighted_weights(len(o)) for o in orders]
-    lay = [("w", (1001,), "float32"), ("b", (7,), "float32"), ("nbt", (), "int64")]
-    layout = StateLayout.from_layout(lay)
-    rng = np.random.default_rng(2)
-    pool = rng.standard_normal((n, layout.n_f32)).astype(np.float32)
-    ipool = rng.integers(0, 10 ** 6, size=(n, 1)).astype(np.int64)
+    layout, pool, ipool = _seg_setup(dtype, n, 2)
     owner = np.array([(5 * i) % world for i in range(n)], np.int32)  # interleaved owners
     srs = [TransposedRound(layout, orders, ws, r, world, cuda, owner=owner) for r in range(world)]
     for sr in srs:
         for k, gid in enumerate(sr.own):
-            sr.pool_a.f32[k, : layout.n_f32] = torch.from_numpy(pool[gid]).to(cuda)
-            sr.pool_a.i64[k, :1] = torch.from_numpy(ipool[gid]).to(cuda)
+            _put_row(sr.pool_a, k, dtype, pool[gid], ipool[gid], cuda)
     base = srs[0].base
     rp, col, w = ra.round_csr(orders, ws)
     ref, iref = pool, ipool
@@ -97,11 +124,11 @@ def test_virtual_ranks_transposed_two_rounds(cuda, graph, world):
                     s.back[p].copy_(src.segs[key].work_out[base[r]: base[r + 1]])
         for sr in srs:
             sr.unpack()
-        ref = oracle.round_f32(ref, rp, col, w, np.arange(n))
+        ref = _oracle_round(dtype, ref, rp, col, w, n)
         iref = oracle.round_i64(iref, rp, col, w, np.arange(n))
     torch.cuda.synchronize()
     for sr in srs:
         assert sr.spot_check()
-        got = sr.own_rows().f32[: sr.local_rows, : layout.n_f32].cpu().numpy()
-        assert np.array_equal(got.view(np.uint32), ref[sr.own].view(np.uint32))
+        got = _get_rows(sr.own_rows(), sr.local_rows, dtype)
+        assert np.array_equal(got, ref[sr.own].view(got.dtype))
         assert np.array_equal(sr.own_rows().i64[: sr.local_rows, :1].cpu().numpy(), iref[sr.own])

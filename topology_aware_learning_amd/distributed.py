@@ -99,33 +99,83 @@ def post_exchange(spec: ShardSpec, tensors: Sequence[torch.Tensor], group=None) 
     return dist.batch_isend_irecv(p2p)
 
 
+_ESIZE = {"f32": 4, "b16": 2, "i64": 8}
+
+
+def float_segments(layout: StateLayout):
+    """(name, elements) of the layout's non-empty floating-point segments."""
+    return [(g, n) for g, n in (("f32", layout.n_f32), ("b16", layout.n_b16)) if n]
+
+
+def tune_segment(layout: StateLayout) -> str:
+    """The segment a round plan is tuned on: bf16 when there is one (its plan forms - sparse,
+    narrow - also run fp32 and int64), else fp32."""
+    return "b16" if layout.n_b16 else "f32"
+
+
+def run_round_segments(layout: StateLayout, seg_in: dict, seg_out: dict, plan, mode: int,
+                       n_of: Optional[dict] = None) -> None:
+    """The K3 round of `plan` on every non-empty segment (seg_*: name -> [rows, ld] tensor;
+    n_of: name -> columns, default the layout's elements per model)."""
+    for g, n in (("f32", layout.n_f32), ("b16", layout.n_b16), ("i64", layout.n_i64)):
+        n = n if n_of is None else n_of.get(g, 0)
+        if not n:
+            continue
+        if g == "f32":
+            ops.round_f32(seg_in[g], seg_out[g], plan, n=n, mode=mode)
+        elif g == "b16":
+            ops.round_bf16(seg_in[g], seg_out[g], plan, n=n, mode=mode)
+        else:
+            ops.round_i64(seg_in[g], seg_out[g], plan, n=n)
+
+
+def _pool_segs(pool: ModelPool) -> dict:
+    return {"f32": pool.f32, "b16": pool.b16, "i64": pool.i64}
+
+
+def spot_check_row(layout: StateLayout, operands: dict, weights, got: dict, mode: int, n_of=None) -> bool:
+    """K1 on one row's operands (per float segment) == the round's output row, bitwise."""
+    for g, n in float_segments(layout):
+        n = n if n_of is None else n_of.get(g, 0)
+        if not n:
+            continue
+        dt = torch.float32 if g == "f32" else torch.bfloat16
+        chk = torch.empty(n, dtype=dt, device=got[g].device)
+        (ops.agg_f32 if g == "f32" else ops.agg_bf16)([x[:n] for x in operands[g]], weights, chk, mode=mode)
+        iv = torch.int32 if g == "f32" else torch.int16
+        if not torch.equal(chk.view(iv), got[g][:n].contiguous().view(iv)):
+            return False
+    return True
+
+
 class ShardedRound:
     """One rank's device-resident round over its shard (K3 kernels + halo exchange)."""
 
     def __init__(self, layout: StateLayout, orders, weights, rank: int, world: int, device,
                  mode: int = ops.MODE_EXACT, owner: Optional[np.ndarray] = None, group=None,
                  exchange: Optional[Callable[["ShardedRound"], list]] = None, tune: bool = False):
-        if layout.n_b16:
-            raise NotImplementedError("sharded rounds move fp32 / int64 pools; bf16 layouts run on one GPU "
-                                      "(RoundExecutor) in this version")
         self.layout = layout
         self.device = torch.device(device)
         self.mode = mode
         self.group = group
         # exchange(self) -> requests; default: RCCL/gloo P2P.  Tests may pass an in-process copy.
-        self._exchange = exchange or (lambda sr: post_exchange(sr.spec, [sr.pool_a.f32, sr.pool_a.i64], sr.group))
+        self._exchange = exchange or (lambda sr: post_exchange(
+            sr.spec, [t for _, t, _ in sr.pool_a.segments()], sr.group))
         owner = partition_contiguous(len(orders), world) if owner is None else np.asarray(owner, np.int32)
         self.spec = build_shard(orders, weights, owner, rank, world)
         self.pool_a = ModelPool(layout, self.spec.rows, self.device)
         self.pool_b = ModelPool(layout, self.spec.rows, self.device)
         self.plans = {}
+        tg = tune_segment(layout)
         for name, idx in (("interior", self.spec.interior), ("boundary", self.spec.boundary)):
             if idx:
                 rp, col, w = csr_from_lists([self.spec.orders_local[k] for k in idx],
                                             [self.spec.weights[k] for k in idx])
-                self.plans[name] = (ops.tune_plan(rp, col, w, np.asarray(idx, np.int32), self.pool_a.f32,
-                                                  self.pool_b.f32, n=layout.n_f32, mode=mode)
-                                    if tune else ops.build_plan(rp, col, w, np.asarray(idx, np.int32)).to(self.device))
+                out = np.asarray(idx, np.int32)
+                self.plans[name] = (
+                    ops.tune_plan(rp, col, w, out, _pool_segs(self.pool_a)[tg], _pool_segs(self.pool_b)[tg],
+                                  n=getattr(layout, "n_" + tg), mode=mode)
+                    if tune else ops.build_plan(rp, col, w, out, dense=0 if layout.n_b16 else -1).to(self.device))
         if exchange is None and dist.is_available() and dist.is_initialized():
             # a collective over the whole group first: RCCL then builds the communicator with
             # every rank, so the first batched P2P does not depend on which ranks have halos
@@ -139,10 +189,7 @@ class ShardedRound:
         plan = self.plans.get(name)
         if plan is None:
             return
-        if self.layout.n_f32:
-            ops.round_f32(a.f32, b.f32, plan, n=self.layout.n_f32, mode=self.mode)
-        if self.layout.n_i64:
-            ops.round_i64(a.i64, b.i64, plan, n=self.layout.n_i64)
+        run_round_segments(self.layout, _pool_segs(a), _pool_segs(b), plan, self.mode)
 
     def step(self, timed: bool = False) -> None:
         """One round: halo exchange overlapped with the interior rows, then the boundary rows.
@@ -178,18 +225,18 @@ class ShardedRound:
     @property
     def kernel_bytes(self) -> int:
         """Algorithmic HBM bytes of one round's local kernels (staged sources + written rows)."""
-        return 4 * self.layout.n_f32 * (self.staged_sources + self.local_rows)
+        return sum(_ESIZE[g] * n for g, n in float_segments(self.layout)) * (self.staged_sources + self.local_rows)
 
     @property
     def link_bytes(self) -> int:
         """Bytes this rank receives over the links per round."""
-        return self.halo_rows_in * (4 * self.layout.n_f32 + 8 * self.layout.n_i64)
+        lay = self.layout
+        return self.halo_rows_in * (4 * lay.n_f32 + 2 * lay.n_b16 + 8 * lay.n_i64)
 
     def spot_check(self) -> bool:
         """After a step: one (boundary if any) row == K1 on its operands as they were received
         (bitwise; the operands are the previous buffer, now pool_b)."""
         k = (self.spec.boundary or self.spec.interior)[0]
-        chk = torch.empty(self.layout.n_f32, dtype=torch.float32, device=self.device)
-        ops.agg_f32([self.pool_b.row_f32(j) for j in self.spec.orders_local[k]], self.spec.weights[k], chk,
-                    mode=self.mode)
-        return bool(torch.equal(chk.view(torch.int32), self.pool_a.row_f32(k).view(torch.int32)))
+        a, b = _pool_segs(self.pool_a), _pool_segs(self.pool_b)
+        ops_ = {g: [b[g][j] for j in self.spec.orders_local[k]] for g in ("f32", "b16")}
+        return spot_check_row(self.layout, ops_, self.spec.weights[k], {g: a[g][k] for g in a}, self.mode)

@@ -30,7 +30,8 @@ import torch.distributed as dist
 
 from . import ops
 from .arena import ModelPool, StateLayout
-from .distributed import ShardedRound, build_shard, partition_contiguous
+from .distributed import (_ESIZE, ShardedRound, _pool_segs, build_shard, float_segments, partition_contiguous,
+                          run_round_segments, spot_check_row, tune_segment)
 from .round import csr_from_lists
 
 
@@ -77,24 +78,24 @@ def positions(owner, world: int):
     return own_by_rank, base, pos
 
 
-def exchange_bytes(orders, owner, world: int, n_f32: int, n_i64: int) -> dict:
+def exchange_bytes(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: int = 0) -> dict:
     """Largest per-rank link volume of one round (bytes in or out, whichever is larger) for
     each exchange: 'halo' = distinct remote neighbor models, 'transpose' = 2 x (world-1)/world
     of the rank's own models."""
     owner = np.asarray(owner)
-    row = 4 * n_f32 + 8 * n_i64
+    row = 4 * n_f32 + 2 * n_b16 + 8 * n_i64
     specs = [build_shard(orders, [[1.0] * len(o) for o in orders], owner, r, world) for r in range(world)]
     halo = max(max(len(s.halo), sum(len(v) for v in s.send.values())) for s in specs) * row
     own = max(len(s.own) for s in specs)
     return dict(halo=int(halo), transpose=int(2 * own * row * (world - 1) // world))
 
 
-def choose_exchange(orders, owner, world: int, n_f32: int, n_i64: int) -> str:
+def choose_exchange(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: int = 0) -> str:
     """'transpose' when it moves clearly fewer bytes than the halo (random expanders at 4+
     ranks), else 'halo' (rings, cliques, community graphs; 2 ranks)."""
     if world < 2:
         return "halo"
-    b = exchange_bytes(orders, owner, world, n_f32, n_i64)
+    b = exchange_bytes(orders, owner, world, n_f32, n_i64, n_b16)
     return "transpose" if b["transpose"] < 0.9 * b["halo"] else "halo"
 
 
@@ -117,9 +118,6 @@ class TransposedRound:
     def __init__(self, layout: StateLayout, orders, weights, rank: int, world: int, device,
                  mode: int = ops.MODE_EXACT, owner: Optional[np.ndarray] = None, group=None,
                  tune: bool = False):
-        if layout.n_b16:
-            raise NotImplementedError("sharded rounds move fp32 / int64 pools; bf16 layouts run on one GPU "
-                                      "(RoundExecutor) in this version")
         self.layout = layout
         self.device = torch.device(device)
         self.mode = mode
@@ -137,7 +135,8 @@ class TransposedRound:
         self.weights_pos = [[float(x) for x in weights[int(inv[q])]] for q in range(n_dev)]
         self.pool_a = ModelPool(layout, self.local_rows, self.device)
         self.segs: Dict[str, _ColSeg] = {}
-        for g, n, dt in (("f32", layout.n_f32, torch.float32), ("i64", layout.n_i64, torch.int64)):
+        for g, n, dt in (("f32", layout.n_f32, torch.float32), ("b16", layout.n_b16, torch.bfloat16),
+                         ("i64", layout.n_i64, torch.int64)):
             if not n:
                 continue
             b, blocks = column_blocks(n, world)
@@ -150,11 +149,12 @@ class TransposedRound:
         self.w_me = {g: s.blocks[rank][1] for g, s in self.segs.items()}
         rp, col, w = csr_from_lists(self.orders_pos, self.weights_pos)
         out_rows = np.arange(n_dev, dtype=np.int32)
-        f = self.segs.get("f32")
-        if tune and f is not None and self.w_me["f32"]:
-            self.plan = ops.tune_plan(rp, col, w, out_rows, f.work_in, f.work_out, n=self.w_me["f32"], mode=mode)
+        tg = tune_segment(layout)
+        f = self.segs.get(tg)
+        if tune and f is not None and self.w_me[tg]:
+            self.plan = ops.tune_plan(rp, col, w, out_rows, f.work_in, f.work_out, n=self.w_me[tg], mode=mode)
         else:
-            self.plan = ops.build_plan(rp, col, w, out_rows).to(self.device)
+            self.plan = ops.build_plan(rp, col, w, out_rows, dense=0 if layout.n_b16 else -1).to(self.device)
         self.plans = {"round": self.plan}
         self.staged_sources = self.plan.staged_rows()
         self.exchange_kind = "transpose"
@@ -164,7 +164,7 @@ class TransposedRound:
 
     # phases: step() runs them in order; the virtual-rank GPU test interleaves ranks between them
     def pack(self) -> None:
-        pools = {"f32": self.pool_a.f32, "i64": self.pool_a.i64}
+        pools = _pool_segs(self.pool_a)
         for g, s in self.segs.items():
             pack_columns(pools[g], self.local_rows, s.blocks, s.b, s.send)
 
@@ -175,14 +175,8 @@ class TransposedRound:
                                    [self.local_rows * s.b] * self.world, group=self.group)
 
     def compute(self) -> None:
-        for g, s in self.segs.items():
-            w = self.w_me[g]
-            if not w:
-                continue
-            if g == "f32":
-                ops.round_f32(s.work_in, s.work_out, self.plan, n=w, mode=self.mode)
-            else:
-                ops.round_i64(s.work_in, s.work_out, self.plan, n=w)
+        run_round_segments(self.layout, {g: s.work_in for g, s in self.segs.items()},
+                           {g: s.work_out for g, s in self.segs.items()}, self.plan, self.mode, n_of=self.w_me)
 
     def backward_exchange(self) -> None:
         for s in self.segs.values():
@@ -191,7 +185,7 @@ class TransposedRound:
                                    [len(o) * s.b for o in self.own_by_rank], group=self.group)
 
     def unpack(self) -> None:
-        pools = {"f32": self.pool_a.f32, "i64": self.pool_a.i64}
+        pools = _pool_segs(self.pool_a)
         for g, s in self.segs.items():
             unpack_columns(s.back, self.local_rows, s.blocks, s.b, pools[g])
 
@@ -221,27 +215,24 @@ class TransposedRound:
     @property
     def kernel_bytes(self) -> int:
         """Algorithmic HBM bytes of one round's K3 launch (staged sources + written rows)."""
-        return 4 * self.w_me.get("f32", 0) * (self.staged_sources + self.rows_all)
+        return sum(_ESIZE[g] * self.w_me[g] for g, _ in float_segments(self.layout)) * (
+            self.staged_sources + self.rows_all)
 
     @property
     def link_bytes(self) -> int:
         """Bytes this rank receives over the links per round (both all-to-alls)."""
         r = 0
         for g, s in self.segs.items():
-            es = 4 if g == "f32" else 8
-            r += es * s.b * ((self.rows_all - self.local_rows) + self.local_rows * (self.world - 1))
+            r += _ESIZE[g] * s.b * ((self.rows_all - self.local_rows) + self.local_rows * (self.world - 1))
         return r
 
     def spot_check(self) -> bool:
         """After a step: the first row of this rank's column block == K1 on its operands'
         blocks (bitwise)."""
-        s = self.segs["f32"]
-        w = self.w_me["f32"]
-        if not w:
-            return True
-        chk = torch.empty(w, dtype=torch.float32, device=self.device)
-        ops.agg_f32([s.work_in[j, :w] for j in self.orders_pos[0]], self.weights_pos[0], chk, mode=self.mode)
-        return bool(torch.equal(chk.view(torch.int32), s.work_out[0, :w].view(torch.int32)))
+        segs = {g: s for g, s in self.segs.items() if g != "i64"}
+        ops_ = {g: [s.work_in[j] for j in self.orders_pos[0]] for g, s in segs.items()}
+        return spot_check_row(self.layout, ops_, self.weights_pos[0], {g: s.work_out[0] for g, s in segs.items()},
+                              self.mode, n_of=self.w_me)
 
 
 def make_round(layout: StateLayout, orders, weights, rank: int, world: int, device, exchange: str = "auto",
@@ -249,7 +240,7 @@ def make_round(layout: StateLayout, orders, weights, rank: int, world: int, devi
     """This rank's sharded round with the given exchange ('halo' | 'transpose' | 'auto')."""
     owner = partition_contiguous(len(orders), world) if owner is None else np.asarray(owner, np.int32)
     if exchange == "auto":
-        exchange = choose_exchange(orders, owner, world, layout.n_f32, layout.n_i64)
+        exchange = choose_exchange(orders, owner, world, layout.n_f32, layout.n_i64, layout.n_b16)
     cls = {"halo": ShardedRound, "transpose": TransposedRound}[exchange]
     r = cls(layout, orders, weights, rank, world, device, mode=mode, owner=owner, group=group, tune=tune)
     r.exchange_kind = exchange
