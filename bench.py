@@ -58,6 +58,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU baseline sample")
     p.add_argument("--no-k1", action="store_true", help="skip the per-call K1 side measurement")
     p.add_argument("--host-path", action="store_true", help="also time the H2D+K1+D2H per-call path")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="N > 1: nccl (RCCL over xGMI, the benchmark); gloo = rehearsal of the same "
+                        "code path with the exchange staged through host memory, ranks may share a GPU")
     p.add_argument("--exchange", default="auto", choices=["auto", "halo", "transpose"],
                    help="N > 1: neighbor models by RCCL P2P (halo) or column blocks by all-to-all "
                         "(transpose); auto = fewer link bytes (transposed.choose_exchange)")
@@ -157,10 +160,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dist_backend == "gloo":
+        local %= torch.cuda.device_count()  # rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     lay = synth.get_layout(args.model)
     if args.dtype == "bf16":
@@ -251,12 +259,13 @@ def main():
         from topology_aware_learning_amd.transposed import make_round
 
         sr = make_round(layout, orders, weights, rank, world, dev, exchange=args.exchange, mode=mode,
-                        tune=not args.no_tune)
+                        tune=not args.no_tune, transport="host" if args.dist_backend == "gloo" else "device")
         fill_pool(sr.pool_a, 1234 + rank)
         sr.step()
         # spot check: one output row (halo) / row block (transpose) of this rank == K1 on its
         # operands as received, bitwise
-        ok = torch.tensor([int(sr.spot_check())], device=dev)
+        cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # collectives' scalars
+        ok = torch.tensor([int(sr.spot_check())], device=cdev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         parity_dist = bool(ok.item())
         for _ in range(args.warmup):
@@ -269,7 +278,7 @@ def main():
         torch.cuda.synchronize(dev)
         dist.barrier()
         el_local = time.perf_counter() - t0
-        t = torch.tensor([el_local], device=dev)
+        t = torch.tensor([el_local], device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
         torch.cuda.synchronize(dev)

@@ -132,3 +132,30 @@ def test_virtual_ranks_transposed_two_rounds(cuda, graph, world, dtype):
         got = _get_rows(sr.own_rows(), sr.local_rows, dtype)
         assert np.array_equal(got, ref[sr.own].view(got.dtype))
         assert np.array_equal(sr.own_rows().i64[: sr.local_rows, :1].cpu().numpy(), iref[sr.own])
+
+
+@pytest.mark.parametrize("exchange,world", [("halo", 2), ("transpose", 2), ("transpose", 3), ("halo", 3)])
+def test_bench_multi_rank_rehearsal(cuda, tmp_path, exchange, world):
+    """bench.py's N > 1 branch end to end (make_round, tuning, exchange, spot check, timing, JSON)
+    with `world` ranks sharing this GPU over gloo (exchange staged through host memory): the
+    same code the 8-GPU RCCL run executes, except the transport."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    port = 29500 + (os.getpid() % 400) + world * 7 + (0 if exchange == "halo" else 3)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", str(ROOT / "bench.py"), "--gpus", str(world),
+           "--dist-backend", "gloo", "--exchange", exchange, "--model", "cifar10", "--devices-per-gpu", "16",
+           "--degree", "4", "--steps", "2", "--warmup", "1", "--no-tune"]
+    out = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1, out.stdout[-2000:]
+    d = json.loads(line[0])
+    assert d["n_gpus"] == world and d["parity"] is True and d["exchange"] == exchange
+    assert d["value"] > 0 and d["link_bytes_in_per_round"] > 0

@@ -148,19 +148,53 @@ def spot_check_row(layout: StateLayout, operands: dict, weights, got: dict, mode
     return True
 
 
+class _StagedRequests:
+    """Requests of a host-staged exchange: wait() completes the receives, then copies the
+    received rows into the device pool."""
+
+    def __init__(self, reqs, fills):
+        self.reqs, self.fills = reqs, fills
+
+    def wait(self):
+        for r in self.reqs:
+            r.wait()
+        for dst, src in self.fills:
+            dst.copy_(src)
+        self.reqs, self.fills = [], []
+
+
+def post_exchange_staged(spec: ShardSpec, tensors: Sequence[torch.Tensor], group=None) -> list:
+    """post_exchange through host memory, for process groups without device transport (gloo):
+    rehearses the multi-GPU path with several ranks on one GPU.  Not a production path."""
+    p2p, fills = [], []
+    for peer in sorted(set(spec.send) | set(spec.recv)):
+        for t in tensors:
+            for r in spec.send.get(peer, []):
+                p2p.append(dist.P2POp(dist.isend, t[r].cpu(), peer, group=group))
+            for r in spec.recv.get(peer, []):
+                buf = torch.empty(t.shape[1], dtype=t.dtype)
+                p2p.append(dist.P2POp(dist.irecv, buf, peer, group=group))
+                fills.append((t[r], buf))
+    if not p2p:
+        return []
+    return [_StagedRequests(dist.batch_isend_irecv(p2p), fills)]
+
+
 class ShardedRound:
     """One rank's device-resident round over its shard (K3 kernels + halo exchange)."""
 
     def __init__(self, layout: StateLayout, orders, weights, rank: int, world: int, device,
                  mode: int = ops.MODE_EXACT, owner: Optional[np.ndarray] = None, group=None,
-                 exchange: Optional[Callable[["ShardedRound"], list]] = None, tune: bool = False):
+                 exchange: Optional[Callable[["ShardedRound"], list]] = None, tune: bool = False,
+                 transport: str = "device"):
         self.layout = layout
         self.device = torch.device(device)
         self.mode = mode
         self.group = group
         # exchange(self) -> requests; default: RCCL/gloo P2P.  Tests may pass an in-process copy.
-        self._exchange = exchange or (lambda sr: post_exchange(
-            sr.spec, [t for _, t, _ in sr.pool_a.segments()], sr.group))
+        # transport "host": the exchange is staged through host memory (gloo rehearsal runs)
+        post = post_exchange_staged if transport == "host" else post_exchange
+        self._exchange = exchange or (lambda sr: post(sr.spec, [t for _, t, _ in sr.pool_a.segments()], sr.group))
         owner = partition_contiguous(len(orders), world) if owner is None else np.asarray(owner, np.int32)
         self.spec = build_shard(orders, weights, owner, rank, world)
         self.pool_a = ModelPool(layout, self.spec.rows, self.device)

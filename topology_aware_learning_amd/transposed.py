@@ -117,8 +117,9 @@ class TransposedRound:
 
     def __init__(self, layout: StateLayout, orders, weights, rank: int, world: int, device,
                  mode: int = ops.MODE_EXACT, owner: Optional[np.ndarray] = None, group=None,
-                 tune: bool = False):
+                 tune: bool = False, transport: str = "device"):
         self.layout = layout
+        self.transport = transport  # "host": all-to-alls staged through host memory (gloo rehearsal)
         self.device = torch.device(device)
         self.mode = mode
         self.group = group
@@ -168,11 +169,18 @@ class TransposedRound:
         for g, s in self.segs.items():
             pack_columns(pools[g], self.local_rows, s.blocks, s.b, s.send)
 
+    def _all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits) -> None:
+        if self.transport == "host":
+            o = torch.empty(out.numel(), dtype=out.dtype)
+            dist.all_to_all_single(o, inp.view(-1).cpu(), out_splits, in_splits, group=self.group)
+            out.view(-1).copy_(o)
+        else:
+            dist.all_to_all_single(out.view(-1), inp.view(-1), out_splits, in_splits, group=self.group)
+
     def forward_exchange(self) -> None:
         for s in self.segs.values():
-            dist.all_to_all_single(s.work_in.view(-1), s.send.view(-1),
-                                   [len(o) * s.b for o in self.own_by_rank],
-                                   [self.local_rows * s.b] * self.world, group=self.group)
+            self._all_to_all(s.work_in, s.send, [len(o) * s.b for o in self.own_by_rank],
+                             [self.local_rows * s.b] * self.world)
 
     def compute(self) -> None:
         run_round_segments(self.layout, {g: s.work_in for g, s in self.segs.items()},
@@ -180,9 +188,8 @@ class TransposedRound:
 
     def backward_exchange(self) -> None:
         for s in self.segs.values():
-            dist.all_to_all_single(s.back.view(-1), s.work_out.view(-1),
-                                   [self.local_rows * s.b] * self.world,
-                                   [len(o) * s.b for o in self.own_by_rank], group=self.group)
+            self._all_to_all(s.back, s.work_out, [self.local_rows * s.b] * self.world,
+                             [len(o) * s.b for o in self.own_by_rank])
 
     def unpack(self) -> None:
         pools = _pool_segs(self.pool_a)
@@ -236,12 +243,15 @@ class TransposedRound:
 
 
 def make_round(layout: StateLayout, orders, weights, rank: int, world: int, device, exchange: str = "auto",
-               mode: int = ops.MODE_EXACT, owner: Optional[np.ndarray] = None, group=None, tune: bool = False):
-    """This rank's sharded round with the given exchange ('halo' | 'transpose' | 'auto')."""
+               mode: int = ops.MODE_EXACT, owner: Optional[np.ndarray] = None, group=None, tune: bool = False,
+               transport: str = "device"):
+    """This rank's sharded round with the given exchange ('halo' | 'transpose' | 'auto');
+    transport 'host' stages the exchange through host memory (gloo rehearsal runs only)."""
     owner = partition_contiguous(len(orders), world) if owner is None else np.asarray(owner, np.int32)
     if exchange == "auto":
         exchange = choose_exchange(orders, owner, world, layout.n_f32, layout.n_i64, layout.n_b16)
     cls = {"halo": ShardedRound, "transpose": TransposedRound}[exchange]
-    r = cls(layout, orders, weights, rank, world, device, mode=mode, owner=owner, group=group, tune=tune)
+    r = cls(layout, orders, weights, rank, world, device, mode=mode, owner=owner, group=group, tune=tune,
+            transport=transport)
     r.exchange_kind = exchange
     return r
