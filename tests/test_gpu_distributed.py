@@ -88,9 +88,10 @@ def test_virtual_ranks_two_rounds(cuda, graph, world, dtype):
         assert np.array_equal(sr.own_rows().i64[: len(sr.spec.own), :1].cpu().numpy(), iref[sr.spec.own])
 
 
+@pytest.mark.parametrize("chunks", [1, 3])
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("graph,world", [("regular", 4), ("barbell", 8), ("ring", 3)])
-def test_virtual_ranks_transposed_two_rounds(cuda, graph, world, dtype):
+def test_virtual_ranks_transposed_two_rounds(cuda, graph, world, dtype, chunks):
     """TransposedRound (column blocks by all-to-all) with the two all-to-alls done by in-process
     copies between virtual ranks: K3 on each rank's column block, bitwise the oracle round."""
     from topology_aware_learning_amd.transposed import TransposedRound
@@ -102,7 +103,7 @@ def test_virtual_ranks_transposed_two_rounds(cuda, graph, world, dtype):
     ws = [ra.unweighted_weights(len(o)) for o in orders]
     layout, pool, ipool = _seg_setup(dtype, n, 2)
     owner = np.array([(5 * i) % world for i in range(n)], np.int32)  # interleaved owners
-    srs = [TransposedRound(layout, orders, ws, r, world, cuda, owner=owner) for r in range(world)]
+    srs = [TransposedRound(layout, orders, ws, r, world, cuda, owner=owner, chunks=chunks) for r in range(world)]
     for sr in srs:
         for k, gid in enumerate(sr.own):
             _put_row(sr.pool_a, k, dtype, pool[gid], ipool[gid], cuda)
@@ -110,20 +111,21 @@ def test_virtual_ranks_transposed_two_rounds(cuda, graph, world, dtype):
     rp, col, w = ra.round_csr(orders, ws)
     ref, iref = pool, ipool
     for _ in range(2):
-        for sr in srs:
-            sr.pack()
-        for r, sr in enumerate(srs):  # forward all-to-all: block r of every rank's models
-            for key, s in sr.segs.items():
-                for p, src in enumerate(srs):
-                    s.work_in[base[p]: base[p + 1]].copy_(src.segs[key].send[r])
-        for sr in srs:
-            sr.compute()
-        for r, sr in enumerate(srs):  # backward all-to-all: my rows of every rank's block
-            for key, s in sr.segs.items():
-                for p, src in enumerate(srs):
-                    s.back[p].copy_(src.segs[key].work_out[base[r]: base[r + 1]])
-        for sr in srs:
-            sr.unpack()
+        for k in range(srs[0].chunks):
+            for sr in srs:
+                sr.pack(k)
+            for r, sr in enumerate(srs):  # forward all-to-all: chunk k of block r of every model
+                for key, s in sr._segs_at(k):
+                    for p, src in enumerate(srs):
+                        s.work_in[k][base[p]: base[p + 1]].copy_(src.segs[key].send[k][r])
+            for sr in srs:
+                sr.compute(k)
+            for r, sr in enumerate(srs):  # backward all-to-all: my rows of every rank's chunk
+                for key, s in sr._segs_at(k):
+                    for p, src in enumerate(srs):
+                        s.back[k][p].copy_(src.segs[key].work_out[k][base[r]: base[r + 1]])
+            for sr in srs:
+                sr.unpack(k)
         ref = _oracle_round(dtype, ref, rp, col, w, n)
         iref = oracle.round_i64(iref, rp, col, w, np.arange(n))
     torch.cuda.synchronize()

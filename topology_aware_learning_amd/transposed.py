@@ -101,23 +101,37 @@ def choose_exchange(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: in
 
 @dataclass
 class _ColSeg:
+    """One segment's buffers.  Rank p's column block (width <= b) is cut into `chunks` column
+    chunks of width bc; chunk k of every block travels and is reduced on its own, so the
+    all-to-alls of one chunk overlap the packing, the round and the unpacking of another."""
     n: int                  # elements per model
-    b: int                  # block width (row stride of the work buffers)
-    blocks: list            # (first column, width) per rank
-    send: torch.Tensor      # [world, own, b]  my models' blocks, by destination rank
-    work_in: torch.Tensor   # [R, b]           block `rank` of every device's model (rank-major)
-    work_out: torch.Tensor  # [R, b]           the round's output for that block
-    back: torch.Tensor      # [world, own, b]  my models' output blocks, by source rank
+    b: int                  # block width
+    blocks: list            # (first column, width) of each rank's block
+    chunks: int
+    bc: int                 # chunk width (row stride of the work buffers)
+    send: torch.Tensor      # [chunks, world, own, bc]  my models' chunks, by destination rank
+    work_in: torch.Tensor   # [chunks, R, bc]           chunk k of block `rank` of every model (rank-major)
+    work_out: torch.Tensor  # [chunks, R, bc]           the round's output for it
+    back: torch.Tensor      # [chunks, world, own, bc]  my models' output chunks, by source rank
+
+    def chunk_blocks(self, k: int):
+        """(first column, width) of chunk k of each rank's block."""
+        return [(c0 + k * self.bc, max(0, min(self.bc, w - k * self.bc))) for c0, w in self.blocks]
 
 
 class TransposedRound:
     """One rank's device-resident round with the transposed exchange (module docstring).  The
-    models update in place in pool_a: the send buffer holds the inputs before any output lands
-    (snapshot semantics)."""
+    models update in place in pool_a: each column chunk is packed into the send buffer before
+    its outputs land (snapshot semantics; chunks touch disjoint columns).
+
+    chunks (default 4): the block is moved and reduced in column chunks,
+    pipelined - the forward all-to-all of chunk k+1 and the backward one of chunk k-1 run on
+    RCCL's stream while chunk k is reduced - so the local work (pack, K3, unpack) hides under
+    the link time.  The int64 segment (tens of elements) moves in one chunk."""
 
     def __init__(self, layout: StateLayout, orders, weights, rank: int, world: int, device,
                  mode: int = ops.MODE_EXACT, owner: Optional[np.ndarray] = None, group=None,
-                 tune: bool = False, transport: str = "device"):
+                 tune: bool = False, transport: str = "device", chunks: Optional[int] = None):
         self.layout = layout
         self.transport = transport  # "host": all-to-alls staged through host memory (gloo rehearsal)
         self.device = torch.device(device)
@@ -135,25 +149,29 @@ class TransposedRound:
         self.orders_pos = [[int(self.pos[j]) for j in orders[int(inv[q])]] for q in range(n_dev)]
         self.weights_pos = [[float(x) for x in weights[int(inv[q])]] for q in range(n_dev)]
         self.pool_a = ModelPool(layout, self.local_rows, self.device)
+        self.chunks = max(1, int(chunks if chunks is not None else 4))
         self.segs: Dict[str, _ColSeg] = {}
         for g, n, dt in (("f32", layout.n_f32, torch.float32), ("b16", layout.n_b16, torch.bfloat16),
                          ("i64", layout.n_i64, torch.int64)):
             if not n:
                 continue
             b, blocks = column_blocks(n, world)
+            c = 1 if g == "i64" else max(1, min(self.chunks, b // 4))
+            bc = _round_up(-(-b // c), 4)
 
             def z(*shape, dt=dt):
                 return torch.zeros(*shape, dtype=dt, device=self.device)
 
-            self.segs[g] = _ColSeg(n, b, blocks, z(world, self.local_rows, b), z(n_dev, b), z(n_dev, b),
-                                   z(world, self.local_rows, b))
+            self.segs[g] = _ColSeg(n, b, blocks, c, bc, z(c, world, self.local_rows, bc), z(c, n_dev, bc),
+                                   z(c, n_dev, bc), z(c, world, self.local_rows, bc))
         self.w_me = {g: s.blocks[rank][1] for g, s in self.segs.items()}
         rp, col, w = csr_from_lists(self.orders_pos, self.weights_pos)
         out_rows = np.arange(n_dev, dtype=np.int32)
         tg = tune_segment(layout)
         f = self.segs.get(tg)
-        if tune and f is not None and self.w_me[tg]:
-            self.plan = ops.tune_plan(rp, col, w, out_rows, f.work_in, f.work_out, n=self.w_me[tg], mode=mode)
+        w0 = f.chunk_blocks(0)[rank][1] if f is not None else 0
+        if tune and w0:
+            self.plan = ops.tune_plan(rp, col, w, out_rows, f.work_in[0], f.work_out[0], n=w0, mode=mode)
         else:
             self.plan = ops.build_plan(rp, col, w, out_rows, dense=0 if layout.n_b16 else -1).to(self.device)
         self.plans = {"round": self.plan}
@@ -163,56 +181,80 @@ class TransposedRound:
         if dist.is_available() and dist.is_initialized():
             dist.barrier(group=group)
 
-    # phases: step() runs them in order; the virtual-rank GPU test interleaves ranks between them
-    def pack(self) -> None:
-        pools = _pool_segs(self.pool_a)
-        for g, s in self.segs.items():
-            pack_columns(pools[g], self.local_rows, s.blocks, s.b, s.send)
+    def _segs_at(self, k: int):
+        return [(g, s) for g, s in self.segs.items() if k < s.chunks]
 
-    def _all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits) -> None:
+    # phases of chunk k: step() pipelines them; the virtual-rank GPU test interleaves ranks
+    def pack(self, k: int = 0) -> None:
+        pools = _pool_segs(self.pool_a)
+        for g, s in self._segs_at(k):
+            pack_columns(pools[g], self.local_rows, s.chunk_blocks(k), s.bc, s.send[k])
+
+    def _all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits):
         if self.transport == "host":
             o = torch.empty(out.numel(), dtype=out.dtype)
-            dist.all_to_all_single(o, inp.view(-1).cpu(), out_splits, in_splits, group=self.group)
+            dist.all_to_all_single(o, inp.reshape(-1).cpu(), out_splits, in_splits, group=self.group)
             out.view(-1).copy_(o)
-        else:
-            dist.all_to_all_single(out.view(-1), inp.view(-1), out_splits, in_splits, group=self.group)
+            return None
+        return dist.all_to_all_single(out.view(-1), inp.view(-1), out_splits, in_splits, group=self.group,
+                                      async_op=True)
 
-    def forward_exchange(self) -> None:
-        for s in self.segs.values():
-            self._all_to_all(s.work_in, s.send, [len(o) * s.b for o in self.own_by_rank],
-                             [self.local_rows * s.b] * self.world)
+    def forward_exchange(self, k: int = 0) -> list:
+        """Chunk k of block `rank` of every model into work_in[k]; returns the pending works."""
+        works = [self._all_to_all(s.work_in[k], s.send[k], [len(o) * s.bc for o in self.own_by_rank],
+                                  [self.local_rows * s.bc] * self.world) for _, s in self._segs_at(k)]
+        return [w for w in works if w is not None]
 
-    def compute(self) -> None:
-        run_round_segments(self.layout, {g: s.work_in for g, s in self.segs.items()},
-                           {g: s.work_out for g, s in self.segs.items()}, self.plan, self.mode, n_of=self.w_me)
+    def compute(self, k: int = 0) -> None:
+        segs = self._segs_at(k)
+        run_round_segments(self.layout, {g: s.work_in[k] for g, s in segs}, {g: s.work_out[k] for g, s in segs},
+                           self.plan, self.mode, n_of={g: s.chunk_blocks(k)[self.rank][1] for g, s in segs})
 
-    def backward_exchange(self) -> None:
-        for s in self.segs.values():
-            self._all_to_all(s.back, s.work_out, [self.local_rows * s.b] * self.world,
-                             [len(o) * s.b for o in self.own_by_rank])
+    def backward_exchange(self, k: int = 0) -> list:
+        works = [self._all_to_all(s.back[k], s.work_out[k], [self.local_rows * s.bc] * self.world,
+                                  [len(o) * s.bc for o in self.own_by_rank]) for _, s in self._segs_at(k)]
+        return [w for w in works if w is not None]
 
-    def unpack(self) -> None:
+    def unpack(self, k: int = 0) -> None:
         pools = _pool_segs(self.pool_a)
-        for g, s in self.segs.items():
-            unpack_columns(s.back, self.local_rows, s.blocks, s.b, pools[g])
+        for g, s in self._segs_at(k):
+            unpack_columns(s.back[k], self.local_rows, s.chunk_blocks(k), s.bc, pools[g])
 
     def step(self, timed: bool = False) -> None:
-        """One round: pack, all-to-all, K3 on this rank's column block, all-to-all back, unpack.
-        With timed=True the kernels are bracketed by events (kernel_ms())."""
-        self.pack()
-        self.forward_exchange()
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if timed else None
-        if ev:
-            ev[0].record()
-        self.compute()
-        if ev:
-            ev[1].record()
+        """One round, chunk-pipelined: pack k+1 and its forward all-to-all are issued before
+        chunk k is reduced; chunk k's backward all-to-all runs while k+1 is reduced; each wait()
+        only makes the compute stream wait on RCCL's.  With timed=True the K3 launches are
+        bracketed by events (kernel_ms(): their sum per step)."""
+        C = self.chunks
+        ev = [] if timed else None
+        fwd, bwd = {}, {}
+        self.pack(0)
+        fwd[0] = self.forward_exchange(0)
+        for k in range(C):
+            if k + 1 < C:
+                self.pack(k + 1)
+                fwd[k + 1] = self.forward_exchange(k + 1)
+            for w in fwd.pop(k):
+                w.wait()
+            if ev is not None:
+                ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+                ev[-1][0].record()
+            self.compute(k)
+            if ev is not None:
+                ev[-1][1].record()
+            bwd[k] = self.backward_exchange(k)
+            if k >= 1:
+                for w in bwd.pop(k - 1):
+                    w.wait()
+                self.unpack(k - 1)
+        for w in bwd.pop(C - 1):
+            w.wait()
+        self.unpack(C - 1)
+        if ev is not None:
             self._events.append(ev)
-        self.backward_exchange()
-        self.unpack()
 
     def kernel_ms(self) -> List[float]:
-        out = [e[0].elapsed_time(e[1]) for e in self._events]
+        out = [sum(a.elapsed_time(b) for a, b in e) for e in self._events]
         self._events = []
         return out
 
@@ -221,7 +263,7 @@ class TransposedRound:
 
     @property
     def kernel_bytes(self) -> int:
-        """Algorithmic HBM bytes of one round's K3 launch (staged sources + written rows)."""
+        """Algorithmic HBM bytes of one round's K3 launches (staged sources + written rows)."""
         return sum(_ESIZE[g] * self.w_me[g] for g, _ in float_segments(self.layout)) * (
             self.staged_sources + self.rows_all)
 
@@ -230,16 +272,16 @@ class TransposedRound:
         """Bytes this rank receives over the links per round (both all-to-alls)."""
         r = 0
         for g, s in self.segs.items():
-            r += _ESIZE[g] * s.b * ((self.rows_all - self.local_rows) + self.local_rows * (self.world - 1))
+            r += _ESIZE[g] * s.chunks * s.bc * ((self.rows_all - self.local_rows) + self.local_rows * (self.world - 1))
         return r
 
     def spot_check(self) -> bool:
-        """After a step: the first row of this rank's column block == K1 on its operands'
-        blocks (bitwise)."""
+        """After a step: the first row of this rank's first column chunk == K1 on its operands'
+        chunks (bitwise)."""
         segs = {g: s for g, s in self.segs.items() if g != "i64"}
-        ops_ = {g: [s.work_in[j] for j in self.orders_pos[0]] for g, s in segs.items()}
-        return spot_check_row(self.layout, ops_, self.weights_pos[0], {g: s.work_out[0] for g, s in segs.items()},
-                              self.mode, n_of=self.w_me)
+        ops_ = {g: [s.work_in[0][j] for j in self.orders_pos[0]] for g, s in segs.items()}
+        return spot_check_row(self.layout, ops_, self.weights_pos[0], {g: s.work_out[0][0] for g, s in segs.items()},
+                              self.mode, n_of={g: s.chunk_blocks(0)[self.rank][1] for g, s in segs.items()})
 
 
 def make_round(layout: StateLayout, orders, weights, rank: int, world: int, device, exchange: str = "auto",
