@@ -58,6 +58,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU baseline sample")
     p.add_argument("--no-k1", action="store_true", help="skip the per-call K1 side measurement")
     p.add_argument("--host-path", action="store_true", help="also time the H2D+K1+D2H per-call path")
+    p.add_argument("--placement-trials", type=int, default=4,
+                   help="N = 1: candidate pools for the placement calibration (arena.select_pool_pair); "
+                        "2 = none (the first two allocations)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="N > 1: nccl (RCCL over xGMI, the benchmark); gloo = rehearsal of the same "
                         "code path with the exchange staged through host memory, ranks may share a GPU")
@@ -153,7 +156,7 @@ def main():
     import torch.distributed as dist
 
     from topology_aware_learning_amd import ops, synth
-    from topology_aware_learning_amd.arena import ModelPool, StateLayout
+    from topology_aware_learning_amd.arena import ModelPool, StateLayout, select_pool_pair
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -190,15 +193,19 @@ def main():
         from topology_aware_learning_amd import ops as _ops
 
         rows = n_dev_total
-        pin = ModelPool(layout, rows, dev)
-        pout = ModelPool(layout, rows, dev)
-        fill_pool(pin, 1234)
         row_ptr, col, w = _round_csr(orders, weights)
         out_rows = np.arange(rows, dtype=np.int32)
         seg = (lambda p: p.b16) if bf16 else (lambda p: p.f32)
         row = (lambda p, r: p.row_b16(r)) if bf16 else (lambda p, r: p.row_f32(r))
         round_fn = _ops.round_bf16 if bf16 else _ops.round_f32
         agg_fn = _ops.agg_bf16 if bf16 else _ops.agg_f32
+        # pool placement (arena.select_pool_pair): as many candidate pools as fit in 70 % of the
+        # free HBM, up to --placement-trials; the plan is tuned on the first pair, then every
+        # ordered pair is timed with it and the best pair is kept
+        pool_bytes = rows * (4 * layout.ld_f32 + 2 * layout.ld_b16 + 8 * layout.ld_i64)
+        trials = max(2, min(args.placement_trials, int(0.7 * torch.cuda.mem_get_info(dev)[0] // pool_bytes)))
+        cand = [ModelPool(layout, rows, dev) for _ in range(trials)]
+        fill_pool(cand[0], 1234)
         if args.plan:
             plan = _ops.plan_from_spec(row_ptr, col, w, out_rows, json.loads(args.plan)).to(dev)
         elif args.stream_rows:
@@ -206,7 +213,26 @@ def main():
         elif args.no_tune or args.c4:
             plan = _ops.build_plan(row_ptr, col, w, out_rows, c4=args.c4, dense=0 if bf16 else -1).to(dev)
         else:  # time every plan candidate on the real pools (a few rounds, once per topology)
-            plan = _ops.tune_plan(row_ptr, col, w, out_rows, seg(pin), seg(pout), n=n_float, mode=mode)
+            plan = _ops.tune_plan(row_ptr, col, w, out_rows, seg(cand[0]), seg(cand[1]), n=n_float, mode=mode)
+        ev_s, ev_e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+        def placement_score(a, b):
+            round_fn(seg(a), seg(b), plan, n=n_float, mode=mode)
+            ev_s.record()
+            for _ in range(3):
+                round_fn(seg(a), seg(b), plan, n=n_float, mode=mode)
+            ev_e.record()
+            ev_e.synchronize()
+            return ev_s.elapsed_time(ev_e) / 3
+
+        if trials > 2:
+            it = iter(cand)
+            pin, pout, placement = select_pool_pair(lambda: next(it), placement_score, trials)
+        else:
+            (pin, pout), placement = cand, None
+        del cand
+        torch.cuda.empty_cache()  # the candidates not kept
+        fill_pool(pin, 1234)
 
         def step(a, b):
             round_fn(seg(a), seg(b), plan, n=n_float, mode=mode)
@@ -249,6 +275,7 @@ def main():
             valu=valu_floor(len(col), rows, n_float, k_ms, mode))
         if tol is not None:
             result_extra["bf16_vs_fp32_reference_row0"] = tol
+        result_extra["placement"] = placement
         steps_done = args.steps
         units = rows * n_params * steps_done
         k1 = None

@@ -13,7 +13,7 @@ from __future__ import annotations
 
 from collections import OrderedDict
 from dataclasses import dataclass
-from typing import Dict, List, Mapping, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Mapping, Optional, Sequence, Tuple
 
 import torch
 import torch.nn as nn
@@ -240,3 +240,25 @@ def bound_row(module: nn.Module) -> Optional[Tuple[ModelPool, int]]:
         return None
     r = pool.row_of(module)
     return None if r is None else (pool, r)
+
+
+def select_pool_pair(make_pool: Callable[[], "ModelPool"], score: Callable[["ModelPool", "ModelPool"], float],
+                     trials: int):
+    """Placement calibration for a double-buffered device-resident round.
+
+    Where a pool lands in HBM changes the round kernel's time bimodally - on config 3 the same
+    plan over the same strides runs 2.0 or 2.45 ms depending on the physical placement of the
+    pools (mostly the one written; tools/alloc_probe.py) - and a placement is fixed
+    for the pool's lifetime, i.e. for every round of a training run.  So the arena allocates
+    `trials` pools once, times every ordered pair with `score(a, b)` (ms of one round a -> b),
+    keeps the pair with the smallest score(a, b) + score(b, a) (the round alternates direction)
+    and frees the others.  Returns (a, b, report)."""
+    pools = [make_pool() for _ in range(max(2, trials))]
+    k = len(pools)
+    ms = {(i, j): float(score(pools[i], pools[j])) for i in range(k) for j in range(k) if i != j}
+    best = min(((i, j) for i in range(k) for j in range(i + 1, k)), key=lambda p: ms[p] + ms[p[::-1]])
+    a, b = pools[best[0]], pools[best[1]]
+    report = dict(pools=k, pair_ms={f"{i}->{j}": round(v, 3) for (i, j), v in ms.items()}, chosen=list(best))
+    del pools
+    torch.cuda.empty_cache()
+    return a, b, report
