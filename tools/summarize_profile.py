@@ -33,6 +33,16 @@ def last_round_kernel(path):
     return best[1]
 
 
+def timed_steps(trace_csv, kernel, steps=20):
+    """Mean duration (ns) of the kernel's last `steps` dispatches in a rocprofv3 kernel trace:
+    the bench's timed steps (tuning candidates and placement trials come earlier)."""
+    d = sorted((int(r["Dispatch_Id"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+               for r in csv.DictReader(open(trace_csv)) if r["Kernel_Name"] == kernel)
+    last = [x for _, x in d[-steps:]]
+    return dict(kernel=kernel, dispatches=len(d), last_n=len(last), mean_ns_last_n=sum(last) / max(1, len(last)),
+                mean_ns_all=sum(x for _, x in d) / max(1, len(d)))
+
+
 def main(tag, sub, key="random-64-resnet50"):
     src = ROOT / "gpurun_out"
     dst = ROOT / "profiles" / sub
@@ -50,6 +60,9 @@ def main(tag, sub, key="random-64-resnet50"):
     stats = {r["Name"]: r for r in csv.DictReader(open(dst / "kernel_stats.csv"))}
     k = last_round_kernel(src / f"{tag}_pmc_fetch" / "pmc_counter_collection.csv")
     if k is not None:
+        trace = src / f"{tag}_prof" / "trace_kernel_trace.csv"
+        if trace.exists():
+            (dst / "round_kernel_timed_steps.json").write_text(json.dumps(timed_steps(trace, k), indent=1))
         t = ROOT / "profiles" / "traffic.json"
         d = json.loads(t.read_text()) if t.exists() else {}
         d.pop("resnet50", None)  # round-1 key, superseded by workload keys
