@@ -198,3 +198,25 @@ def test_prox_term_matches_torch_loop(cuda, k):
     assert abs(float(fused) - float(ref)) <= 1e-5 * abs(float(ref)) + 1e-6
     for a, b in zip(g_fused, g_ref):
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-6)
+
+
+def test_round_executor_scratch_placement(cuda):
+    """A multi-group round through RoundExecutor with scratch placement trials: the fastest of
+    three scratch candidates is kept and the round is still bitwise the oracle's."""
+    import networkx as nx
+
+    import oracle
+
+    g = nx.random_regular_graph(8, 1000, seed=4)  # 1000 sources: more than one LDS group
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(1000)]
+    ws = [ra.unweighted_weights(9)] * 1000
+    layout = StateLayout.from_layout([("w", (4093,), "float32"), ("nbt", (), "int64")])
+    pool = ModelPool(layout, 1000, cuda)
+    x = np.random.default_rng(9).standard_normal((1000, 4093)).astype(np.float32)
+    pool.f32[:, :4093] = torch.from_numpy(x).to(cuda)
+    ex = RoundExecutor(pool, placement_trials=3)
+    ex.run(orders, ws)
+    assert ex.placement is not None and len(ex.placement["scratch_ms"]) == 3
+    rp, col, w = ra.round_csr(orders, ws)
+    ref = oracle.round_f32(x, rp, col, w, np.arange(1000))
+    assert bits_equal(pool.f32[:, :4093].cpu().numpy(), ref)

@@ -38,11 +38,46 @@ def csr_from_lists(orders: Sequence[Sequence[int]], weights: Sequence[Sequence[f
 
 
 class RoundExecutor:
-    def __init__(self, pool: ModelPool, scratch: Optional[ModelPool] = None, mode: int = ops.MODE_EXACT):
+    """Rounds over one pool.  Multi-group plans write a scratch pool (snapshot semantics);
+    placement_trials > 1 allocates that many scratch candidates the first time one is needed,
+    times the round into each and keeps the fastest (HBM placement of the written pool changes
+    the round time bimodally, see arena.select_pool_pair); `placement` records the times."""
+
+    def __init__(self, pool: ModelPool, scratch: Optional[ModelPool] = None, mode: int = ops.MODE_EXACT,
+                 placement_trials: int = 1):
         self.pool = pool
         self.scratch = scratch
         self.mode = mode
+        self.placement_trials = placement_trials
+        self.placement: Optional[dict] = None
         self._plans: Dict[Tuple, ops.RoundPlan] = {}
+
+    def _new_scratch(self, plan) -> ModelPool:
+        lay = self.pool.layout
+        make = lambda: ModelPool(lay, self.pool.rows, self.pool.device)  # noqa: E731
+        if self.placement_trials <= 1:
+            return make()
+        seg = "b16" if lay.n_b16 else "f32"
+        n = lay.n_b16 if lay.n_b16 else lay.n_f32
+        run = ops.round_bf16 if lay.n_b16 else ops.round_f32
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        cands, ms = [], []
+        for _ in range(self.placement_trials):
+            c = make()
+            run(getattr(self.pool, seg), getattr(c, seg), plan, n=n, mode=self.mode)
+            s.record()
+            for _ in range(2):
+                run(getattr(self.pool, seg), getattr(c, seg), plan, n=n, mode=self.mode)
+            e.record()
+            e.synchronize()
+            cands.append(c)
+            ms.append(round(s.elapsed_time(e) / 2, 3))
+        best = int(np.argmin(ms))
+        self.placement = dict(scratch_ms=ms, chosen=best)
+        keep = cands[best]
+        del cands
+        torch.cuda.empty_cache()
+        return keep
 
     def plan(self, orders, weights, out_rows) -> ops.RoundPlan:
         key = (tuple(tuple(o) for o in orders), tuple(tuple(float(x) for x in w) for w in weights), tuple(out_rows))
@@ -77,7 +112,7 @@ class RoundExecutor:
         # every workgroup stages all sources of its tile before writing: with one group in place
         # is safe; otherwise the round goes through the scratch pool
         if not plan.single_group and self.scratch is None:
-            self.scratch = ModelPool(lay, self.pool.rows, self.pool.device)
+            self.scratch = self._new_scratch(plan)
         dst = self.pool if plan.single_group else self.scratch
         if lay.n_f32:
             ops.round_f32(self.pool.f32, dst.f32, plan, n=lay.n_f32, mode=self.mode)
