@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--plan", default="", help="JSON plan spec (a previous run's plan.spec): build it, no tuning")
     p.add_argument("--stream-rows", type=int, default=0,
                    help="force a streamed plan with groups of at most this many rows (profiling)")
+    p.add_argument("--in-place", action="store_true",
+                   help="N = 1, single-group plans: every round in place on one pool (RoundExecutor's own form)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU baseline sample")
     p.add_argument("--no-k1", action="store_true", help="skip the per-call K1 side measurement")
@@ -225,7 +227,13 @@ def main():
             ev_e.synchronize()
             return ev_s.elapsed_time(ev_e) / 3
 
-        if trials > 2:
+        in_place = args.in_place and plan.single_group
+        if in_place:  # one pool, rounds in place: keep the fastest placement, a second pool for the check
+            ms = [placement_score(c, c) for c in cand]
+            best = int(np.argmin(ms))
+            pin, pout = cand[best], cand[(best + 1) % len(cand)]
+            placement = dict(pools=len(cand), in_place_ms=[round(v, 3) for v in ms], chosen=[best])
+        elif trials > 2:
             it = iter(cand)
             pin, pout, placement = select_pool_pair(lambda: next(it), placement_score, trials)
         else:
@@ -246,7 +254,7 @@ def main():
                                      row(pout, 0).view(torch.int16 if bf16 else torch.int32)))
         tol = bf16_tolerance(pin, pout, orders[0], weights[0], n_float, dev) if bf16 else None
 
-        pools = [pin, pout]
+        pools = [pin, pin] if in_place else [pin, pout]
         for i in range(args.warmup):
             step(pools[i % 2], pools[(i + 1) % 2])
         stream = torch.cuda.current_stream(dev)
@@ -276,6 +284,7 @@ def main():
         if tol is not None:
             result_extra["bf16_vs_fp32_reference_row0"] = tol
         result_extra["placement"] = placement
+        result_extra["in_place"] = in_place
         steps_done = args.steps
         units = rows * n_params * steps_done
         k1 = None
