@@ -776,6 +776,28 @@ __device__ __forceinline__ NarrowLds stage_narrow_roww(const PlanView& p, int g,
   return L;
 }
 
+// LDS byte address of the float4 slot in the low / high 16 bits of `word`, from the lane's
+// column base: one v_mad_u32_u16 (op_sel picks the half) instead of an extract and a shift-add.
+__device__ __forceinline__ uint32_t slot_addr_lo(uint32_t word, uint32_t base) {
+  uint32_t a;
+  asm("v_mad_u32_u16 %0, %1, 16, %2" : "=v"(a) : "v"(word), "v"(base));
+  return a;
+}
+__device__ __forceinline__ uint32_t slot_addr_hi(uint32_t word, uint32_t base) {
+  uint32_t a;
+  asm("v_mad_u32_u16 %0, %1, 16, %2 op_sel:[1,0,0,0]" : "=v"(a) : "v"(word), "v"(base));
+  return a;
+}
+__device__ __forceinline__ uint2 lds_u2(uint32_t addr) {
+  typedef unsigned int u32x2_lds __attribute__((ext_vector_type(2)));
+  const u32x2_lds q = *reinterpret_cast<__attribute__((address_space(3))) const u32x2_lds*>(static_cast<uintptr_t>(addr));
+  return make_uint2(q.x, q.y);
+}
+__device__ __forceinline__ float4 lds_f4(uint32_t addr) {
+  const v4f q = *reinterpret_cast<__attribute__((address_space(3))) const v4f*>(static_cast<uintptr_t>(addr));
+  return make_float4(q.x, q.y, q.z, q.w);
+}
+
 // One ROWW row: the accumulator starts at -0.0, every batch of four slots is one 8-B LDS read
 // (the next batch's read is issued ahead of this batch's data reads).
 template <typename T, bool EXACT>
@@ -784,16 +806,26 @@ __device__ __forceinline__ float4 narrow_row_roww(const float4* s_data, const Na
   const float w = L.rw[r];
   float4 acc = make_float4(-0.f, -0.f, -0.f, -0.f);
   const uint2* s4 = reinterpret_cast<const uint2*>(L.slots);
-  uint2 e = s4[b0];
-  for (uint32_t b = b0; b < b1; ++b) {
+  const uint32_t base = static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)(s_data + cl)));
+  // the batch cursor is the LDS address itself: one add and one compare per batch (the add in
+  // asm so that the cursor keeps one register across the loop)
+  uint32_t q = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)(s4 + b0)));
+  const uint32_t qe = q + 8 * (b1 - b0);
+  uint2 e = lds_u2(q);
+  while (q < qe) {
     float4 x[4];
-    x[0] = s_data[(e.x & 0xffffu) + cl];
-    x[1] = s_data[(e.x >> 16) + cl];
-    x[2] = s_data[(e.y & 0xffffu) + cl];
-    x[3] = s_data[(e.y >> 16) + cl];
-    e = s4[b + 1];  // next batch (or the read-ahead pad), in flight with this batch's data reads
+    x[0] = lds_f4(slot_addr_lo(e.x, base));
+    x[1] = lds_f4(slot_addr_hi(e.x, base));
+    x[2] = lds_f4(slot_addr_lo(e.y, base));
+    x[3] = lds_f4(slot_addr_hi(e.y, base));
+    asm("v_add_u32 %0, 8, %0" : "+v"(q));
+    e = lds_u2(q);  // next batch (or the read-ahead pad), in flight with this batch's data reads
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc = next4t<T, EXACT>(acc, w, x[u]);
+    // keep the read-ahead where it is: without this the compiler sinks the next batch's slot
+    // read to the loop head and waits on it before the data reads
+    asm volatile("" : "+v"(e.x), "+v"(e.y));
   }
   return acc;
 }
