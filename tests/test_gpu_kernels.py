@@ -239,8 +239,12 @@ def test_round_narrow_row_uniform_weights_signed_zero(cuda, sign):
         assert np.array_equal(ob.cpu().view(torch.int16).numpy().view(np.uint16), refb), c4
 
 
-def test_round_narrow_sbm256_one_group(cuda):
-    """BASELINE config 5's topology (256-device SBM) fits one narrow group: each source read once."""
+@pytest.mark.parametrize("c4", [16, 32])
+def test_round_narrow_sbm256_one_group(cuda, c4):
+    """BASELINE config 5's topology (256-device SBM) fits one narrow group: each source read once.
+    Unweighted, so the row-uniform-weight encoding runs (16-bit slots up to the zero tiles at
+    slot 256 * c4, decoded by v_mad_u32_u16 incl. its high-half form); c4 = 16: two resident
+    workgroups per CU (row extents from LDS), c4 = 32: one (extents in registers)."""
     sizes = [32] * 8
     p = [[14 / 31 if a == b else 2 / 224 for b in range(8)] for a in range(8)]
     g = nx.stochastic_block_model(sizes, p, seed=0)
@@ -248,8 +252,10 @@ def test_round_narrow_sbm256_one_group(cuda):
     rows = len(orders)
     row_ptr, col, w = ra.round_csr(orders, ws)
     out_rows = np.arange(rows, dtype=np.int32)
-    plan = ops.build_plan(row_ptr, col, w, out_rows, c4=16, lds_bytes=160 * 1024)
-    assert plan.info.n_groups == 1 and plan.info.total_src == rows
+    plan = ops.build_plan(row_ptr, col, w, out_rows, c4=c4, lds_bytes=160 * 1024)
+    assert plan.info.narrow_roww == 1 and plan.info.c4 == c4
+    if c4 == 16:
+        assert plan.info.n_groups == 1 and plan.info.total_src == rows
     n = 8195
     rng = np.random.default_rng(5)
     pool = rng.standard_normal((rows, n)).astype(np.float32)
