@@ -57,7 +57,12 @@ def parse():
     p.add_argument("--in-place", action="store_true",
                    help="N = 1, single-group plans: every round in place on one pool (RoundExecutor's own form)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU baseline sample")
+    p.add_argument("--cpu-seconds", type=float, default=4.0,
+                   help="bound of the CPU baseline sample (one call at a time; the two-concurrent-calls "
+                        "configuration runs half as long)")
+    p.add_argument("--max-params", type=int, default=0,
+                   help="rehearsal only: keep the model layout's leading float entries up to this many "
+                        "elements (int64 buffers kept); the config names the reduced layout")
     p.add_argument("--no-k1", action="store_true", help="skip the per-call K1 side measurement")
     p.add_argument("--host-path", action="store_true", help="also time the H2D+K1+D2H per-call path")
     p.add_argument("--placement-trials", type=int, default=4,
@@ -146,10 +151,24 @@ def cpu_baseline(layout_list, m: int, budget_s: float):
         t.join()
     el2 = time.perf_counter() - t1
     return dict(value=calls * n_out / el, unit="params/s", cores=torch.get_num_threads(), kind="port",
-                sample=f"{calls} reference aggregation calls (M={m}, {n_out} params each, state_dicts in host "
-                       f"memory, torch CPU ops clone/mul/add_/copy_, one call at a time) in {el:.2f} s",
+                sample=f"{calls} reference calls (M={m}, {n_out} params) one at a time in {el:.2f} s; "
+                       "torch CPU clone/mul/add_/copy_ on host state_dicts",
                 ms_per_call=1e3 * el / calls,
-                two_concurrent_calls=dict(value=sum(counts) * n_out / el2, calls=sum(counts), seconds=round(el2, 2)))
+                os_cpu_count=os.cpu_count(), torch_threads=torch.get_num_threads(), cpu_model=cpu_model(),
+                # the reference's effective configuration: Parsl ThreadPoolExecutor(max_threads=2)
+                two_concurrent_calls_value=sum(counts) * n_out / el2, two_concurrent_calls=sum(counts),
+                two_concurrent_seconds=round(el2, 2))
+
+
+def cpu_model() -> str:
+    """The host CPU's model name (lscpu's "Model name", read from /proc/cpuinfo)."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def main():
@@ -176,6 +195,8 @@ def main():
             dist.init_process_group("gloo")
 
     lay = synth.get_layout(args.model)
+    if args.max_params:
+        lay = synth.truncate_layout(lay, args.max_params)
     if args.dtype == "bf16":
         lay = synth.as_bf16(lay)
     layout = StateLayout.from_layout(lay)
@@ -202,8 +223,8 @@ def main():
         round_fn = _ops.round_bf16 if bf16 else _ops.round_f32
         agg_fn = _ops.agg_bf16 if bf16 else _ops.agg_f32
         # pool placement (arena.select_pool_pair): as many candidate pools as fit in 70 % of the
-        # free HBM, up to --placement-trials; the plan is tuned on the first pair, then every
-        # ordered pair is timed with it and the best pair is kept
+        # free HBM, up to --placement-trials; the plan is tuned on the first pair, then a round
+        # into each candidate is timed with it and the two fastest destinations are kept
         pool_bytes = rows * (4 * layout.ld_f32 + 2 * layout.ld_b16 + 8 * layout.ld_i64)
         trials = max(2, min(args.placement_trials, int(0.7 * torch.cuda.mem_get_info(dev)[0] // pool_bytes)))
         cand = [ModelPool(layout, rows, dev) for _ in range(trials)]
@@ -213,7 +234,8 @@ def main():
         elif args.stream_rows:
             plan = _ops.build_stream_plan(row_ptr, col, w, out_rows, args.stream_rows).to(dev)
         elif args.no_tune or args.c4:
-            plan = _ops.build_plan(row_ptr, col, w, out_rows, c4=args.c4, dense=0 if bf16 else -1).to(dev)
+            plan = (_ops.build_plan(row_ptr, col, w, out_rows, c4=args.c4) if args.c4 else
+                    _ops.default_plan(row_ptr, col, w, out_rows, bf16=bf16)).to(dev)
         else:  # time every plan candidate on the real pools (a few rounds, once per topology)
             plan = _ops.tune_plan(row_ptr, col, w, out_rows, seg(cand[0]), seg(cand[1]), n=n_float, mode=mode)
         ev_s, ev_e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -221,11 +243,11 @@ def main():
         def placement_score(a, b):
             round_fn(seg(a), seg(b), plan, n=n_float, mode=mode)
             ev_s.record()
-            for _ in range(3):
+            for _ in range(2):
                 round_fn(seg(a), seg(b), plan, n=n_float, mode=mode)
             ev_e.record()
             ev_e.synchronize()
-            return ev_s.elapsed_time(ev_e) / 3
+            return ev_s.elapsed_time(ev_e) / 2
 
         in_place = args.in_place and plan.single_group
         if in_place:  # one pool, rounds in place: keep the fastest placement, a second pool for the check
@@ -335,7 +357,10 @@ def main():
         return
 
     achieved = bytes_round / (k_ms * 1e-3) / 1e9
-    traffic = load_traffic(workload_key(args.graph, n_dev_total, args.model))
+    traffic = None
+    if world == 1:  # PMC bytes of exactly this kernel + plan spec + workload, when profiled
+        traffic = load_traffic(traffic_key(result_extra["kernel"], result_extra["plan"]["spec"],
+                                           workload_key(args.graph, n_dev_total, args.model, args.dtype)))
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(lay, M, args.cpu_seconds)  # bf16 layouts: the reference's loop on bf16 tensors
@@ -357,7 +382,8 @@ def main():
                                + (f" ({args.degree}-regular, seed 0)" if args.graph == "random" else "")
                                + f", {args.model} state_dicts, max M={M} (self last), unweighted, "
                                "one full aggregation round per step, snapshot semantics",
-                   "model_layout": args.model, "devices": n_dev_total, "devices_per_gpu": args.devices_per_gpu,
+                   "model_layout": args.model + (f" (first {args.max_params} float params: rehearsal)"
+                                                 if args.max_params else ""), "devices": n_dev_total, "devices_per_gpu": args.devices_per_gpu,
                    "params_per_model": n_params, "parallelism": f"{result_extra.get('exchange', '')}-sharded x{world}" if world > 1 else "1 GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
@@ -470,13 +496,19 @@ def valu_floor(nnz: int, rows: int, n: int, k_ms: float, mode) -> dict:
     return dict(lane_ops=ops_round, floor_ms=floor_ms, frac=floor_ms / k_ms)
 
 
-def workload_key(graph: str, devices: int, model: str) -> str:
-    return f"{graph}-{devices}-{model}"
+def workload_key(graph: str, devices: int, model: str, dtype: str = "f32") -> str:
+    return f"{graph}-{devices}-{model}" + ("" if dtype == "f32" else f"-{dtype}")
+
+
+def traffic_key(kernel: str, spec, workload: str) -> str:
+    """profiles/traffic.json key: the round kernel, the plan spec it ran and the workload - a
+    PMC byte count is only reported for the kernel and plan that produced it."""
+    return f"{kernel}|{json.dumps(spec, sort_keys=True)}|{workload}"
 
 
 def load_traffic(key: str):
-    """HBM bytes per launch of this workload's round kernel from the committed rocprofv3 PMC
-    summary (tools/summarize_profile.py), or None when that workload was not profiled."""
+    """HBM bytes per launch of this kernel + plan + workload from the committed rocprofv3 PMC
+    summary (tools/summarize_profile.py), or None when that combination was not profiled."""
     f = ROOT / "profiles" / "traffic.json"
     if not f.exists():
         return None

@@ -159,7 +159,7 @@ int64_t tal_round_plan_words(int32_t rows, int64_t nnz);
  * share a group while the union of their sources fits; a group's staged sources are in
  * ascending pool row order.  dense_rb: 0 = sparse form, 8 = dense row blocks of 8 (falls back
  * to sparse if a row is not in reference order), -1 = dense when it cuts the LDS operand reads
- * by at least a quarter.  Returns
+ * to at most a quarter (one read serves >= 4 operands: cliques).  Returns
  * TAL_ERR_CAPACITY if one row alone has more distinct sources than fit, or if plan_capacity_words
  * is too small (info->words then holds the size needed). */
 int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host,

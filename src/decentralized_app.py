@@ -5,7 +5,8 @@ checkpoint/resume protocol follow the reference (decentralized_app.py:96-644).  
 difference: when a GPU is visible every client's model is bound to one device-resident
 ModelPool row (topology_aware_learning_amd.arena), so local training and the aggregation
 kernels work on the same HBM bytes and no model crosses PCIe between rounds
-(TAL_DEVICE_POOL=0 keeps the reference's CPU-resident models).
+(TAL_DEVICE_POOL=0 keeps the reference's CPU-resident models).  TAL_BATCHED_ROUND=1 (opt-in)
+runs each round's aggregations as one K3 launch over that pool, with snapshot semantics.
 """
 from __future__ import annotations
 
@@ -15,6 +16,7 @@ import logging
 import os
 import pathlib
 import shutil
+from concurrent.futures import Future
 from pathlib import Path
 
 import numpy
@@ -147,6 +149,10 @@ class DecentrallearnApp:
                                       label_alpha, sample_alpha, self.rng, self.topology, prox_coeff, self.run_dir,
                                       train_test_val)
         self.pool = self._bind_device_pool()
+        # opt-in (no CLI change): the round's aggregations as one K3 launch with snapshot
+        # semantics instead of one app call per client (the reference's form, the default)
+        self.batched_round = os.environ.get("TAL_BATCHED_ROUND", "0") == "1" and self.pool is not None
+        self._executor = None
         self.centrality_dict = create_centrality_dict(self.topology, self.rng)
         logger.log(APP_LOG_LEVEL, f"Created {len(self.clients)} clients")
         self.client_results: list[Result] = []
@@ -204,6 +210,7 @@ class DecentrallearnApp:
         selected = self.rng.choice(list(range(len(self.clients))), size=size, replace=False).tolist()
         print(f"{selected=}")
         futures = []
+        batch = [] if self.batched_round else None
         nxt = self.round_states[round_idx + 1] = {}
         cur = self.round_states[round_idx]
         for client in self.clients:
@@ -233,11 +240,57 @@ class DecentrallearnApp:
                 continue
             neighbor_idxs.append(client.idx)  # self is the last operand (:625)
             agg_neighbors = [nxt[i]["train"] for i in neighbor_idxs]
-            future = self.aggregation_function(
-                agg_client, self.seed, *agg_neighbors, centrality_metric=self.centrality_metric,
-                centrality_dict=self.centrality_dict, softmax=self.softmax,
-                softmax_coeff=self.aggregation_scheduler.get_softmax_coeff())
+            kwargs = dict(centrality_metric=self.centrality_metric, centrality_dict=self.centrality_dict,
+                          softmax=self.softmax, softmax_coeff=self.aggregation_scheduler.get_softmax_coeff())
+            if batch is not None:  # collected; the whole round runs below as one K3 launch
+                future = Future()
+                batch.append((future, agg_client, agg_neighbors, kwargs))
+            else:
+                future = self.aggregation_function(agg_client, self.seed, *agg_neighbors, **kwargs)
             futures.append(future)
             nxt[client.idx]["agg"] = future
+        if batch:
+            self._batched_aggregation(batch)
         self.aggregation_scheduler.step(round_idx)
         return futures
+
+    def _batched_aggregation(self, batch) -> None:
+        """The round's aggregations as ONE K3 launch over the device pool (RoundExecutor):
+        every aggregation reads the models as they were after training (snapshot semantics,
+        SURVEY §8(a)).  The reference's per-call apps instead read neighbors that an earlier
+        call of the same round may already have overwritten, in an order its 2-thread pool
+        decides; per call each result is the same arithmetic (same operands in the same order,
+        same fp32 weights)."""
+        from topology_aware_learning_amd.arena import bound_row
+        from topology_aware_learning_amd.round import RoundExecutor
+
+        from src.decentralized_client import aggregation_weights
+
+        def res(x):
+            return x.result() if isinstance(x, Future) else x
+
+        orders, weights, out_rows, done = [], [], [], []
+        for future, agg_client, agg_neighbors, kwargs in batch:
+            me = res(agg_client)
+            nbrs = [res(f) for f in agg_neighbors]
+            got = aggregation_weights(self.aggregation_function, me, *nbrs, **kwargs)
+            done.append((future, me))
+            if got is None:  # test_agg: no-op
+                continue
+            rows = []
+            for m in list(got[0]) + [me[1].model]:
+                b = bound_row(m)
+                if b is None or b[0] is not self.pool:
+                    raise RuntimeError("TAL_BATCHED_ROUND needs every model bound to the device pool")
+                rows.append(b[1])
+            orders.append(rows[:-1])
+            weights.append([float(x) for x in got[1]])
+            out_rows.append(rows[-1])
+        if self.seed is not None:  # the apps seed torch per call (reference :395); same end state
+            torch.manual_seed(self.seed)
+        if orders:
+            if self._executor is None:
+                self._executor = RoundExecutor(self.pool)
+            self._executor.run(orders, weights, out_rows)
+        for future, me in done:
+            future.set_result(me)

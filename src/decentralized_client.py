@@ -140,33 +140,21 @@ def _models(futures) -> list:
     return [f[1].model for f in futures]
 
 
-@python_app(executors=["threadpool_executor"])
-def weighted_module_avg(client_future, seed: int, *neighbor_futures, **kwargs):
-    """Data-size weighted average (reference :383-415)."""
-    if seed is not None:
-        torch.manual_seed(seed)
+# Each app = its weight rule (the `_*_weights` functions: operands and float64 weights, computed
+# on the host with the reference's arithmetic) + one aggregation.  The weight rules are also
+# what the opt-in batched round (src/decentralized_app.py, TAL_BATCHED_ROUND=1) collects for
+# every client of a round before running them as one K3 launch.
+def _weighted_weights(client_future, neighbor_futures, **kwargs):
     print("weighted aggregate round")
-    w = _w.weighted([len(f[1].train_data) for f in neighbor_futures])
-    aggregate_models(_models(neighbor_futures), w, client_future[1].model)
-    return client_future
+    return _models(neighbor_futures), _w.weighted([len(f[1].train_data) for f in neighbor_futures])
 
 
-@python_app(executors=["threadpool_executor"])
-def unweighted_module_avg(client_future, seed: int, *neighbor_futures, **kwargs):
-    """Plain average, w = 1/M (reference :418-448)."""
-    if seed is not None:
-        torch.manual_seed(seed)
+def _unweighted_weights(client_future, neighbor_futures, **kwargs):
     print("unweighted aggregate round")
-    aggregate_models(_models(neighbor_futures), _w.unweighted(len(neighbor_futures)), client_future[1].model)
-    return client_future
+    return _models(neighbor_futures), _w.unweighted(len(neighbor_futures))
 
 
-@python_app(executors=["threadpool_executor"])
-def sim_centrality_module_avg(client_future, seed: int, *neighbor_futures, **kwargs):
-    """Centrality weights whose softmax sign follows the least similar neighbor
-    (reference :451-550); the similarities come from one K2 launch."""
-    if seed is not None:
-        torch.manual_seed(seed)
+def _sim_centrality_weights(client_future, neighbor_futures, **kwargs):
     cent_dict = kwargs["centrality_dict"]
     metric = kwargs["centrality_metric"]
     softmax = kwargs["softmax"]
@@ -182,41 +170,64 @@ def sim_centrality_module_avg(client_future, seed: int, *neighbor_futures, **kwa
         print(f"client_idx={me.idx} softmaxing aggregation weights w/ softmax_coeff={coeff}")
     else:
         print("1/N aggregation weights")
-    aggregate_models(_models(neighbor_futures), w, me.model)
-    return client_future
+    return _models(neighbor_futures), w
 
 
-@python_app(executors=["threadpool_executor"])
-def centrality_module_avg(client_future, seed: int, *neighbor_futures, **kwargs):
-    """Centrality weights, softmax(coeff * c) or c / sum(c) (reference :553-612)."""
-    if seed is not None:
-        torch.manual_seed(seed)
+def _centrality_weights(client_future, neighbor_futures, **kwargs):
     cent_dict = kwargs["centrality_dict"]
     metric = kwargs["centrality_metric"]
     softmax = kwargs["softmax"]
     coeff = kwargs["softmax_coeff"]
     print(f"{metric} aggregate round w/ {softmax=}")
     order = [f[1].idx for f in neighbor_futures]
-    w = _w.centrality(order, cent_dict[metric], softmax, coeff)
-    aggregate_models(_models(neighbor_futures), w, client_future[1].model)
-    return client_future
+    return _models(neighbor_futures), _w.centrality(order, cent_dict[metric], softmax, coeff)
 
 
-@python_app(executors=["threadpool_executor"])
-def scale_agg(client_future, seed: int, *neighbor_futures, **kwargs):
-    """Self model scaled by 1/M (only self is read; reference :615-647)."""
-    if seed is not None:
-        torch.manual_seed(seed)
+def _scale_weights(client_future, neighbor_futures, **kwargs):
     print("unweighted aggregate round")
-    w = 1 / len(neighbor_futures)
-    aggregate_models([client_future[1].model], [w], client_future[1].model)
-    return client_future
+    return [client_future[1].model], [1 / len(neighbor_futures)]
+
+
+def _app(name, weights_fn, doc):
+    def app(client_future, seed: int, *neighbor_futures, **kwargs):
+        if seed is not None:
+            torch.manual_seed(seed)
+        operands, w = weights_fn(client_future, neighbor_futures, **kwargs)
+        aggregate_models(operands, w, client_future[1].model)
+        return client_future
+
+    app.__doc__ = doc
+    app.__name__ = app.__qualname__ = name
+    app._tal_weights = weights_fn
+    return app
+
+
+_APP = python_app(executors=["threadpool_executor"])
+weighted_module_avg = _APP(_app("weighted_module_avg", _weighted_weights,
+                                "Data-size weighted average (reference :383-415)."))
+unweighted_module_avg = _APP(_app("unweighted_module_avg", _unweighted_weights,
+                                  "Plain average, w = 1/M (reference :418-448)."))
+sim_centrality_module_avg = _APP(_app("sim_centrality_module_avg", _sim_centrality_weights,
+                                      "Centrality weights whose softmax sign follows the least similar neighbor "
+                                      "(reference :451-550); the similarities come from one K2 launch."))
+centrality_module_avg = _APP(_app("centrality_module_avg", _centrality_weights,
+                                  "Centrality weights, softmax(coeff * c) or c / sum(c) (reference :553-612)."))
+scale_agg = _APP(_app("scale_agg", _scale_weights, "Self model scaled by 1/M (only self is read; reference :615-647)."))
 
 
 @python_app(executors=["threadpool_executor"])
 def test_agg(client_future, seed: int, *neighbor_futures, **kwargs):
     """No-op aggregation (reference :650-658)."""
     return client_future
+
+
+def aggregation_weights(app, client_future, *neighbor_futures, **kwargs):
+    """(operand models, float64 weights) the app would aggregate for this call, without
+    aggregating; None for test_agg.  Used by the batched round (TAL_BATCHED_ROUND=1)."""
+    fn = getattr(getattr(app, "__wrapped__", app), "_tal_weights", None)
+    if fn is None:
+        return None
+    return fn(client_future, neighbor_futures, **kwargs)
 
 
 def cosine_similarity(model_1, model_2):

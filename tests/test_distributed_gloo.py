@@ -13,11 +13,18 @@ import torch.multiprocessing as mp
 
 import oracle
 from oracle import reference_alg as ra
-from topology_aware_learning_amd.distributed import build_shard, partition_contiguous, post_exchange
+from topology_aware_learning_amd.distributed import (HaloPacker, build_shard, partition_contiguous, post_exchange,
+                                                    recv_range)
 
 
-def problem(n=14, k=4, seed=3, width=203):
-    g = nx.random_regular_graph(k, n, seed=seed)
+def problem(n=14, k=4, seed=3, width=203, kind="regular"):
+    if kind == "regular":
+        g = nx.random_regular_graph(k, n, seed=seed)
+    else:  # BASELINE config 4 / 5 topologies (bench.make_graph), at reduced width
+        import bench
+
+        g = bench.make_graph({"barbell60": "barbell", "sbm256": "sbm"}[kind], 256, 0)
+        n = g.number_of_nodes()
     orders = [sorted(g.neighbors(i)) + [i] for i in range(n)]
     ws = [ra.centrality_weights(o, nx.degree_centrality(g), True, 3.0) for o in orders]
     rng = np.random.default_rng(seed)
@@ -42,16 +49,38 @@ def test_shard_specs_cover_the_round():
             assert mine == theirs
 
 
+@pytest.mark.parametrize("kind", ["barbell60", "sbm256"])
+def test_halo_messages_one_per_peer(kind):
+    """Per rank and segment: one send per peer (its rows gathered in the receiver's order) and
+    one receive per peer into a contiguous halo block."""
+    orders, ws, pool, _ = problem(kind=kind)
+    owner = partition_contiguous(len(orders), 8)
+    specs = [build_shard(orders, ws, owner, r, 8) for r in range(8)]
+    tens = []
+    for s in specs:
+        t = torch.zeros(s.rows, pool.shape[1])
+        for k, g in enumerate(s.own):
+            t[k] = torch.from_numpy(pool[g])
+        tens.append(t)
+    for s, t in zip(specs, tens):
+        for p in s.recv:
+            r0, r1 = recv_range(s, p)
+            msg = HaloPacker(specs[p], tens[p]).send_tensor(tens[p], s.rank)
+            t[r0:r1] = msg
+        glob = s.own + s.halo
+        assert np.array_equal(t.numpy(), pool[glob])
+
+
 def _free_port():
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         return sk.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, kind="regular"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    orders, ws, pool, ipool = problem()
+    orders, ws, pool, ipool = problem(kind=kind)
     owner = partition_contiguous(len(orders), world)
     spec = build_shard(orders, ws, owner, rank, world)
     glob_ids = spec.own + spec.halo
@@ -73,10 +102,13 @@ def _worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_exchange_matches_global_round(tmp_path, world):
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
-    orders, ws, pool, ipool = problem()
+@pytest.mark.parametrize("world,kind", [(2, "regular"), (3, "regular"), (8, "barbell60"), (8, "sbm256")])
+def test_gloo_exchange_matches_global_round(tmp_path, world, kind):
+    """Halo exchange (one packed message per peer per segment) + local round on `world` gloo
+    ranks == the single-process oracle round; barbell60 / sbm256 are BASELINE configs 4 / 5
+    sharded 8 ways as bench.py --gpus 8 does (contiguous blocks)."""
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), kind), nprocs=world, join=True)
+    orders, ws, pool, ipool = problem(kind=kind)
     rp, col, w = ra.round_csr(orders, ws)
     ref = oracle.round_f32(pool, rp, col, w, np.arange(len(orders)))
     iref = oracle.round_i64(ipool, rp, col, w, np.arange(len(orders)))

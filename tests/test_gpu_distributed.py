@@ -10,7 +10,8 @@ import oracle
 from oracle import reference_alg as ra
 from topology_aware_learning_amd import synth
 from topology_aware_learning_amd.arena import StateLayout
-from topology_aware_learning_amd.distributed import ShardedRound, partition_contiguous
+from topology_aware_learning_amd import ops
+from topology_aware_learning_amd.distributed import ShardedRound, partition_contiguous, recv_range
 
 pytestmark = pytest.mark.gpu
 
@@ -41,44 +42,60 @@ def _get_rows(pool_obj, rows, dtype):
     return pool_obj.b16[:rows, :1008].cpu().view(torch.int16).numpy().view(np.uint16)
 
 
-def _oracle_round(dtype, pool, rp, col, w, n):
-    if dtype == "f32":
-        return oracle.round_f32(pool, rp, col, w, np.arange(n))
-    return oracle.round_bf16(pool, rp, col, w, np.arange(n), exact=True)
+def _virtual_halo_exchange(srs):
+    """The halo exchange between virtual ranks through the same per-peer messages the RCCL path
+    sends (HaloPacker.send_tensor -> the receiver's contiguous halo block, recv_range)."""
+    for sr in srs:
+        for peer in sr.spec.recv:
+            r0, r1 = recv_range(sr.spec, peer)
+            src = srs[peer]
+            for si, (_, t, _) in enumerate(sr.pool_a.segments()):
+                ts = src.pool_a.segments()[si][1]
+                msg = src.packers[si].send_tensor(ts, sr.spec.rank)
+                assert msg.shape[0] == r1 - r0
+                t[r0:r1].copy_(msg)
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
-@pytest.mark.parametrize("graph,world", [("regular", 4), ("barbell", 8), ("ring", 2)])
-def test_virtual_ranks_two_rounds(cuda, graph, world, dtype):
-    g = {"regular": nx.random_regular_graph(8, 48, seed=0), "barbell": nx.barbell_graph(20, 8),
-         "ring": nx.cycle_graph(12)}[graph]
+def _graph(name):
+    import bench
+
+    return {"regular": lambda: nx.random_regular_graph(8, 48, seed=0), "barbell": lambda: nx.barbell_graph(20, 8),
+            "ring": lambda: nx.cycle_graph(12),
+            # BASELINE config 4 / 5 topologies at their own size (reduced columns)
+            "barbell60": lambda: bench.make_graph("barbell", 128, 0),
+            "sbm256": lambda: bench.make_graph("sbm", 256, 0)}[name]()
+
+
+@pytest.mark.parametrize("dtype,mode", [("f32", ops.MODE_EXACT), ("bf16", ops.MODE_EXACT), ("bf16", ops.MODE_FMA)])
+@pytest.mark.parametrize("graph,world", [("regular", 4), ("barbell", 8), ("ring", 2), ("barbell60", 8), ("sbm256", 8)])
+def test_virtual_ranks_two_rounds(cuda, graph, world, dtype, mode):
+    """ShardedRound on `world` virtual ranks (halo exchange by in-process copies of the packed
+    per-peer messages), two rounds, bitwise the oracle's snapshot rounds.  barbell60 / sbm256 are
+    BASELINE configs 4 / 5 sharded 8 ways (16 / 32 devices per rank)."""
+    if dtype == "f32" and mode == ops.MODE_FMA:
+        pytest.skip("fp32 FMA rounds are checked against K1-FMA elsewhere")
+    g = _graph(graph)
     n = g.number_of_nodes()
     orders = [sorted(g.neighbors(i)) + [i] for i in range(n)]
     ws = [ra.unweighted_weights(len(o)) for o in orders]
     layout, pool, ipool = _seg_setup(dtype, n, 1)
     owner = partition_contiguous(n, world)
-    srs = [ShardedRound(layout, orders, ws, r, world, cuda, exchange=lambda sr: []) for r in range(world)]
+    srs = [ShardedRound(layout, orders, ws, r, world, cuda, mode=mode, exchange=lambda sr: []) for r in range(world)]
     for sr in srs:
         for k, gid in enumerate(sr.spec.own):
             _put_row(sr.pool_a, k, dtype, pool[gid], ipool[gid], cuda)
-
-    def exchange_all():
-        for sr in srs:
-            base = len(sr.spec.own)
-            for k, gid in enumerate(sr.spec.halo):
-                src = srs[owner[gid]]
-                for _, t, _ in sr.pool_a.segments():
-                    st = {id(sr.pool_a.f32): src.pool_a.f32, id(sr.pool_a.b16): src.pool_a.b16,
-                          id(sr.pool_a.i64): src.pool_a.i64}[id(t)]
-                    t[base + k].copy_(st[src.spec.local_of[gid]])
-
+    if graph in ("barbell60", "sbm256"):  # one message per peer per segment, each way
+        assert all(len(sr.spec.send) <= world - 1 and len(sr.spec.recv) <= world - 1 for sr in srs)
     rp, col, w = ra.round_csr(orders, ws)
     ref, iref = pool, ipool
     for _ in range(2):
-        exchange_all()
+        _virtual_halo_exchange(srs)
         for sr in srs:
             sr.step()
-        ref = _oracle_round(dtype, ref, rp, col, w, n)
+        if dtype == "f32":
+            ref = oracle.round_f32(ref, rp, col, w, np.arange(n))
+        else:
+            ref = oracle.round_bf16(ref, rp, col, w, np.arange(n), exact=(mode == ops.MODE_EXACT))
         iref = oracle.round_i64(iref, rp, col, w, np.arange(n))
     torch.cuda.synchronize()
     for sr in srs:
@@ -89,21 +106,23 @@ def test_virtual_ranks_two_rounds(cuda, graph, world, dtype):
 
 
 @pytest.mark.parametrize("chunks", [1, 3])
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
-@pytest.mark.parametrize("graph,world", [("regular", 4), ("barbell", 8), ("ring", 3)])
-def test_virtual_ranks_transposed_two_rounds(cuda, graph, world, dtype, chunks):
+@pytest.mark.parametrize("dtype,mode", [("f32", ops.MODE_EXACT), ("bf16", ops.MODE_EXACT), ("bf16", ops.MODE_FMA)])
+@pytest.mark.parametrize("graph,world", [("regular", 4), ("barbell", 8), ("ring", 3), ("barbell60", 8), ("sbm256", 8)])
+def test_virtual_ranks_transposed_two_rounds(cuda, graph, world, dtype, mode, chunks):
     """TransposedRound (column blocks by all-to-all) with the two all-to-alls done by in-process
     copies between virtual ranks: K3 on each rank's column block, bitwise the oracle round."""
     from topology_aware_learning_amd.transposed import TransposedRound
 
-    g = {"regular": nx.random_regular_graph(8, 48, seed=0), "barbell": nx.barbell_graph(20, 8),
-         "ring": nx.cycle_graph(13)}[graph]
+    g = nx.cycle_graph(13) if graph == "ring" else _graph(graph)
     n = g.number_of_nodes()
     orders = [sorted(g.neighbors(i)) + [i] for i in range(n)]
     ws = [ra.unweighted_weights(len(o)) for o in orders]
     layout, pool, ipool = _seg_setup(dtype, n, 2)
-    owner = np.array([(5 * i) % world for i in range(n)], np.int32)  # interleaved owners
-    srs = [TransposedRound(layout, orders, ws, r, world, cuda, owner=owner, chunks=chunks) for r in range(world)]
+    # interleaved owners for the small graphs; BASELINE configs 4 / 5 in contiguous blocks (bench)
+    owner = (partition_contiguous(n, world) if graph in ("barbell60", "sbm256")
+             else np.array([(5 * i) % world for i in range(n)], np.int32))
+    srs = [TransposedRound(layout, orders, ws, r, world, cuda, owner=owner, chunks=chunks, mode=mode)
+           for r in range(world)]
     for sr in srs:
         for k, gid in enumerate(sr.own):
             _put_row(sr.pool_a, k, dtype, pool[gid], ipool[gid], cuda)
@@ -126,7 +145,10 @@ def test_virtual_ranks_transposed_two_rounds(cuda, graph, world, dtype, chunks):
                         s.back[k][p].copy_(src.segs[key].work_out[k][base[r]: base[r + 1]])
             for sr in srs:
                 sr.unpack(k)
-        ref = _oracle_round(dtype, ref, rp, col, w, n)
+        if dtype == "f32":
+            ref = oracle.round_f32(ref, rp, col, w, np.arange(n))
+        else:
+            ref = oracle.round_bf16(ref, rp, col, w, np.arange(n), exact=(mode == ops.MODE_EXACT))
         iref = oracle.round_i64(iref, rp, col, w, np.arange(n))
     torch.cuda.synchronize()
     for sr in srs:
@@ -161,3 +183,37 @@ def test_bench_multi_rank_rehearsal(cuda, tmp_path, exchange, world):
     d = json.loads(line[0])
     assert d["n_gpus"] == world and d["parity"] is True and d["exchange"] == exchange
     assert d["value"] > 0 and d["link_bytes_in_per_round"] > 0
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("graph,model,dtype,exchange", [("barbell", "resnet50", "f32", "auto"),
+                                                        ("sbm", "vit_b16", "bf16", "auto"),
+                                                        ("sbm", "vit_b16", "bf16", "transpose")])
+def test_bench_world8_rehearsal(cuda, tmp_path, graph, model, dtype, exchange):
+    """bench.py --gpus 8 on BASELINE config 4 (barbell(60, 8), ResNet-50 layout) and config 5
+    (SBM 8 x 32, ViT-B/16 layout, bf16) with 8 gloo ranks sharing this GPU: the driver's 8-GPU
+    command with the exchange staged through host memory and the layouts cut to their first
+    131,072 float params (--max-params)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    port = 29900 + (os.getpid() % 300) + (0 if graph == "barbell" else 11) + (0 if exchange == "auto" else 5)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", str(ROOT / "bench.py"), "--gpus", "8",
+           "--dist-backend", "gloo", "--graph", graph, "--model", model, "--dtype", dtype, "--devices", "256"
+           if graph == "sbm" else "128", "--exchange", exchange, "--max-params", "131072",
+           "--steps", "2", "--warmup", "1", "--no-tune"]
+    out = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=280)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1, out.stdout[-2000:]
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 8 and d["parity"] is True and d["config"]["devices"] == (256 if graph == "sbm" else 128)
+    assert d["value"] > 0 and d["link_bytes_in_per_round"] > 0
+    if exchange != "auto":
+        assert d["exchange"] == exchange

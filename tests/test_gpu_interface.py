@@ -148,6 +148,41 @@ def test_driver_config1_on_gpu(cuda, tmp_path, monkeypatch):
     assert rc == 0 and checked == [3] * 16
 
 
+def test_driver_batched_round(cuda, tmp_path, monkeypatch):
+    """TAL_BATCHED_ROUND=1: decentralized_main.py issues each round's aggregations as ONE
+    RoundExecutor.run (K3) with snapshot semantics; the pool after every round equals the
+    oracle's snapshot round over the pool as it was after training, bit for bit."""
+    import oracle
+
+    monkeypatch.setenv("TAL_SYNTHETIC_DATA", "1")
+    monkeypatch.setenv("TAL_SYNTHETIC_SAMPLES", "64")
+    monkeypatch.setenv("TAL_BATCHED_ROUND", "1")
+    real_run = RoundExecutor.run
+    runs = []
+
+    def checked_run(self, orders, weights, out_rows=None, sequential=False):
+        lay = self.pool.layout
+        f_in = self.pool.f32[:, : lay.n_f32].cpu().numpy().copy()
+        i_in = self.pool.i64[:, : lay.n_i64].cpu().numpy().copy()
+        real_run(self, orders, weights, out_rows, sequential)
+        rp, col, w = ra.round_csr(orders, weights)
+        ref = oracle.round_f32(f_in, rp, col, w, np.asarray(out_rows))
+        iref = oracle.round_i64(i_in, rp, col, w, np.asarray(out_rows))
+        assert np.array_equal(self.pool.f32[:, : lay.n_f32].cpu().numpy().view(np.uint32), ref.view(np.uint32))
+        assert np.array_equal(self.pool.i64[:, : lay.n_i64].cpu().numpy(), iref)
+        runs.append(len(orders))
+
+    monkeypatch.setattr(RoundExecutor, "run", checked_run)
+    topo = tmp_path / "ring8.txt"
+    np.savetxt(topo, nx.to_numpy_array(nx.cycle_graph(8)), fmt="%d")
+    from src.experiments import decentralized_main
+
+    rc = decentralized_main.main(["--dataset", "cifar10", "--aggregation_strategy", "degCent", "--softmax",
+                                  "--rounds", "2", "--epochs", "1", "--topology_file", str(topo), "--out_dir",
+                                  str(tmp_path / "logs"), "--batch_size", "32"])
+    assert rc == 0 and runs == [8, 8]
+
+
 def test_checkpoint_from_device_pool(cuda, tmp_path):
     """SURVEY §8(f) row 2 on the GPU: the checkpoint is written from the pool rows and reads
     back (reference loader and pool loader) bit-identically."""

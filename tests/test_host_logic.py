@@ -483,3 +483,47 @@ def test_clique_plan_table_and_spec():
     ring = _orders_of(nx.cycle_graph(16))
     rp, col, w = ra.round_csr(ring, [ra.unweighted_weights(3)] * 16)
     assert ops.build_clique_plan(rp, col, w, np.arange(16)) is None
+
+
+def _bench_round(kind, n, deg):
+    import bench
+    from topology_aware_learning_amd.round import csr_from_lists
+
+    orders, weights = bench.round_spec(n, deg, kind=kind)
+    rp, col, w = csr_from_lists(orders, weights)
+    return rp, col, w, np.arange(len(orders), dtype=np.int32)
+
+
+@pytest.mark.parametrize("kind,n,deg,form", [
+    ("ring", 32, 2, "sparse-wide"),      # config 2: c4 64/128 sparse won (0.55-0.58 ms), dense 0.72-0.85
+    ("random", 64, 8, "sparse-wide"),    # config 3: c4 64 sparse 2.45 ms, dense 6.22 ms
+    ("barbell", 128, 0, "clique"),       # config 4: K3c 4.95 ms, best LDS-tiled plan 10.3 ms
+    ("sbm", 256, 0, "narrow-16"),        # config 5: narrow c4 16 (one group) 36.5 ms, c4 64 83 ms
+])
+def test_default_plan_forms(kind, n, deg, form):
+    """The untimed plan the round components build (RoundExecutor, ShardedRound,
+    TransposedRound with tune=False) has the form that won the round-1 tuner A/B on the driver's
+    box for each BASELINE config (BENCH_r01 / profiles/r01/config_c*.json candidates)."""
+    p = ops.default_plan(*_bench_round(kind, n, deg))
+    if form == "clique":
+        assert isinstance(p, ops.CliquePlan) and p.n_cliques == 2 and p.rest.info.dense_rb == 0
+        return
+    assert isinstance(p, ops.RoundPlan) and p.info.dense_rb == 0 and p.info.stream_cs == 0
+    if form == "sparse-wide":
+        assert p.info.c4 >= 64 and p.info.n_groups == 1
+    else:
+        assert p.info.c4 == 16 and p.info.n_groups == 1 and p.staged_rows() == 256
+
+
+def test_auto_dense_only_for_cliques():
+    """dense_rb = -1 (library's choice) keeps random graphs sparse and takes dense row blocks on
+    a complete graph (one LDS read serves every row of a block)."""
+    p = ops.build_plan(*_bench_round("random", 64, 8), c4=64, lds_bytes=80 * 1024, dense=-1)
+    assert p.info.dense_rb == 0
+    g = nx.complete_graph(40)
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(40)]
+    from topology_aware_learning_amd.round import csr_from_lists
+
+    rp, col, w = csr_from_lists(orders, [[1 / 40] * 40] * 40)
+    p = ops.build_plan(rp, col, w, np.arange(40, dtype=np.int32), c4=64, lds_bytes=160 * 1024, dense=-1)
+    assert p.info.dense_rb == 8

@@ -1,0 +1,28 @@
+# Profiling pass (round 2): the driver's bench command under rocprofv3 --kernel-trace --stats
+# (bench line + kernel trace from ONE process), then FETCH_SIZE / WRITE_SIZE passes per plan
+# spec the tuner can pick, for tools/summarize_r02.py.   Usage: bash tools/gpu_profile.sh <tag>
+set -o pipefail
+TAG=${1:-r02prof}
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c3_trace -o trace -- \
+  python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/c3_trace.log 2>&1 || { echo FAIL c3_trace; exit 1; }
+pmc() {  # name spec workload [bench args]
+  local name=$1 spec=$2 wl=$3; shift 3
+  echo "{\"spec\": $spec, \"workload\": \"$wl\"}" > $OUT/pmc_$name.spec
+  for c in FETCH_SIZE WRITE_SIZE; do
+    local s=fetch; [ $c = WRITE_SIZE ] && s=write
+    timeout -s KILL 180 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_${name}_$s -o pmc -- \
+      python3 $R/bench.py --plan "$spec" --steps 4 --warmup 1 --no-cpu-baseline --no-k1 --placement-trials 2 "$@" \
+      > $OUT/pmc_${name}_$s.log 2>&1 || { echo FAIL pmc $name $c; return 1; }
+  done
+}
+pmc c3_c64 '{"c4": 64, "dense": 0, "lds": 81920}' random-64-resnet50 && \
+pmc c3_c32 '{"c4": 32, "dense": 0, "lds": 81920}' random-64-resnet50 && \
+pmc c3_c16 '{"c4": 16, "dense": 0, "lds": 81920}' random-64-resnet50 && \
+pmc c2_c128 '{"c4": 128, "dense": 0, "lds": 81920}' ring-32-resnet18 --graph ring --model resnet18 --devices 32 --degree 2 && \
+pmc c2_c64 '{"c4": 64, "dense": 0, "lds": 81920}' ring-32-resnet18 --graph ring --model resnet18 --devices 32 --degree 2
+echo PROFILE EXIT $?

@@ -248,17 +248,24 @@ def select_pool_pair(make_pool: Callable[[], "ModelPool"], score: Callable[["Mod
 
     Where a pool lands in HBM changes the round kernel's time bimodally - on config 3 the same
     plan over the same strides runs 2.0 or 2.45 ms depending on the physical placement of the
-    pools (mostly the one written; tools/alloc_probe.py) - and a placement is fixed
-    for the pool's lifetime, i.e. for every round of a training run.  So the arena allocates
-    `trials` pools once, times every ordered pair with `score(a, b)` (ms of one round a -> b),
-    keeps the pair with the smallest score(a, b) + score(b, a) (the round alternates direction)
-    and frees the others.  Returns (a, b, report)."""
+    pool it WRITES (tools/placement_probe.py, DESIGN.md §5: the slow allocations show the same
+    TLB hit/miss counts and the same sequential-fill rate as the fast ones, but 1.5-2x the
+    memory-side write-credit stalls and 2-3x the L2 tag stalls, i.e. DRAM-side contention of
+    the concurrent row streams, not translation) - and a placement is fixed for the pool's
+    lifetime, i.e. for every round of a training run.  So the arena allocates `trials` pools
+    once, times a round INTO each (`score(src, dst)`, src = the next pool), keeps the two
+    fastest destinations as the pair (the double-buffered round writes each in turn) and frees
+    the others: `trials` timed rounds instead of every ordered pair.  Returns (a, b, report);
+    report["first_pair_ms"] is what the first two allocations would have run."""
     pools = [make_pool() for _ in range(max(2, trials))]
     k = len(pools)
-    ms = {(i, j): float(score(pools[i], pools[j])) for i in range(k) for j in range(k) if i != j}
-    best = min(((i, j) for i in range(k) for j in range(i + 1, k)), key=lambda p: ms[p] + ms[p[::-1]])
+    ms = [float(score(pools[(j + 1) % k], pools[j])) for j in range(k)]
+    order = sorted(range(k), key=lambda j: ms[j])
+    best = sorted(order[:2])
     a, b = pools[best[0]], pools[best[1]]
-    report = dict(pools=k, pair_ms={f"{i}->{j}": round(v, 3) for (i, j), v in ms.items()}, chosen=list(best))
+    report = dict(pools=k, dest_ms=[round(v, 3) for v in ms], chosen=best,
+                  first_pair_ms=round((ms[0] + ms[1]) / 2, 3),
+                  chosen_pair_ms=round((ms[best[0]] + ms[best[1]]) / 2, 3))
     del pools
     torch.cuda.empty_cache()
     return a, b, report

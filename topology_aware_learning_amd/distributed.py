@@ -83,17 +83,58 @@ def build_shard(orders: Sequence[Sequence[int]], weights: Sequence[Sequence[floa
     return spec
 
 
-def post_exchange(spec: ShardSpec, tensors: Sequence[torch.Tensor], group=None) -> list:
+def recv_range(spec: ShardSpec, peer: int):
+    """The halo rows `peer` fills: one contiguous block of local rows (the halo is grouped by
+    owner, ascending global id on both sides), or None."""
+    rows = spec.recv.get(peer)
+    if not rows:
+        return None
+    r0, r1 = rows[0], rows[-1] + 1
+    if r1 - r0 != len(rows):
+        raise AssertionError("halo rows of one peer are not contiguous")
+    return r0, r1
+
+
+class HaloPacker:
+    """Per-peer send buffers of one pool tensor: the rows a peer needs, in its receive order,
+    as ONE contiguous [k, ld] tensor, so a round moves one message per peer per segment
+    (instead of one per model row).  Rows that are already consecutive in the pool are sent as
+    a view (no copy); otherwise they are gathered into a buffer allocated once."""
+
+    def __init__(self, spec: ShardSpec, t: torch.Tensor):
+        self.spec = spec
+        self.bufs: Dict[int, torch.Tensor] = {}
+        self.idx: Dict[int, torch.Tensor] = {}
+        for peer, rows in spec.send.items():
+            if rows == list(range(rows[0], rows[0] + len(rows))):
+                continue  # consecutive: sent as t[r0:r1]
+            self.idx[peer] = torch.as_tensor(rows, dtype=torch.long, device=t.device)
+            self.bufs[peer] = torch.empty((len(rows), t.shape[1]), dtype=t.dtype, device=t.device)
+
+    def send_tensor(self, t: torch.Tensor, peer: int) -> torch.Tensor:
+        """The message for `peer` from pool tensor t (gathers on the current stream)."""
+        rows = self.spec.send[peer]
+        if peer not in self.idx:
+            return t[rows[0]: rows[0] + len(rows)]
+        return torch.index_select(t, 0, self.idx[peer], out=self.bufs[peer])
+
+
+def post_exchange(spec: ShardSpec, tensors: Sequence[torch.Tensor], group=None,
+                  packers: Optional[Sequence[HaloPacker]] = None) -> list:
     """Post the halo sends/receives of one round for each [rows, ld] pool tensor; returns the
-    requests (wait on them before reading halo rows).  One P2P group: RCCL batches it into a
-    single ncclGroupStart/End."""
+    requests (wait on them before reading halo rows).  One message per peer per segment each
+    way (HaloPacker), all in one P2P group: RCCL batches it into a single
+    ncclGroupStart / ncclSend+ncclRecv per peer / ncclGroupEnd."""
+    if packers is None:
+        packers = [HaloPacker(spec, t) for t in tensors]
     p2p = []
     for peer in sorted(set(spec.send) | set(spec.recv)):
-        for t in tensors:
-            for r in spec.send.get(peer, []):
-                p2p.append(dist.P2POp(dist.isend, t[r], peer, group=group))
-            for r in spec.recv.get(peer, []):
-                p2p.append(dist.P2POp(dist.irecv, t[r], peer, group=group))
+        for t, pk in zip(tensors, packers):
+            if peer in spec.send:
+                p2p.append(dist.P2POp(dist.isend, pk.send_tensor(t, peer), peer, group=group))
+            rr = recv_range(spec, peer)
+            if rr is not None:
+                p2p.append(dist.P2POp(dist.irecv, t[rr[0]: rr[1]], peer, group=group))
     if not p2p:
         return []
     return dist.batch_isend_irecv(p2p)
@@ -163,18 +204,23 @@ class _StagedRequests:
         self.reqs, self.fills = [], []
 
 
-def post_exchange_staged(spec: ShardSpec, tensors: Sequence[torch.Tensor], group=None) -> list:
+def post_exchange_staged(spec: ShardSpec, tensors: Sequence[torch.Tensor], group=None,
+                         packers: Optional[Sequence[HaloPacker]] = None) -> list:
     """post_exchange through host memory, for process groups without device transport (gloo):
-    rehearses the multi-GPU path with several ranks on one GPU.  Not a production path."""
+    rehearses the multi-GPU path (same packed per-peer messages) with several ranks on one GPU.
+    Not a production path."""
+    if packers is None:
+        packers = [HaloPacker(spec, t) for t in tensors]
     p2p, fills = [], []
     for peer in sorted(set(spec.send) | set(spec.recv)):
-        for t in tensors:
-            for r in spec.send.get(peer, []):
-                p2p.append(dist.P2POp(dist.isend, t[r].cpu(), peer, group=group))
-            for r in spec.recv.get(peer, []):
-                buf = torch.empty(t.shape[1], dtype=t.dtype)
+        for t, pk in zip(tensors, packers):
+            if peer in spec.send:
+                p2p.append(dist.P2POp(dist.isend, pk.send_tensor(t, peer).cpu(), peer, group=group))
+            rr = recv_range(spec, peer)
+            if rr is not None:
+                buf = torch.empty((rr[1] - rr[0], t.shape[1]), dtype=t.dtype)
                 p2p.append(dist.P2POp(dist.irecv, buf, peer, group=group))
-                fills.append((t[r], buf))
+                fills.append((t[rr[0]: rr[1]], buf))
     if not p2p:
         return []
     return [_StagedRequests(dist.batch_isend_irecv(p2p), fills)]
@@ -194,11 +240,14 @@ class ShardedRound:
         # exchange(self) -> requests; default: RCCL/gloo P2P.  Tests may pass an in-process copy.
         # transport "host": the exchange is staged through host memory (gloo rehearsal runs)
         post = post_exchange_staged if transport == "host" else post_exchange
-        self._exchange = exchange or (lambda sr: post(sr.spec, [t for _, t, _ in sr.pool_a.segments()], sr.group))
+        self._exchange = exchange or (lambda sr: post(sr.spec, [t for _, t, _ in sr.pool_a.segments()], sr.group,
+                                                      sr.packers))
         owner = partition_contiguous(len(orders), world) if owner is None else np.asarray(owner, np.int32)
         self.spec = build_shard(orders, weights, owner, rank, world)
         self.pool_a = ModelPool(layout, self.spec.rows, self.device)
         self.pool_b = ModelPool(layout, self.spec.rows, self.device)
+        # one packer per segment serves both pools (same shape; the row lists do not change)
+        self.packers = [HaloPacker(self.spec, t) for _, t, _ in self.pool_a.segments()]
         self.plans = {}
         tg = tune_segment(layout)
         for name, idx in (("interior", self.spec.interior), ("boundary", self.spec.boundary)):
@@ -209,7 +258,7 @@ class ShardedRound:
                 self.plans[name] = (
                     ops.tune_plan(rp, col, w, out, _pool_segs(self.pool_a)[tg], _pool_segs(self.pool_b)[tg],
                                   n=getattr(layout, "n_" + tg), mode=mode)
-                    if tune else ops.build_plan(rp, col, w, out, dense=0 if layout.n_b16 else -1).to(self.device))
+                    if tune else ops.default_plan(rp, col, w, out, bf16=bool(layout.n_b16)).to(self.device))
         if exchange is None and dist.is_available() and dist.is_initialized():
             # a collective over the whole group first: RCCL then builds the communicator with
             # every rank, so the first batched P2P does not depend on which ranks have halos

@@ -119,7 +119,7 @@ class RoundPlan:
         return int(self.info.total_src)
 
 
-def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0, dense: int = -1) -> RoundPlan:
+def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0, dense: int = 0) -> RoundPlan:
     """Tile plan for a round given as CSR (row r: operands col[row_ptr[r]:row_ptr[r+1]] with
     float64 weights w, written to pool row out_row[r]).
 
@@ -130,8 +130,10 @@ def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0, dense:
       LDS  = 4 B x operands (one LDS read per operand)         at ~150 TB/s x eff(workgroups/CU)
     (eff = 0.33 / 0.6 / 0.8 for 1 / 2 / >= 3 resident workgroups, halved at c4 = 64; fitted to
     tools/tune/round_variants.hip on MI355X); ties go to more resident workgroups.
-    dense: -1 lets the library pick the dense row-block form by density (rows that use a large
-    share of their group's sources: cliques), 0 forces the sparse form, 8 requests dense."""
+    dense: 0 (default) = the sparse form; 8 requests dense row blocks; -1 lets the library
+    pick dense when one LDS read serves >= 4 operands on average.  The dense form lost every
+    measured A/B outside cliques (config 3: 6.2 vs 2.45 ms, config 5: 171 vs 83 ms; round-1
+    tuner candidates), and clique rounds take the K3c plan (default_plan)."""
     row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int32)
     col = np.ascontiguousarray(col, dtype=np.int32)
     w = np.ascontiguousarray(w, dtype=np.float64)
@@ -161,7 +163,8 @@ def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0, dense:
         if rc != _lib.TAL_OK:
             last_err = _lib.TalError(rc, L.tal_last_error().decode())
             continue
-        plan = RoundPlan(info=info, host=blob[: info.words].copy(), rows=rows, nnz=len(col))
+        plan = RoundPlan(info=info, host=blob[: info.words].copy(), rows=rows, nnz=len(col),
+                         spec=dict(c4=int(cand), lds=int(budget), dense=int(dense)))
         key = (_plan_cost(plan.info), -_blocks_per_cu(plan.info))
         if best is None or key < best[0]:
             best = (key, plan)
@@ -403,7 +406,7 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
                 cp.spec["rest"] = cp.rest.spec
             cands.append((("clique", cp.n_cliques, cp.staged_rows(), 0, cp.mmax, 0), cp))
     if not cands:
-        return build_plan(row_ptr, col, w, out_row, dense=0 if bf16 else -1)
+        return build_plan(row_ptr, col, w, out_row, dense=0)
     if len(cands) == 1:
         return cands[0][1].to(pool_in.device)
     best, best_t = None, None
@@ -445,6 +448,20 @@ def plan_from_spec(row_ptr, col, w, out_row, spec: dict) -> RoundPlan:
                        dense=int(spec["dense"]))
     p.spec = dict(spec)
     return p
+
+
+def default_plan(row_ptr, col, w, out_row, bf16: bool = False):
+    """The plan the round components build when they do not time candidates (tune=False):
+    the round's uniform-weight clique blocks by K3c when it has any (fp32 pools; the other rows
+    by their own sparse plan), else build_plan's sparse form at the tile width and LDS budget
+    its cost model picks.  On the round-1 A/B tables this is the measured winner's form for
+    configs 2-5 (tests/test_host_logic.py::test_default_plan_forms)."""
+    if not bf16:
+        cp = build_clique_plan(row_ptr, col, w, out_row)
+        if cp is not None:
+            cp.spec = dict(clique=1, rest=cp.rest.spec if cp.rest is not None else None)
+            return cp
+    return build_plan(row_ptr, col, w, out_row, dense=0)
 
 
 def round_kernel_name(plan) -> str:

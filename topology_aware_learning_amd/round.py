@@ -84,8 +84,8 @@ class RoundExecutor:
         p = self._plans.get(key)
         if p is None:
             row_ptr, col, w = csr_from_lists(orders, weights)
-            dense = 0 if self.pool.layout.n_b16 else -1  # bf16 rounds take sparse / narrow plans
-            p = ops.build_plan(row_ptr, col, w, np.asarray(out_rows, np.int32), dense=dense).to(self.pool.device)
+            p = ops.default_plan(row_ptr, col, w, np.asarray(out_rows, np.int32),
+                                 bf16=bool(self.pool.layout.n_b16)).to(self.pool.device)
             if len(self._plans) > 64:
                 self._plans.clear()
             self._plans[key] = p

@@ -213,3 +213,21 @@ def param_names(layout: Layout, buffers: Iterable[str] = ("running_mean", "runni
     """Entries that are nn.Parameters (named_parameters order = state_dict order minus buffers)."""
     bufs = tuple(buffers)
     return [n for n, _, _ in layout if not n.endswith(bufs)]
+
+
+def truncate_layout(layout: Layout, max_float: int) -> Layout:
+    """The layout's leading float entries up to `max_float` elements in all (the entry that
+    crosses the budget is cut to a flat remainder), every int64 entry kept: a reduced model of
+    the same segment structure for multi-rank rehearsals (bench.py --max-params)."""
+    out: Layout = []
+    left = int(max_float)
+    for name, shape, dt in layout:
+        if dt == "int64":
+            out.append((name, shape, dt))
+            continue
+        if left <= 0:
+            continue
+        n = numel(shape)
+        out.append((name, shape, dt) if n <= left else (name, (left,), dt))
+        left -= min(n, left)
+    return out
