@@ -14,6 +14,8 @@ Outputs (all data, no reference source):
   centrality.json                    reference centrality dicts for those graphs
   schedulers.json                    softmax_coeff sequences of every scheduler (100 rounds)
   round_4ring.npz / .json            sequential in-place round driven through the reference
+  big_round_resnet18_ring32.json     BASELINE config 2 at full size: a snapshot round's outputs
+                                     (sha256 per output model)
 
 Usage:  python tests/golden/make_golden.py
 """
@@ -221,6 +223,36 @@ def gen_big(dc, resnet, out):
                                    cases=results), indent=1))
 
 
+def gen_big_round(dc, resnet, out):
+    """BASELINE config 2 at full size: one snapshot round of the 32-ring with ResNet-18 (M = 3,
+    unweighted).  Each device's call runs the reference app on fresh copies of the pre-round
+    models, so every aggregation reads the snapshot; per output model the sha256 of its fp32
+    entries and of its int64 entries, each concatenated in state_dict order."""
+    n = 32
+    g = nx.cycle_graph(n)
+    layout = synth.layout_of(resnet.ResNet18().state_dict())
+    seeds = [9100 + i for i in range(n)]
+    pre = [synth.synth_state_dict(layout, s) for s in seeds]
+    rows = []
+    for i in range(n):
+        order = sorted(g.neighbors(i)) + [i]
+        clients = []
+        for idx in order:
+            m = resnet.ResNet18()
+            m.load_state_dict(pre[idx])
+            clients.append((["r"], make_client(dc, idx, m)))
+        res = dc.unweighted_module_avg(clients[-1], 0, *clients)
+        sd = sd_np(res[1].model)
+        f32 = np.concatenate([v.reshape(-1) for v in sd.values() if v.dtype == np.float32])
+        i64 = np.concatenate([v.reshape(-1) for v in sd.values() if v.dtype == np.int64])
+        rows.append(dict(order=order, sha256_f32=sha(f32), sha256_i64=sha(i64),
+                         f32_head=[float(x) for x in f32[:3]]))
+    out.write_text(json.dumps(dict(model="resnet18", graph="cycle_graph(32)", fn="unweighted_module_avg",
+                                   seeds=seeds, semantics="snapshot (every call reads the pre-round models)",
+                                   rows=rows), indent=1))
+    print("big round: resnet18 32-ring snapshot")
+
+
 def gen_weights(dc, out_w, out_c):
     graphs = {
         "cycle_graph(8)": nx.cycle_graph(8),
@@ -387,7 +419,7 @@ def gen_bf16(dc, out_json, out_npz):
     print(f"bf16: {len(cases)} cases")
 
 
-GENERATORS = ("layouts", "tiny", "weights", "schedulers", "round", "big", "gossip", "bf16")
+GENERATORS = ("layouts", "tiny", "weights", "schedulers", "round", "big", "gossip", "bf16", "big_round")
 
 
 def main(which=GENERATORS):
@@ -408,6 +440,8 @@ def main(which=GENERATORS):
         gen_gossip(HERE / "gossip.json")
     if "bf16" in which:
         gen_bf16(dc, HERE / "bf16_cases.json", HERE / "bf16_cases.npz")
+    if "big_round" in which:
+        gen_big_round(dc, resnet, HERE / "big_round_resnet18_ring32.json")
 
 
 if __name__ == "__main__":

@@ -77,3 +77,26 @@ def test_load_checkpoint_into_bound_pool(tmp_path):
     for c, c2 in zip(cl, cl2):  # client k restored into its own (different) row
         _check_same(c.model.state_dict(), c2.model.state_dict())
         assert common_pool([c2.model]) is not None  # still bound: the pool rows were written
+
+
+def test_bound_row_tracks_rebinding():
+    """row_of: a bound module stays bound while every state entry is its row view; param.data
+    assignment, a re-registered buffer or module.to() copies unbind it (checked per entry
+    through the tables kept at bind time)."""
+    from topology_aware_learning_amd.arena import bound_row
+
+    cl, pool = _bound([0, 1])
+    m = cl[0].model
+    assert bound_row(m) == (pool, 0) and pool.row_of(cl[1].model) == 1
+    m.fc.weight.data = m.fc.weight.data.clone()
+    assert bound_row(m) is None
+    pool.bind(m, 0)
+    assert bound_row(m) == (pool, 0)
+    m.bn.running_mean = m.bn.running_mean.clone()
+    assert bound_row(m) is None
+    pool.bind(m, 0)
+    m.bn2.num_batches_tracked = m.bn2.num_batches_tracked.clone()
+    assert bound_row(m) is None
+    pool.bind(m, 0)
+    m.to(torch.float64)
+    assert bound_row(m) is None

@@ -583,3 +583,29 @@ def test_round_clique_attached_rows_general(cuda, n):
     for r in (rows - 2, rows - 1, 3):
         ops.agg_f32([pin[j] for j in orders[r]], ws[r], chk, mode=ops.MODE_FMA)
         assert torch.equal(chk.view(torch.int32), pout[r].view(torch.int32))
+
+
+@pytest.mark.parametrize("spec", [None, {"c4": 128, "lds": 81920, "dense": 0}, {"c4": 64, "lds": 81920, "dense": 0},
+                                  {"c4": 32, "lds": 81920, "dense": 0}, {"c4": 16, "lds": 81920, "dense": 0}])
+def test_full_size_ring32_round_vs_reference(cuda, spec):
+    """BASELINE config 2 at full size (32-ring, ResNet-18, M = 3): one K3 round over the
+    device pool equals the REFERENCE's outputs (sha256 per output model, generated by its own
+    unweighted_module_avg; tests/golden/make_golden.py big_round) for every plan form the tuner
+    can pick (None = default_plan)."""
+    from test_oracle_golden import RING32, ring32_pools
+
+    f, i = ring32_pools()
+    orders = [r["order"] for r in RING32["rows"]]
+    rp, col, w = ra.round_csr(orders, [ra.unweighted_weights(len(o)) for o in orders])
+    out_rows = np.arange(32, dtype=np.int32)
+    plan = ops.default_plan(rp, col, w, out_rows) if spec is None else ops.plan_from_spec(rp, col, w, out_rows, spec)
+    pin = torch.from_numpy(f).to(cuda)
+    pout = torch.empty_like(pin)
+    iin = torch.from_numpy(i).to(cuda)
+    iout = torch.empty_like(iin)
+    ops.round_f32(pin, pout, plan)
+    ops.round_i64(iin, iout, plan)
+    got, igot = pout.cpu().numpy(), iout.cpu().numpy()
+    for r, row in enumerate(RING32["rows"]):
+        assert hashlib.sha256(got[r].tobytes()).hexdigest() == row["sha256_f32"], r
+        assert hashlib.sha256(igot[r].tobytes()).hexdigest() == row["sha256_i64"], r

@@ -1,5 +1,6 @@
 """Pin the oracle (C restatement + numpy host logic + torch CPU port) against golden vectors
 generated from the reference itself (tests/golden/make_golden.py).  CPU only."""
+import functools
 import hashlib
 import json
 
@@ -194,3 +195,34 @@ def test_c_oracle_full_size_sha256(idx):
         xs = [sd[name].numpy().reshape(-1) for sd in sds]
         out = oracle.agg_f32(xs, w) if dt == "float32" else oracle.agg_i64(xs, w)
         assert hashlib.sha256(out.tobytes()).hexdigest() == case["sha256"][name], name
+
+
+RING32 = json.loads((GOLDEN / "big_round_resnet18_ring32.json").read_text())
+
+
+@functools.lru_cache(maxsize=1)
+def ring32_pools():
+    """BASELINE config 2's inputs at full size (ResNet-18, 32 devices): [32, n] fp32 / int64
+    pools, each row the model's entries of that dtype concatenated in state_dict order."""
+    from topology_aware_learning_amd import synth
+
+    lay = [(n, tuple(s), d) for n, s, d in json.loads((GOLDEN / "layouts.json").read_text())["resnet18"]]
+    f, i = [], []
+    for seed in RING32["seeds"]:
+        sd = synth.synth_state_dict(lay, seed)
+        f.append(np.concatenate([v.reshape(-1).numpy() for v in sd.values() if v.dtype == torch.float32]))
+        i.append(np.concatenate([v.reshape(-1).numpy() for v in sd.values() if v.dtype == torch.int64]))
+    return np.stack(f), np.stack(i)
+
+
+def test_oracle_full_size_ring32_round():
+    """The C oracle's snapshot round over BASELINE config 2 at full size (32 x 11.2 M params)
+    reproduces the reference's outputs (sha256 per output model, make_golden.py big_round)."""
+    f, i = ring32_pools()
+    orders = [r["order"] for r in RING32["rows"]]
+    rp, col, w = ra.round_csr(orders, [ra.unweighted_weights(len(o)) for o in orders])
+    out = oracle.round_f32(f, rp, col, w, np.arange(32))
+    iout = oracle.round_i64(i, rp, col, w, np.arange(32))
+    for r, row in enumerate(RING32["rows"]):
+        assert hashlib.sha256(out[r].tobytes()).hexdigest() == row["sha256_f32"], r
+        assert hashlib.sha256(iout[r].tobytes()).hexdigest() == row["sha256_i64"], r

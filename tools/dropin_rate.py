@@ -1,0 +1,124 @@
+"""Drop-in path rate (not part of the product): BASELINE config 3 (64 devices, random 8-regular
+graph, ResNet-50, unweighted) through the reference call surface, i.e. the round driver
+src/decentralized_app.py with its clients' models bound to the device pool:
+
+  per_call   the default: one unweighted_module_avg app call per client (64 per round) on
+             the 2-thread app pool, each a K1 launch (the reference's form)
+  batched    TAL_BATCHED_ROUND=1: the round's 64 aggregations as one RoundExecutor.run (K3)
+
+Training is replaced by a no-op app (the model as it stands) so a round is the driver's own
+Python plus the aggregation.  Also
+times RoundExecutor(pool).run directly on the round (its default plan, in place) against the
+bench's K1 floor (64 x one K1 call).  One JSON line per measurement.
+
+usage: python tools/dropin_rate.py [rounds]"""
+import json
+import os
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+os.environ.setdefault("TAL_SYNTHETIC_DATA", "1")
+os.environ.setdefault("TAL_SYNTHETIC_SAMPLES", "64")
+
+import networkx as nx  # noqa: E402
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    from src.decentralized_app import DecentrallearnApp
+    from topology_aware_learning_amd import ops
+    from topology_aware_learning_amd.round import RoundExecutor
+
+    import src.decentralized_app as da
+    from src._parsl_compat import python_app
+
+    @python_app(executors=["decentral_train"])
+    def no_train(future, *args):  # training is outside the measured path: the model as trained
+        return [], future[1]
+
+    da.local_train = da.no_local_train = no_train
+    tmp = Path(tempfile.mkdtemp())
+    topo = tmp / "random64.txt"
+    np.savetxt(topo, nx.to_numpy_array(nx.random_regular_graph(8, 64, seed=0)), fmt="%d")
+    t0 = time.perf_counter()
+    app = DecentrallearnApp(dataset="cifar10_resnet50", topology_path=str(topo), epochs=1, rounds=10 ** 6,
+                            aggregation_strategy="unweighted", log_dir=str(tmp / "logs"), batch_size=32)
+    print(json.dumps(dict(setup_s=round(time.perf_counter() - t0, 1), clients=len(app.clients),
+                          params=sum(v.numel() for v in app.clients[0].model.state_dict().values()))), flush=True)
+    dev = app.pool.device
+    app.round_states = {0: {i: {"agg": ([{}], app.clients[i])} for i in range(len(app.clients))}}
+    r = 0
+    for mode in ("per_call", "batched", "per_call", "batched"):
+        app.batched_round = mode == "batched"
+        ts = []
+        for k in range(rounds + 1):
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            futs = app._federated_round(r)
+            for f in futs:
+                f.result()
+            torch.cuda.synchronize(dev)
+            if k:  # the first round of each mode warms up (plan build, app pool threads)
+                ts.append(time.perf_counter() - t)
+            app.round_states.pop(r, None)
+            r += 1
+        ms = 1e3 * float(np.median(ts))
+        print(json.dumps(dict(mode=mode, rounds=len(ts), ms_per_round_median=round(ms, 3),
+                              ms_per_round_all=[round(1e3 * x, 3) for x in ts],
+                              params_per_s=64 * 23_574_015 / (ms * 1e-3))), flush=True)
+    # the K1 floor: one aggregation call per client with nothing around it
+    pool = app.pool
+    orders = [sorted(c.neighbors) + [c.idx] for c in app.clients]
+    ws = [[1 / len(o)] * len(o) for o in orders]
+    out = torch.empty(pool.layout.n_f32, device=dev)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(3):
+        ops.agg_f32([pool.row_f32(j) for j in orders[0]], ws[0], out)
+    s.record()
+    for o, w in zip(orders, ws):
+        ops.agg_f32([pool.row_f32(j) for j in o], w, out)
+    e.record()
+    e.synchronize()
+    k1 = s.elapsed_time(e)
+    print(json.dumps(dict(k1_floor_ms_per_round=round(k1, 3), k1_ms_per_call=round(k1 / 64, 4))), flush=True)
+    # RoundExecutor.run on the whole round (default plan; single group -> in place on the pool)
+    ex = RoundExecutor(pool)
+    ex.run(orders, ws)
+    ts = []
+    for _ in range(10):
+        s.record()
+        ex.run(orders, ws)
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e))
+    p = ex.plan(orders, ws, list(range(64)))
+    print(json.dumps(dict(round_executor_ms=round(float(np.median(ts)), 3), plan=p.spec,
+                          kernel=ops.round_kernel_name(p), in_place=bool(p.single_group))), flush=True)
+    # the same round out of place into a scratch pool: default plan vs the tuner's pick (bench)
+    from topology_aware_learning_amd.arena import ModelPool
+    from topology_aware_learning_amd.round import csr_from_lists
+
+    scratch = ModelPool(pool.layout, 64, dev)
+    rp, col, w = csr_from_lists(orders, ws)
+    rows = np.arange(64, dtype=np.int32)
+    tuned = ops.tune_plan(rp, col, w, rows, pool.f32, scratch.f32, n=pool.layout.n_f32)
+    for name, plan in (("default", ops.default_plan(rp, col, w, rows).to(dev)), ("tuned", tuned)):
+        ts = []
+        for _ in range(12):
+            s.record()
+            ops.round_f32(pool.f32, scratch.f32, plan, n=pool.layout.n_f32)
+            e.record()
+            e.synchronize()
+            ts.append(s.elapsed_time(e))
+        print(json.dumps(dict(out_of_place=name, ms=round(float(np.median(ts[2:])), 3), spec=plan.spec,
+                              kernel=ops.round_kernel_name(plan))), flush=True)
+
+
+if __name__ == "__main__":
+    main()

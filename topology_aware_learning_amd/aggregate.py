@@ -128,14 +128,20 @@ def aggregate_models(operands: Sequence[nn.Module], weights: Sequence[float], ta
         raise ValueError("no operands")
     if len(weights) != len(operands):
         raise ValueError("one weight per operand is required")
-    layout = layout_of_module(target)
-    device = _device_for(list(operands) + [target])
+    # pool-bound models are checked once each (bound_row: every entry still a view of its
+    # row); the target's pool then gives the layout without rebuilding its state_dict
+    tb = bound_row(target)
+    bounds = [bound_row(m) for m in operands]
+    layout = tb[0].layout if tb is not None else layout_of_module(target)
+    device = next((b[0].device for b in [tb, *bounds] if b is not None), None)
+    if device is None:
+        device = _device_for(list(operands) + [target])
     sizes = {g: n for g, n in _seg_sizes(layout).items() if n}
 
     ptrs: dict = {g: [None] * len(operands) for g in sizes}
     unbound = []
     for j, m in enumerate(operands):
-        b = bound_row(m)
+        b = bounds[j]
         if b is not None and b[0].device == device and b[0].layout == layout:
             pool, r = b
             rows = {"f32": pool.row_f32, "b16": pool.row_b16, "i64": pool.row_i64}
@@ -149,7 +155,6 @@ def aggregate_models(operands: Sequence[nn.Module], weights: Sequence[float], ta
             for g in sizes:
                 ptrs[g][j] = staged[g][k]
 
-    tb = bound_row(target)
     if tb is not None and tb[0].device == device and tb[0].layout == layout:
         rows = {"f32": tb[0].row_f32, "b16": tb[0].row_b16, "i64": tb[0].row_i64}
         outs = {g: rows[g](tb[1]) for g in sizes}
