@@ -218,28 +218,32 @@ int32_t tal_agg_round_bf16(const uint16_t* pool_in, int64_t ld_in, uint16_t* poo
                            int64_t ld_out, int64_t n, const int32_t* plan_dev,
                            const tal_round_plan_info* info, int32_t mode, void* stream);
 
-/* ---- K2: cosine similarity of two models' parameters --------------------------------------
+/* ---- K2: cosine similarity of two models' parameters, bit for bit -------------------------
  * Reference: cosine_similarity, decentralized_client.py:661-681: for each parameter tensor
  * viewed as [A, I, B] (dim 1 = the reduced dim; 1-D tensors are unsqueezed to [n, 1]),
  * nn.CosineSimilarity(dim=1, eps=1e-6) gives A*B values whose mean is taken; the result is
- * the average of those means over tensors.
+ * the average of those means over tensors.  Every fp32 operation is the reference's, in the
+ * order of the torch CPU kernels it runs on (vector_norm, the cascade sum, sum / numel; see
+ * oracle/cosine_oracle.c, pinned bitwise by the reference's own values, near-ties included):
+ * the result is the reference's fp32 value, so sim_centrality_module_avg's least-similar
+ * neighbor (:511-516) is the reference's.  Tensors whose A*B exceeds 32768 are reduced in
+ * torch's serial order (torch's own order there depends on its thread count).
  *
  * seg_host: 4*n_seg int64 {offset (elements into the flat parameter arena), A, I, B}.
- * The host cuts the segments into workgroup chunks (plan, int64 words, copied to the device
- * by the caller); each chunk is either "row" work (B == 1, I > 1: one wavefront per output,
- * lanes stride the contiguous row and reduce with cross-lane shuffles) or "column" work
- * (one lane per output).  One pass reads each model once (dot, |a|^2, |b|^2 fused).
+ * The plan (int64 words, tal_cosine_plan_words; copied to the device by the caller, and the
+ * host copy passed too) = {n_seg, n_outputs}, per tensor {offset, A, I, B, first output,
+ * kind}, per workgroup chunk {tensor, first output, count, 0}.
  *
  * a_ptrs_host / b_ptrs_host: n_pairs device pointers; pair j compares model a_j with b_j
  * (flat fp32 parameter arenas of the same layout).  scratch: device buffer of at least
- * tal_cosine_scratch_bytes(n_chunks, n_pairs) bytes.  out_dev: n_pairs fp32 results. */
+ * tal_cosine_scratch_bytes(plan_host, n_pairs) bytes.  out_dev: n_pairs fp32 results. */
 int64_t tal_cosine_plan_words(const int64_t* seg_host, int32_t n_seg);
 int32_t tal_cosine_plan_build(const int64_t* seg_host, int32_t n_seg, int64_t* plan_host,
                               int64_t plan_capacity_words, int32_t* n_chunks);
-int64_t tal_cosine_scratch_bytes(int32_t n_chunks, int32_t n_pairs);
+int64_t tal_cosine_scratch_bytes(const int64_t* plan_host, int32_t n_pairs);
 int32_t tal_cosine_params(const float* const* a_ptrs_host, const float* const* b_ptrs_host,
-                          int32_t n_pairs, const int64_t* plan_dev, int32_t n_chunks,
-                          int32_t n_seg, void* scratch, float* out_dev, void* stream);
+                          int32_t n_pairs, const int64_t* plan_dev, const int64_t* plan_host,
+                          int32_t n_chunks, void* scratch, float* out_dev, void* stream);
 
 /* ---- FedProx proximal term ------------------------------------------------
  * Reference: local_train, tasks.py:277-286: loss += (prox_coeff / 2) * sum_t sum_p

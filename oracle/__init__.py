@@ -5,6 +5,8 @@ and only as the checker / the timed CPU baseline: the product (topology_aware_le
 src/) never imports it and has no CPU fallback.
 
 Contents
+  cosine_oracle.c          the reference's model cosine similarity in torch's exact CPU
+                           reduction order (`cosine_model`, bitwise; decentralized_client.py:661-681)
   agg_oracle.c / Makefile  plain-C restatement of the reference arithmetic
                            (src/decentralized_client.py:399-413) — `agg_f32`, `agg_i64`,
                            `round_f32`, `round_i64`, and for bf16 tensors `agg_bf16`,
@@ -40,8 +42,8 @@ _lib = None
 def lib() -> ctypes.CDLL:
     global _lib
     if _lib is None:
-        src = HERE / "agg_oracle.c"
-        if not LIB.exists() or LIB.stat().st_mtime < src.stat().st_mtime:
+        srcs = [HERE / "agg_oracle.c", HERE / "cosine_oracle.c"]
+        if not LIB.exists() or any(LIB.stat().st_mtime < s.stat().st_mtime for s in srcs):
             build()
         L = ctypes.CDLL(str(LIB))
         P = ctypes.c_void_p
@@ -53,6 +55,10 @@ def lib() -> ctypes.CDLL:
         L.oracle_agg_bf16.argtypes = [P, P, ctypes.c_int32, P, ctypes.c_int64, ctypes.c_int32]
         L.oracle_round_bf16.argtypes = rargs + [ctypes.c_int32]
         L.oracle_f32_to_bf16.argtypes = [P, P, ctypes.c_int64]
+        L.oracle_cosine_scratch.argtypes = [P, ctypes.c_int32]
+        L.oracle_cosine_scratch.restype = ctypes.c_int64
+        L.oracle_cosine_model.argtypes = [P, P, P, ctypes.c_int32, P, P]
+        L.oracle_cosine_model.restype = ctypes.c_float
         _lib = L
     return _lib
 
@@ -143,3 +149,19 @@ def round_bf16(pool_in, row_ptr, col, w, out_row, pool_out=None, exact: bool = T
                             pool_in.shape[1], len(out_row), row_ptr.ctypes.data, col.ctypes.data, w.ctypes.data,
                             out_row.ctypes.data, int(bool(exact)))
     return pool_out
+
+
+def cosine_model(a, b, segments, per_tensor: bool = False):
+    """The reference's cosine_similarity(model_1, model_2) of two flat fp32 parameter rows,
+    bit for bit (torch's CPU reduction order; cosine_oracle.c).  segments: (offset, A, I, B)
+    per parameter in named_parameters order (arena.StateLayout.param_segments)."""
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    b = np.ascontiguousarray(b, dtype=np.float32)
+    seg = np.ascontiguousarray(np.asarray(segments, dtype=np.int64).reshape(-1, 4))
+    L = lib()
+    scratch = np.empty(max(1, L.oracle_cosine_scratch(seg.ctypes.data, len(seg))), np.float32)
+    per = np.empty(len(seg), np.float32)
+    v = L.oracle_cosine_model(a.ctypes.data, b.ctypes.data, seg.ctypes.data, len(seg), scratch.ctypes.data,
+                              per.ctypes.data)
+    v = np.float32(v)
+    return (v, per) if per_tensor else v

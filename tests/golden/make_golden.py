@@ -14,6 +14,9 @@ Outputs (all data, no reference source):
   centrality.json                    reference centrality dicts for those graphs
   schedulers.json                    softmax_coeff sequences of every scheduler (100 rounds)
   round_4ring.npz / .json            sequential in-place round driven through the reference
+  near_ties.json / .npz              sim_centrality_module_avg where two neighbors' similarities
+                                     tie in fp32, are 1-4 ulp apart, or order differently in
+                                     fp32 than in exact arithmetic
   big_round_resnet18_ring32.json     BASELINE config 2 at full size: a snapshot round's outputs
                                      (sha256 per output model)
 
@@ -165,6 +168,92 @@ def gen_tiny(dc, out_json, out_npz):
     out_json.write_text(json.dumps(meta, indent=1))
     np.savez_compressed(out_npz, **arrays)
     print(f"tiny: {len(cases)} cases")
+
+
+def _cos64(m1, m2):
+    """float64 value of the reference's similarity formula (what a near-exact kernel returns)."""
+    tot = 0.0
+    ps1 = [p.detach().double().numpy() for p in m1.parameters()]
+    ps2 = [p.detach().double().numpy() for p in m2.parameters()]
+    for a, b in zip(ps1, ps2):
+        if a.ndim < 2:
+            a, b = a[:, None], b[:, None]
+        n1 = np.maximum(np.sqrt((a * a).sum(1, keepdims=True)), 1e-6)
+        n2 = np.maximum(np.sqrt((b * b).sum(1, keepdims=True)), 1e-6)
+        tot += ((a / n1) * (b / n2)).sum(1).mean()
+    return tot / len(ps1)
+
+
+def gen_near_ties(dc, out_json, out_npz):
+    """sim_centrality_module_avg on near-ties: two neighbors whose similarities to the client
+    are equal in fp32, or 1-4 ulp apart, or ordered differently in fp32 than in exact
+    arithmetic; their centralities lie on opposite sides of the client's, so the least-similar
+    pick decides the softmax sign and with it every output bit (reference :509-516)."""
+    torch.manual_seed(0)
+    layout = synth.layout_of(TinyNet().state_dict())
+    rng = np.random.default_rng(77)
+    base_c = synth.synth_state_dict(layout, 50000)
+    noise = synth.synth_state_dict(layout, 50003)
+    far = synth.synth_state_dict(layout, 50001)
+    base_1 = {k: (v + 0.3 * far[k]) if v.dtype == torch.float32 else v.clone() for k, v in base_c.items()}
+    base_3 = {k: (v + 0.05 * noise[k]) if v.dtype == torch.float32 else v.clone() for k, v in base_c.items()}
+    fkeys = [k for k, v in base_1.items() if v.dtype == torch.float32 and not k.endswith(("running_mean", "running_var"))]
+    want = {"tie": 6, "flip": 6, "close": 4}
+    got = {k: 0 for k in want}
+    cases, arrays = [], {}
+    for trial in range(20000):
+        if all(got[k] >= want[k] for k in want):
+            break
+        sd2 = {k: v.clone() for k, v in base_1.items()}
+        for _ in range(int(rng.integers(1, 4))):  # relative nudges from 1e-7 to 1e-3
+            k = fkeys[int(rng.integers(len(fkeys)))]
+            flat = sd2[k].view(-1).numpy()
+            i = int(rng.integers(flat.size))
+            flat[i] = np.float32(flat[i] * (1.0 + rng.choice([-1.0, 1.0]) * 10.0 ** rng.uniform(-7, -3)))
+        ms = {}
+        for name, sd in (("c", base_c), ("n1", base_1), ("n2", sd2), ("n3", base_3)):
+            m = TinyNet()
+            m.load_state_dict(sd)
+            ms[name] = m
+        s1 = np.float32(dc.cosine_similarity(ms["c"], ms["n1"]).item())
+        s2 = np.float32(dc.cosine_similarity(ms["c"], ms["n2"]).item())
+        e1, e2 = _cos64(ms["c"], ms["n1"]), _cos64(ms["c"], ms["n2"])
+        ulp = abs(int(s1.view(np.int32)) - int(s2.view(np.int32)))
+        if s1 == s2:
+            kind = "tie"
+        elif (s1 < s2) != (e1 < e2):
+            kind = "flip"
+        elif ulp <= 4:
+            kind = "close"
+        else:
+            continue
+        if got[kind] >= want[kind]:
+            continue
+        got[kind] += 1
+        ci = len(cases)
+        swap = bool(rng.integers(2))  # which of the two near-tied neighbors comes first
+        ids = {"n1": 3, "n2": 7} if not swap else {"n1": 7, "n2": 3}
+        ids.update(n3=9, c=12)
+        order_names = sorted(["n1", "n2", "n3"], key=lambda q: ids[q]) + ["c"]
+        cent = {"degree": {3: 0.2, 7: 0.8, 9: 0.35, 12: 0.5}}
+        clients = []
+        for oi, q in enumerate(order_names):
+            clients.append((["r"], make_client(dc, ids[q], ms[q])))
+            for k2, v in sd_np(ms[q]).items():
+                arrays[f"c{ci}_in{oi}_{k2}"] = v
+        pre_cos = [float(dc.cosine_similarity(ms["c"], ms[q]).item()) for q in order_names[:-1]]
+        pre_f64 = [_cos64(ms["c"], ms[q]) for q in order_names[:-1]]
+        res = dc.sim_centrality_module_avg(clients[-1], 0, *clients, centrality_metric="degree",
+                                           centrality_dict=cent, softmax=True, softmax_coeff=10.0)
+        for k2, v in sd_np(res[1].model).items():
+            arrays[f"c{ci}_out_{k2}"] = v
+        cases.append(dict(case=ci, kind=kind, order=[ids[q] for q in order_names], ulp_gap=ulp,
+                          cosine=pre_cos, cosine_f64=pre_f64))
+    meta = dict(layout=layout, centrality={"degree": {"3": 0.2, "7": 0.8, "9": 0.35, "12": 0.5}},
+                softmax=True, softmax_coeff=10.0, centrality_metric="degree", cases=cases)
+    out_json.write_text(json.dumps(meta, indent=1))
+    np.savez_compressed(out_npz, **arrays)
+    print("near ties:", got, "trials", trial)
 
 
 def gen_layouts(resnet, modules, out):
@@ -419,7 +508,7 @@ def gen_bf16(dc, out_json, out_npz):
     print(f"bf16: {len(cases)} cases")
 
 
-GENERATORS = ("layouts", "tiny", "weights", "schedulers", "round", "big", "gossip", "bf16", "big_round")
+GENERATORS = ("layouts", "tiny", "weights", "schedulers", "round", "big", "gossip", "bf16", "big_round", "near_ties")
 
 
 def main(which=GENERATORS):
@@ -440,6 +529,8 @@ def main(which=GENERATORS):
         gen_gossip(HERE / "gossip.json")
     if "bf16" in which:
         gen_bf16(dc, HERE / "bf16_cases.json", HERE / "bf16_cases.npz")
+    if "near_ties" in which:
+        gen_near_ties(dc, HERE / "near_ties.json", HERE / "near_ties.npz")
     if "big_round" in which:
         gen_big_round(dc, resnet, HERE / "big_round_resnet18_ring32.json")
 

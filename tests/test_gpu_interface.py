@@ -79,14 +79,56 @@ def test_every_app_bit_exact(cuda, placement):
 
 
 def test_cosine_similarity_matches_reference(cuda):
+    """K2 through the reference interface returns the reference's fp32 similarity bit for bit."""
     import src.decentralized_client as dc
 
     for case in [c for c in TINY["cases"] if c["fn"] == "sim_centrality_module_avg"]:
         for placement in ("cpu", "pool"):
             clients, _ = build_clients(case, placement, cuda)
             for j, ref in enumerate(case["cosine"]):
-                got = float(dc.cosine_similarity(clients[-1][1].model, clients[j][1].model))
-                assert abs(got - ref) < 2e-5, (case["case"], j, got, ref)
+                got = dc.cosine_similarity(clients[-1][1].model, clients[j][1].model)
+                assert got.dtype == torch.float32
+                assert np.float32(got.item()).view(np.uint32) == np.float32(ref).view(np.uint32), \
+                    (case["case"], j, float(got), ref)
+
+
+NEAR = json.loads((GOLDEN / "near_ties.json").read_text())
+NEARZ = np.load(GOLDEN / "near_ties.npz")
+
+
+@pytest.mark.parametrize("placement", ["cpu", "pool"])
+def test_sim_centrality_near_ties_bit_exact(cuda, placement):
+    """sim_centrality_module_avg where two neighbors' similarities tie in fp32, are 1-4 ulp
+    apart, or are ordered differently in fp32 than in exact arithmetic (make_golden.py
+    near_ties): the least-similar pick - and so the softmax sign and every output bit - is the
+    reference's."""
+    import src.decentralized_client as dc
+
+    layout = StateLayout.from_layout([(n, tuple(s), d) for n, s, d in NEAR["layout"]])
+    cent = {k: {int(i): v for i, v in d.items()} for k, d in NEAR["centrality"].items()}
+    kinds = set()
+    for case in NEAR["cases"]:
+        ci = case["case"]
+        pool = ModelPool(layout, len(case["order"]), cuda) if placement == "pool" else None
+        clients = []
+        for oi, idx in enumerate(case["order"]):
+            m = TinyNet()
+            m.load_state_dict({n: torch.from_numpy(NEARZ[f"c{ci}_in{oi}_{n}"].copy()) for n, _, _ in NEAR["layout"]})
+            if pool is not None:
+                m = m.to(cuda)
+                pool.bind(m, oi)
+            clients.append((["r"], make_client(idx, m, 10)))
+        for j, ref in enumerate(case["cosine"]):
+            got = dc.cosine_similarity(clients[-1][1].model, clients[j][1].model)
+            assert np.float32(got.item()).view(np.uint32) == np.float32(ref).view(np.uint32), (ci, j)
+        res = dc.sim_centrality_module_avg(clients[-1], 0, *clients, centrality_metric=NEAR["centrality_metric"],
+                                           centrality_dict=cent, softmax=NEAR["softmax"],
+                                           softmax_coeff=NEAR["softmax_coeff"]).result()
+        sd = res[1].model.state_dict()
+        for name, _, _ in NEAR["layout"]:
+            assert bits_equal(sd[name].detach().cpu().numpy(), NEARZ[f"c{ci}_out_{name}"]), (ci, case["kind"], name)
+        kinds.add(case["kind"])
+    assert kinds == {"tie", "flip", "close"}
 
 
 def test_round_executor_snapshot_and_sequential(cuda):

@@ -473,9 +473,11 @@ def test_cosine_kernel_vs_numpy(cuda):
     for j, b in enumerate(bs):
         pool.load_row(1 + j, b)
     got = ops.cosine([pool.row_f32(0)] * 3, [pool.row_f32(1 + j) for j in range(3)], plan).cpu().numpy()
+    fa = pool.row_f32(0).cpu().numpy()
     for j, b in enumerate(bs):
-        ref = ra.cosine_similarity([a[n].numpy() for n in names], [b[n].numpy() for n in names])
-        assert abs(got[j] - ref) < 2e-5, (j, got[j], ref)
+        ref = oracle.cosine_model(fa, pool.row_f32(1 + j).cpu().numpy(), segs)  # torch's order, bitwise
+        assert got[j].view(np.uint32) == ref.view(np.uint32), (j, got[j], ref)
+        assert abs(got[j] - ra.cosine_similarity([a[n].numpy() for n in names], [b[n].numpy() for n in names])) < 2e-5
 
 
 _CLIQUE_GRAPHS = {

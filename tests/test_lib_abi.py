@@ -47,7 +47,7 @@ def test_error_status_and_message():
     rc = L.tal_agg_round_f32(None, 4, None, 4, 4, None, ctypes.byref(info), 1, None)
     assert rc == _lib.TAL_ERR_INVALID
     assert L.tal_round_plan_words(-1, 0) == -1
-    assert L.tal_cosine_scratch_bytes(0, 1) == -1
+    assert L.tal_cosine_scratch_bytes(None, 1) == -1
 
 
 def test_in_place_multi_group_rejected():

@@ -150,6 +150,23 @@ def test_cosine_restatement_matches_reference(case):
         assert abs(got - ref) < 1e-5, (j, got, ref)
 
 
+@pytest.mark.parametrize("case", [c for c in TINY["cases"] if c["fn"] == "sim_centrality_module_avg"],
+                         ids=lambda c: f"{c['case']}")
+def test_cosine_oracle_bitwise_reference(case):
+    """The C oracle's cosine (torch's CPU reduction order, cosine_oracle.c) equals the
+    reference's cosine_similarity values bit for bit."""
+    from topology_aware_learning_amd.arena import StateLayout
+
+    ci, M = case["case"], case["M"]
+    ins = inputs(ci, M)
+    layout = StateLayout.from_layout(LAYOUT)
+    segs = layout.param_segments(synth.param_names(LAYOUT))
+    flat = [np.concatenate([ins[j][n].reshape(-1) for n, _, d in LAYOUT if d == "float32"]) for j in range(M)]
+    for j, ref in enumerate(case["cosine"]):
+        got = oracle.cosine_model(flat[-1], flat[j], segs)
+        assert got.view(np.uint32) == np.float32(ref).view(np.uint32), (j, got, ref)
+
+
 def test_onehot_weights_bitwise():
     for rec in json.loads((GOLDEN / "weights_onehot.json").read_text()):
         cent = {k: {int(i): v for i, v in d.items()} for k, d in
@@ -226,3 +243,35 @@ def test_oracle_full_size_ring32_round():
     for r, row in enumerate(RING32["rows"]):
         assert hashlib.sha256(out[r].tobytes()).hexdigest() == row["sha256_f32"], r
         assert hashlib.sha256(iout[r].tobytes()).hexdigest() == row["sha256_i64"], r
+
+
+NEAR = json.loads((GOLDEN / "near_ties.json").read_text())
+NEARZ = np.load(GOLDEN / "near_ties.npz")
+
+
+@pytest.mark.parametrize("case", NEAR["cases"], ids=lambda c: f"{c['case']}-{c['kind']}")
+def test_cosine_oracle_near_ties(case):
+    """Near-tied similarities (fp32 ties, 1-4 ulp gaps, fp32 order != exact order): the C
+    oracle reproduces the reference's values bitwise, and with them its least-similar pick and
+    the aggregation output (oracle weights + oracle aggregation)."""
+    from topology_aware_learning_amd.arena import StateLayout
+
+    lay = [(n, tuple(s), d) for n, s, d in NEAR["layout"]]
+    layout = StateLayout.from_layout(lay)
+    segs = layout.param_segments(synth.param_names(lay))
+    ci, order = case["case"], case["order"]
+    M = len(order)
+    ins = [{n: NEARZ[f"c{ci}_in{i}_{n}"] for n, _, _ in lay} for i in range(M)]
+    flat = [np.concatenate([ins[j][n].reshape(-1) for n, _, d in lay if d == "float32"]) for j in range(M)]
+    sims = {}
+    for j, ref in enumerate(case["cosine"]):
+        got = oracle.cosine_model(flat[-1], flat[j], segs)
+        assert got.view(np.uint32) == np.float32(ref).view(np.uint32), (j, got, ref)
+        sims[order[j]] = float(got)
+    cent = {int(i): v for i, v in NEAR["centrality"]["degree"].items()}
+    w, _ = ra.sim_centrality_weights(order, order[-1], cent, sims, NEAR["softmax"], NEAR["softmax_coeff"])
+    for n, _, d in lay:
+        if d != "float32":
+            continue
+        out = oracle.agg_f32([ins[j][n].reshape(-1) for j in range(M)], w)
+        assert np.array_equal(out.view(np.uint32), NEARZ[f"c{ci}_out_{n}"].reshape(-1).view(np.uint32)), n

@@ -23,7 +23,7 @@ TAL_ERR_HIP = 2
 TAL_ERR_CAPACITY = 3
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 EXPORTED = (
     "tal_last_error",
@@ -127,8 +127,8 @@ _SIGS = {
     "tal_agg_round_clique_f32": (_I32, [_P, _I64, _P, _I64, _I64, _P, _I32, _I32, _I32, _P]),
     "tal_cosine_plan_words": (_I64, [_PI64, _I32]),
     "tal_cosine_plan_build": (_I32, [_PI64, _I32, _PI64, _I64, _PI32]),
-    "tal_cosine_scratch_bytes": (_I64, [_I32, _I32]),
-    "tal_cosine_params": (_I32, [_PP, _PP, _I32, _P, _I32, _I32, _P, _P, _P]),
+    "tal_cosine_scratch_bytes": (_I64, [_PI64, _I32]),
+    "tal_cosine_params": (_I32, [_PP, _PP, _I32, _P, _PI64, _I32, _P, _P, _P]),
     "tal_prox_plan_words": (_I64, [_PI64, _I32]),
     "tal_prox_plan_build": (_I32, [_PI64, _I32, _PI64, _I64, _PI32]),
     "tal_prox_scratch_bytes": (_I64, [_I32, _I32]),

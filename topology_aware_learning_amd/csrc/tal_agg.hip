@@ -33,7 +33,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 10;
+constexpr int kAbiVersion = 11;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -1779,133 +1779,231 @@ int32_t launch_round_vec(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, i
 }
 
 // ------------------------------------------------------------------------------------------
-// K2: cosine similarity of parameter tensors (plan of chunks; see tal_agg.h)
+// K2: the reference's model cosine similarity, bit for bit (see tal_agg.h and the C restatement
+// oracle/cosine_oracle.c, which pins the operation order against the reference's own values).
+// Reference: cosine_similarity, decentralized_client.py:661-681 over torch's CPU kernels:
+//   n = clamp_min(vector_norm(x, 2, dim=1), 1e-6);  s = sum_dim1((x1 / n1) * (x2 / n2));
+//   mean = cascade_sum(s) / numel;  result = (0 + mean_0 + mean_1 + ...) / n_params.
+// Every output of a tensor viewed [A, I, B] is one element (I == 1), one row (B == 1: 8
+// threads per row, one per lane of torch's 8-wide vector accumulators) or one column (B > 1:
+// one thread, strided); the per-tensor means and the final average follow in two small
+// kernels.  All arithmetic is single-rounding fp32 (__f*_rn), in torch's order.
 // ------------------------------------------------------------------------------------------
 constexpr int kCosMaxPairs = 32;
-constexpr int64_t kCosRowsPerChunk = 32;     // ROW kind: 8 rows per wave
-constexpr int64_t kCosColsPerChunk = 1024;   // COL kind: 4 outputs per lane
-enum { kCosRow = 0, kCosCol = 1 };
+constexpr int kCosHdr = 2;         // plan words: {n_seg, n_out}
+constexpr int kCosSegWords = 6;    // {offset, A, I, B, out_offset, kind}
+constexpr int kCosChunkWords = 4;  // {seg, first output, count, 0}
+constexpr int kCosBlock = 256;
+constexpr int kCosVw = 8;          // Vectorized<float> width of torch's sum kernel (as run)
+enum { kCosElem = 0, kCosRow = 1, kCosCol = 2 };
+constexpr int64_t cos_chunk_outputs(int kind) { return kind == kCosRow ? kCosBlock / kCosVw : kCosBlock; }
 
 struct CosPairs {
   const float* a[kCosMaxPairs];
   const float* b[kCosMaxPairs];
 };
 
-__device__ __forceinline__ float wave_sum(float v) {
+__device__ __forceinline__ int64_t cos_ceil_log2(int64_t x) {
+  int64_t r = 0;
+  while ((int64_t{1} << r) < x) ++r;
+  return r;
+}
+
+// torch multi_row_sum: NR interleaved streams load(i, k), a 4-level cascade whose level
+// boundaries depend only on i (so one column of a 32-column chunk is the NR = 1 case)
+template <int NR, class Load>
+__device__ __forceinline__ void cos_multi_row(Load load, int64_t size, float* out) {
+  constexpr int kL = 4;
+  const int64_t lp = cos_ceil_log2(size) / kL > 4 ? cos_ceil_log2(size) / kL : 4;
+  const int64_t step = int64_t{1} << lp;
+  const int64_t mask0 = step - 1;
+  float acc[kL][NR];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  for (int j = 0; j < kL; ++j)
+#pragma unroll
+    for (int k = 0; k < NR; ++k) acc[j][k] = 0.f;
+  int64_t i = 0;
+  while (i + step <= size) {
+    for (int64_t j = 0; j < step; ++j, ++i)
+#pragma unroll
+      for (int k = 0; k < NR; ++k) acc[0][k] = __fadd_rn(acc[0][k], load(i, k));
+#pragma unroll
+    for (int j = 1; j < kL; ++j) {
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        acc[j][k] = __fadd_rn(acc[j][k], acc[j - 1][k]);
+        acc[j - 1][k] = 0.f;
+      }
+      if ((i & (mask0 << (j * lp))) != 0) break;
+    }
+  }
+  for (; i < size; ++i)
+#pragma unroll
+    for (int k = 0; k < NR; ++k) acc[0][k] = __fadd_rn(acc[0][k], load(i, k));
+#pragma unroll
+  for (int j = 1; j < kL; ++j)
+#pragma unroll
+    for (int k = 0; k < NR; ++k) acc[0][k] = __fadd_rn(acc[0][k], acc[j][k]);
+#pragma unroll
+  for (int k = 0; k < NR; ++k) out[k] = acc[0][k];
 }
 
-__device__ __forceinline__ float clamp_norm(float n2) { return fmaxf(sqrtf(n2), 1e-6f); }
-
-// nn.CosineSimilarity(eps=1e-6) = sum_i (x_i/max(|x|,eps)) * (y_i/max(|y|,eps)).  The fused
-// one-pass value dot/|x|/|y| equals it up to rounding whenever the fp32 sums stayed finite;
-// when a sum of squares (or the dot) overflowed, torch's fp32 norm is inf and zeroes the row's
-// terms, so the caller recomputes that row in the normalize-first form (rare path).
-__device__ __forceinline__ bool fused_ok(float dot, float na2, float nb2) {
-  return isfinite(dot) && isfinite(na2) && isfinite(nb2);
+// torch row_sum: 4 interleaved partial sums (element 4 i + k), the remainder into partial 0,
+// partials 1..3 added to partial 0 in order
+template <class Load>
+__device__ __forceinline__ float cos_row_sum(Load load, int64_t size) {
+  float ps[4];
+  const int64_t si = size / 4;
+  cos_multi_row<4>([&](int64_t i, int k) { return load(i * 4 + k); }, si, ps);
+  for (int64_t i = si * 4; i < size; ++i) ps[0] = __fadd_rn(ps[0], load(i));
+  for (int k = 1; k < 4; ++k) ps[0] = __fadd_rn(ps[0], ps[k]);
+  return ps[0];
 }
 
-__device__ __forceinline__ float cos_fused(float dot, float na2, float nb2) {
-  return (dot / clamp_norm(na2)) / clamp_norm(nb2);
+__device__ __forceinline__ float cos_clamp(float n) { return n < 1e-6f ? 1e-6f : n; }  // NaN stays NaN
+
+// Lane sums of one 8-thread group (threads g*8 .. g*8+7 of the wave) delivered to its thread 0
+// in lane order: out = first + v_0 + v_1 + ... + v_7 (every thread of the wave must call it).
+__device__ __forceinline__ float cos_group_fold(float first, float v, int gbase) {
+  float r = first;
+#pragma unroll
+  for (int l = 0; l < kCosVw; ++l) r = __fadd_rn(r, __shfl(v, gbase + l, 64));
+  return r;
 }
 
-// plan: [n_seg x {off, A, I, B}] then [n_chunks x {seg, first, count, kind}]  (int64 words)
-__global__ __launch_bounds__(kBlock) void k_cosine_chunks(CosPairs pr, const int64_t* __restrict__ plan,
-                                                          int n_seg, int n_chunks,
-                                                          double* __restrict__ partial) {
-  __shared__ double s_part[kBlock / 64];
-  const int chunk = blockIdx.x;
+__global__ __launch_bounds__(kCosBlock) void k_cosine_outputs(CosPairs pr, const int64_t* __restrict__ plan,
+                                                              int n_seg, float* __restrict__ s_all) {
   const int pair = blockIdx.y;
-  const int64_t* ch = plan + 4 * static_cast<int64_t>(n_seg) + 4 * static_cast<int64_t>(chunk);
-  const int64_t seg = ch[0], first = ch[1], count = ch[2], kind = ch[3];
-  const int64_t off = plan[4 * seg + 0];
-  const int64_t I = plan[4 * seg + 2];
-  const int64_t B = plan[4 * seg + 3];
-  const float* a = pr.a[pair] + off;
-  const float* b = pr.b[pair] + off;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  double sum = 0.0;
-  if (kind == kCosRow) {
-    for (int64_t r = first + wave; r < first + count; r += kBlock / 64) {
-      float dot = 0.f, na = 0.f, nb = 0.f;
-      const float* ar = a + r * I;
-      const float* br = b + r * I;
-      for (int64_t i = lane; i < I; i += 64) {
-        const float x = ar[i], y = br[i];
-        dot += x * y;
-        na += x * x;
-        nb += y * y;
-      }
-      dot = wave_sum(dot);
-      na = wave_sum(na);
-      nb = wave_sum(nb);
-      float cv;
-      if (fused_ok(dot, na, nb)) {
-        cv = cos_fused(dot, na, nb);
-      } else {
-        const float ia = clamp_norm(na), ib = clamp_norm(nb);
-        float t = 0.f;
-        for (int64_t i = lane; i < I; i += 64) t += (ar[i] / ia) * (br[i] / ib);
-        cv = wave_sum(t);
-      }
-      if (lane == 0) sum += static_cast<double>(cv);
+  const int64_t n_out = plan[1];
+  const int64_t* ch = plan + kCosHdr + kCosSegWords * static_cast<int64_t>(n_seg) +
+                      kCosChunkWords * static_cast<int64_t>(blockIdx.x);
+  const int64_t* sg = plan + kCosHdr + kCosSegWords * ch[0];
+  const int64_t first = ch[1], count = ch[2];
+  const int64_t I = sg[2], B = sg[3];
+  const int kind = static_cast<int>(sg[5]);
+  const float* a = pr.a[pair] + sg[0];
+  const float* b = pr.b[pair] + sg[0];
+  float* s = s_all + static_cast<int64_t>(pair) * n_out + sg[4];
+  const int tid = threadIdx.x;
+  if (kind == kCosElem) {  // 1-D parameter unsqueezed to [n, 1]: norm |x|, one product
+    const int64_t q = first + tid;
+    if (q < first + count) {
+      const float x = a[q], y = b[q];
+      const float n1 = cos_clamp(__fsqrt_rn(__fmaf_rn(x, x, 0.f)));
+      const float n2 = cos_clamp(__fsqrt_rn(__fmaf_rn(y, y, 0.f)));
+      s[q] = __fadd_rn(0.f, __fmul_rn(__fdiv_rn(x, n1), __fdiv_rn(y, n2)));
     }
-  } else {
-    for (int64_t o = first + threadIdx.x; o < first + count; o += kBlock) {
-      const int64_t ai = o / B, bi = o % B;
-      const float* ap = a + ai * I * B + bi;
-      const float* bp = b + ai * I * B + bi;
-      float dot = 0.f, na = 0.f, nb = 0.f;
-      for (int64_t i = 0; i < I; ++i) {
-        const float x = ap[i * B], y = bp[i * B];
-        dot += x * y;
-        na += x * x;
-        nb += y * y;
-      }
-      if (fused_ok(dot, na, nb)) {
-        sum += static_cast<double>(cos_fused(dot, na, nb));
-      } else {
-        const float ia = clamp_norm(na), ib = clamp_norm(nb);
-        float t = 0.f;
-        for (int64_t i = 0; i < I; ++i) t += (ap[i * B] / ia) * (bp[i * B] / ib);
-        sum += static_cast<double>(t);
-      }
+    return;
+  }
+  if (kind == kCosCol) {  // B > 1: reduced dim strided by B; one thread per (row, column)
+    const int64_t q = first + tid;
+    if (q >= first + count) return;
+    const int64_t o = q / B, k = q % B;
+    const float* x1 = a + o * I * B + k;
+    const float* x2 = b + o * I * B + k;
+    float m1 = 0.f, m2 = 0.f;  // torch NormTwoOps: fma in index order
+    for (int64_t i = 0; i < I; ++i) {
+      m1 = __fmaf_rn(x1[i * B], x1[i * B], m1);
+      m2 = __fmaf_rn(x2[i * B], x2[i * B], m2);
     }
-    // reduce lanes of the wave
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    const float n1 = cos_clamp(__fsqrt_rn(m1)), n2 = cos_clamp(__fsqrt_rn(m2));
+    auto prod = [&](int64_t i) { return __fmul_rn(__fdiv_rn(x1[i * B], n1), __fdiv_rn(x2[i * B], n2)); };
+    float r;
+    if (B >= kCosVw && k < B / 32 * 32) {  // columns in chunks of 32 share one cascade
+      float c[1];
+      cos_multi_row<1>([&](int64_t i, int) { return prod(i); }, I, c);
+      r = c[0];
+    } else {  // chunks of 8 and single columns: row_sum per column
+      r = cos_row_sum(prod, I);
+    }
+    s[q] = __fadd_rn(0.f, r);
+    return;
   }
-  if (lane == 0) s_part[wave] = sum;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double t = 0.0;
-    for (int w = 0; w < kBlock / 64; ++w) t += s_part[w];
-    partial[static_cast<int64_t>(pair) * n_chunks + chunk] = t;
+  // kCosRow (B == 1, I > 1): reduced dim contiguous; 8 threads per row (torch's vector lanes)
+  const int lane = tid & 63;
+  const int l = lane & (kCosVw - 1);
+  const int gbase = lane & ~(kCosVw - 1);
+  const int64_t q = first + tid / kCosVw;
+  const bool live = q < first + count;
+  const float* x1 = a + (live ? q : first) * I;
+  const float* x2 = b + (live ? q : first) * I;
+  const int64_t vec_end = I - I % kCosVw;
+  // vector_norm (reduce-lastdim kernel): lane accumulators fma over whole vectors
+  float m1 = 0.f, m2 = 0.f;
+  if (live)
+    for (int64_t d = l; d < vec_end; d += kCosVw) {
+      m1 = __fmaf_rn(x1[d], x1[d], m1);
+      m2 = __fmaf_rn(x2[d], x2[d], m2);
+    }
+  float t1 = __shfl(m1, gbase, 64), t2 = __shfl(m2, gbase, 64);  // lane 0 starts the fold
+  for (int j = 1; j < kCosVw; ++j) {
+    t1 = __fadd_rn(t1, __shfl(m1, gbase + j, 64));
+    t2 = __fadd_rn(t2, __shfl(m2, gbase + j, 64));
   }
+  float n1 = 0.f, n2 = 0.f;
+  if (l == 0 && live) {  // the tail: groups of 4 as square-then-add, the rest fused
+    int64_t d = vec_end;
+    const int64_t sep = (I - vec_end) / 4 * 4;
+    for (int64_t e = 0; e < sep; ++e, ++d) {
+      t1 = __fadd_rn(t1, __fmul_rn(x1[d], x1[d]));
+      t2 = __fadd_rn(t2, __fmul_rn(x2[d], x2[d]));
+    }
+    for (; d < I; ++d) {
+      t1 = __fmaf_rn(x1[d], x1[d], t1);
+      t2 = __fmaf_rn(x2[d], x2[d], t2);
+    }
+    n1 = cos_clamp(__fsqrt_rn(t1));
+    n2 = cos_clamp(__fsqrt_rn(t2));
+  }
+  n1 = __shfl(n1, gbase, 64);
+  n2 = __shfl(n2, gbase, 64);
+  auto prod = [&](int64_t i) { return __fmul_rn(__fdiv_rn(x1[i], n1), __fdiv_rn(x2[i], n2)); };
+  if (I < kCosVw) {  // scalar_inner_sum
+    if (l == 0 && live) s[q] = __fadd_rn(0.f, cos_row_sum(prod, I));
+    return;
+  }
+  // vectorized_inner_sum: lane l sums elements 8 i + l by row_sum; then the scalar tail from 0,
+  // then the lanes in order
+  const int64_t nv = I / kCosVw;
+  const float lane_sum = live ? cos_row_sum([&](int64_t i) { return prod(i * kCosVw + l); }, nv) : 0.f;
+  float tail = 0.f;
+  if (l == 0 && live)
+    for (int64_t k2 = nv * kCosVw; k2 < I; ++k2) tail = __fadd_rn(tail, prod(k2));
+  const float fin = cos_group_fold(tail, lane_sum, gbase);
+  if (l == 0 && live) s[q] = __fadd_rn(0.f, fin);
 }
 
-__global__ void k_cosine_finish(const int64_t* __restrict__ plan, int n_seg, int n_chunks,
-                                const double* __restrict__ partial, float* __restrict__ out,
-                                int pair0) {
+// per (tensor, pair): mean = inner_sum(s) / numel (torch sum then div_); 8 threads = the lanes
+__global__ void k_cosine_means(const int64_t* __restrict__ plan, int n_seg, const float* __restrict__ s_all,
+                               float* __restrict__ means) {
+  const int seg = blockIdx.x, pair = blockIdx.y;
+  const int64_t n_out = plan[1];
+  const int64_t* sg = plan + kCosHdr + kCosSegWords * static_cast<int64_t>(seg);
+  const int64_t n = sg[1] * sg[3];
+  const float* s = s_all + static_cast<int64_t>(pair) * n_out + sg[4];
+  const int l = threadIdx.x & 63;
+  float fin;
+  if (n < kCosVw) {
+    fin = l == 0 ? cos_row_sum([&](int64_t i) { return s[i]; }, n) : 0.f;
+  } else {
+    const int64_t nv = n / kCosVw;
+    const float lane_sum = l < kCosVw ? cos_row_sum([&](int64_t i) { return s[i * kCosVw + l]; }, nv) : 0.f;
+    float tail = 0.f;
+    if (l == 0)
+      for (int64_t k = nv * kCosVw; k < n; ++k) tail = __fadd_rn(tail, s[k]);
+    fin = cos_group_fold(tail, lane_sum, 0);
+  }
+  if (l == 0) means[static_cast<int64_t>(pair) * n_seg + seg] = __fdiv_rn(__fadd_rn(0.f, fin), static_cast<float>(n));
+}
+
+// avg_cos = 0 + mean_0, += mean_t in parameter order; / len(params)
+__global__ void k_cosine_finish(int n_seg, const float* __restrict__ means, float* __restrict__ out, int pair0) {
   if (threadIdx.x != 0) return;
   const int pair = blockIdx.x;
-  const int64_t* chunks = plan + 4 * static_cast<int64_t>(n_seg);
-  double total = 0.0, seg_sum = 0.0;
-  int64_t cur = -1;
-  for (int c = 0; c < n_chunks; ++c) {
-    const int64_t seg = chunks[4 * c];
-    if (seg != cur) {
-      if (cur >= 0) total += seg_sum / static_cast<double>(plan[4 * cur + 1] * plan[4 * cur + 3]);
-      cur = seg;
-      seg_sum = 0.0;
-    }
-    seg_sum += partial[static_cast<int64_t>(pair) * n_chunks + c];
-  }
-  if (cur >= 0) total += seg_sum / static_cast<double>(plan[4 * cur + 1] * plan[4 * cur + 3]);
-  out[pair0 + pair] = static_cast<float>(total / static_cast<double>(n_seg));
+  const float* m = means + static_cast<int64_t>(pair) * n_seg;
+  float avg = __fadd_rn(0.f, m[0]);
+  for (int t = 1; t < n_seg; ++t) avg = __fadd_rn(avg, m[t]);
+  out[pair0 + pair] = __fdiv_rn(avg, static_cast<float>(n_seg));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2686,16 +2784,18 @@ int32_t tal_agg_round_bf16(const uint16_t* pool_in, int64_t ld_in, uint16_t* poo
   return launch_round_scalar<uint16_t>(pool_in, ld_in, pool_out, ld_out, e_vec, n, v, *info, exact, s);
 }
 
+static int cos_kind(int64_t I, int64_t B) { return I == 1 ? kCosElem : (B == 1 ? kCosRow : kCosCol); }
+
 int64_t tal_cosine_plan_words(const int64_t* seg_host, int32_t n_seg) {
   if (!seg_host || n_seg <= 0) return -1;
   int64_t chunks = 0;
   for (int s = 0; s < n_seg; ++s) {
     const int64_t A = seg_host[4 * s + 1], I = seg_host[4 * s + 2], B = seg_host[4 * s + 3];
-    if (A <= 0 || I <= 0 || B <= 0) return -1;
-    if (B == 1 && I > 1) chunks += (A + kCosRowsPerChunk - 1) / kCosRowsPerChunk;
-    else chunks += (A * B + kCosColsPerChunk - 1) / kCosColsPerChunk;
+    if (A <= 0 || I <= 0 || B <= 0 || seg_host[4 * s] < 0) return -1;
+    const int64_t per = cos_chunk_outputs(cos_kind(I, B));
+    chunks += (A * B + per - 1) / per;
   }
-  return 4 * (static_cast<int64_t>(n_seg) + chunks);
+  return kCosHdr + kCosSegWords * static_cast<int64_t>(n_seg) + kCosChunkWords * chunks;
 }
 
 int32_t tal_cosine_plan_build(const int64_t* seg_host, int32_t n_seg, int64_t* plan_host,
@@ -2704,39 +2804,49 @@ int32_t tal_cosine_plan_build(const int64_t* seg_host, int32_t n_seg, int64_t* p
   if (words < 0 || !plan_host || !n_chunks)
     return fail(TAL_ERR_INVALID, "tal_cosine_plan_build: bad segments");
   if (plan_capacity_words < words) return fail(TAL_ERR_INVALID, "tal_cosine_plan_build: buffer too small");
-  memcpy(plan_host, seg_host, sizeof(int64_t) * 4 * n_seg);
-  int64_t* ch = plan_host + 4 * n_seg;
-  int64_t c = 0;
+  int64_t* sg = plan_host + kCosHdr;
+  int64_t* ch = sg + kCosSegWords * static_cast<int64_t>(n_seg);
+  int64_t c = 0, out = 0;
   for (int s = 0; s < n_seg; ++s) {
     const int64_t A = seg_host[4 * s + 1], I = seg_host[4 * s + 2], B = seg_host[4 * s + 3];
-    const bool row = (B == 1 && I > 1);
-    const int64_t total = row ? A : A * B;
-    const int64_t per = row ? kCosRowsPerChunk : kCosColsPerChunk;
+    const int kind = cos_kind(I, B);
+    sg[kCosSegWords * s + 0] = seg_host[4 * s];
+    sg[kCosSegWords * s + 1] = A;
+    sg[kCosSegWords * s + 2] = I;
+    sg[kCosSegWords * s + 3] = B;
+    sg[kCosSegWords * s + 4] = out;
+    sg[kCosSegWords * s + 5] = kind;
+    const int64_t total = A * B, per = cos_chunk_outputs(kind);
     for (int64_t f = 0; f < total; f += per) {
-      ch[4 * c + 0] = s;
-      ch[4 * c + 1] = f;
-      ch[4 * c + 2] = std::min(per, total - f);
-      ch[4 * c + 3] = row ? kCosRow : kCosCol;
+      ch[kCosChunkWords * c + 0] = s;
+      ch[kCosChunkWords * c + 1] = f;
+      ch[kCosChunkWords * c + 2] = std::min(per, total - f);
+      ch[kCosChunkWords * c + 3] = 0;
       ++c;
     }
+    out += total;
   }
   if (c > 0x7fffffff) return fail(TAL_ERR_INVALID, "tal_cosine_plan_build: too many chunks");
+  plan_host[0] = n_seg;
+  plan_host[1] = out;
   *n_chunks = static_cast<int32_t>(c);
   g_err.clear();
   return TAL_OK;
 }
 
-int64_t tal_cosine_scratch_bytes(int32_t n_chunks, int32_t n_pairs) {
-  if (n_chunks <= 0 || n_pairs <= 0) return -1;
-  return static_cast<int64_t>(sizeof(double)) * n_chunks * std::min(n_pairs, kCosMaxPairs);
+int64_t tal_cosine_scratch_bytes(const int64_t* plan_host, int32_t n_pairs) {
+  if (!plan_host || n_pairs <= 0 || plan_host[0] <= 0 || plan_host[1] <= 0) return -1;
+  return static_cast<int64_t>(sizeof(float)) * (plan_host[1] + plan_host[0]) * std::min(n_pairs, kCosMaxPairs);
 }
 
 int32_t tal_cosine_params(const float* const* a_ptrs_host, const float* const* b_ptrs_host,
-                          int32_t n_pairs, const int64_t* plan_dev, int32_t n_chunks,
-                          int32_t n_seg, void* scratch, float* out_dev, void* stream) {
-  if (!a_ptrs_host || !b_ptrs_host || !plan_dev || !scratch || !out_dev || n_pairs <= 0 ||
-      n_chunks <= 0 || n_seg <= 0)
+                          int32_t n_pairs, const int64_t* plan_dev, const int64_t* plan_host, int32_t n_chunks,
+                          void* scratch, float* out_dev, void* stream) {
+  if (!a_ptrs_host || !b_ptrs_host || !plan_dev || !plan_host || !scratch || !out_dev || n_pairs <= 0 ||
+      n_chunks <= 0 || plan_host[0] <= 0 || plan_host[1] <= 0)
     return fail(TAL_ERR_INVALID, "tal_cosine_params: bad arguments");
+  const int n_seg = static_cast<int>(plan_host[0]);
+  const int64_t n_out = plan_host[1];
   hipStream_t s = static_cast<hipStream_t>(stream);
   for (int base = 0; base < n_pairs; base += kCosMaxPairs) {
     const int cnt = std::min(kCosMaxPairs, n_pairs - base);
@@ -2747,9 +2857,11 @@ int32_t tal_cosine_params(const float* const* a_ptrs_host, const float* const* b
       if (j < cnt && (!pr.a[j] || !pr.b[j]))
         return fail(TAL_ERR_INVALID, "tal_cosine_params: null model pointer");
     }
-    double* part = static_cast<double*>(scratch);
-    k_cosine_chunks<<<dim3(n_chunks, cnt), kBlock, 0, s>>>(pr, plan_dev, n_seg, n_chunks, part);
-    k_cosine_finish<<<cnt, 64, 0, s>>>(plan_dev, n_seg, n_chunks, part, out_dev, base);
+    float* s_all = static_cast<float*>(scratch);
+    float* means = s_all + n_out * cnt;
+    k_cosine_outputs<<<dim3(n_chunks, cnt), kCosBlock, 0, s>>>(pr, plan_dev, n_seg, s_all);
+    k_cosine_means<<<dim3(n_seg, cnt), 64, 0, s>>>(plan_dev, n_seg, s_all, means);
+    k_cosine_finish<<<cnt, 64, 0, s>>>(n_seg, means, out_dev, base);
   }
   return check_launch("tal_cosine_params");
 }

@@ -614,7 +614,8 @@ def build_cosine_plan(segments: Sequence[Sequence[int]]) -> CosinePlan:
 
 def cosine(a_list: Sequence[torch.Tensor], b_list: Sequence[torch.Tensor], plan: CosinePlan,
            stream=None) -> torch.Tensor:
-    """K2: cosine_similarity(a_j, b_j) for every pair (flat fp32 parameter arenas)."""
+    """K2: cosine_similarity(a_j, b_j) for every pair (flat fp32 parameter arenas), the
+    reference's fp32 value bit for bit."""
     if len(a_list) != len(b_list) or not a_list:
         raise ValueError("need matching, non-empty a/b lists")
     dev = a_list[0].device
@@ -625,11 +626,13 @@ def cosine(a_list: Sequence[torch.Tensor], b_list: Sequence[torch.Tensor], plan:
     if plan.device is None or plan.device.device != dev:
         plan.device = torch.from_numpy(plan.host).to(dev)
     L = _lib.load()
-    scratch = torch.empty(int(L.tal_cosine_scratch_bytes(plan.n_chunks, len(a_list))), dtype=torch.uint8, device=dev)
+    P64 = ctypes.POINTER(ctypes.c_int64)
+    hp = plan.host.ctypes.data_as(P64)
+    scratch = torch.empty(int(L.tal_cosine_scratch_bytes(hp, len(a_list))), dtype=torch.uint8, device=dev)
     out = torch.empty(len(a_list), dtype=torch.float32, device=dev)
     check(L.tal_cosine_params(_lib.ptr_array([t.data_ptr() for t in a_list]),
                               _lib.ptr_array([t.data_ptr() for t in b_list]), len(a_list),
-                              ctypes.c_void_p(plan.device.data_ptr()), plan.n_chunks, plan.n_seg,
+                              ctypes.c_void_p(plan.device.data_ptr()), hp, plan.n_chunks,
                               ctypes.c_void_p(scratch.data_ptr()), ctypes.c_void_p(out.data_ptr()),
                               _stream(dev, stream)))
     return out

@@ -2,10 +2,11 @@
 
 Reference: cosine_similarity, src/decentralized_client.py:661-681 — over `named_parameters`
 (buffers excluded), nn.CosineSimilarity(dim=1, eps=1e-6) per tensor (1-D tensors get a
-trailing unit dim), mean per tensor, average over tensors.  The kernel fuses dot and both
-squared norms in one pass over each model (reference: normalise-then-dot in fp32); results
-agree with the reference to ~1e-6 (tests: tolerance 2e-5), which is what the only consumer
-— the arg-min neighbour of sim_centrality_module_avg (:511) — needs.
+trailing unit dim), mean per tensor, average over tensors.  K2 performs the reference's fp32
+operations in the order of the torch CPU kernels it runs on (include/tal_agg.h), so the
+values are the reference's bit for bit and sim_centrality_module_avg's arg-min (:511) —
+near-ties and exact fp32 ties included — picks the reference's neighbor
+(tests/golden/near_ties.*).
 """
 from __future__ import annotations
 
