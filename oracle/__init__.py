@@ -59,6 +59,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_cosine_scratch.restype = ctypes.c_int64
         L.oracle_cosine_model.argtypes = [P, P, P, ctypes.c_int32, P, P]
         L.oracle_cosine_model.restype = ctypes.c_float
+        L.oracle_cosine_outputs.argtypes = [P, P, P, ctypes.c_int32, P, P, P]
         _lib = L
     return _lib
 
@@ -165,3 +166,18 @@ def cosine_model(a, b, segments, per_tensor: bool = False):
                               per.ctypes.data)
     v = np.float32(v)
     return (v, per) if per_tensor else v
+
+
+def cosine_outputs(a, b, segments):
+    """Debug view of cosine_model: (per-output values s of every tensor, per-tensor means)."""
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    b = np.ascontiguousarray(b, dtype=np.float32)
+    seg = np.ascontiguousarray(np.asarray(segments, dtype=np.int64).reshape(-1, 4))
+    L = lib()
+    scratch = np.empty(max(1, L.oracle_cosine_scratch(seg.ctypes.data, len(seg))), np.float32)
+    n_out = int(sum(int(r[1]) * int(r[3]) for r in seg))
+    s = np.empty(n_out, np.float32)
+    means = np.empty(len(seg), np.float32)
+    L.oracle_cosine_outputs(a.ctypes.data, b.ctypes.data, seg.ctypes.data, len(seg), scratch.ctypes.data,
+                            s.ctypes.data, means.ctypes.data)
+    return s, means

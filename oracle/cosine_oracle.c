@@ -226,3 +226,15 @@ float oracle_cosine_model(const float* a, const float* b, const int64_t* segs, i
   }
   return avg / (float)nseg;
 }
+
+/* Debug view: every tensor's per-output values s (concatenated, tensor order) and means. */
+void oracle_cosine_outputs(const float* a, const float* b, const int64_t* segs, int32_t nseg, float* scratch,
+                           float* s_out, float* means) {
+  int64_t pos = 0;
+  for (int32_t t = 0; t < nseg; ++t) {
+    const int64_t off = segs[4 * t], O = segs[4 * t + 1], I = segs[4 * t + 2], K = segs[4 * t + 3];
+    means[t] = cos_tensor(a + off, b + off, O, I, K, scratch);
+    memcpy(s_out + pos, scratch, sizeof(float) * O * K);
+    pos += O * K;
+  }
+}

@@ -174,10 +174,12 @@ class DecentrallearnApp:
         if os.environ.get("TAL_DEVICE_POOL", "1") == "0" or not torch.cuda.is_available():
             return None
         from topology_aware_learning_amd.aggregate import layout_of_module
-        from topology_aware_learning_amd.arena import ModelPool
+        from topology_aware_learning_amd.round import calibrated_pool
 
         layout = layout_of_module(self.clients[0].model)
-        pool = ModelPool(layout, len(self.clients), torch.device("cuda", torch.cuda.current_device()))
+        # the pool the models live in for the whole run, placed where in-place rounds are fast
+        pool = calibrated_pool(layout, len(self.clients), torch.device("cuda", torch.cuda.current_device()),
+                               trials=int(os.environ.get("TAL_POOL_PLACEMENT_TRIALS", "3")))
         for c in self.clients:
             c.model.to(pool.device)
             pool.bind(c.model, c.idx)
@@ -270,6 +272,17 @@ class DecentrallearnApp:
             return x.result() if isinstance(x, Future) else x
 
         orders, weights, out_rows, done = [], [], [], []
+        row_of: dict = {}  # id(model) -> pool row: each model's binding is checked once per round
+
+        def pool_row(m) -> int:
+            r = row_of.get(id(m))
+            if r is None:
+                b = bound_row(m)
+                if b is None or b[0] is not self.pool:
+                    raise RuntimeError("TAL_BATCHED_ROUND needs every model bound to the device pool")
+                r = row_of[id(m)] = b[1]
+            return r
+
         for future, agg_client, agg_neighbors, kwargs in batch:
             me = res(agg_client)
             nbrs = [res(f) for f in agg_neighbors]
@@ -277,12 +290,7 @@ class DecentrallearnApp:
             done.append((future, me))
             if got is None:  # test_agg: no-op
                 continue
-            rows = []
-            for m in list(got[0]) + [me[1].model]:
-                b = bound_row(m)
-                if b is None or b[0] is not self.pool:
-                    raise RuntimeError("TAL_BATCHED_ROUND needs every model bound to the device pool")
-                rows.append(b[1])
+            rows = [pool_row(m) for m in list(got[0]) + [me[1].model]]
             orders.append(rows[:-1])
             weights.append([float(x) for x in got[1]])
             out_rows.append(rows[-1])

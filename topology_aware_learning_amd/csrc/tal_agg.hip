@@ -1860,6 +1860,10 @@ __device__ __forceinline__ float cos_row_sum(Load load, int64_t size) {
   return ps[0];
 }
 
+// correctly rounded sqrt (llvm.sqrt.f32 under HIP's default correctly-rounded divide/sqrt);
+// HIP's __fsqrt_rn is the native approximation unless OCML_BASIC_ROUNDED_OPERATIONS is set
+__device__ __forceinline__ float cos_sqrt_rn(float x) { return __builtin_sqrtf(x); }
+
 __device__ __forceinline__ float cos_clamp(float n) { return n < 1e-6f ? 1e-6f : n; }  // NaN stays NaN
 
 // Lane sums of one 8-thread group (threads g*8 .. g*8+7 of the wave) delivered to its thread 0
@@ -1889,8 +1893,8 @@ __global__ __launch_bounds__(kCosBlock) void k_cosine_outputs(CosPairs pr, const
     const int64_t q = first + tid;
     if (q < first + count) {
       const float x = a[q], y = b[q];
-      const float n1 = cos_clamp(__fsqrt_rn(__fmaf_rn(x, x, 0.f)));
-      const float n2 = cos_clamp(__fsqrt_rn(__fmaf_rn(y, y, 0.f)));
+      const float n1 = cos_clamp(cos_sqrt_rn(__fmaf_rn(x, x, 0.f)));
+      const float n2 = cos_clamp(cos_sqrt_rn(__fmaf_rn(y, y, 0.f)));
       s[q] = __fadd_rn(0.f, __fmul_rn(__fdiv_rn(x, n1), __fdiv_rn(y, n2)));
     }
     return;
@@ -1906,7 +1910,7 @@ __global__ __launch_bounds__(kCosBlock) void k_cosine_outputs(CosPairs pr, const
       m1 = __fmaf_rn(x1[i * B], x1[i * B], m1);
       m2 = __fmaf_rn(x2[i * B], x2[i * B], m2);
     }
-    const float n1 = cos_clamp(__fsqrt_rn(m1)), n2 = cos_clamp(__fsqrt_rn(m2));
+    const float n1 = cos_clamp(cos_sqrt_rn(m1)), n2 = cos_clamp(cos_sqrt_rn(m2));
     auto prod = [&](int64_t i) { return __fmul_rn(__fdiv_rn(x1[i * B], n1), __fdiv_rn(x2[i * B], n2)); };
     float r;
     if (B >= kCosVw && k < B / 32 * 32) {  // columns in chunks of 32 share one cascade
@@ -1952,8 +1956,8 @@ __global__ __launch_bounds__(kCosBlock) void k_cosine_outputs(CosPairs pr, const
       t1 = __fmaf_rn(x1[d], x1[d], t1);
       t2 = __fmaf_rn(x2[d], x2[d], t2);
     }
-    n1 = cos_clamp(__fsqrt_rn(t1));
-    n2 = cos_clamp(__fsqrt_rn(t2));
+    n1 = cos_clamp(cos_sqrt_rn(t1));
+    n2 = cos_clamp(cos_sqrt_rn(t2));
   }
   n1 = __shfl(n1, gbase, 64);
   n2 = __shfl(n2, gbase, 64);
