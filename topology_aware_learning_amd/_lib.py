@@ -15,7 +15,9 @@ from pathlib import Path
 # runtime, so torch's streams and device pointers are valid in our calls.
 import torch  # noqa: F401  (import order matters, see above)
 
-LIB_PATH = Path(__file__).resolve().parent / "libtal_agg.so"
+# TAL_LIB_PATH: an alternative build of the same library (A/B probes under tools/); default the
+# in-tree product build
+LIB_PATH = Path(os.environ.get("TAL_LIB_PATH") or Path(__file__).resolve().parent / "libtal_agg.so")
 
 TAL_OK = 0
 TAL_ERR_INVALID = 1

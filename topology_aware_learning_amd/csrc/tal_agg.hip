@@ -957,6 +957,9 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   const int n_sets = (L.nr + kRpw - 1) / kRpw;
   float4 v[J];
   auto load_tile = [&](int64_t tt) {
+#ifdef TAL_PROBE_NOLOAD  // A/B probe: no HBM reads (the tile keeps the first tile's values)
+    if (tt != blockIdx.x) return;
+#endif
     const int64_t col = tt * C4 + c;
     if (col < n4) {
 #pragma unroll
@@ -974,6 +977,13 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
     __syncthreads();
     if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
     const int64_t col = t * C4 + cl;
+#ifdef TAL_PROBE_NOCOMP  // A/B probe (tools/gpu_k3n_probe.sh): stores without the row arithmetic
+    for (int k = 0; k * kW < n_sets; ++k) {
+      const int r = narrow_set(k, wave, kW) * kRpw + sub;
+      if (r < L.nr && col < n4) Io<T>::st(pout, static_cast<int64_t>(L.out[r]) * ld_out4 + col, make_float4(0.f, 0.f, 0.f, 0.f));
+    }
+    continue;
+#endif
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       if (rq1[k] > rq0[k]) {

@@ -79,24 +79,31 @@ def positions(owner, world: int):
 
 
 def exchange_bytes(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: int = 0) -> dict:
-    """Largest per-rank link volume of one round (bytes in or out, whichever is larger) for
-    each exchange: 'halo' = distinct remote neighbor models, 'transpose' = 2 x (world-1)/world
-    of the rank's own models."""
+    """Link volumes of one round for each exchange.  'halo' / 'transpose': the largest per-rank
+    volume (bytes in or out, whichever is larger): distinct remote neighbor models, resp.
+    2 x (world-1)/world of the rank's own models.  'halo_link' / 'transpose_link': the largest
+    volume on one directed GPU pair (each pair has its own xGMI link): the halo's biggest
+    per-peer message, resp. 2 x own / world (both all-to-alls spread every rank's models evenly
+    over its links)."""
     owner = np.asarray(owner)
     row = 4 * n_f32 + 2 * n_b16 + 8 * n_i64
     specs = [build_shard(orders, [[1.0] * len(o) for o in orders], owner, r, world) for r in range(world)]
     halo = max(max(len(s.halo), sum(len(v) for v in s.send.values())) for s in specs) * row
+    halo_link = max([len(v) for s in specs for v in list(s.send.values()) + list(s.recv.values())] or [0]) * row
     own = max(len(s.own) for s in specs)
-    return dict(halo=int(halo), transpose=int(2 * own * row * (world - 1) // world))
+    return dict(halo=int(halo), transpose=int(2 * own * row * (world - 1) // world),
+                halo_link=int(halo_link), transpose_link=int(-(-2 * own * row // world)))
 
 
 def choose_exchange(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: int = 0) -> str:
-    """'transpose' when it moves clearly fewer bytes than the halo (random expanders at 4+
-    ranks), else 'halo' (rings, cliques, community graphs; 2 ranks)."""
+    """'transpose' when its busiest link carries clearly fewer bytes than the halo's busiest
+    link (random expanders at 4+ ranks, 60-cliques spread over 4 GPUs), else 'halo' (rings,
+    community graphs, 2 ranks).  Both exchanges use the pairs' xGMI links concurrently, so the
+    round's link time is set by the busiest pair, not by a rank's total."""
     if world < 2:
         return "halo"
     b = exchange_bytes(orders, owner, world, n_f32, n_i64, n_b16)
-    return "transpose" if b["transpose"] < 0.9 * b["halo"] else "halo"
+    return "transpose" if b["transpose_link"] < 0.9 * b["halo_link"] else "halo"
 
 
 @dataclass
