@@ -87,8 +87,21 @@ __device__ __forceinline__ float4 first4(float w, float4 x) {
                      first_term<EXACT>(w, x.z), first_term<EXACT>(w, x.w));
 }
 
+typedef float v2f_t __attribute__((ext_vector_type(2)));
+
+// FMA mode: two packed fmas on the natural register pairs (x, y) and (z, w).  Written per
+// component, the SLP vectorizer paired (x, z) / (y, w) and shuffled with 12 v_mov_b32 per batch
+// of four operands in the narrow row loop (config 5 bf16: 1.46e10 VALU instructions per round).
+__device__ __forceinline__ float4 fma4(float w, float4 x, float4 a) {
+  const v2f_t w2 = {w, w};
+  const v2f_t lo = __builtin_elementwise_fma(w2, v2f_t{x.x, x.y}, v2f_t{a.x, a.y});
+  const v2f_t hi = __builtin_elementwise_fma(w2, v2f_t{x.z, x.w}, v2f_t{a.z, a.w});
+  return make_float4(lo.x, lo.y, hi.x, hi.y);
+}
+
 template <bool EXACT>
 __device__ __forceinline__ float4 next4(float4 a, float w, float4 x) {
+  if constexpr (!EXACT) return fma4(w, x, a);
   return make_float4(next_term<EXACT>(a.x, w, x.x), next_term<EXACT>(a.y, w, x.y),
                      next_term<EXACT>(a.z, w, x.z), next_term<EXACT>(a.w, w, x.w));
 }
@@ -828,6 +841,46 @@ __device__ __forceinline__ float4 narrow_row_roww(const float4* s_data, const Na
   // asm so that the cursor keeps one register across the loop)
   uint32_t q = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)(s4 + b0)));
   const uint32_t qe = q + 8 * (b1 - b0);
+#ifdef TAL_PROBE_PIPE
+  // probe: data reads one batch ahead, unrolled twice (two register batches alternate, no
+  // moves); slots two batches ahead (the staged pad covers both)
+  auto rd4 = [&](uint2 w, float4* x) {
+    x[0] = lds_f4(slot_addr_lo(w.x, base));
+    x[1] = lds_f4(slot_addr_hi(w.x, base));
+    x[2] = lds_f4(slot_addr_lo(w.y, base));
+    x[3] = lds_f4(slot_addr_hi(w.y, base));
+  };
+  if (q < qe) {
+    float4 x[4], y[4];
+    uint2 e = lds_u2(q);
+    rd4(e, x);
+    asm("v_add_u32 %0, 8, %0" : "+v"(q));
+    e = lds_u2(q);
+    while (true) {
+      if (q >= qe) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = next4t<T, EXACT>(acc, w, x[u]);
+        break;
+      }
+      rd4(e, y);
+      asm("v_add_u32 %0, 8, %0" : "+v"(q));
+      e = lds_u2(q);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = next4t<T, EXACT>(acc, w, x[u]);
+      if (q >= qe) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = next4t<T, EXACT>(acc, w, y[u]);
+        break;
+      }
+      rd4(e, x);
+      asm("v_add_u32 %0, 8, %0" : "+v"(q));
+      e = lds_u2(q);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = next4t<T, EXACT>(acc, w, y[u]);
+    }
+  }
+  return acc;
+#endif
   uint2 e = lds_u2(q);
   while (q < qe) {
     float4 x[4];
@@ -1497,8 +1550,10 @@ int32_t launch_round_narrow_jr(const T* pin, int64_t ld_in, T* pout, int64_t ld_
   // row extents in registers
   constexpr int kNP = J >= 12 ? kNarrowPasses / 2 : kNarrowPasses;  // J = 12: VGPRs for the staging
   auto k = k_round_f32_narrow<C4, kNarrowThreads, J, kNP, EXACT, T, ROWW>;
+#ifndef TAL_PROBE_ONEWG  // probe: keep one workgroup per CU (the register-rich variant)
   if constexpr (J <= 4)
     if (2 * lds <= 160 * 1024) k = k_round_f32_narrow<C4, kNarrowThreads, J, 0, EXACT, T, ROWW>;
+#endif
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;
   const int64_t tiles = (n4 + C4 - 1) / C4;
