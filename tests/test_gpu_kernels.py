@@ -237,6 +237,16 @@ def test_round_narrow_row_uniform_weights_signed_zero(cuda, sign):
         ob = torch.zeros_like(pb)
         ops.round_bf16(pb, ob, plan)
         assert np.array_equal(ob.cpu().view(torch.int16).numpy().view(np.uint16), refb), c4
+        # FMA mode: the accumulator starts at -0.0 and padding is fma(w, +-0, acc); bitwise
+        # against the bf16 oracle's fused chain and, for fp32, against K1-FMA row by row
+        refbf = oracle.round_bf16(bits, row_ptr, col, w, out_rows, exact=False)
+        ops.round_bf16(pb, ob, plan, mode=ops.MODE_FMA)
+        assert np.array_equal(ob.cpu().view(torch.int16).numpy().view(np.uint16), refbf), c4
+        ops.round_f32(pin, pout, plan, mode=ops.MODE_FMA)
+        chk = torch.empty(n, dtype=torch.float32, device=cuda)
+        for r in range(rows):
+            ops.agg_f32([pin[j] for j in orders[r]], ws[r], chk, mode=ops.MODE_FMA)
+            assert torch.equal(chk.view(torch.int32), pout[r].view(torch.int32)), (c4, r)
 
 
 @pytest.mark.parametrize("c4", [16, 32])

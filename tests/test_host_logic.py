@@ -236,6 +236,44 @@ def test_narrow_roww_encoding():
     assert plan.info.narrow_roww == 0
 
 
+@pytest.mark.parametrize("c4", [16, 32])
+def test_narrow_roww_pass_uniform_batches(c4):
+    """ROWW rows ordered by operand count; every pass of 64 / c4 consecutive rows padded to the
+    batch count of its first row (the kernel's row loop then counts on the scalar unit); the
+    padding reads the zero tile."""
+    g = nx.barabasi_albert_graph(61, 3, seed=2)  # degrees 3 .. 30
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(61)]
+    ws = [ra.unweighted_weights(len(o)) for o in orders]
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    plan = ops.build_plan(row_ptr, col, w, np.arange(61, dtype=np.int32), c4=c4, lds_bytes=160 * 1024)
+    i, h = plan.info, plan.host
+    assert i.narrow_roww == 1 and i.n_groups == 1
+    rp = h[i.off_nrow_ptr: i.off_nrow_ptr + i.rows + 1]
+    slots = h[i.off_npairs: i.off_npairs + (i.npairs + 1) // 2].view(np.uint16)[: i.npairs]
+    orow = h[i.off_out_row: i.off_out_row + i.rows]
+    src = h[i.off_src_row: i.off_src_row + i.total_src]
+    lens = [len(orders[orow[r]]) for r in range(i.rows)]
+    assert lens == sorted(lens, reverse=True)
+    rpw = 64 // c4
+    for r in range(i.rows):
+        lead = r // rpw * rpw
+        assert rp[r + 1] - rp[r] == 4 * ((lens[lead] + 3) // 4)
+        run = slots[rp[r]: rp[r + 1]] // c4
+        assert [int(src[x]) for x in run[: lens[r]]] == orders[orow[r]]
+        assert np.all(run[lens[r]:] == i.total_src)  # the -0.0 tile (positive weights)
+
+
+def test_narrow_roww_needs_16bit_slots():
+    """ROWW slots are 16-bit (slot * c4): a round whose sources could overflow them takes the
+    pairs form instead of silently wrapping."""
+    n = 5000
+    orders = [[(i - 1) % n, (i + 1) % n, i] for i in range(n)]
+    orders = [sorted(o[:2]) + [o[2]] for o in orders]
+    row_ptr, col, w = ra.round_csr(orders, [ra.unweighted_weights(3)] * n)
+    plan = ops.build_plan(row_ptr, col, w, np.arange(n, dtype=np.int32), c4=16, lds_bytes=80 * 1024)
+    assert plan.info.narrow_roww == 0
+
+
 def test_round_plan_reconstructs_csr():
     g = nx.random_regular_graph(8, 64, seed=0)
     orders = [sorted(g.neighbors(i)) + [i] for i in range(64)]

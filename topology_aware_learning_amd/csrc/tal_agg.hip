@@ -736,11 +736,10 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const T* __restrict
 constexpr int kNarrowPasses = 4;
 
 struct NarrowLds {
-  const int32_t* rowptr;  // [nr + 1], group-relative pair (ROWW: slot) index
+  const int32_t* rowptr;  // [nr + 1], group-relative pair index (pairs form)
   const int2* pairs;      // [group pairs + 4 read-ahead] (slot * C4, fp32 weight bits)
-  const uint16_t* slots;  // ROWW: [group slots + 8 read-ahead] slot * C4
-  const float* rw;        // ROWW: [nr] row weights
-  const int32_t* out;     // [nr] pool_out row
+  const int32_t* out;     // [nr] pool_out row (pairs form)
+  uint32_t rec;           // ROWW: LDS byte address of the row records (16 B each, see below)
   int nr;
 };
 
@@ -749,9 +748,21 @@ __host__ __device__ constexpr size_t narrow_lds_bytes(int64_t max_src, int64_t m
   return static_cast<size_t>((max_src + 1) * c4 * 16 + (2 * max_rows + 2 + 2 * (max_pairs + 4)) * 4 + 16);
 }
 
-// ROWW carve: [ns + 2 tiles (-0.0, +0.0)][rowptr nr+1][w nr][out nr][pad to 8 B][slots + 8]
+// ROWW (row-uniform weights) carve: [ns + 2 tiles (-0.0, +0.0)][records][slots + 8 read-ahead].
+// The rows of a pass (kRpw = 64 / c4 consecutive plan rows, one per lane group of a wavefront)
+// are padded on the host to one batch count, so the row loop's trip count is wave-uniform and
+// runs on the scalar unit; one 16-B record per row (rows padded to whole passes; a padding row
+// reads its pass's first row and stores nothing): {LDS byte address of the row's first slot
+// word, batches of four slots, fp32 weight bits, pool_out row or -1}.
+__host__ __device__ constexpr int64_t narrow_roww_records(int64_t nr, int c4) {
+  return (nr + 64 / c4 - 1) / (64 / c4) * (64 / c4);
+}
 __host__ __device__ constexpr size_t narrow_roww_lds_bytes(int64_t ns, int64_t nr, int64_t nslots, int c4) {
-  return static_cast<size_t>((ns + 2) * c4 * 16 + (3 * nr + 2) * 4 + (nslots + 8) * 2 + 16);
+  return static_cast<size_t>((ns + 2) * c4 * 16 + narrow_roww_records(nr, c4) * 16 + (nslots + 8) * 2 + 16);
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)p));
 }
 
 template <int C4>
@@ -762,30 +773,32 @@ __device__ __forceinline__ NarrowLds stage_narrow_roww(const PlanView& p, int g,
   const int e_beg = p.nrow_ptr[r_beg];  // a multiple of 4 (every run is)
   const int ne = p.nrow_ptr[r_beg + L.nr] - e_beg;
   const int ns = p.grp_src_ptr[g + 1] - p.grp_src_ptr[g];
+  constexpr int kRpw = 64 / C4;
+  const int nrec = static_cast<int>(narrow_roww_records(L.nr, C4));
   // offsets in 32-bit words from s_data (index arithmetic keeps the LDS address space: a
   // pointer rebuilt from an integer would become a generic one and every read a flat load)
   int32_t* base32 = reinterpret_cast<int32_t*>(s_data);
-  const int o_rowptr = (ns + 2) * C4 * 4;
-  int32_t* rowptr = base32 + o_rowptr;
-  float* rw = reinterpret_cast<float*>(rowptr + L.nr + 1);
-  int32_t* out = reinterpret_cast<int32_t*>(rw + L.nr);
-  uint32_t* slots = reinterpret_cast<uint32_t*>(base32 + ((o_rowptr + 3 * L.nr + 2) & ~1));  // 8-B aligned
+  int32_t* rec = base32 + (ns + 2) * C4 * 4;
+  uint32_t* slots = reinterpret_cast<uint32_t*>(rec + 4 * nrec);
+  const uint32_t slots_addr = lds_addr(slots);
   for (int k = threadIdx.x; k < 2 * C4; k += nthreads)  // zero tiles: slot ns = -0.0, ns + 1 = +0.0
     s_data[static_cast<size_t>(ns) * C4 + k] = k < C4 ? make_float4(-0.f, -0.f, -0.f, -0.f)
                                                       : make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int k = threadIdx.x; k <= L.nr; k += nthreads) rowptr[k] = p.nrow_ptr[r_beg + k] - e_beg;
-  for (int k = threadIdx.x; k < L.nr; k += nthreads) {
-    rw[k] = __int_as_float(p.nrow_w[r_beg + k]);
-    out[k] = p.out_row[r_beg + k];
+  for (int k = threadIdx.x; k < nrec; k += nthreads) {
+    const int row = k < L.nr ? k : k / kRpw * kRpw;  // padding rows: their pass's first row
+    const int q0 = p.nrow_ptr[r_beg + row] - e_beg, q1 = p.nrow_ptr[r_beg + row + 1] - e_beg;
+    rec[4 * k + 0] = static_cast<int32_t>(slots_addr + 2u * static_cast<uint32_t>(q0));
+    rec[4 * k + 1] = (q1 - q0) / 4;
+    rec[4 * k + 2] = p.nrow_w[r_beg + row];
+    rec[4 * k + 3] = k < L.nr ? p.out_row[r_beg + k] : -1;
   }
   const int nw = ne / 2;  // ne is a multiple of 4: whole words
   for (int k = threadIdx.x; k < nw + 4; k += nthreads)  // + 4 read-ahead words (never used)
     slots[k] = k < nw ? static_cast<uint32_t>(p.npairs[e_beg / 2 + k]) : 0u;
-  L.rowptr = rowptr;
+  L.rowptr = nullptr;
   L.pairs = nullptr;
-  L.slots = reinterpret_cast<const uint16_t*>(slots);
-  L.rw = rw;
-  L.out = out;
+  L.out = nullptr;
+  L.rec = lds_addr(rec);
   return L;
 }
 
@@ -811,78 +824,40 @@ __device__ __forceinline__ float4 lds_f4(uint32_t addr) {
   return make_float4(q.x, q.y, q.z, q.w);
 }
 
-// One ROWW row: the accumulator starts at -0.0, every batch of four slots is one 8-B LDS read
-// (the next batch's read is issued ahead of this batch's data reads).
+__device__ __forceinline__ uint4 lds_u4(uint32_t addr) {
+  typedef unsigned int u32x4_lds __attribute__((ext_vector_type(4)));
+  const u32x4_lds q = *reinterpret_cast<__attribute__((address_space(3))) const u32x4_lds*>(static_cast<uintptr_t>(addr));
+  return make_uint4(q.x, q.y, q.z, q.w);
+}
+
+// One ROWW row from its record: the accumulator starts at -0.0 and takes `nb` batches of four
+// slots (one 8-B LDS read each, the next batch's read issued ahead of this batch's data reads).
+// nb is the same for every row of the pass (host padding), so the loop counts on the scalar
+// unit: per batch 4 address + 16 (EXACT) or 8 (FMA) arithmetic VALU and one cursor add.
 template <typename T, bool EXACT>
-__device__ __forceinline__ float4 narrow_row_roww(const float4* s_data, const NarrowLds& L, int r, int cl) {
-  const uint32_t b0 = static_cast<uint32_t>(L.rowptr[r]) >> 2, b1 = static_cast<uint32_t>(L.rowptr[r + 1]) >> 2;
-  const float w = L.rw[r];
+__device__ __forceinline__ float4 narrow_row_roww(uint4 rc, uint32_t base) {
+  const int nb = __builtin_amdgcn_readfirstlane(static_cast<int>(rc.y));
+  const float w = __uint_as_float(rc.z);
+  uint32_t q = rc.x;
   float4 acc = make_float4(-0.f, -0.f, -0.f, -0.f);
-  const uint2* s4 = reinterpret_cast<const uint2*>(L.slots);
+  uint2 e = lds_u2(q);
   if constexpr (kIsBf16<T> && EXACT) {
-    // bf16 EXACT (two roundings per operand): the compiler's own schedule of the plain loop
-    // measured 64.6 ms on config 5 against 74.6 ms with the decode below
-    uint2 e = s4[b0];
-    for (uint32_t b = b0; b < b1; ++b) {
+    // bf16 EXACT (two roundings per operand): plain extraction (the compiler's own schedule of
+    // this form measured faster than the decode below for this instantiation)
+    for (int b = 0; b < nb; ++b) {
       float4 x[4];
-      x[0] = s_data[(e.x & 0xffffu) + cl];
-      x[1] = s_data[(e.x >> 16) + cl];
-      x[2] = s_data[(e.y & 0xffffu) + cl];
-      x[3] = s_data[(e.y >> 16) + cl];
-      e = s4[b + 1];
+      x[0] = lds_f4(base + ((e.x & 0xffffu) << 4));
+      x[1] = lds_f4(base + ((e.x >> 16) << 4));
+      x[2] = lds_f4(base + ((e.y & 0xffffu) << 4));
+      x[3] = lds_f4(base + ((e.y >> 16) << 4));
+      q += 8;
+      e = lds_u2(q);
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc = next4t<T, EXACT>(acc, w, x[u]);
     }
     return acc;
   }
-  const uint32_t base = static_cast<uint32_t>(
-      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)(s_data + cl)));
-  // the batch cursor is the LDS address itself: one add and one compare per batch (the add in
-  // asm so that the cursor keeps one register across the loop)
-  uint32_t q = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)(s4 + b0)));
-  const uint32_t qe = q + 8 * (b1 - b0);
-#ifdef TAL_PROBE_PIPE
-  // probe: data reads one batch ahead, unrolled twice (two register batches alternate, no
-  // moves); slots two batches ahead (the staged pad covers both)
-  auto rd4 = [&](uint2 w, float4* x) {
-    x[0] = lds_f4(slot_addr_lo(w.x, base));
-    x[1] = lds_f4(slot_addr_hi(w.x, base));
-    x[2] = lds_f4(slot_addr_lo(w.y, base));
-    x[3] = lds_f4(slot_addr_hi(w.y, base));
-  };
-  if (q < qe) {
-    float4 x[4], y[4];
-    uint2 e = lds_u2(q);
-    rd4(e, x);
-    asm("v_add_u32 %0, 8, %0" : "+v"(q));
-    e = lds_u2(q);
-    while (true) {
-      if (q >= qe) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) acc = next4t<T, EXACT>(acc, w, x[u]);
-        break;
-      }
-      rd4(e, y);
-      asm("v_add_u32 %0, 8, %0" : "+v"(q));
-      e = lds_u2(q);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc = next4t<T, EXACT>(acc, w, x[u]);
-      if (q >= qe) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) acc = next4t<T, EXACT>(acc, w, y[u]);
-        break;
-      }
-      rd4(e, x);
-      asm("v_add_u32 %0, 8, %0" : "+v"(q));
-      e = lds_u2(q);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc = next4t<T, EXACT>(acc, w, y[u]);
-    }
-  }
-  return acc;
-#endif
-  uint2 e = lds_u2(q);
-  while (q < qe) {
+  for (int b = 0; b < nb; ++b) {
     float4 x[4];
     x[0] = lds_f4(slot_addr_lo(e.x, base));
     x[1] = lds_f4(slot_addr_hi(e.x, base));
@@ -998,16 +973,22 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
     srow[j] = src < ns ? p.src_row[s_beg + src] : -1;
   }
   __syncthreads();  // plan slice staged
-  constexpr int kNP = NP > 0 ? NP : 1;
+  // pairs form: the first NP row sets' extents in registers (ROWW reads its records instead)
+  constexpr int kNP = (NP > 0 && !ROWW) ? NP : 1;
   int rq0[kNP], rq1[kNP], rout[kNP];
+  if constexpr (!ROWW) {
 #pragma unroll
-  for (int k = 0; k < NP; ++k) {
-    const int r = narrow_set(k, wave, kW) * kRpw + sub;
-    rq0[k] = r < L.nr ? L.rowptr[r] : 0;
-    rq1[k] = r < L.nr ? L.rowptr[r + 1] : 0;
-    rout[k] = r < L.nr ? L.out[r] : 0;
+    for (int k = 0; k < NP; ++k) {
+      const int r = narrow_set(k, wave, kW) * kRpw + sub;
+      rq0[k] = r < L.nr ? L.rowptr[r] : 0;
+      rq1[k] = r < L.nr ? L.rowptr[r + 1] : 0;
+      rout[k] = r < L.nr ? L.out[r] : 0;
+    }
   }
   const int n_sets = (L.nr + kRpw - 1) / kRpw;
+  // ROWW: this lane's column base in the data tile, and its record offset within a pass
+  const uint32_t col_base = lds_addr(s_data + cl);
+  const uint32_t rec_lane = L.rec + 16u * static_cast<uint32_t>(sub);
   float4 v[J];
   auto load_tile = [&](int64_t tt) {
 #ifdef TAL_PROBE_NOLOAD  // A/B probe: no HBM reads (the tile keeps the first tile's values)
@@ -1030,32 +1011,32 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
     __syncthreads();
     if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
     const int64_t col = t * C4 + cl;
+    if constexpr (ROWW) {
+      for (int k = 0; k * kW < n_sets; ++k) {  // passes: row sets in snake order
+        const int set = narrow_set(k, wave, kW);
+        if (set >= n_sets) continue;  // wave-uniform
+        const uint4 rc = lds_u4(rec_lane + 16u * static_cast<uint32_t>(set * kRpw));
 #ifdef TAL_PROBE_NOCOMP  // A/B probe (tools/gpu_k3n_probe.sh): stores without the row arithmetic
-    for (int k = 0; k * kW < n_sets; ++k) {
-      const int r = narrow_set(k, wave, kW) * kRpw + sub;
-      if (r < L.nr && col < n4) Io<T>::st(pout, static_cast<int64_t>(L.out[r]) * ld_out4 + col, make_float4(0.f, 0.f, 0.f, 0.f));
-    }
-    continue;
+        const float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#else
+        const float4 acc = narrow_row_roww<T, EXACT>(rc, col_base);
 #endif
+        if (static_cast<int32_t>(rc.w) >= 0 && col < n4)
+          Io<T>::st(pout, static_cast<int64_t>(static_cast<int32_t>(rc.w)) * ld_out4 + col, acc);
+      }
+      continue;
+    }
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       if (rq1[k] > rq0[k]) {
-        float4 acc;
-        if constexpr (ROWW)
-          acc = narrow_row_roww<T, EXACT>(s_data, L, narrow_set(k, wave, kW) * kRpw + sub, cl);
-        else
-          acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, rq0[k], rq1[k], cl);
+        const float4 acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, rq0[k], rq1[k], cl);
         if (col < n4) Io<T>::st(pout, static_cast<int64_t>(rout[k]) * ld_out4 + col, acc);
       }
     }
     for (int k = NP; k * kW < n_sets; ++k) {  // row sets beyond the register-held ones
       const int r = narrow_set(k, wave, kW) * kRpw + sub;
       if (r < L.nr) {
-        float4 acc;
-        if constexpr (ROWW)
-          acc = narrow_row_roww<T, EXACT>(s_data, L, r, cl);
-        else
-          acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, L.rowptr[r], L.rowptr[r + 1], cl);
+        const float4 acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, L.rowptr[r], L.rowptr[r + 1], cl);
         if (col < n4) Io<T>::st(pout, static_cast<int64_t>(L.out[r]) * ld_out4 + col, acc);
       }
     }
@@ -2224,7 +2205,8 @@ bool rows_uniform_weights(int32_t rows, const int32_t* row_ptr_host, const doubl
   return true;
 }
 
-// Greedy grouping: a row joins the current group unless that breaks `fits(n_src, n_rows, n_ops)`.
+// Greedy grouping: a row joins the current group unless that breaks
+// `fits(n_src, n_rows, n_ops, first_row)` (the candidate group is rows first_row .. +n_rows-1).
 template <class Fits>
 int32_t group_rows(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host, int32_t max_col,
                    Fits fits, Groups* out) {
@@ -2245,7 +2227,8 @@ int32_t group_rows(int32_t rows, const int32_t* row_ptr_host, const int32_t* col
     fresh_of(r, g, &fresh);
     const int64_t row_nnz = row_ptr_host[r + 1] - row_ptr_host[r];
     const int64_t cur_rows = r - G.row_ptr.back();
-    if (!fits(static_cast<int64_t>(G.srcs[g].size() + fresh.size()), cur_rows + 1, cur_nnz + row_nnz)) {
+    if (!fits(static_cast<int64_t>(G.srcs[g].size() + fresh.size()), cur_rows + 1, cur_nnz + row_nnz,
+              static_cast<int64_t>(G.row_ptr.back()))) {
       if (cur_rows > 0) {
         G.row_ptr.push_back(r);
         G.srcs.emplace_back();
@@ -2253,7 +2236,7 @@ int32_t group_rows(int32_t rows, const int32_t* row_ptr_host, const int32_t* col
         g = static_cast<int>(G.srcs.size()) - 1;
         fresh_of(r, g, &fresh);
       }
-      if (!fits(static_cast<int64_t>(fresh.size()), 1, row_nnz))
+      if (!fits(static_cast<int64_t>(fresh.size()), 1, row_nnz, static_cast<int64_t>(r)))
         return fail(TAL_ERR_CAPACITY, "tal_round_plan_build: row " + std::to_string(r) +
                                           " has more distinct sources than one LDS tile holds");
     }
@@ -2265,6 +2248,26 @@ int32_t group_rows(int32_t rows, const int32_t* row_ptr_host, const int32_t* col
   }
   G.row_ptr.push_back(rows);
   return TAL_OK;
+}
+
+// ROWW slots are 16-bit (slot * c4 float4 units, the zero tiles at ns and ns + 1 included).
+bool roww_slots_fit(int32_t max_col, int32_t c4) {
+  return (static_cast<int64_t>(max_col) + 3) * c4 <= 0xffff;
+}
+
+// Slots a group of rows r0 .. r0+nr-1 takes in the ROWW encoding: the narrow builder orders a
+// group's rows by operand count (descending) and pads each pass of 64 / c4 consecutive rows to
+// the batch count of its first (longest) row.
+int64_t roww_padded_slots(const int32_t* row_ptr_host, int64_t r0, int64_t nr, int32_t c4,
+                          std::vector<int32_t>* batches) {
+  batches->resize(static_cast<size_t>(nr));
+  for (int64_t i = 0; i < nr; ++i)
+    (*batches)[i] = (row_ptr_host[r0 + i + 1] - row_ptr_host[r0 + i] + 3) / 4;
+  std::sort(batches->begin(), batches->end(), std::greater<int32_t>());
+  const int64_t rpw = 64 / c4;
+  int64_t slots = 0;
+  for (int64_t i = 0; i < nr; i += rpw) slots += 4LL * (*batches)[i] * std::min(rpw, nr - i);
+  return slots;
 }
 
 // Lay the plan blob out (see tal_round_plan_info).  rb = dense row-block size (0 = sparse
@@ -2355,7 +2358,7 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
     lds_need = std::max(lds_need, group_lds_bytes(grp_src_ptr[g + 1] - grp_src_ptr[g], nr, no, c4));
   }
   const int64_t scalar_need = lds_need;
-  const bool roww = c4 < 64 && rows_uniform_weights(rows, row_ptr_host, w_host);
+  const bool roww = c4 < 64 && rows_uniform_weights(rows, row_ptr_host, w_host) && roww_slots_fit(max_col, c4);
   std::vector<uint16_t> nsl;   // ROWW slots
   std::vector<int32_t> nrw;    // ROWW row weights
   if (c4 < 64) {
@@ -2369,14 +2372,19 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
       const int64_t g0 = roww ? static_cast<int64_t>(nsl.size()) : static_cast<int64_t>(npr.size()) / 2;
       for (int r = grp_row_ptr[g]; r < grp_row_ptr[g + 1]; ++r) {
         const int32_t k0 = row_ptr_host[r], k1 = row_ptr_host[r + 1];
-        if (roww) {  // slots only, whole batches of 4; the pad reads the zero tile that keeps -0
+        if (roww) {  // slots only, in batches of 4, every row of a pass padded to the batch count
+          // of the pass's first (longest: rows are ordered by count) row; the pad reads the zero
+          // tile that keeps -0: fl(w * z) is -0.0 for z = -0.0 (w >= 0) or +0.0 (w < 0)
           const float wf = static_cast<float>(w_host[k0]);
           int32_t wb;
           memcpy(&wb, &wf, 4);
           nrw.push_back(wb);
+          const int32_t lead = grp_row_ptr[g] + (r - grp_row_ptr[g]) / (64 / c4) * (64 / c4);
+          const int64_t nb = (row_ptr_host[lead + 1] - row_ptr_host[lead] + 3) / 4;
+          const size_t start = nsl.size();
           for (int32_t k = k0; k < k1; ++k) nsl.push_back(static_cast<uint16_t>(slot[k] * c4));
           const uint16_t zero = static_cast<uint16_t>((std::signbit(wf) ? ns + 1 : ns) * c4);
-          while (nsl.size() % 4) nsl.push_back(zero);
+          while (nsl.size() < start + 4 * static_cast<size_t>(nb)) nsl.push_back(zero);
           nrp[r + 1] = static_cast<int32_t>(nsl.size());
           continue;
         }
@@ -2614,14 +2622,16 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
     return fail(TAL_ERR_INVALID, "tal_round_plan_build: dense_rb must be 0, 8 or -1");
   // group consecutive rows while the union of their sources fits the LDS budget (both round
   // kernels stage 16*c4 bytes per source; the scalar one also the plan slice)
-  const bool roww = c4 < 64 && rows_uniform_weights(rows, row_ptr_host, w_host);
-  auto fits = [&](int64_t ns, int64_t nr, int64_t no) {
+  const bool roww = c4 < 64 && rows_uniform_weights(rows, row_ptr_host, w_host) && roww_slots_fit(max_col, c4);
+  std::vector<int32_t> batches;
+  auto fits = [&](int64_t ns, int64_t nr, int64_t no, int64_t r0) {
     const int64_t sliced = group_lds_bytes(ns, nr, no, c4);
     if (c4 >= 64) return sliced <= lds_bytes;
-    // narrow kernel: its own carve (padding <= 3 per row, read-ahead) within the budget; the
-    // staged scalar tail kernel within the hardware's 160 KiB
-    const int64_t narrow = static_cast<int64_t>(roww ? narrow_roww_lds_bytes(ns, nr, no + 3 * nr, c4)
-                                                     : narrow_lds_bytes(ns, nr, no + 3 * nr, c4));
+    // narrow kernel: its own carve (exact ROWW padding; pairs: <= 3 per row) and read-ahead
+    // within the budget; the staged scalar tail kernel within the hardware's 160 KiB
+    const int64_t narrow = static_cast<int64_t>(
+        roww ? narrow_roww_lds_bytes(ns, nr, roww_padded_slots(row_ptr_host, r0, nr, c4, &batches), c4)
+             : narrow_lds_bytes(ns, nr, no + 3 * nr, c4));
     return narrow <= lds_bytes && sliced <= 160 * 1024;
   };
   Groups grp;
@@ -2671,7 +2681,7 @@ int32_t tal_round_plan_build_stream(int32_t rows, const int32_t* row_ptr_host,
                                      std::to_string(kStreamMaxRows) + ", max_group_src >= 0");
   if (!reference_order(rows, row_ptr_host, col_host))
     return fail(TAL_ERR_INVALID, "tal_round_plan_build_stream: rows must list operands in reference order");
-  auto fits = [&](int64_t ns, int64_t nr, int64_t) {
+  auto fits = [&](int64_t ns, int64_t nr, int64_t, int64_t) {
     return nr <= max_group_rows && (max_group_src == 0 || ns <= max_group_src || nr == 1);
   };
   Groups grp;
