@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 TAG=${1:-k3n2}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG; mkdir -p $OUT
 SPEC='{"c4": 16, "dense": 0, "lds": 81920}'
-for v in ${VARIANTS:-base onewg pipe onewgnoload pipenoload}; do
+for v in ${VARIANTS:-base nocomp noload}; do
   if [ $v = base ]; then unset TAL_LIB_PATH; else export TAL_LIB_PATH=$GRAFT_REPO_ROOT/tools/tune/libtal_agg_$v.so; fi
   for dt in f32 bf16; do
     timeout -k 10 300 python bench.py --graph sbm --devices 256 --model vit_b16 --dtype $dt --steps 3 --warmup 1 \

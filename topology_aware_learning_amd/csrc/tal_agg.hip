@@ -419,7 +419,10 @@ struct Io;
 
 template <>
 struct Io<float> {
+  typedef float4 raw_t;  // a staged chunk as loaded (converted when written to LDS)
   static __device__ __forceinline__ float4 ld(const float* b, int64_t i4) { return ld_stream(b, i4); }
+  static __device__ __forceinline__ raw_t ld_raw(const float* b, int64_t i4) { return ld_stream(b, i4); }
+  static __device__ __forceinline__ float4 f4(raw_t r) { return r; }
   static __device__ __forceinline__ void st(float* b, int64_t i4, float4 v) { st_stream(b, i4, v); }
   static __device__ __forceinline__ float ld1(const float* b, int64_t e) { return b[e]; }
   static __device__ __forceinline__ void st1(float* b, int64_t e, float v) { b[e] = v; }
@@ -427,12 +430,22 @@ struct Io<float> {
 
 template <>
 struct Io<uint16_t> {
-  static __device__ __forceinline__ float4 ld(const uint16_t* b, int64_t i4) {
-    const u32x2 q = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(b) + i4);
+  typedef u32x2 raw_t;
+  static __device__ __forceinline__ float4 ld(const uint16_t* b, int64_t i4) { return f4(ld_raw(b, i4)); }
+  static __device__ __forceinline__ raw_t ld_raw(const uint16_t* b, int64_t i4) {
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(b) + i4);
+  }
+  static __device__ __forceinline__ float4 f4(raw_t q) {
     return make_float4(bf16_lo(q.x), bf16_hi(q.x), bf16_lo(q.y), bf16_hi(q.y));
   }
   static __device__ __forceinline__ void st(uint16_t* b, int64_t i4, float4 v) {
-    const u32x2 q = {store_bf16x2(v.x, v.y), store_bf16x2(v.z, v.w)};
+    u32x2 q = {cvt_bf16x2(v.x, v.y), cvt_bf16x2(v.z, v.w)};
+    // NaN canonicalisation (store_bf16x2) only where a lane holds one: two unordered compares
+    // on the common path instead of four compare-and-selects
+    if (__builtin_isunordered(v.x, v.y) || __builtin_isunordered(v.z, v.w)) {
+      q.x = store_bf16x2(v.x, v.y);
+      q.y = store_bf16x2(v.z, v.w);
+    }
     __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(b) + i4);
   }
   static __device__ __forceinline__ float ld1(const uint16_t* b, int64_t e) {
@@ -966,11 +979,16 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int sub = lane / C4;
   const int cl = lane % C4;
-  int srow[J];
+  // Staging is branch-free, so that the compiler's wait analysis sees every load land in its
+  // register unconditionally (a conditional load made it wait for each load before issuing the
+  // next: four serial HBM round trips per tile).  A lane past the group's sources reloads
+  // source 0's chunk of its column and writes it where source 0's own lane does (same value).
+  int srow[J], widx[J];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int src = (j * NT + threadIdx.x) / C4;
-    srow[j] = src < ns ? p.src_row[s_beg + src] : -1;
+    srow[j] = p.src_row[s_beg + (src < ns ? src : 0)];
+    widx[j] = src < ns ? j * NT + threadIdx.x : c;
   }
   __syncthreads();  // plan slice staged
   // pairs form: the first NP row sets' extents in registers (ROWW reads its records instead)
@@ -989,25 +1007,21 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   // ROWW: this lane's column base in the data tile, and its record offset within a pass
   const uint32_t col_base = lds_addr(s_data + cl);
   const uint32_t rec_lane = L.rec + 16u * static_cast<uint32_t>(sub);
-  float4 v[J];
+  typename Io<T>::raw_t v[J];  // converted to fp32 when written to LDS, not when loaded
   auto load_tile = [&](int64_t tt) {
 #ifdef TAL_PROBE_NOLOAD  // A/B probe: no HBM reads (the tile keeps the first tile's values)
     if (tt != blockIdx.x) return;
 #endif
-    const int64_t col = tt * C4 + c;
-    if (col < n4) {
+    const int64_t col = min(tt * C4 + c, n4 - 1);  // past the end: a duplicate (cache hit)
 #pragma unroll
-      for (int j = 0; j < J; ++j)
-        if (srow[j] >= 0) v[j] = Io<T>::ld(pin, static_cast<int64_t>(srow[j]) * ld_in4 + col);
-    }
+    for (int j = 0; j < J; ++j) v[j] = Io<T>::ld_raw(pin, static_cast<int64_t>(srow[j]) * ld_in4 + col);
   };
   int64_t t = blockIdx.x;
   if (t < n_tiles) load_tile(t);
   for (; t < n_tiles; t += gridDim.x) {
     __syncthreads();  // the previous tile's readers are done with s_data
 #pragma unroll
-    for (int j = 0; j < J; ++j)
-      if (srow[j] >= 0) s_data[j * NT + threadIdx.x] = v[j];
+    for (int j = 0; j < J; ++j) s_data[widx[j]] = Io<T>::f4(v[j]);
     __syncthreads();
     if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
     const int64_t col = t * C4 + cl;
