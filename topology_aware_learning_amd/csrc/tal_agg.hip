@@ -704,29 +704,38 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const T* __restrict
   // lane-fixed staging slots: slot k = j*NT + tid holds column c = tid % C4 (NT is a multiple
   // of C4) of staged source k / C4; only the source's pool row is kept per slot (-1 = unused)
   static_assert(NT % C4 == 0, "a block stages whole source tiles");
+  // Branch-free staging (see k_round_f32_narrow): a slot past the group's sources reloads source
+  // 0's chunk of its column and writes it where source 0's own slot does (the same value).
+  // The write index and (dense form, whose registers are tight) the load addresses are recomputed
+  // per tile behind an empty asm, so the compiler does not hoist them into more registers.
   const int c = threadIdx.x % C4;
   int srow[J];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int src = (j * NT + threadIdx.x) / C4;
-    srow[j] = src < ns ? p.src_row[s_beg + src] : -1;
+    srow[j] = p.src_row[s_beg + (src < ns ? src : 0)];
   }
-  float4 v[J];
+  typename Io<T>::raw_t v[J];
   auto load_tile = [&](int64_t tt) {
-    const int64_t col = tt * C4 + c;
-    if (col < n4) {
+    const int64_t col = min(tt * C4 + c, n4 - 1);  // past the end: a duplicate (cache hit)
 #pragma unroll
-      for (int j = 0; j < J; ++j)
-        if (srow[j] >= 0) v[j] = Io<T>::ld(pin, static_cast<int64_t>(srow[j]) * ld_in4 + col);
+    for (int j = 0; j < J; ++j) {
+      int r = srow[j];
+      if constexpr (DENSE) asm volatile("" : "+v"(r));
+      v[j] = Io<T>::ld_raw(pin, static_cast<int64_t>(r) * ld_in4 + col);
     }
   };
   int64_t t = blockIdx.x;
   if (t < n_tiles) load_tile(t);
   for (; t < n_tiles; t += gridDim.x) {
     __syncthreads();  // the previous tile's readers are done with s_data
+    int staged = ns * C4;  // float4 slots of real sources
+    asm volatile("" : "+s"(staged));
 #pragma unroll
-    for (int j = 0; j < J; ++j)
-      if (srow[j] >= 0) s_data[j * NT + threadIdx.x] = v[j];
+    for (int j = 0; j < J; ++j) {
+      const int k = j * NT + static_cast<int>(threadIdx.x);
+      s_data[k < staged ? k : c] = Io<T>::f4(v[j]);
+    }
     __syncthreads();
     if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
     if constexpr (DENSE)
@@ -983,12 +992,14 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   // register unconditionally (a conditional load made it wait for each load before issuing the
   // next: four serial HBM round trips per tile).  A lane past the group's sources reloads
   // source 0's chunk of its column and writes it where source 0's own lane does (same value).
-  int srow[J], widx[J];
+  // The write index and (pairs form, whose registers are tight) the load addresses are
+  // recomputed per tile behind an empty asm, so the compiler does not hoist them into J more
+  // registers each (it spilled).
+  int srow[J];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int src = (j * NT + threadIdx.x) / C4;
     srow[j] = p.src_row[s_beg + (src < ns ? src : 0)];
-    widx[j] = src < ns ? j * NT + threadIdx.x : c;
   }
   __syncthreads();  // plan slice staged
   // pairs form: the first NP row sets' extents in registers (ROWW reads its records instead)
@@ -1014,14 +1025,23 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
 #endif
     const int64_t col = min(tt * C4 + c, n4 - 1);  // past the end: a duplicate (cache hit)
 #pragma unroll
-    for (int j = 0; j < J; ++j) v[j] = Io<T>::ld_raw(pin, static_cast<int64_t>(srow[j]) * ld_in4 + col);
+    for (int j = 0; j < J; ++j) {
+      int r = srow[j];
+      if constexpr (!ROWW) asm volatile("" : "+v"(r));
+      v[j] = Io<T>::ld_raw(pin, static_cast<int64_t>(r) * ld_in4 + col);
+    }
   };
   int64_t t = blockIdx.x;
   if (t < n_tiles) load_tile(t);
   for (; t < n_tiles; t += gridDim.x) {
     __syncthreads();  // the previous tile's readers are done with s_data
+    int staged = ns * C4;  // float4 slots of real sources
+    asm volatile("" : "+s"(staged));
 #pragma unroll
-    for (int j = 0; j < J; ++j) s_data[widx[j]] = Io<T>::f4(v[j]);
+    for (int j = 0; j < J; ++j) {
+      const int k = j * NT + static_cast<int>(threadIdx.x);
+      s_data[k < staged ? k : c] = Io<T>::f4(v[j]);
+    }
     __syncthreads();
     if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
     const int64_t col = t * C4 + cl;
