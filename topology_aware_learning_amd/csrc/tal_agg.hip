@@ -29,6 +29,13 @@
 
 #include "../../include/tal_agg.h"
 
+// The device code is gfx950 only: the inline asm below (v_mad_u32_u16 with op_sel, v_add_u32
+// with an inline constant, global_load_lds_dwordx4 through M0, counted s_waitcnt vmcnt) is CDNA4
+// ISA, and the kernels' tilings assume its 64-wide wavefronts and 160 KiB of LDS per CU.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "tal_agg.hip targets gfx950 (MI355X) only: build with --offload-arch=gfx950"
+#endif
+
 #pragma clang fp contract(off)
 
 namespace {
@@ -826,6 +833,9 @@ __device__ __forceinline__ NarrowLds stage_narrow_roww(const PlanView& p, int g,
 
 // LDS byte address of the float4 slot in the low / high 16 bits of `word`, from the lane's
 // column base: one v_mad_u32_u16 (op_sel picks the half) instead of an extract and a shift-add.
+// gfx950 VOP3 encoding (see the target check at the top); the plain form is
+// ((word >> (16 * half)) & 0xffff) * 16 + base, which tests/test_gpu_kernels.py's narrow cases
+// check bit for bit against the oracle.
 __device__ __forceinline__ uint32_t slot_addr_lo(uint32_t word, uint32_t base) {
   uint32_t a;
   asm("v_mad_u32_u16 %0, %1, 16, %2" : "=v"(a) : "v"(word), "v"(base));
