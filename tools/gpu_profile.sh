@@ -20,9 +20,26 @@ pmc() {  # name spec workload [bench args]
       > $OUT/pmc_${name}_$s.log 2>&1 || { echo FAIL pmc $name $c; return 1; }
   done
 }
-pmc c3_c64 '{"c4": 64, "dense": 0, "lds": 81920}' random-64-resnet50 && \
-pmc c3_c32 '{"c4": 32, "dense": 0, "lds": 81920}' random-64-resnet50 && \
-pmc c3_c16 '{"c4": 16, "dense": 0, "lds": 81920}' random-64-resnet50 && \
-pmc c2_c128 '{"c4": 128, "dense": 0, "lds": 81920}' ring-32-resnet18 --graph ring --model resnet18 --devices 32 --degree 2 && \
-pmc c2_c64 '{"c4": 64, "dense": 0, "lds": 81920}' ring-32-resnet18 --graph ring --model resnet18 --devices 32 --degree 2
+# every sparse spec the tuner builds (tile width x LDS budget) on configs 3 and 2, plus config 5's
+rc=0
+for c4 in 16 32 64 128; do
+  for lds in 81920 163840; do
+    spec="{\"c4\": $c4, \"dense\": 0, \"lds\": $lds}"
+    pmc c3_c${c4}_l$lds "$spec" random-64-resnet50 && \
+    pmc c2_c${c4}_l$lds "$spec" ring-32-resnet18 --graph ring --model resnet18 --devices 32 --degree 2 || { rc=1; break 2; }
+  done
+done
+# config 3's other candidates: dense row blocks (c4 >= 64) and the streamed groupings
+for c4 in 64 128; do
+  for lds in 81920 163840; do
+    [ $rc = 0 ] && { pmc c3_c${c4}_l${lds}_d8 "{\"c4\": $c4, \"dense\": 8, \"lds\": $lds}" random-64-resnet50 || rc=1; }
+  done
+done
+for g in "64 0" "128 0" "64 96"; do
+  set -- $g
+  [ $rc = 0 ] && { pmc c3_s$1_$2 "{\"stream_rows\": $1, \"stream_src\": $2}" random-64-resnet50 || rc=1; }
+done
+[ $rc = 0 ] && \
+pmc c5_c16 '{"c4": 16, "dense": 0, "lds": 81920}' sbm-256-vit_b16 --graph sbm --model vit_b16 --devices 256 && \
+pmc c5_c16_bf16 '{"c4": 16, "dense": 0, "lds": 81920}' sbm-256-vit_b16-bf16 --graph sbm --model vit_b16 --devices 256 --dtype bf16
 echo PROFILE EXIT $?
