@@ -71,6 +71,9 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="N > 1: nccl (RCCL over xGMI, the benchmark); gloo = rehearsal of the same "
                         "code path with the exchange staged through host memory, ranks may share a GPU")
+    p.add_argument("--halo-transport", default="device", choices=["device", "cabi"],
+                   help="N > 1, halo exchange over nccl: torch.distributed's RCCL (device) or the "
+                        "library's own communicator and gather kernel (cabi, include/tal_agg.h)")
     p.add_argument("--exchange", default="auto", choices=["auto", "halo", "transpose"],
                    help="N > 1: neighbor models by RCCL P2P (halo) or column blocks by all-to-all "
                         "(transpose); auto = fewer link bytes (transposed.choose_exchange)")
@@ -317,7 +320,8 @@ def main():
         from topology_aware_learning_amd.transposed import make_round
 
         sr = make_round(layout, orders, weights, rank, world, dev, exchange=args.exchange, mode=mode,
-                        tune=not args.no_tune, transport="host" if args.dist_backend == "gloo" else "device")
+                        tune=not args.no_tune,
+                        transport="host" if args.dist_backend == "gloo" else args.halo_transport)
         fill_pool(sr.pool_a, 1234 + rank)
         sr.step()
         # spot check: one output row (halo) / row block (transpose) of this rank == K1 on its

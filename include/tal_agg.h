@@ -43,6 +43,7 @@ extern "C" {
 #define TAL_ERR_INVALID 1   /* bad argument (null pointer, size, alias, plan mismatch) */
 #define TAL_ERR_HIP 2       /* HIP runtime error (launch / attribute) */
 #define TAL_ERR_CAPACITY 3  /* plan does not fit (a row has more sources than the LDS tile) */
+#define TAL_ERR_COMM 4      /* RCCL error (multi-GPU halo exchange) */
 
 #define TAL_MODE_FMA 0
 #define TAL_MODE_EXACT 1
@@ -270,6 +271,33 @@ int32_t tal_prox_grad(const float* w, const float* const* wt_host, int32_t k,
                       const int64_t* plan_dev, int32_t n_chunks, int32_t n_seg,
                       const float* norms, const float* scale_dev, float* gw,
                       float* const* gwt_host, void* stream);
+
+/* ---- Multi-GPU halo exchange (SURVEY §8(b) tal_halo_exchange, §8(e)) ---------------------
+ * Reference: the models that cross workers are shipped by Parsl as Python objects
+ * (decentralized_app.py:627-629, parsl_setup.py:191-203).  Sharded one process per GPU, each
+ * rank needs the neighbor models other ranks own: per ordered pair (g -> h) the unique set of
+ * g's rows that h's rows reference, sent once.  One RCCL communicator per process, made from a
+ * unique id that rank 0 creates and the caller broadcasts (any channel: torch.distributed, a
+ * file, MPI); tal_comm_init selects `device` for the communicator and restores the caller's
+ * current device.
+ *
+ * tal_halo_pack gathers rows rows_dev[0..n_rows) (device int32, rows < pool_rows; others are
+ * skipped) of a pool segment (row pitch ld_bytes) into buf, row_bytes each, back to back: the
+ * message for one peer.  tal_halo_exchange posts in one RCCL group on `stream` a send of
+ * send_bytes[p] bytes from send_bufs[p] and a receive of recv_bytes[p] bytes into recv_bufs[p]
+ * for every peer p in [0, world) with a non-zero count (p == own rank: a local copy through
+ * RCCL).  A peer's rows arrive back to back, so a contiguous block of ghost rows of the
+ * receiving pool (its halo rows are grouped by owner) is a valid receive buffer and the round
+ * kernels read it in place.  world must equal the communicator's size. */
+#define TAL_COMM_ID_BYTES 128
+int32_t tal_comm_unique_id(void* id_out);
+int32_t tal_comm_init(void** comm_out, int32_t world, int32_t rank, const void* id, int32_t device);
+int32_t tal_comm_destroy(void* comm);
+int32_t tal_halo_pack(const void* pool, int64_t ld_bytes, int64_t pool_rows, const int32_t* rows_dev,
+                      int32_t n_rows, int64_t row_bytes, void* buf, void* stream);
+int32_t tal_halo_exchange(void* comm, int32_t world, const void* const* send_bufs,
+                          const int64_t* send_bytes, void* const* recv_bufs,
+                          const int64_t* recv_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,100 @@
+"""The C-ABI halo exchange (include/tal_agg.h, halo section) on one GPU: the gather kernel
+against torch indexing, a world-1 RCCL communicator sending to itself, argument errors, and a
+sharded round whose exchange goes through the library (transport "cabi") against the oracle.
+Multi-rank transport needs one GPU per rank (the driver's 8-GPU run); the same per-peer
+messages are rehearsed across ranks by tests/test_distributed_gloo.py."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from topology_aware_learning_amd import _lib
+from topology_aware_learning_amd.comm import HaloComm
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def comm1(cuda):
+    c = HaloComm(1, 0, HaloComm.unique_id(), cuda)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("dtype,ld", [(torch.float32, 1028), (torch.bfloat16, 1030), (torch.int64, 53),
+                                      (torch.float32, 4096)])
+def test_pack_gathers_rows(cuda, dtype, ld):
+    """16-B lanes when rows and pitch allow it (fp32 1028 / 4096), 4-B lanes otherwise."""
+    g = torch.Generator().manual_seed(ld)
+    pool = (torch.randn(10, ld, generator=g) * 1e3).to(dtype).to(cuda)
+    rows = torch.tensor([5, 2, 7, 2, 9], dtype=torch.int32, device=cuda)
+    out = torch.empty((5, ld), dtype=dtype, device=cuda)
+    HaloComm.pack(pool, rows, out)
+    assert torch.equal(out, pool[rows.long()])
+
+
+def test_pack_skips_rows_out_of_range(cuda):
+    pool = torch.arange(40, dtype=torch.float32, device=cuda).view(4, 10)
+    out = torch.full((2, 10), -7.0, device=cuda)
+    HaloComm.pack(pool, torch.tensor([1, 99], dtype=torch.int32, device=cuda), out)
+    assert torch.equal(out[0], pool[1]) and bool((out[1] == -7.0).all())
+
+
+def test_exchange_to_self(cuda, comm1):
+    g = torch.Generator().manual_seed(3)
+    pool = torch.randn(12, 2048, generator=g).to(cuda)
+    rows = torch.tensor([11, 0, 4], dtype=torch.int32, device=cuda)
+    send = HaloComm.pack(pool, rows, torch.empty((3, 2048), device=cuda))
+    recv = torch.zeros_like(send)
+    comm1.exchange([send], [recv])
+    torch.cuda.synchronize()
+    assert torch.equal(recv, pool[rows.long()])
+    comm1.exchange([None], [None])  # nothing to move: an empty group
+    torch.cuda.synchronize()
+
+
+def test_exchange_rejects_wrong_world(cuda, comm1):
+    x = torch.zeros(4, device=cuda)
+    with pytest.raises(ValueError):
+        comm1.exchange([x, x], [x, x])
+    L = _lib.load()
+    import ctypes
+
+    sb = (ctypes.c_void_p * 2)()
+    n = (ctypes.c_int64 * 2)(0, 0)
+    assert L.tal_halo_exchange(comm1._comm, 2, sb, n, sb, n, None) == _lib.TAL_ERR_INVALID
+    assert b"communicator's size" in L.tal_last_error()
+
+
+def test_sharded_round_through_cabi_transport(cuda, tmp_path):
+    """A world-1 torch.distributed group (gloo, for the unique-id broadcast) and a ShardedRound
+    whose exchange is the library's: the round equals the oracle bit for bit."""
+    import networkx as nx
+    import torch.distributed as dist
+
+    from topology_aware_learning_amd.arena import StateLayout
+    from topology_aware_learning_amd.distributed import ShardedRound
+
+    init = f"file://{tmp_path}/pg"
+    dist.init_process_group("gloo", init_method=init, rank=0, world_size=1)
+    try:
+        g = nx.random_regular_graph(4, 12, seed=1)
+        orders = [sorted(g.neighbors(i)) + [i] for i in range(12)]
+        weights = [[1 / len(o)] * len(o) for o in orders]
+        lay = StateLayout.from_layout([("w", (70001,), "float32"), ("b", (13,), "float32"), ("nbt", (), "int64")])
+        sr = ShardedRound(lay, orders, weights, 0, 1, cuda, transport="cabi")
+        gen = torch.Generator(device=cuda).manual_seed(7)
+        sr.pool_a.f32.normal_(generator=gen)
+        sr.pool_a.i64.random_(0, 1000, generator=gen)
+        before = sr.pool_a.f32[:, : lay.n_f32].cpu().numpy().copy()
+        sr.step()
+        torch.cuda.synchronize()
+        row_ptr = np.cumsum([0] + [len(o) for o in orders]).astype(np.int32)
+        col = np.concatenate(orders).astype(np.int32)
+        w = np.concatenate(weights)
+        ref = oracle.round_f32(before, row_ptr, col, w, np.arange(12, dtype=np.int32))
+        got = sr.pool_a.f32[:, : lay.n_f32].cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+        sr.comm.close()
+    finally:
+        dist.destroy_process_group()

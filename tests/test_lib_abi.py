@@ -50,6 +50,26 @@ def test_error_status_and_message():
     assert L.tal_cosine_scratch_bytes(None, 1) == -1
 
 
+def test_halo_exchange_argument_errors():
+    """The halo section's entry points validate before touching a GPU or RCCL."""
+    L = _lib.load()
+    comm = ctypes.c_void_p()
+    uid = ctypes.create_string_buffer(_lib.TAL_COMM_ID_BYTES)
+    assert L.tal_comm_init(None, 1, 0, uid, 0) == _lib.TAL_ERR_INVALID
+    assert L.tal_comm_init(ctypes.byref(comm), 0, 0, uid, 0) == _lib.TAL_ERR_INVALID
+    assert L.tal_comm_init(ctypes.byref(comm), 2, 2, uid, 0) == _lib.TAL_ERR_INVALID
+    assert L.tal_comm_unique_id(None) == _lib.TAL_ERR_INVALID
+    assert L.tal_comm_destroy(None) == _lib.TAL_ERR_INVALID
+    n = (ctypes.c_int64 * 1)(0)
+    assert L.tal_halo_exchange(None, 1, None, n, None, n, None) == _lib.TAL_ERR_INVALID
+    assert b"bad arguments" in L.tal_last_error()
+    fake = ctypes.c_void_p(0x1000)
+    assert L.tal_halo_pack(fake, 64, 4, fake, 0, 64, fake, None) == _lib.TAL_OK  # no rows: nothing
+    assert L.tal_halo_pack(fake, 64, 4, fake, 2, 6, fake, None) == _lib.TAL_ERR_INVALID  # 6-byte rows
+    assert b"aligned" in L.tal_last_error()
+    assert L.tal_halo_pack(fake, 32, 4, fake, 2, 64, fake, None) == _lib.TAL_ERR_INVALID  # pitch < row
+
+
 def test_in_place_multi_group_rejected():
     import networkx as nx
 

@@ -23,9 +23,11 @@ TAL_OK = 0
 TAL_ERR_INVALID = 1
 TAL_ERR_HIP = 2
 TAL_ERR_CAPACITY = 3
+TAL_ERR_COMM = 4
+TAL_COMM_ID_BYTES = 128
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 EXPORTED = (
     "tal_last_error",
@@ -49,6 +51,11 @@ EXPORTED = (
     "tal_prox_scratch_bytes",
     "tal_prox_norms",
     "tal_prox_grad",
+    "tal_comm_unique_id",
+    "tal_comm_init",
+    "tal_comm_destroy",
+    "tal_halo_pack",
+    "tal_halo_exchange",
 )
 
 
@@ -136,6 +143,11 @@ _SIGS = {
     "tal_prox_scratch_bytes": (_I64, [_I32, _I32]),
     "tal_prox_norms": (_I32, [_P, _PP, _I32, _P, _I32, _I32, _P, _P, _P]),
     "tal_prox_grad": (_I32, [_P, _PP, _I32, _P, _I32, _I32, _P, _P, _P, _PP, _P]),
+    "tal_comm_unique_id": (_I32, [_P]),
+    "tal_comm_init": (_I32, [_PP, _I32, _I32, _P, _I32]),
+    "tal_comm_destroy": (_I32, [_P]),
+    "tal_halo_pack": (_I32, [_P, _I64, _I64, _P, _I32, _I64, _P, _P]),
+    "tal_halo_exchange": (_I32, [_P, _I32, _PP, _PI64, _PP, _PI64, _P]),
 }
 
 _lock = threading.Lock()

@@ -27,6 +27,8 @@
 #include <type_traits>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "../../include/tal_agg.h"
 
 // The device code is gfx950 only: the inline asm below (v_mad_u32_u16 with op_sel, v_add_u32
@@ -40,7 +42,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 11;
+constexpr int kAbiVersion = 12;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -3072,6 +3074,126 @@ int32_t tal_prox_grad(const float* w, const float* const* wt_host, int32_t k, co
     int32_t rc = check_launch("prox grad");
     if (rc) return rc;
   }
+  g_err.clear();
+  return TAL_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------
+// Multi-GPU halo exchange: pack kernel + RCCL group (include/tal_agg.h, halo section)
+// ------------------------------------------------------------------------------------------
+namespace {
+
+// rows -> contiguous: block (x, r) copies part of row rows[r]; W = 16 or 4 bytes per lane
+template <typename V>
+__global__ __launch_bounds__(kBlock) void k_halo_pack(const V* __restrict__ pool, int64_t ld, int64_t pool_rows,
+                                                      const int32_t* __restrict__ rows, int64_t row_n,
+                                                      V* __restrict__ buf) {
+  const int64_t src = rows[blockIdx.y];
+  if (src < 0 || src >= pool_rows) return;  // out-of-range rows are skipped, never read
+  const V* in = pool + src * ld;
+  V* out = buf + static_cast<int64_t>(blockIdx.y) * row_n;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < row_n;
+       i += static_cast<int64_t>(gridDim.x) * kBlock)
+    out[i] = in[i];
+}
+
+int32_t comm_fail(const char* what, ncclResult_t r) {
+  return fail(TAL_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t tal_comm_unique_id(void* id_out) {
+  if (!id_out) return fail(TAL_ERR_INVALID, "tal_comm_unique_id: null output");
+  ncclUniqueId id;
+  const ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return comm_fail("ncclGetUniqueId", r);
+  memcpy(id_out, &id, sizeof(id));
+  g_err.clear();
+  return TAL_OK;
+}
+
+int32_t tal_comm_init(void** comm_out, int32_t world, int32_t rank, const void* id, int32_t device) {
+  if (!comm_out || !id || world <= 0 || rank < 0 || rank >= world || device < 0)
+    return fail(TAL_ERR_INVALID, "tal_comm_init: bad arguments");
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess)
+    return fail(TAL_ERR_HIP, "tal_comm_init: cannot select device " + std::to_string(device));
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof(uid));
+  ncclComm_t c = nullptr;
+  const ncclResult_t r = ncclCommInitRank(&c, world, uid, rank);
+  (void)hipSetDevice(prev);
+  if (r != ncclSuccess) return comm_fail("ncclCommInitRank", r);
+  *comm_out = c;
+  g_err.clear();
+  return TAL_OK;
+}
+
+int32_t tal_comm_destroy(void* comm) {
+  if (!comm) return fail(TAL_ERR_INVALID, "tal_comm_destroy: null communicator");
+  const ncclResult_t r = ncclCommDestroy(static_cast<ncclComm_t>(comm));
+  if (r != ncclSuccess) return comm_fail("ncclCommDestroy", r);
+  g_err.clear();
+  return TAL_OK;
+}
+
+int32_t tal_halo_pack(const void* pool, int64_t ld_bytes, int64_t pool_rows, const int32_t* rows_dev,
+                      int32_t n_rows, int64_t row_bytes, void* buf, void* stream) {
+  if (n_rows == 0) {
+    g_err.clear();
+    return TAL_OK;
+  }
+  if (!pool || !rows_dev || !buf || n_rows < 0 || n_rows > 65535 || row_bytes <= 0 || ld_bytes < row_bytes ||
+      pool_rows <= 0)
+    return fail(TAL_ERR_INVALID, "tal_halo_pack: bad arguments");
+  if ((row_bytes | ld_bytes) & 3 || (reinterpret_cast<uintptr_t>(pool) | reinterpret_cast<uintptr_t>(buf)) & 3)
+    return fail(TAL_ERR_INVALID, "tal_halo_pack: rows, pitch and pointers must be 4-byte aligned");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool v16 = ((row_bytes | ld_bytes) & 15) == 0 && aligned16(pool) && aligned16(buf);
+  const int64_t w = v16 ? 16 : 4;
+  const int64_t row_n = row_bytes / w;
+  const dim3 grid(static_cast<unsigned>(std::min<int64_t>((row_n + kBlock - 1) / kBlock, 1024)),
+                  static_cast<unsigned>(n_rows));
+  if (v16)
+    k_halo_pack<uint4><<<grid, kBlock, 0, s>>>(static_cast<const uint4*>(pool), ld_bytes / 16, pool_rows, rows_dev,
+                                              row_n, static_cast<uint4*>(buf));
+  else
+    k_halo_pack<uint32_t><<<grid, kBlock, 0, s>>>(static_cast<const uint32_t*>(pool), ld_bytes / 4, pool_rows,
+                                                  rows_dev, row_n, static_cast<uint32_t*>(buf));
+  return check_launch("halo pack");
+}
+
+int32_t tal_halo_exchange(void* comm, int32_t world, const void* const* send_bufs, const int64_t* send_bytes,
+                          void* const* recv_bufs, const int64_t* recv_bytes, void* stream) {
+  if (!comm || world <= 0 || !send_bytes || !recv_bytes)
+    return fail(TAL_ERR_INVALID, "tal_halo_exchange: bad arguments");
+  ncclComm_t c = static_cast<ncclComm_t>(comm);
+  int n = 0;
+  ncclResult_t r = ncclCommCount(c, &n);
+  if (r != ncclSuccess) return comm_fail("ncclCommCount", r);
+  if (n != world) return fail(TAL_ERR_INVALID, "tal_halo_exchange: world differs from the communicator's size");
+  for (int p = 0; p < world; ++p) {
+    if (send_bytes[p] < 0 || recv_bytes[p] < 0 || (send_bytes[p] && (!send_bufs || !send_bufs[p])) ||
+        (recv_bytes[p] && (!recv_bufs || !recv_bufs[p])))
+      return fail(TAL_ERR_INVALID, "tal_halo_exchange: bad buffer for peer " + std::to_string(p));
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  r = ncclGroupStart();
+  if (r != ncclSuccess) return comm_fail("ncclGroupStart", r);
+  ncclResult_t first = ncclSuccess;
+  for (int p = 0; p < world && first == ncclSuccess; ++p) {
+    if (send_bytes[p]) first = ncclSend(send_bufs[p], static_cast<size_t>(send_bytes[p]), ncclUint8, p, c, s);
+    if (first == ncclSuccess && recv_bytes[p])
+      first = ncclRecv(recv_bufs[p], static_cast<size_t>(recv_bytes[p]), ncclUint8, p, c, s);
+  }
+  r = ncclGroupEnd();
+  if (first != ncclSuccess) return comm_fail("ncclSend / ncclRecv", first);
+  if (r != ncclSuccess) return comm_fail("ncclGroupEnd", r);
   g_err.clear();
   return TAL_OK;
 }

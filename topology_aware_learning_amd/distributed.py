@@ -105,10 +105,12 @@ class HaloPacker:
         self.spec = spec
         self.bufs: Dict[int, torch.Tensor] = {}
         self.idx: Dict[int, torch.Tensor] = {}
+        self.idx32: Dict[int, torch.Tensor] = {}
         for peer, rows in spec.send.items():
             if rows == list(range(rows[0], rows[0] + len(rows))):
                 continue  # consecutive: sent as t[r0:r1]
             self.idx[peer] = torch.as_tensor(rows, dtype=torch.long, device=t.device)
+            self.idx32[peer] = self.idx[peer].to(torch.int32)  # the C-ABI gather's row list
             self.bufs[peer] = torch.empty((len(rows), t.shape[1]), dtype=t.dtype, device=t.device)
 
     def send_tensor(self, t: torch.Tensor, peer: int) -> torch.Tensor:
@@ -226,6 +228,43 @@ def post_exchange_staged(spec: ShardSpec, tensors: Sequence[torch.Tensor], group
     return [_StagedRequests(dist.batch_isend_irecv(p2p), fills)]
 
 
+class _StreamRequest:
+    """An exchange enqueued on a side stream: wait() makes the current stream wait for it."""
+
+    def __init__(self, event, device):
+        self.event, self.device = event, device
+
+    def wait(self):
+        torch.cuda.current_stream(self.device).wait_event(self.event)
+
+
+def post_exchange_cabi(spec: ShardSpec, tensors: Sequence[torch.Tensor], comm, stream,
+                       packers: Sequence[HaloPacker]) -> list:
+    """post_exchange through the C-ABI (comm.HaloComm): on `stream`, after the work already
+    queued on the current stream, each peer's rows are packed by the library's gather kernel
+    and every segment's messages go out in one RCCL group; the returned request makes the
+    current stream wait for the receives."""
+    cur = torch.cuda.current_stream(comm.device)
+    stream.wait_stream(cur)
+    world = spec.world
+    with torch.cuda.stream(stream):
+        for t, pk in zip(tensors, packers):
+            sends, recvs = [None] * world, [None] * world
+            for peer in spec.send:
+                if peer in pk.idx32:
+                    sends[peer] = comm.pack(t, pk.idx32[peer], pk.bufs[peer], stream)
+                else:
+                    rows = spec.send[peer]
+                    sends[peer] = t[rows[0]: rows[0] + len(rows)]
+            for peer in spec.recv:
+                r0, r1 = recv_range(spec, peer)
+                recvs[peer] = t[r0:r1]
+            comm.exchange(sends, recvs, stream)
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    return [_StreamRequest(ev, comm.device)]
+
+
 class ShardedRound:
     """One rank's device-resident round over its shard (K3 kernels + halo exchange)."""
 
@@ -238,10 +277,23 @@ class ShardedRound:
         self.mode = mode
         self.group = group
         # exchange(self) -> requests; default: RCCL/gloo P2P.  Tests may pass an in-process copy.
-        # transport "host": the exchange is staged through host memory (gloo rehearsal runs)
-        post = post_exchange_staged if transport == "host" else post_exchange
-        self._exchange = exchange or (lambda sr: post(sr.spec, [t for _, t, _ in sr.pool_a.segments()], sr.group,
-                                                      sr.packers))
+        # transport "host": the exchange is staged through host memory (gloo rehearsal runs);
+        # "cabi": the library's own RCCL communicator and gather kernel (comm.HaloComm) on a
+        # side stream, the unique id broadcast through the torch.distributed group
+        if transport not in ("device", "host", "cabi"):
+            raise ValueError(f"unknown transport {transport!r}")
+        self.transport = transport
+        if transport == "cabi" and exchange is None:
+            from .comm import shared_halo_comm
+
+            self.comm = shared_halo_comm(world, rank, device, group)
+            self.comm_stream = torch.cuda.Stream(torch.device(device))
+            self._exchange = lambda sr: post_exchange_cabi(sr.spec, [t for _, t, _ in sr.pool_a.segments()],
+                                                           sr.comm, sr.comm_stream, sr.packers)
+        else:
+            post = post_exchange_staged if transport == "host" else post_exchange
+            self._exchange = exchange or (lambda sr: post(sr.spec, [t for _, t, _ in sr.pool_a.segments()],
+                                                          sr.group, sr.packers))
         owner = partition_contiguous(len(orders), world) if owner is None else np.asarray(owner, np.int32)
         self.spec = build_shard(orders, weights, owner, rank, world)
         self.pool_a = ModelPool(layout, self.spec.rows, self.device)

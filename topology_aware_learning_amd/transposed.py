@@ -295,11 +295,15 @@ def make_round(layout: StateLayout, orders, weights, rank: int, world: int, devi
                mode: int = ops.MODE_EXACT, owner: Optional[np.ndarray] = None, group=None, tune: bool = False,
                transport: str = "device"):
     """This rank's sharded round with the given exchange ('halo' | 'transpose' | 'auto');
-    transport 'host' stages the exchange through host memory (gloo rehearsal runs only)."""
+    transport 'host' stages the exchange through host memory (gloo rehearsal runs only),
+    'cabi' moves a halo exchange through the library's own RCCL communicator (the transposed
+    exchange's all-to-alls stay on torch.distributed)."""
     owner = partition_contiguous(len(orders), world) if owner is None else np.asarray(owner, np.int32)
     if exchange == "auto":
         exchange = choose_exchange(orders, owner, world, layout.n_f32, layout.n_i64, layout.n_b16)
     cls = {"halo": ShardedRound, "transpose": TransposedRound}[exchange]
+    if exchange == "transpose" and transport == "cabi":
+        transport = "device"
     r = cls(layout, orders, weights, rank, world, device, mode=mode, owner=owner, group=group, tune=tune,
             transport=transport)
     r.exchange_kind = exchange
