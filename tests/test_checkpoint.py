@@ -100,3 +100,7 @@ def test_bound_row_tracks_rebinding():
     pool.bind(m, 0)
     m.to(torch.float64)
     assert bound_row(m) is None
+    pool.bind(m.to(torch.float32), 0)
+    assert bound_row(m) == (pool, 0)
+    m.fc.bias = None  # an entry removed from its table
+    assert bound_row(m) is None

@@ -11,7 +11,8 @@ Python plus the aggregation.  Also
 times RoundExecutor(pool).run directly on the round (its default plan, in place) against the
 bench's K1 floor (64 x one K1 call).  One JSON line per measurement.
 
-usage: python tools/dropin_rate.py [rounds]"""
+usage: python tools/dropin_rate.py [rounds] [--profile]   (--profile: cProfile of the batched
+rounds only, top functions by cumulative time)"""
 import json
 import os
 import sys
@@ -30,7 +31,9 @@ import torch  # noqa: E402
 
 
 def main():
-    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    rounds = int(args[0]) if args else 5
+    profile = "--profile" in sys.argv
     from src.decentralized_app import DecentrallearnApp
     from topology_aware_learning_amd import ops
     from topology_aware_learning_amd.round import RoundExecutor
@@ -54,6 +57,31 @@ def main():
     dev = app.pool.device
     app.round_states = {0: {i: {"agg": ([{}], app.clients[i])} for i in range(len(app.clients))}}
     r = 0
+    if profile:
+        import cProfile
+        import io
+        import pstats
+
+        app.batched_round = True
+        for _ in range(2):  # warm: plan build, pools
+            for f in app._federated_round(r):
+                f.result()
+            app.round_states.pop(r, None)
+            r += 1
+        torch.cuda.synchronize(dev)
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(rounds):
+            for f in app._federated_round(r):
+                f.result()
+            torch.cuda.synchronize(dev)
+            app.round_states.pop(r, None)
+            r += 1
+        pr.disable()
+        out = io.StringIO()
+        pstats.Stats(pr, stream=out).sort_stats("cumulative").print_stats(45)
+        print(out.getvalue(), flush=True)
+        return
     for mode in ("per_call", "batched", "per_call", "batched"):
         app.batched_round = mode == "batched"
         ts = []

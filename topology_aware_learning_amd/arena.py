@@ -222,7 +222,8 @@ class ModelPool:
             slots.append((table, attr, v.data_ptr()))
         module._tal_pool = self  # type: ignore[attr-defined]
         module._tal_row = r  # type: ignore[attr-defined]
-        module._tal_slots = slots  # type: ignore[attr-defined]
+        module._tal_slots = [(table, attr) for table, attr, _ in slots]  # type: ignore[attr-defined]
+        module._tal_ptrs = [ptr for _, _, ptr in slots]  # type: ignore[attr-defined]
         self._bound[id(module)] = r
         return module
 
@@ -234,16 +235,15 @@ class ModelPool:
         # every state entry must still be the row view bound to it (module.to(), param.data
         # assignment or a re-registered buffer re-point it); checked through the tables kept at
         # bind time - no state_dict / view rebuild per call (~1 ms for ResNet-50's 320 entries)
-        first = True
-        for table, attr, ptr in module._tal_slots:  # type: ignore[attr-defined]
-            t = table.get(attr)
-            if t is None or t.data_ptr() != ptr:
-                return None
-            if first:
-                if t.device != self.device:
-                    return None
-                first = False
-        return r
+        slots = module._tal_slots  # type: ignore[attr-defined]
+        try:
+            ptrs = [table[attr].data_ptr() for table, attr in slots]
+        except (KeyError, AttributeError):  # an entry removed or set to None
+            return None
+        if ptrs != module._tal_ptrs:  # type: ignore[attr-defined]
+            return None
+        table, attr = slots[0]
+        return r if table[attr].device == self.device else None
 
 
 def bound_row(module: nn.Module) -> Optional[Tuple[ModelPool, int]]:
