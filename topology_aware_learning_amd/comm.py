@@ -9,6 +9,7 @@ This is the binding a host without torch.distributed would use (INTEGRATION.md Â
 from __future__ import annotations
 
 import ctypes
+import sys
 from typing import Optional, Sequence
 
 import torch
@@ -48,6 +49,10 @@ class HaloComm:
             self._comm = ctypes.c_void_p()
 
     def __del__(self):  # pragma: no cover - interpreter teardown order
+        # at interpreter exit the HIP runtime may already be torn down: leave the communicator
+        # to the process exit instead of calling into RCCL
+        if sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:
