@@ -32,10 +32,12 @@ class HaloComm:
             raise ValueError(f"the unique id is {_lib.TAL_COMM_ID_BYTES} bytes")
         self.world, self.rank = int(world), int(rank)
         self.device = torch.device(device)
+        if self.device.index is None:  # "cuda": the current device
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self._comm = ctypes.c_void_p()
         idbuf = ctypes.create_string_buffer(bytes(uid), len(uid))
         _check(_lib.load().tal_comm_init(ctypes.byref(self._comm), self.world, self.rank, idbuf,
-                                         self.device.index or 0))
+                                         self.device.index))
 
     @staticmethod
     def unique_id() -> bytes:
