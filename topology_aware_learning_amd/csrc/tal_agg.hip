@@ -1638,6 +1638,15 @@ __device__ __forceinline__ v2f clique_term(v2f acc, float w, v2f p) {
   else return v2f{__builtin_fmaf(w, p.x, acc.x), __builtin_fmaf(w, p.y, acc.y)};
 }
 
+typedef float v8f __attribute__((ext_vector_type(8)));
+
+// Four clique chains stepped at once (k-th pair of lanes = chain k): one IR operation per step.
+template <bool EXACT>
+__device__ __forceinline__ v8f clique_term4(v8f acc, float w, v8f p) {
+  if constexpr (EXACT) return acc + p;  // IEEE adds, one rounding each (no contraction: -ffp-contract=off)
+  else return __builtin_elementwise_fma(v8f{w, w, w, w, w, w, w, w}, p, acc);
+}
+
 // A zero the compiler cannot see through: table reads indexed with it stay where they are
 // instead of being hoisted to the top of the kernel, where 128 live row indices would spill
 // the scalar register file.
@@ -1710,18 +1719,48 @@ __global__ __launch_bounds__(kBlock) void k_round_clique(const float* __restrict
     if constexpr (EXACT) p[j] = v2f{__fmul_rn(w, p[j].x), __fmul_rn(w, p[j].y)};
     if (j >= m) p[j] = v2f{pad, pad};
   }
+  // Rows four at a time: row r = ((S_r + p[r+1]) + ... + p[MMAX-1]) + p[r], S_{r+1} = S_r + p[r]
+  // (each row its own in-order chain, as the reference sums it).  The four chains are
+  // independent, so their packed adds interleave: one chain's back-to-back dependent
+  // v_pk_add_f32 needed an s_nop between every pair (1,512 per column pair at MMAX 60), which
+  // stretched each wavefront's compute phase and with it the time without loads in flight.
+  static_assert(MMAX % 4 == 0, "rows are taken in fours");
   v2f s = v2f{-0.f, -0.f};
 #pragma unroll
-  for (int i = 0; i < MMAX; ++i) {
-    const int orow = i < m ? t[4 + kCliqueMax + i + opaque_zero()] : -1;  // wave-uniform
-    if (orow >= 0) {
-      v2f acc = s;
+  for (int i = 0; i < MMAX; i += 4) {
+    int orow[4];
 #pragma unroll
-      for (int j = i + 1; j < MMAX; ++j) acc = clique_term<EXACT>(acc, w, p[j]);
-      acc = clique_term<EXACT>(acc, w, p[i]);
-      __builtin_nontemporal_store(acc, reinterpret_cast<v2f*>(pout + static_cast<int64_t>(orow) * ld_out + e));
+    for (int k = 0; k < 4; ++k) orow[k] = i + k < m ? t[4 + kCliqueMax + i + k + opaque_zero()] : -1;  // wave-uniform
+    v2f sp[4];  // S_i .. S_{i+3}
+    sp[0] = s;
+#pragma unroll
+    for (int k = 1; k < 4; ++k) sp[k] = clique_term<EXACT>(sp[k - 1], w, p[i + k - 1]);
+    if (orow[0] >= 0 || orow[1] >= 0 || orow[2] >= 0 || orow[3] >= 0) {
+      // heads: row i+k takes p[i+k+1 .. i+3] before the four chains run in step
+      v2f a[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        a[k] = sp[k];
+#pragma unroll
+        for (int j = i + k + 1; j < i + 4; ++j) a[k] = clique_term<EXACT>(a[k], w, p[j]);
+      }
+      // the four chains as one 8-wide vector: each step is one IR operation (four packed adds
+      // on natural register pairs), which the compiler can neither split into four loops nor
+      // sink into the stores' branches
+      v8f q = {a[0].x, a[0].y, a[1].x, a[1].y, a[2].x, a[2].y, a[3].x, a[3].y};
+#pragma unroll
+      for (int j = i + 4; j < MMAX; ++j) q = clique_term4<EXACT>(q, w, v8f{p[j].x, p[j].y, p[j].x, p[j].y,
+                                                                           p[j].x, p[j].y, p[j].x, p[j].y});
+      q = clique_term4<EXACT>(q, w, v8f{p[i].x, p[i].y, p[i + 1].x, p[i + 1].y, p[i + 2].x, p[i + 2].y,
+                                        p[i + 3].x, p[i + 3].y});
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] = v2f{q[2 * k], q[2 * k + 1]};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (orow[k] >= 0)
+          __builtin_nontemporal_store(a[k], reinterpret_cast<v2f*>(pout + static_cast<int64_t>(orow[k]) * ld_out + e));
     }
-    s = clique_term<EXACT>(s, w, p[i]);
+    s = clique_term<EXACT>(sp[3], w, p[i + 3]);
   }
 }
 
