@@ -1,11 +1,12 @@
-# Build A/B probe variants of the library into tools/tune/ (not the product).
+# Build A/B probe variants of the library into tools/tune/ (not the product), with the product's
+# own hipcc flags (topology_aware_learning_amd/build.py) plus the variant's.
 # Usage: bash tools/build_probe_libs.sh NAME:FLAGS ...   e.g. nocomp:-DTAL_PROBE_NOCOMP
 cd "$(dirname "$0")/.."
+base=$(python -c "from topology_aware_learning_amd.build import HIPCC_FLAGS; print(' '.join(HIPCC_FLAGS))")
 pids=()
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}; flags=${flags//,/ }
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -mcode-object-version=5 \
-    $flags topology_aware_learning_amd/csrc/tal_agg.hip -o tools/tune/libtal_agg_$name.so &
+  /opt/rocm/bin/hipcc $base $flags topology_aware_learning_amd/csrc/tal_agg.hip -o tools/tune/libtal_agg_$name.so &
   pids+=($!)
 done
 rc=0
