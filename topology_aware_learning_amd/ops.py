@@ -364,7 +364,7 @@ def build_stream_plan(row_ptr, col, w, out_row, max_group_rows: int = 64, max_gr
 
 
 def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.Tensor,
-              n: Optional[int] = None, reps: int = 2, mode: int = MODE_EXACT) -> RoundPlan:
+              n: Optional[int] = None, reps: int = 3, mode: int = MODE_EXACT) -> RoundPlan:
     """Pick the plan by measurement: every (tile width, LDS budget, sparse/dense) candidate that
     builds runs `reps` times on the real pools (pool_out must not alias pool_in) and the fastest
     median wins.  Costs a few rounds once per topology; the model-based choice of build_plan is
@@ -412,17 +412,21 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
     best, best_t = None, None
     timings = []
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for key, p in cands:
+    for _, p in cands:
         p.to(pool_in.device)
         run(pool_in, pool_out, p, n=n, mode=mode)  # warm (LDS attribute, code load)
-        ts = []
-        for _ in range(reps):
+    # candidates interleaved rep by rep, so a clock or thermal drift during tuning does not
+    # favour the ones timed first
+    ts = [[] for _ in cands]
+    for _ in range(reps):
+        for k, (_, p) in enumerate(cands):
             s.record()
             run(pool_in, pool_out, p, n=n, mode=mode)
             e.record()
             e.synchronize()
-            ts.append(s.elapsed_time(e))
-        t = float(np.median(ts))
+            ts[k].append(s.elapsed_time(e))
+    for (key, p), tk in zip(cands, ts):
+        t = float(np.median(tk))
         timings.append({"c4": key[0], "groups": key[1], "staged": key[2], "dense_rb": key[3],
                         "max_src": key[4], "stream_cs": key[5], "ms": round(t, 4), "spec": p.spec})
         if best_t is None or t < best_t:
