@@ -71,6 +71,9 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="N > 1: nccl (RCCL over xGMI, the benchmark); gloo = rehearsal of the same "
                         "code path with the exchange staged through host memory, ranks may share a GPU")
+    p.add_argument("--weights", default="unweighted", choices=["unweighted", "degcent"],
+                   help="unweighted_module_avg (1/M, the metric's config) or centrality_module_avg "
+                        "with softmax(10 x degree centrality): per-operand weights")
     p.add_argument("--halo-transport", default="device", choices=["device", "cabi"],
                    help="N > 1, halo exchange over nccl: torch.distributed's RCCL (device) or the "
                         "library's own communicator and gather kernel (cabi, include/tal_agg.h)")
@@ -95,12 +98,21 @@ def make_graph(kind: str, n_devices: int, degree: int, seed: int = 0):
     return nx.stochastic_block_model(sizes, p, seed=seed)
 
 
-def round_spec(n_devices: int, degree: int, seed: int = 0, kind: str = "random"):
+def round_spec(n_devices: int, degree: int, seed: int = 0, kind: str = "random", weights: str = "unweighted"):
+    """(orders, weights) of one round: neighbors ascending then self (SURVEY §8(a) A7);
+    unweighted_module_avg's 1/M (client.py:431) or centrality_module_avg's softmax of 10 x the
+    degree centrality (client.py:572-593, SURVEY §8(d)'s softmax-centrality variant)."""
+    import networkx as nx
+
+    from topology_aware_learning_amd import weights as tw
+
     g = make_graph(kind, n_devices, degree, seed)
     n_devices = g.number_of_nodes()
     orders = [sorted(g.neighbors(i)) + [i] for i in range(n_devices)]
-    weights = [[1 / len(o)] * len(o) for o in orders]  # unweighted_module_avg, client.py:431
-    return orders, weights
+    if weights == "degcent":
+        cent = nx.degree_centrality(g)
+        return orders, [tw.centrality(o, cent, True, 10.0) for o in orders]
+    return orders, [tw.unweighted(len(o)) for o in orders]
 
 
 def fill_pool(pool, seed: int):
@@ -211,7 +223,7 @@ def main():
     n_float = layout.n_b16 if bf16 else layout.n_f32  # the streamed segment
     esize = 2 if bf16 else 4
     n_dev_total = args.devices or args.devices_per_gpu * world
-    orders, weights = round_spec(n_dev_total, args.degree, kind=args.graph)
+    orders, weights = round_spec(n_dev_total, args.degree, kind=args.graph, weights=args.weights)
     n_dev_total = len(orders)
     M = max(len(o) for o in orders)
 
@@ -364,7 +376,7 @@ def main():
     traffic = None
     if world == 1:  # PMC bytes of exactly this kernel + plan spec + workload, when profiled
         traffic = load_traffic(traffic_key(result_extra["kernel"], result_extra["plan"]["spec"],
-                                           workload_key(args.graph, n_dev_total, args.model, args.dtype)))
+                                           workload_key(args.graph, n_dev_total, args.model, args.dtype, args.weights)))
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(lay, M, args.cpu_seconds)  # bf16 layouts: the reference's loop on bf16 tensors
@@ -384,8 +396,9 @@ def main():
         "data": f"synthetic (random {'bf16' if bf16 else 'fp32'} / int64 state_dicts of the reference layout in HBM)",
         "config": {"workload": f"{n_dev_total}-device {args.graph} graph"
                                + (f" ({args.degree}-regular, seed 0)" if args.graph == "random" else "")
-                               + f", {args.model} state_dicts, max M={M} (self last), unweighted, "
-                               "one full aggregation round per step, snapshot semantics",
+                               + f", {args.model} state_dicts, max M={M} (self last), "
+                               + ("unweighted, " if args.weights == "unweighted" else "degree-centrality softmax weights, ")
+                               + "one full aggregation round per step, snapshot semantics",
                    "model_layout": args.model + (f" (first {args.max_params} float params: rehearsal)"
                                                  if args.max_params else ""), "devices": n_dev_total, "devices_per_gpu": args.devices_per_gpu,
                    "params_per_model": n_params, "parallelism": f"{result_extra.get('exchange', '')}-sharded x{world}" if world > 1 else "1 GPU"},
@@ -500,8 +513,9 @@ def valu_floor(nnz: int, rows: int, n: int, k_ms: float, mode) -> dict:
     return dict(lane_ops=ops_round, floor_ms=floor_ms, frac=floor_ms / k_ms)
 
 
-def workload_key(graph: str, devices: int, model: str, dtype: str = "f32") -> str:
-    return f"{graph}-{devices}-{model}" + ("" if dtype == "f32" else f"-{dtype}")
+def workload_key(graph: str, devices: int, model: str, dtype: str = "f32", weights: str = "unweighted") -> str:
+    return (f"{graph}-{devices}-{model}" + ("" if dtype == "f32" else f"-{dtype}")
+            + ("" if weights == "unweighted" else f"-{weights}"))
 
 
 def traffic_key(kernel: str, spec, workload: str) -> str:
