@@ -495,6 +495,9 @@ _CLIQUE_GRAPHS = {
     "barbell20": lambda: nx.barbell_graph(20, 3),   # m = 20: the 32-register kernel
     "complete64": lambda: nx.complete_graph(64),    # m = 64: the largest block
     "complete9": lambda: nx.complete_graph(9),      # m = 9: the 16-register kernel
+    "complete37": lambda: nx.complete_graph(37),    # m = 37: the 40-member instantiation, a partial row group
+    "barbell45": lambda: nx.barbell_graph(45, 2),   # m = 45: the 48-member instantiation, bridges attached
+    "complete53": lambda: nx.complete_graph(53),    # m = 53: the 56-member instantiation
     "mixed": lambda: nx.disjoint_union(nx.complete_graph(12), nx.random_regular_graph(4, 30, seed=1)),
 }
 
