@@ -819,7 +819,12 @@ __device__ __forceinline__ NarrowLds stage_narrow_roww(const PlanView& p, int g,
     const int row = k < L.nr ? k : k / kRpw * kRpw;  // padding rows: their pass's first row
     const int q0 = p.nrow_ptr[r_beg + row] - e_beg, q1 = p.nrow_ptr[r_beg + row + 1] - e_beg;
     rec[4 * k + 0] = static_cast<int32_t>(slots_addr + 2u * static_cast<uint32_t>(q0));
-    rec[4 * k + 1] = (q1 - q0) / 4;
+    // operands the pass computes: its first (longest) row's count, as whole batches of four
+    // plus a tail of 1-3; the slot storage stays padded to whole batches (8-B aligned reads)
+    const int lead = r_beg + k / kRpw * kRpw;
+    const int m = p.row_ptr[lead + 1] - p.row_ptr[lead];
+    rec[4 * k + 1] = (m / 4) | ((m % 4) << 16);
+    (void)q1;
     rec[4 * k + 2] = p.nrow_w[r_beg + row];
     rec[4 * k + 3] = k < L.nr ? p.out_row[r_beg + k] : -1;
   }
@@ -865,12 +870,31 @@ __device__ __forceinline__ uint4 lds_u4(uint32_t addr) {
 }
 
 // One ROWW row from its record: the accumulator starts at -0.0 and takes `nb` batches of four
-// slots (one 8-B LDS read each, the next batch's read issued ahead of this batch's data reads).
-// nb is the same for every row of the pass (host padding), so the loop counts on the scalar
-// unit: per batch 4 address + 16 (EXACT) or 8 (FMA) arithmetic VALU and one cursor add.
+// slots (one 8-B LDS read each, the next batch's read issued ahead of this batch's data reads),
+// then a tail of `rem` < 4 slots from the word read last.  nb and rem are the same for every
+// row of the pass (host padding), so the loop counts on the scalar unit: per batch 4 address +
+// 16 (EXACT) or 8 (FMA) arithmetic VALU and one cursor add.  (Before the tail, rows padded to
+// whole batches of four read 9.6 % zero-tile slots on config 5.)
+template <typename T, bool EXACT>
+__device__ __forceinline__ float4 narrow_row_tail(float4 acc, float w, uint2 e, uint32_t base, int rem) {
+  // one operand at a time (a 1-3 long tail per row; read and use back to back keeps the
+  // register budget of two workgroups per CU)
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    if (rem <= u) break;  // wave-uniform
+    const uint32_t word = u < 2 ? e.x : e.y;
+    uint32_t addr;
+    if constexpr (kIsBf16<T> && EXACT) addr = base + (((u == 1 ? word >> 16 : word) & 0xffffu) << 4);
+    else addr = u == 1 ? slot_addr_hi(word, base) : slot_addr_lo(word, base);
+    acc = next4t<T, EXACT>(acc, w, lds_f4(addr));
+  }
+  return acc;
+}
+
 template <typename T, bool EXACT>
 __device__ __forceinline__ float4 narrow_row_roww(uint4 rc, uint32_t base) {
-  const int nb = __builtin_amdgcn_readfirstlane(static_cast<int>(rc.y));
+  const int nb = __builtin_amdgcn_readfirstlane(static_cast<int>(rc.y & 0xffffu));
+  const int rem = __builtin_amdgcn_readfirstlane(static_cast<int>(rc.y >> 16));
   const float w = __uint_as_float(rc.z);
   uint32_t q = rc.x;
   float4 acc = make_float4(-0.f, -0.f, -0.f, -0.f);
@@ -889,7 +913,7 @@ __device__ __forceinline__ float4 narrow_row_roww(uint4 rc, uint32_t base) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc = next4t<T, EXACT>(acc, w, x[u]);
     }
-    return acc;
+    return narrow_row_tail<T, EXACT>(acc, w, e, base, rem);
   }
   for (int b = 0; b < nb; ++b) {
     float4 x[4];
@@ -905,7 +929,7 @@ __device__ __forceinline__ float4 narrow_row_roww(uint4 rc, uint32_t base) {
     // read to the loop head and waits on it before the data reads
     asm volatile("" : "+v"(e.x), "+v"(e.y));
   }
-  return acc;
+  return narrow_row_tail<T, EXACT>(acc, w, e, base, rem);
 }
 
 template <int C4>
