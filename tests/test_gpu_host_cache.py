@@ -1,0 +1,48 @@
+"""The host-memory path with the opt-in operand cache (TAL_HOST_CACHE_GB): a sequential round of
+per-call aggregations over CPU models (the reference's placement after training) gives the
+same bits with and without the cache, and the cache serves most operands."""
+import networkx as nx
+import pytest
+import torch
+
+from topology_aware_learning_amd import aggregate
+
+pytestmark = pytest.mark.gpu
+
+
+def _models(n, seed):
+    torch.manual_seed(seed)
+    ms = []
+    for _ in range(n):
+        m = torch.nn.Sequential(torch.nn.Linear(257, 129), torch.nn.BatchNorm1d(129), torch.nn.Linear(129, 11))
+        with torch.no_grad():
+            m[1].running_mean.normal_()
+            m[1].num_batches_tracked.fill_(1000)
+        ms.append(m)
+    return ms
+
+
+def _round(models, orders):
+    for i, o in enumerate(orders):  # reference order: one call per client, in place, in sequence
+        aggregate.aggregate_models([models[j] for j in o], [1 / len(o)] * len(o), models[i])
+
+
+def test_cached_round_equals_uncached(cuda, monkeypatch):
+    g = nx.random_regular_graph(4, 12, seed=3)
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(12)]
+    monkeypatch.setenv("TAL_HOST_CACHE_GB", "0")
+    a = _models(12, 5)
+    _round(a, orders)
+    _round(a, orders)
+    monkeypatch.setenv("TAL_HOST_CACHE_GB", "1")
+    b = _models(12, 5)
+    _round(b, orders)
+    with torch.no_grad():  # a "training step" on one model between rounds: its entry goes stale
+        b[4][0].weight.mul_(1.0)
+        a[4][0].weight.mul_(1.0)
+    _round(b, orders)
+    for ma, mb in zip(a, b):
+        for (k, ta), tb in zip(ma.state_dict().items(), mb.state_dict().values()):
+            assert ta.device.type == "cpu" and torch.equal(ta, tb), k
+    c = aggregate._host_cache()
+    assert c is not None and c.hits > c.misses

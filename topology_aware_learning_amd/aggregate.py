@@ -15,7 +15,10 @@ There is no CPU arithmetic path.
 """
 from __future__ import annotations
 
+import os
 import threading
+import weakref
+from collections import OrderedDict
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -83,36 +86,116 @@ def _seg_sizes(layout: StateLayout):
     return {"f32": layout.n_f32, "b16": layout.n_b16, "i64": layout.n_i64}
 
 
-def _stage(models: Sequence[nn.Module], layout: StateLayout, device) -> dict:
-    """Pack non-bound models' segments into [k, n] device tensors (one per non-empty segment).
+class _OperandCache:
+    """Opt-in (TAL_HOST_CACHE_GB > 0) device copies of host-memory operand models.
+
+    In a round of the reference's per-call apps on CPU models every model is an operand of up
+    to M calls, and each call would copy it host -> device again.  An entry is reused only while
+    the model object is alive (weak reference) and every state tensor has the data pointer and
+    version counter it had when it was copied: training steps, load_state_dict, this module's
+    own write-back and module.to() all change one of them.  What it cannot see is an in-place
+    write through `tensor.data` (a detached alias with its own version counter), hence opt-in.
+    The aggregating model's result is kept as its entry after the write-back, so a later call
+    that reads it as a neighbor copies nothing."""
+
+    def __init__(self, cap_bytes: int):
+        self.cap = cap_bytes
+        self.used = 0
+        self.lock = threading.Lock()
+        self.entries: "OrderedDict[int, tuple]" = OrderedDict()  # id -> (wref, sig, device, segs, nbytes)
+        self.hits = self.misses = 0
+
+    @staticmethod
+    def signature(sd) -> tuple:
+        return tuple((t.data_ptr(), t._version) for t in sd.values())
+
+    def get(self, model: nn.Module, sig: tuple, device):
+        with self.lock:
+            ent = self.entries.get(id(model))
+            if ent is not None and ent[0]() is model and ent[1] == sig and ent[2] == device:
+                self.entries.move_to_end(id(model))
+                self.hits += 1
+                return ent[3]
+            self.misses += 1
+            return None
+
+    def put(self, model: nn.Module, sig: tuple, device, segs: dict) -> None:
+        nbytes = sum(t.numel() * t.element_size() for t in segs.values())
+        if nbytes > self.cap:
+            return
+        with self.lock:
+            old = self.entries.pop(id(model), None)
+            if old is not None:
+                self.used -= old[4]
+            while self.entries and self.used + nbytes > self.cap:
+                self.used -= self.entries.popitem(last=False)[1][4]
+            key = id(model)
+            wref = weakref.ref(model, lambda _r, k=key: self._drop(k, _r))
+            self.entries[key] = (wref, sig, device, segs, nbytes)
+            self.used += nbytes
+
+    def _drop(self, key: int, wref) -> None:
+        with self.lock:
+            ent = self.entries.get(key)
+            if ent is not None and ent[0] is wref:
+                self.used -= ent[4]
+                del self.entries[key]
+
+
+def _host_cache() -> Optional[_OperandCache]:
+    global _CACHE
+    gb = float(os.environ.get("TAL_HOST_CACHE_GB", "0") or 0)
+    if gb <= 0:
+        return None
+    if _CACHE is None or _CACHE.cap != int(gb * (1 << 30)):
+        _CACHE = _OperandCache(int(gb * (1 << 30)))
+    return _CACHE
+
+
+_CACHE: Optional[_OperandCache] = None
+
+
+def _stage(models: Sequence[nn.Module], layout: StateLayout, device) -> List[dict]:
+    """Each non-bound model's segments as flat device tensors ({segment: [n]} per model).
 
     Models already on `device` are packed there; the others are packed into one pinned host
     buffer per segment, each operand's H2D copy issued as soon as that operand is packed so the
-    copy overlaps packing the next one (the host-memory path of the reference's CPU models)."""
-    k = len(models)
+    copy overlaps packing the next one (the host-memory path of the reference's CPU models);
+    with TAL_HOST_CACHE_GB set, an unchanged host model copied before is not copied again."""
     sizes = {g: n for g, n in _seg_sizes(layout).items() if n}
-    dev = {g: torch.empty(k, n, dtype=_SEG_DTYPE[g], device=device) for g, n in sizes.items()}
-    host_rows = []
-    sds = []
+    cache = _host_cache()
+    out: List[dict] = [None] * len(models)  # type: ignore[list-item]
+    host_rows, sds, sigs = [], [], []
     for j, m in enumerate(models):
         sd = m.state_dict()
         layout.check_compatible(sd, f"operand {j}")
         sds.append(sd)
+        sigs.append(None)
         if all(t.device == device for t in sd.values()):
-            for g in sizes:
-                torch.cat(layout.flatten_cat(sd, g), out=dev[g][j])
-        else:
-            host_rows.append(j)
+            out[j] = {g: torch.cat(layout.flatten_cat(sd, g)) for g in sizes}
+            continue
+        if cache is not None:
+            sigs[j] = _OperandCache.signature(sd)
+            hit = cache.get(m, sigs[j], device)
+            if hit is not None:
+                out[j] = hit
+                continue
+        host_rows.append(j)
     if host_rows:
         h = len(host_rows)
+        for j in host_rows:
+            out[j] = {g: torch.empty(n, dtype=_SEG_DTYPE[g], device=device) for g, n in sizes.items()}
         for g, n in sizes.items():
             esz = torch.empty((), dtype=_SEG_DTYPE[g]).element_size()
             hb = _pinned(esz * h * n, "in_" + g).view(_SEG_DTYPE[g]).view(h, n)
             for q, j in enumerate(host_rows):
                 torch.cat([t.detach().to("cpu") for t in layout.flatten_cat(sds[j], g)], out=hb[q])
-                dev[g][j].copy_(hb[q], non_blocking=True)  # in flight while the next one packs
+                out[j][g].copy_(hb[q], non_blocking=True)  # in flight while the next one packs
             _mark_used("in_" + g, device)
-    return dev
+        if cache is not None:
+            for j in host_rows:
+                cache.put(models[j], sigs[j], device, out[j])
+    return out
 
 
 _AGG = {"f32": lambda xs, w, out, mode: ops.agg_f32(xs, w, out, mode=mode),
@@ -153,7 +236,7 @@ def aggregate_models(operands: Sequence[nn.Module], weights: Sequence[float], ta
         staged = _stage([operands[j] for j in unbound], layout, device)
         for k, j in enumerate(unbound):
             for g in sizes:
-                ptrs[g][j] = staged[g][k]
+                ptrs[g][j] = staged[k][g]
 
     if tb is not None and tb[0].device == device and tb[0].layout == layout:
         rows = {"f32": tb[0].row_f32, "b16": tb[0].row_b16, "i64": tb[0].row_i64}
@@ -169,6 +252,11 @@ def aggregate_models(operands: Sequence[nn.Module], weights: Sequence[float], ta
 
     if not in_place:
         _write_back(target, layout, outs)
+        cache = _host_cache()
+        if cache is not None:  # the target's new state is this output: its next use copies nothing
+            sd = target.state_dict()
+            if not all(t.device == device for t in sd.values()):
+                cache.put(target, _OperandCache.signature(sd), device, outs)
     return target
 
 

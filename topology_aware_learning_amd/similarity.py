@@ -36,9 +36,9 @@ def _flat(models: Sequence[nn.Module], layout, device) -> List[torch.Tensor]:
         else:
             rest.append(j)
     if rest:
-        df = _stage([models[j] for j in rest], layout, device)["f32"]
+        staged = _stage([models[j] for j in rest], layout, device)
         for k, j in enumerate(rest):
-            out[j] = df[k]
+            out[j] = staged[k]["f32"]
     return out
 
 
