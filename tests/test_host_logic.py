@@ -565,31 +565,3 @@ def test_auto_dense_only_for_cliques():
     rp, col, w = csr_from_lists(orders, [[1 / 40] * 40] * 40)
     p = ops.build_plan(rp, col, w, np.arange(40, dtype=np.int32), c4=64, lds_bytes=160 * 1024, dense=-1)
     assert p.info.dense_rb == 8
-
-
-def test_dense_narrow_plan_config5():
-    """K3d plan (c4 = 32, dense_rb = 8) of BASELINE config 5's SBM-256: one group of all 256
-    sources (a 128 KiB data tile; unweighted, so compact tables in LDS beside it), about 0.41 LDS
-    reads per operand, and a staged scalar tail
-    whose c4 = 16 tile keeps the group within 160 KiB."""
-    p = ops.build_plan(*_bench_round("sbm", 256, 0), c4=32, lds_bytes=160 * 1024, dense=8)
-    i = p.info
-    assert (i.c4, i.dense_rb, i.n_groups, i.max_src, i.narrow_roww) == (32, 8, 1, 256, 1)
-    assert 256 * 512 < i.lds_bytes <= 160 * 1024  # the data tile + the LDS-resident compact tables
-    assert i.dense_reads < 0.45 * i.nnz
-    assert i.scalar_lds_bytes <= 160 * 1024
-    assert ops.round_kernel_name(p) == "k_round_dense_narrow"
-    # c4 = 16 stays sparse; c4 = 32 sparse is still the narrow kernel
-    assert ops.build_plan(*_bench_round("sbm", 256, 0), c4=16, lds_bytes=160 * 1024, dense=8).info.dense_rb == 0
-    assert ops.round_kernel_name(ops.build_plan(*_bench_round("ring", 32, 2), c4=32, lds_bytes=80 * 1024)) == \
-        "k_round_f32_narrow"
-    assert ops._dense_choices(16, False) == (0,) and ops._dense_choices(32, True) == (0, 8)
-    assert ops._dense_choices(64, True) == (0,) and ops._dense_choices(64, False) == (0, 8)
-
-
-def test_dense_narrow_needs_reference_order():
-    rp = np.array([0, 3, 5], np.int32)
-    col = np.array([2, 1, 0, 0, 1], np.int32)  # row 0's neighbours descend
-    w = np.full(5, 0.5)
-    with pytest.raises(ops._lib.TalError):
-        ops.build_plan(rp, col, w, np.arange(2, dtype=np.int32), c4=32, lds_bytes=80 * 1024, dense=8)

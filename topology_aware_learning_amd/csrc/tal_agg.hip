@@ -690,14 +690,6 @@ __device__ __forceinline__ void emit_tile_dense(const float4* s_data, const Plan
 }
 
 constexpr int kDenseRb = 8;
-constexpr int kDnC4 = 32;        // K3d (dense c4 = 32): float4 columns per staged source per tile (512 B)
-constexpr int kDnThreads = 1024;  // K3d workgroup
-constexpr uint32_t kDnUniform = 0x100u;  // compact K3d entry: one product for every row taking it
-// compact K3d entries per block: a multiple of 8 (one scalar load of eight per step)
-constexpr int64_t dn_compact_entries(int64_t n) { return (n + 7) / 8 * 8; }
-// compact K3d block table: {n, 7 pad, w[8], own_addr[8], own_w[8], out_row[8], entry[n], 8 read-ahead}
-constexpr int kDnHdr = 40;
-constexpr int64_t dn_compact_words(int64_t n_used) { return kDnHdr + dn_compact_entries(n_used) + 8; }
 constexpr int kStreamDepth = 3;        // chunks in flight ahead of the one being read
 constexpr int kStreamPerWave = 2;      // sources each wavefront moves per chunk (1 KiB DMA each)
 constexpr int kStreamMaxRows = 128;    // 16 wavefronts x one 8-row block
@@ -1508,11 +1500,6 @@ constexpr int64_t group_lds_bytes(int64_t ns, int64_t nr, int64_t no, int c4) {
   return ns * 16 * c4 + (nr + 1 + 2 * no + ns + nr) * 4;
 }
 
-// Tile width (float4 units) of the staged scalar kernel for a plan: the plan's own, except K3d
-// plans (c4 32, dense), whose 256-source groups stage a c4 = 16 tile there so the tile and the
-// plan slice fit 160 KiB.
-constexpr int scalar_c4(int c4, int dense_rb) { return c4 == 32 && dense_rb != 0 ? 16 : c4; }
-
 std::mutex g_lds_mu;
 std::vector<const void*> g_lds_raised;
 
@@ -1535,10 +1522,8 @@ int32_t validate_info(const tal_round_plan_info* info) {
     return fail(TAL_ERR_INVALID, "empty round plan");
   if (info->c4 != 16 && info->c4 != 32 && info->c4 != 64 && info->c4 != 128)
     return fail(TAL_ERR_INVALID, "plan c4 must be 16, 32, 64 or 128");
-  if (info->c4 == 16 && info->dense_rb != 0)
-    return fail(TAL_ERR_INVALID, "c4 = 16 plans are sparse (dense row blocks need c4 >= 32)");
-  if (info->c4 == 32 && info->dense_rb != 0 && info->max_src * kDnC4 > 8 * kDnThreads)
-    return fail(TAL_ERR_INVALID, "dense c4 = 32 plans stage at most 256 sources per group");
+  if (info->c4 < 64 && info->dense_rb != 0)
+    return fail(TAL_ERR_INVALID, "narrow plans (c4 16 / 32) are sparse");
   if (info->dense_rb != 0 && info->dense_rb != kDenseRb)
     return fail(TAL_ERR_INVALID, "plan dense_rb must be 0 or 8");
   if (info->stream_cs != 0 && info->stream_cs != 8 * kStreamPerWave && info->stream_cs != 16 * kStreamPerWave)
@@ -1554,7 +1539,7 @@ int32_t launch_round_scalar(const T* pin, int64_t ld_in, T* pout, int64_t ld_out
                             int64_t e0, int64_t n, const PlanView& v,
                             const tal_round_plan_info& in, bool exact, hipStream_t s) {
   if (n <= e0) return TAL_OK;
-  const int tile = 4 * scalar_c4(in.c4, in.dense_rb);
+  const int tile = 4 * in.c4;
   const size_t lds = static_cast<size_t>(in.scalar_lds_bytes);  // the largest group's tile + plan slice
   const int64_t tiles = (n - e0 + tile - 1) / tile;
   if (tiles > 0x7fffffff) return fail(TAL_ERR_INVALID, "too many tiles");
@@ -1929,354 +1914,6 @@ int32_t launch_round_stream_scalar(const void* pin, int64_t ld_in, void* pout, i
   const dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(in.n_groups));
   k<<<grid, kBlock, lds, s>>>(pin, ld_in, pout, ld_out, e0, n, v, static_cast<int>(tc));
   return check_launch("round scalar kernel (streamed plan)");
-}
-
-// ------------------------------------------------------------------------------------------
-// K3d: dense row blocks over 512-B source tiles (plan c4 = 32, dense_rb = 8).  The narrow
-// kernel's lanes split a wavefront over 64 / c4 rows, so a wavefront never shares one LDS read
-// between rows; here a lane owns 8 B (two fp32) of a source's 512-B tile, so a whole wavefront
-// covers one tile row and computes one block of 8 rows at a time with wave-uniform masks: each
-// staged source the block uses is read from LDS once (ds_read_b64) and added to every row of
-// the block that takes it (scalar branch per row bit), the rows' own models last.  A community
-// graph whose 256 sources fit one 128 KiB tile (BASELINE config 5: SBM 8 x 32) is read from HBM
-// once per round, as in the narrow kernel, with 0.4 LDS reads per operand instead of one.
-// Tables: the dense form's (tal_round_plan_info, finish_plan); the plan is read through the
-// constant address space (scalar loads).  One workgroup of 16 wavefronts per CU, the next
-// tile's loads in flight in registers during this tile's arithmetic (as K3 persistent).
-// ------------------------------------------------------------------------------------------
-
-template <typename T, bool EXACT>
-__device__ __forceinline__ v2f dn_mul(float w, v2f x) {
-  if constexpr (kIsBf16<T>) return v2f{round_bf16(__fmul_rn(w, x.x)), round_bf16(__fmul_rn(w, x.y))};
-  else return v2f{__fmul_rn(w, x.x), __fmul_rn(w, x.y)};
-}
-
-template <typename T, bool EXACT>
-__device__ __forceinline__ v2f dn_add(v2f acc, v2f pr) {
-  if constexpr (kIsBf16<T>) return v2f{round_bf16(__fadd_rn(acc.x, pr.x)), round_bf16(__fadd_rn(acc.y, pr.y))};
-  else return acc + pr;  // IEEE adds (-ffp-contract=off)
-}
-
-// acc + w * x: EXACT = the reference's rounded product then rounded add (bf16: each rounded to
-// bf16); FMA = one fused fp32 operation
-template <typename T, bool EXACT>
-__device__ __forceinline__ v2f dn_term(v2f acc, float w, v2f x) {
-  if constexpr (EXACT) return dn_add<T, EXACT>(acc, dn_mul<T, EXACT>(w, x));
-  else return __builtin_elementwise_fma(v2f{w, w}, x, acc);
-}
-
-// One table entry of a K3d block: for every row r whose mask bit is set, acc[r] += w[r] * x
-// (EXACT: v_pk_mul_f32 then v_pk_add_f32, one rounding each; FMA: v_pk_fma_f32), in inline
-// asm so that each row's update sits behind a real scalar branch (s_bitcmp1 / s_cbranch): in
-// C++ the compiler if-converts the eight conditionals into the arithmetic for every row plus
-// v_cndmask selects, 4x the vector work of the rows that take the entry.  Weights arrive as
-// four SGPR pairs (w0,w1) .. (w6,w7); op_sel picks the row's half and broadcasts it to both
-// lanes.  Bit 31 (kMaskUniform, EXACT only): one rounded product serves every row.  One wait
-// state (s_nop 0) separates a packed result from its packed reader, as the compiler's own
-// hazard recognizer places it; the block ends with one so the compiler's next reader is safe.
-typedef uint64_t u64x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(4))) const u64x4* ConstU64x4;
-
-#define DN_MUL_E(R, P) "v_pk_mul_f32 %[t], %[x], %[w" #P "] op_sel_hi:[1,0]\n\t"
-#define DN_MUL_O(R, P) "v_pk_mul_f32 %[t], %[x], %[w" #P "] op_sel:[0,1] op_sel_hi:[1,1]\n\t"
-#define DN_ROW_X(R, MUL)                                                     \
-  "s_bitcmp1_b32 %[m], " #R "\n\t"                                          \
-  "s_cbranch_scc0 .Ldn%=_x" #R "\n\t" MUL "s_nop 0\n\t"                      \
-  "v_pk_add_f32 %[a" #R "], %[a" #R "], %[t]\n"                              \
-  ".Ldn%=_x" #R ":\n\t"
-#define DN_ROW_U(R)                                                          \
-  "s_bitcmp1_b32 %[m], " #R "\n\t"                                          \
-  "s_cbranch_scc0 .Ldn%=_u" #R "\n\t"                                       \
-  "v_pk_add_f32 %[a" #R "], %[a" #R "], %[t]\n"                              \
-  ".Ldn%=_u" #R ":\n\t"
-#define DN_ROW_F_E(R, P)                                                     \
-  "s_bitcmp1_b32 %[m], " #R "\n\t"                                          \
-  "s_cbranch_scc0 .Ldn%=_f" #R "\n\t"                                       \
-  "v_pk_fma_f32 %[a" #R "], %[x], %[w" #P "], %[a" #R "] op_sel_hi:[1,0,1]\n" \
-  ".Ldn%=_f" #R ":\n\t"
-#define DN_ROW_F_O(R, P)                                                     \
-  "s_bitcmp1_b32 %[m], " #R "\n\t"                                          \
-  "s_cbranch_scc0 .Ldn%=_f" #R "\n\t"                                       \
-  "v_pk_fma_f32 %[a" #R "], %[x], %[w" #P "], %[a" #R "] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n" \
-  ".Ldn%=_f" #R ":\n\t"
-
-template <typename T, bool EXACT>
-constexpr bool kDnAsm = !(kIsBf16<T> && EXACT);  // bf16 EXACT rounds each step to bf16 (C++)
-
-template <bool EXACT, int UBIT = 31>
-__device__ __forceinline__ void dn_entry(v2f (&a)[8], v2f x, uint32_t m, u64x4 wp) {
-  const uint64_t w0 = wp[0], w1 = wp[1], w2 = wp[2], w3 = wp[3];
-  if constexpr (EXACT) {
-    v2f t;
-    asm volatile(
-        "s_bitcmp1_b32 %[m], %[ub]\n\t"
-        "s_cbranch_scc1 .Ldn%=_uni\n\t"
-        DN_ROW_X(0, DN_MUL_E(0, 0)) DN_ROW_X(1, DN_MUL_O(1, 0)) DN_ROW_X(2, DN_MUL_E(2, 1))
-        DN_ROW_X(3, DN_MUL_O(3, 1)) DN_ROW_X(4, DN_MUL_E(4, 2)) DN_ROW_X(5, DN_MUL_O(5, 2))
-        DN_ROW_X(6, DN_MUL_E(6, 3)) DN_ROW_X(7, DN_MUL_O(7, 3))
-        "s_branch .Ldn%=_end\n"
-        ".Ldn%=_uni:\n\t"
-        "v_pk_mul_f32 %[t], %[x], %[w0] op_sel_hi:[1,0]\n\t"
-        "s_nop 0\n\t"
-        DN_ROW_U(0) DN_ROW_U(1) DN_ROW_U(2) DN_ROW_U(3) DN_ROW_U(4) DN_ROW_U(5) DN_ROW_U(6) DN_ROW_U(7)
-        "\n.Ldn%=_end:\n\t"
-        "s_nop 0"
-        : [a0] "+v"(a[0]), [a1] "+v"(a[1]), [a2] "+v"(a[2]), [a3] "+v"(a[3]), [a4] "+v"(a[4]),
-          [a5] "+v"(a[5]), [a6] "+v"(a[6]), [a7] "+v"(a[7]), [t] "=&v"(t)
-        : [m] "s"(m), [x] "v"(x), [w0] "s"(w0), [w1] "s"(w1), [w2] "s"(w2), [w3] "s"(w3), [ub] "i"(UBIT)
-        : "scc");
-  } else {
-    asm volatile(
-        DN_ROW_F_E(0, 0) DN_ROW_F_O(1, 0) DN_ROW_F_E(2, 1) DN_ROW_F_O(3, 1) DN_ROW_F_E(4, 2)
-        DN_ROW_F_O(5, 2) DN_ROW_F_E(6, 3) DN_ROW_F_O(7, 3)
-        "s_nop 0"
-        : [a0] "+v"(a[0]), [a1] "+v"(a[1]), [a2] "+v"(a[2]), [a3] "+v"(a[3]), [a4] "+v"(a[4]),
-          [a5] "+v"(a[5]), [a6] "+v"(a[6]), [a7] "+v"(a[7])
-        : [m] "s"(m), [x] "v"(x), [w0] "s"(w0), [w1] "s"(w1), [w2] "s"(w2), [w3] "s"(w3)
-        : "scc");
-  }
-}
-
-// a wave-uniform LDS word as a scalar
-__device__ __forceinline__ int dn_lds_word(uint32_t addr) {
-  return __builtin_amdgcn_readfirstlane(*reinterpret_cast<__attribute__((address_space(3))) const int*>(static_cast<uintptr_t>(addr)));
-}
-
-__device__ __forceinline__ v2f lds_v2(uint32_t addr) {
-  return *reinterpret_cast<__attribute__((address_space(3))) const v2f*>(static_cast<uintptr_t>(addr));
-}
-
-// two elements at element index e (even) of an fp32 / bf16 pool
-__device__ __forceinline__ void st2(float* b, int64_t e, v2f v) {
-  __builtin_nontemporal_store(v, reinterpret_cast<v2f*>(b + e));
-}
-__device__ __forceinline__ void st2(uint16_t* b, int64_t e, v2f v) {
-  uint32_t q = cvt_bf16x2(v.x, v.y);
-  if (__builtin_isunordered(v.x, v.y)) q = store_bf16x2(v.x, v.y);
-  __builtin_nontemporal_store(q, reinterpret_cast<uint32_t*>(b + e));
-}
-
-// A block's own models (each row's last operand: all reads in flight together), then its stores.
-template <typename T, bool EXACT>
-__device__ __forceinline__ void dn_finish(v2f (&acc)[kDenseRb], uint32_t lbase, int gr0, int rows_here,
-                                          ConstI32 row_ptr, ConstI32 op_slot, ConstF32 op_w, ConstI32 out_row,
-                                          T* pout, int64_t ld_out4, int64_t e_col, bool col_ok) {
-  // rows past the group's end (a last partial block) recompute its last row and store nothing:
-  // the arithmetic stays unconditional, so the accumulators need no per-row control flow
-#pragma unroll
-  for (int r = 0; r < kDenseRb; ++r) {
-    const int gr = gr0 + min(r, rows_here - 1);
-    const int q = row_ptr[gr + 1] - 1;
-    const v2f y = dn_term<T, EXACT>(acc[r], op_w[q], lds_v2(lbase + static_cast<uint32_t>(op_slot[q]) * (kDnC4 * 16)));
-    if (r < rows_here && col_ok) st2(pout, static_cast<int64_t>(out_row[gr]) * ld_out4 * 4 + e_col, y);
-  }
-}
-
-template <int J, bool EXACT, typename T, bool CMP>
-__global__ __launch_bounds__(kDnThreads) void k_round_dense_narrow(const T* __restrict__ pin, int64_t ld_in4,
-                                                                  T* __restrict__ pout, int64_t ld_out4,
-                                                                  int64_t n4, PlanView p, int64_t n_tiles) {
-  constexpr int C4 = kDnC4;
-  constexpr int NT = kDnThreads;
-  constexpr int RB = kDenseRb;
-  constexpr int kWaves = NT / 64;
-  extern __shared__ float4 s_data[];
-  const int g = blockIdx.y;
-  const int s_beg = p.grp_src_ptr[g];
-  const int ns = p.grp_src_ptr[g + 1] - s_beg;
-  const int r_beg = p.grp_row_ptr[g];
-  const int nr = p.grp_row_ptr[g + 1] - r_beg;
-  // staging as in k_round_f32_persistent: lane-fixed slots, branch-free (a slot past the
-  // group's sources reloads source 0's chunk of its column and writes it where source 0's own
-  // slot does)
-  const int c = threadIdx.x % C4;
-  int srow[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int src = (j * NT + threadIdx.x) / C4;
-    srow[j] = p.src_row[s_beg + (src < ns ? src : 0)];
-  }
-  typename Io<T>::raw_t v[J];
-  auto load_tile = [&](int64_t tt) {
-    const int64_t col = min(tt * C4 + c, n4 - 1);  // past the end: a duplicate (cache hit)
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      int r = srow[j];
-      asm volatile("" : "+v"(r));
-      v[j] = Io<T>::ld_raw(pin, static_cast<int64_t>(r) * ld_in4 + col);
-    }
-  };
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-  const uint32_t lbase = lds_addr(s_data) + 8u * static_cast<uint32_t>(lane);
-  const ConstI32 row_ptr = (ConstI32)p.row_ptr;
-  const ConstI32 out_row = (ConstI32)p.out_row;
-  const ConstI32 op_slot = (ConstI32)p.op_slot;
-  const ConstF32 op_w = (ConstF32)p.op_w;
-  const ConstI32 base = (ConstI32)p.base;
-  const int blk0 = ((ConstI32)p.grp_blk_ptr)[g];
-  const int nblk = (nr + RB - 1) / RB;
-  // compact tables: [per-block word offsets (nblk)][block tables] after the data tile
-  int32_t* tbl_off = reinterpret_cast<int32_t*>(s_data + static_cast<size_t>(ns) * C4);
-  const uint32_t tbl_base = lds_addr(tbl_off + nblk);
-  if constexpr (CMP) {
-    int32_t* tw = tbl_off + nblk;
-    int off = 0;
-    for (int b = 0; b < nblk; ++b) {  // block tables are variable-sized: one after another
-      const ConstI32 src = base + ((ConstI32)p.blk_tab)[blk0 + b];
-      const int words = static_cast<int>(dn_compact_words(src[0]));
-      for (int k = threadIdx.x; k < words; k += NT) tw[off + k] = src[k];
-      if (threadIdx.x == 0) tbl_off[b] = off;
-      off += words;
-    }
-  }
-  int64_t t = blockIdx.x;
-  if (t < n_tiles) load_tile(t);
-  for (; t < n_tiles; t += gridDim.x) {
-    __syncthreads();  // the previous tile's readers are done with s_data (and tables staged)
-    int staged = ns * C4;
-    asm volatile("" : "+s"(staged));
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const int k = j * NT + static_cast<int>(threadIdx.x);
-      s_data[k < staged ? k : c] = Io<T>::f4(v[j]);
-    }
-    __syncthreads();
-    if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
-    const bool col_ok = t * C4 + (lane >> 1) < n4;
-    const int64_t e_col = t * C4 * 4 + 2 * lane;  // this lane's first element in a pool row
-    for (int lb = wave; lb < nblk; lb += kWaves) {
-      const ConstI32 tab = base + ((ConstI32)p.blk_tab)[blk0 + lb];
-      const int rows_here = min(RB, nr - lb * RB);
-      const int n_used = tab[0];  // multiple of 4 (compact: of 8)
-      if constexpr (CMP) {
-        // compact tables (one weight per row), staged in LDS after the data tile before the tile
-        // loop: no scalar loads in the walk (the scalar cache missed 35 % of the table reads).
-        // The block's header and each step's eight entries are broadcast LDS reads turned into
-        // scalars by readfirstlane; the next eight are read while this step's data reads fly.
-        const uint32_t tb = tbl_base + 4u * static_cast<uint32_t>(tbl_off[lb]);
-        const int n_used = dn_lds_word(tb);
-        u64x4 wp;
-        f32x8 wr;
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          const uint32_t wbits = static_cast<uint32_t>(dn_lds_word(tb + 32u + 4u * r));
-          wr[r] = __uint_as_float(wbits);
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          wp[k] = static_cast<uint64_t>(__float_as_uint(wr[2 * k])) |
-                  (static_cast<uint64_t>(__float_as_uint(wr[2 * k + 1])) << 32);
-        v2f acc[RB];
-#pragma unroll
-        for (int r = 0; r < RB; ++r) acc[r] = v2f{-0.f, -0.f};
-        uint32_t ea = tb + 4u * kDnHdr;
-        uint4 c0 = lds_u4(ea), c1 = lds_u4(ea + 16u);
-        for (int e = 0; e < n_used; e += 8) {
-          ea += 32u;
-          const uint4 n0 = lds_u4(ea), n1 = lds_u4(ea + 16u);  // 8 read-ahead words at the end
-          const uint32_t cw[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-          v2f x[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) x[u] = lds_v2(lbase + (cw[u] & ~0x1ffu));
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const uint32_t m = __builtin_amdgcn_readfirstlane(cw[u]);
-            if constexpr (kDnAsm<T, EXACT>) {
-              dn_entry<EXACT, 8>(acc, x[u], m, wp);
-            } else if (m & kDnUniform) {  // block-uniform weight: one rounded product
-              const v2f pr = dn_mul<T, EXACT>(wr[0], x[u]);
-#pragma unroll
-              for (int r = 0; r < RB; ++r)
-                if (m & (1u << r)) acc[r] = dn_add<T, EXACT>(acc[r], pr);
-            } else {
-#pragma unroll
-              for (int r = 0; r < RB; ++r)
-                if (m & (1u << r)) acc[r] = dn_term<T, EXACT>(acc[r], wr[r], x[u]);
-            }
-          }
-          c0 = n0;
-          c1 = n1;
-        }
-        // own models (header: address, weight, out row per row), then the stores
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          const uint32_t oa = static_cast<uint32_t>(dn_lds_word(tb + 64u + 4u * r));
-          const float ow = __uint_as_float(static_cast<uint32_t>(dn_lds_word(tb + 96u + 4u * r)));
-          const int orow = dn_lds_word(tb + 128u + 4u * r);
-          const v2f y = dn_term<T, EXACT>(acc[r], ow, lds_v2(lbase + oa));
-          if (orow >= 0 && col_ok) st2(pout, static_cast<int64_t>(orow) * ld_out4 * 4 + e_col, y);
-        }
-        continue;
-      }
-      const ConstI32x4 slots4 = (ConstI32x4)(tab + 8);
-      const ConstI32x4 masks4 = (ConstI32x4)(tab + 8 + n_used);
-      const ConstF32x8 wts8 = (ConstF32x8)(tab + 8 + 2 * n_used);
-      const ConstU64x4 wts4p = (ConstU64x4)(tab + 8 + 2 * n_used);  // the same, as weight pairs
-      v2f acc[RB];
-#pragma unroll
-      for (int r = 0; r < RB; ++r) acc[r] = v2f{-0.f, -0.f};  // -0 + y == y for every y
-      for (int e = 0; e < n_used; e += 4) {
-        const i32x4 sl = slots4[e >> 2];
-        const i32x4 mk = masks4[e >> 2];
-        v2f x[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) x[u] = lds_v2(lbase + static_cast<uint32_t>(sl[u]) * (C4 * 16));
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const uint32_t m = static_cast<uint32_t>(mk[u]);
-          if constexpr (kDnAsm<T, EXACT>) {
-            const u64x4 wp = wts4p[e + u];
-            dn_entry<EXACT>(acc, x[u], m, wp);
-          } else {  // bf16 EXACT: the compiler's form (its updates become selects for every row)
-            const f32x8 wv = wts8[e + u];
-            if (m & kMaskUniform) {
-              const v2f pr = dn_mul<T, EXACT>(wv[0], x[u]);
-#pragma unroll
-              for (int r = 0; r < RB; ++r)
-                if (m & (1u << r)) acc[r] = dn_add<T, EXACT>(acc[r], pr);
-            } else {
-#pragma unroll
-              for (int r = 0; r < RB; ++r)
-                if (m & (1u << r)) acc[r] = dn_term<T, EXACT>(acc[r], wv[r], x[u]);
-            }
-          }
-        }
-      }
-      dn_finish<T, EXACT>(acc, lbase, r_beg + lb * RB, rows_here, row_ptr, op_slot, op_w, out_row, pout,
-                          ld_out4, e_col, col_ok);
-    }
-  }
-}
-
-template <bool EXACT, typename T, bool CMP>
-int32_t launch_round_dense_narrow_t(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
-                                    const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
-  // the data tile (compact tables: + the group's tables, the plan's lds_bytes)
-  const size_t lds = CMP ? static_cast<size_t>(in.lds_bytes) : static_cast<size_t>(in.max_src) * kDnC4 * 16;
-  const int64_t loads = static_cast<int64_t>(in.max_src) * kDnC4;  // float4 staging loads per tile
-  auto k = k_round_dense_narrow<8, EXACT, T, CMP>;
-  if (loads <= 1LL * kDnThreads) k = k_round_dense_narrow<1, EXACT, T, CMP>;
-  else if (loads <= 2LL * kDnThreads) k = k_round_dense_narrow<2, EXACT, T, CMP>;
-  else if (loads <= 4LL * kDnThreads) k = k_round_dense_narrow<4, EXACT, T, CMP>;
-  else if (loads > 8LL * kDnThreads) return fail(TAL_ERR_CAPACITY, "dense narrow plan: more than 256 sources per group");
-  int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
-  if (rc) return rc;
-  const int64_t tiles = (n4 + kDnC4 - 1) / kDnC4;
-  const int64_t per_cu = resident_per_cu(reinterpret_cast<const void*>(k), kDnThreads, lds);
-  int64_t gx = std::max<int64_t>(1, 256 * per_cu / in.n_groups);
-  gx = std::min<int64_t>(gx, tiles);
-  const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(in.n_groups));
-  k<<<grid, kDnThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles);
-  return check_launch("round kernel (dense narrow)");
-}
-
-// compact tables (narrow_roww set on a K3d plan) or the wide per-entry weight tables
-template <bool EXACT, typename T>
-int32_t launch_round_dense_narrow(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
-                                  const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
-  if (in.narrow_roww) return launch_round_dense_narrow_t<EXACT, T, true>(pin, ld_in, pout, ld_out, n4, v, in, s);
-  return launch_round_dense_narrow_t<EXACT, T, false>(pin, ld_in, pout, ld_out, n4, v, in, s);
 }
 
 template <int C4, bool EXACT, bool DENSE, typename T = float>
@@ -2817,16 +2454,12 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
   if (stream_cs > 0 && !dense_ok)
     return fail(TAL_ERR_INVALID, "tal_round_plan_build_stream: rows must list operands in reference order");
   const int32_t rb = dense_ok ? kDenseRb : 0;
-  // K3d with one weight per row (unweighted, scale_agg): compact tables, see tal_round_plan_info
-  const bool dn_compact = rb && c4 == kDnC4 && stream_cs == 0 && rows_uniform_weights(rows, row_ptr_host, w_host);
   std::vector<int32_t> grp_blk_ptr{0};
   int64_t dense_words = 0;
   if (rb) {
     for (int g = 0; g < G; ++g)
       grp_blk_ptr.push_back(grp_blk_ptr.back() + (grp_row_ptr[g + 1] - grp_row_ptr[g] + rb - 1) / rb);
-    for (const auto& u : blk_used)
-      dense_words += dn_compact ? dn_compact_words(static_cast<int64_t>(u.size()))
-                                : 8 + static_cast<int64_t>(u.size()) * (rb + 2);
+    for (const auto& u : blk_used) dense_words += 8 + static_cast<int64_t>(u.size()) * (rb + 2);
   }
   const int32_t n_blocks = rb ? grp_blk_ptr.back() : 0;
 
@@ -2838,22 +2471,13 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
   for (int g = 0; g < G; ++g) {
     const int64_t nr = grp_row_ptr[g + 1] - grp_row_ptr[g];
     const int64_t no = row_ptr_host[grp_row_ptr[g + 1]] - row_ptr_host[grp_row_ptr[g]];
-    lds_need = std::max(lds_need, group_lds_bytes(grp_src_ptr[g + 1] - grp_src_ptr[g], nr, no, scalar_c4(c4, rb)));
+    lds_need = std::max(lds_need, group_lds_bytes(grp_src_ptr[g + 1] - grp_src_ptr[g], nr, no, c4));
   }
   const int64_t scalar_need = lds_need;
-  const bool roww = c4 < 64 && !rb && rows_uniform_weights(rows, row_ptr_host, w_host) && roww_slots_fit(max_col, c4);
+  const bool roww = c4 < 64 && rows_uniform_weights(rows, row_ptr_host, w_host) && roww_slots_fit(max_col, c4);
   std::vector<uint16_t> nsl;   // ROWW slots
   std::vector<int32_t> nrw;    // ROWW row weights
-  if (c4 < 64 && rb) {  // K3d: the data tile (+ compact: the group's block tables, LDS-resident)
-    lds_need = 0;
-    for (int g = 0, b = 0; g < G; ++g) {
-      int64_t tw = 0;
-      for (int r0 = grp_row_ptr[g]; r0 < grp_row_ptr[g + 1]; r0 += rb, ++b)
-        tw += dn_compact ? 1 + dn_compact_words(static_cast<int64_t>(blk_used[b].size())) : 0;
-      lds_need = std::max<int64_t>(lds_need, static_cast<int64_t>(grp_src_ptr[g + 1] - grp_src_ptr[g]) * kDnC4 * 16 + 4 * tw);
-    }
-  }
-  if (c4 < 64 && !rb) {
+  if (c4 < 64) {
     lds_need = 0;  // the narrow kernel's carve replaces the staged one
     nrp.assign(static_cast<size_t>(rows) + 1, 0);
     const float one = 1.0f;
@@ -2935,7 +2559,7 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
   in.off_npairs = static_cast<int32_t>(off); off += static_cast<int64_t>(npr.size());
   in.npairs = static_cast<int32_t>(roww ? nsl.size() : npr.size() / 2);
   in.max_npairs = static_cast<int32_t>(max_np);
-  in.narrow_roww = (roww || dn_compact) ? 1 : 0;
+  in.narrow_roww = roww ? 1 : 0;
   in.off_nrow_w = static_cast<int32_t>(off); off += static_cast<int64_t>(nrw.size());
   in.scalar_lds_bytes = static_cast<int32_t>(scalar_need);
   if (off > 0x7fffffff) return fail(TAL_ERR_INVALID, "tal_round_plan_build: plan larger than 2^31 words");
@@ -2971,12 +2595,8 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
         const std::vector<int32_t>& tabs = blk_used[b];
         const int64_t nu = static_cast<int64_t>(tabs.size());  // multiple of 4
         plan_host[in.off_blk_tab + b] = static_cast<int32_t>(pos);
+        int32_t* tab = plan_host + pos;
         const int64_t words = 8 + nu * (rb + 2);  // multiple of 8: the next table stays aligned
-        // (compact K3d tables are built in this wide form first, in a scratch copy)
-        std::vector<int32_t> scratch;
-        if (dn_compact) scratch.assign(static_cast<size_t>(words), 0);
-        int32_t* tab = dn_compact ? scratch.data() : plan_host + pos;
-        int32_t* out_tab = plan_host + pos;
         memset(tab, 0, 4 * static_cast<size_t>(words));
         tab[0] = static_cast<int32_t>(nu);
         int32_t* t_slot = tab + 8;
@@ -3015,42 +2635,6 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
           if (t_mask[e] == 0 || !uniform[e] || __builtin_popcount(static_cast<uint32_t>(t_mask[e])) < 2) continue;
           t_mask[e] = static_cast<int32_t>(static_cast<uint32_t>(t_mask[e]) | kMaskUniform);
           for (int r = 0; r < rb; ++r) memcpy(t_w + e * rb + r, &wbits[e], 4);
-        }
-        if (dn_compact) {  // re-encode (dn_compact_words): row weights, own models, out rows, entries
-          const int rows_here = std::min(r0 + rb, grp_row_ptr[g + 1]) - r0;
-          const int64_t nc = dn_compact_entries(nu);
-          std::vector<int32_t> ent(static_cast<size_t>(nc) + 8, 0);
-          uint32_t rw[kDenseRb] = {0, 0, 0, 0, 0, 0, 0, 0};
-          int32_t own[3 * kDenseRb];
-          bool block_uniform = true;
-          for (int r = 0; r < kDenseRb; ++r) {  // rows past a partial block repeat its last row
-            const int rr = r0 + std::min(r, rows_here - 1);
-            const int32_t ks = row_ptr_host[rr + 1] - 1;  // own model: the row's last operand
-            const float wf = static_cast<float>(w_host[row_ptr_host[rr]]);
-            const float ws = static_cast<float>(w_host[ks]);
-            memcpy(&rw[r], &wf, 4);
-            own[r] = slot[ks] * (kDnC4 * 16);
-            memcpy(&own[kDenseRb + r], &ws, 4);
-            own[2 * kDenseRb + r] = r < rows_here ? out_row_host[rr] : -1;
-            if (r < rows_here) block_uniform = block_uniform && rw[r] == rw[0];
-          }
-          int32_t last_slot = 0;
-          for (int64_t e = 0; e < nc; ++e) {
-            const uint32_t m = e < nu ? static_cast<uint32_t>(t_mask[e]) & 0xffu : 0u;
-            const int32_t sl = e < nu && m ? t_slot[e] : last_slot;  // padding re-reads a real slot
-            last_slot = sl;
-            const bool uni = block_uniform && __builtin_popcount(m) >= 2;
-            ent[e] = static_cast<int32_t>(static_cast<uint32_t>(sl) * (kDnC4 * 16) | (uni ? kDnUniform : 0u) | m);
-          }
-          for (int64_t e = nc; e < nc + 8; ++e) ent[e] = ent[nc - 1] & ~0x1ff;  // read-ahead: mask 0
-          const int64_t cw = dn_compact_words(nu);
-          memset(out_tab, 0, 4 * static_cast<size_t>(cw));
-          out_tab[0] = static_cast<int32_t>(nc);
-          memcpy(out_tab + 8, rw, sizeof(rw));
-          memcpy(out_tab + 16, own, sizeof(own));
-          memcpy(out_tab + kDnHdr, ent.data(), 4 * ent.size());
-          pos += cw;
-          continue;
         }
         if (stream_cs > 0) {  // bit 8+r: the entry is row r's own model (captured, added last)
           for (int r = r0; r < std::min(r0 + rb, grp_row_ptr[g + 1]); ++r) {
@@ -3149,27 +2733,16 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
   if (rc) return rc;
   if (c4 != 16 && c4 != 32 && c4 != 64 && c4 != 128)
     return fail(TAL_ERR_INVALID, "tal_round_plan_build: c4 must be 16, 32, 64 or 128");
+  if (c4 < 64) dense_rb = 0;  // narrow tiles: sparse form (a wavefront covers 64 / c4 rows)
   if (dense_rb != 0 && dense_rb != kDenseRb && dense_rb != -1)
     return fail(TAL_ERR_INVALID, "tal_round_plan_build: dense_rb must be 0, 8 or -1");
-  // c4 = 16 (and c4 = 32 unless dense_rb = 8 is asked for): the narrow kernel, sparse form (a
-  // wavefront covers 64 / c4 rows); c4 = 32 with dense_rb = 8: K3d (one row block per wavefront)
-  const bool dense_narrow = c4 == 32 && dense_rb == kDenseRb;
-  if (c4 < 64 && !dense_narrow) dense_rb = 0;
-  if (dense_narrow && !reference_order(rows, row_ptr_host, col_host))
-    return fail(TAL_ERR_INVALID, "tal_round_plan_build: dense row blocks need every row in reference order "
-                                 "(sorted neighbors, then self)");
   // group consecutive rows while the union of their sources fits the LDS budget (both round
   // kernels stage 16*c4 bytes per source; the scalar one also the plan slice)
-  const bool roww = c4 < 64 && !dense_narrow && rows_uniform_weights(rows, row_ptr_host, w_host) &&
-                    roww_slots_fit(max_col, c4);
-  const bool dn_rows_uniform = dense_narrow && rows_uniform_weights(rows, row_ptr_host, w_host);
+  const bool roww = c4 < 64 && rows_uniform_weights(rows, row_ptr_host, w_host) && roww_slots_fit(max_col, c4);
   std::vector<int32_t> batches;
   auto fits = [&](int64_t ns, int64_t nr, int64_t no, int64_t r0) {
-    const int64_t sliced = group_lds_bytes(ns, nr, no, scalar_c4(c4, dense_narrow ? kDenseRb : 0));
+    const int64_t sliced = group_lds_bytes(ns, nr, no, c4);
     if (c4 >= 64) return sliced <= lds_bytes;
-    if (dense_narrow)  // K3d: the data tile (+ compact tables, bounded by operands), 8 loads per lane
-      return ns * kDnC4 * 16 + (dn_rows_uniform ? 4 * ((nr + 7) / 8 * (1 + kDnHdr + 15) + no) : 0) <= lds_bytes &&
-             ns * kDnC4 <= 8 * kDnThreads && sliced <= 160 * 1024;
     // narrow kernel: its own carve (exact ROWW padding; pairs: <= 3 per row) and read-ahead
     // within the budget; the staged scalar tail kernel within the hardware's 160 KiB
     const int64_t narrow = static_cast<int64_t>(
@@ -3180,7 +2753,7 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
   Groups grp;
   rc = group_rows(rows, row_ptr_host, col_host, max_col, fits, &grp);
   if (rc) return rc;
-  if (c4 >= 64 || dense_narrow)
+  if (c4 >= 64)
     return finish_plan(rows, row_ptr_host, col_host, w_host, out_row_host, max_col, grp, c4, dense_rb, 0,
                        plan_host, plan_capacity_words, info);
   // Narrow tiles: a wavefront pass computes 64 / c4 consecutive plan rows in lock step, so the
@@ -3258,10 +2831,6 @@ int32_t tal_agg_round_f32(const float* pool_in, int64_t ld_in, float* pool_out, 
     e_vec = n4 * 4;
     if (n4 > 0 && info->stream_cs > 0) {
       rc = launch_round_stream(pool_in, ld_in, pool_out, ld_out, n4, v, *info, exact, s);
-      if (rc) return rc;
-    } else if (n4 > 0 && info->c4 < 64 && info->dense_rb) {
-      rc = exact ? launch_round_dense_narrow<true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s)
-                 : launch_round_dense_narrow<false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s);
       if (rc) return rc;
     } else if (n4 > 0 && info->c4 < 64) {
       if (info->c4 == 16)
@@ -3373,9 +2942,9 @@ int32_t tal_agg_round_bf16(const uint16_t* pool_in, int64_t ld_in, uint16_t* poo
                            int32_t mode, void* stream) {
   int32_t rc = validate_info(info);
   if (rc) return rc;
-  if ((info->dense_rb != 0 && info->c4 != kDnC4) || info->stream_cs != 0)
-    return fail(TAL_ERR_INVALID, "tal_agg_round_bf16: bf16 rounds take sparse, narrow or dense c4 = 32 "
-                                 "plans (stream_cs 0)");
+  if (info->dense_rb != 0 || info->stream_cs != 0)
+    return fail(TAL_ERR_INVALID, "tal_agg_round_bf16: bf16 rounds take sparse or narrow plans "
+                                 "(dense_rb 0, stream_cs 0)");
   if (!pool_in || !pool_out || !plan_dev) return fail(TAL_ERR_INVALID, "tal_agg_round_bf16: null pointer");
   if (n < 0 || ld_in < n || ld_out < n) return fail(TAL_ERR_INVALID, "tal_agg_round_bf16: bad n / ld");
   if (pool_in == pool_out && info->n_groups > 1)
@@ -3390,11 +2959,7 @@ int32_t tal_agg_round_bf16(const uint16_t* pool_in, int64_t ld_in, uint16_t* poo
   if (vec) {
     const int64_t n4 = n / 4;
     e_vec = n4 * 4;
-    if (n4 > 0 && info->dense_rb) {
-      rc = exact ? launch_round_dense_narrow<true>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s)
-                 : launch_round_dense_narrow<false>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s);
-      if (rc) return rc;
-    } else if (n4 > 0) {
+    if (n4 > 0) {
       switch (info->c4 * 2 + (exact ? 1 : 0)) {
         case 33: rc = launch_round_narrow<16, true, uint16_t>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
         case 32: rc = launch_round_narrow<16, false, uint16_t>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;

@@ -371,12 +371,12 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
     the fallback when only one candidate builds."""
     if pool_in.data_ptr() == pool_out.data_ptr():
         raise ValueError("tune_plan needs distinct input / output pools")
-    bf16 = pool_in.dtype == torch.bfloat16  # bf16 rounds: sparse, narrow and K3d plans
+    bf16 = pool_in.dtype == torch.bfloat16  # bf16 rounds: sparse and narrow plans only
     run = round_bf16 if bf16 else round_f32
     cands = []
     for c4 in TILE_WIDTHS:
         for budget in LDS_BUDGETS:
-            for dense in _dense_choices(c4, bf16):
+            for dense in ((0,) if c4 < 64 or bf16 else (0, 8)):
                 try:
                     p = build_plan(row_ptr, col, w, out_row, c4=c4, lds_bytes=budget, dense=dense)
                 except _lib.TalError:
@@ -436,17 +436,6 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
     return best
 
 
-def _dense_choices(c4: int, bf16: bool):
-    """dense_rb values tune_plan tries at a tile width: c4 = 16 is sparse only; c4 = 32 also
-    takes K3d (dense row blocks over 512-B tiles, fp32 and bf16); c4 >= 64 dense blocks are fp32
-    only."""
-    if c4 == 16:
-        return (0,)
-    if c4 == 32:
-        return (0, 8)
-    return (0,) if bf16 else (0, 8)
-
-
 def plan_from_spec(row_ptr, col, w, out_row, spec: dict) -> RoundPlan:
     """Rebuild a plan tune_plan chose (its `spec`): profiling runs then time the same plan
     without re-tuning."""
@@ -488,7 +477,7 @@ def round_kernel_name(plan) -> str:
     if info.stream_cs:
         return "k_round_stream"
     if info.c4 < 64:
-        return "k_round_dense_narrow" if info.dense_rb else "k_round_f32_narrow"
+        return "k_round_f32_narrow"
     threads = 1024 if info.c4 == 64 else 512
     j_max = 20 if threads <= 512 else 8
     loads = info.max_src * info.c4
@@ -562,7 +551,7 @@ def round_i64(pool_in: torch.Tensor, pool_out: torch.Tensor, plan: RoundPlan, n:
 
 def round_bf16(pool_in: torch.Tensor, pool_out: torch.Tensor, plan: RoundPlan, n: Optional[int] = None,
                mode: int = MODE_EXACT, stream=None) -> torch.Tensor:
-    """K3 on [models, ld] bf16 pools (sparse, narrow or K3d plans; modes as agg_bf16)."""
+    """K3 on [models, ld] bf16 pools (sparse or narrow plans; modes as agg_bf16)."""
     if isinstance(plan, CliquePlan):
         plan = plan.full
     return _round(pool_in, pool_out, plan, n, torch.bfloat16, mode, stream)
