@@ -46,3 +46,32 @@ def test_cached_round_equals_uncached(cuda, monkeypatch):
             assert ta.device.type == "cpu" and torch.equal(ta, tb), k
     c = aggregate._host_cache()
     assert c is not None and c.hits > c.misses
+
+
+@pytest.mark.parametrize("cache_gb", ["0", "1"])
+def test_pinned_rows_round_equals_default(cuda, monkeypatch, cache_gb):
+    """TAL_HOST_PIN: CPU models bound to pinned host rows (one DMA per segment each way, no
+    packing) give the default path's bits, with and without the operand cache, across an
+    in-place training-like update (version counters) and a replaced tensor (a re-bind)."""
+    g = nx.random_regular_graph(4, 12, seed=3)
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(12)]
+
+    def run(pin, gb):
+        monkeypatch.setenv("TAL_HOST_PIN", pin)
+        monkeypatch.setenv("TAL_HOST_CACHE_GB", gb)
+        ms = _models(12, 7)
+        _round(ms, orders)
+        with torch.no_grad():
+            ms[4][0].weight.add_(0.25)                       # in place: version counter moves
+            ms[7][2].weight.data = ms[7][2].weight.data * 2  # replaced storage: binding is lost
+        _round(ms, orders)
+        return ms
+
+    ref = run("0", "0")
+    got = run("1", cache_gb)
+    for ma, mb in zip(ref, got):
+        for (k, ta), tb in zip(ma.state_dict().items(), mb.state_dict().values()):
+            assert tb.device.type == "cpu" and torch.equal(ta, tb), k
+    assert all(t.is_pinned() for t in got[7].state_dict().values())  # re-bound after the swap
+    b = aggregate.bound_row(got[0])
+    assert b is not None and b[0].device.type == "cpu" and b[0].f32.is_pinned()

@@ -1,6 +1,7 @@
 """Host-memory path, one round (not part of the product): 64 CPU ResNet-50 models (the
 reference's placement after training), random 8-regular graph, 64 per-call aggregations in
-client order, without and with the opt-in operand cache (TAL_HOST_CACHE_GB).
+client order, without and with the opt-in operand cache (TAL_HOST_CACHE_GB), then with the models
+bound to pinned host rows (TAL_HOST_PIN; bound on the warm-up call, the steady state is timed).
 usage: python tools/host_round_rate.py [rounds]"""
 import json
 import os
@@ -24,9 +25,13 @@ def main():
     g = nx.random_regular_graph(8, 64, seed=0)
     orders = [sorted(g.neighbors(i)) + [i] for i in range(64)]
     n = sum(v.numel() for v in models[0].state_dict().values())
-    for gb in ("0", "16"):
+    for pin, gb in (("0", "0"), ("0", "16"), ("1", "0"), ("1", "16")):
         os.environ["TAL_HOST_CACHE_GB"] = gb
+        os.environ["TAL_HOST_PIN"] = pin
         aggregate.aggregate_models([models[j] for j in orders[0]], [1 / 9] * 9, models[0])  # warm
+        if pin == "1":  # bind every model (one host copy each) before timing
+            for i, o in enumerate(orders):
+                aggregate.aggregate_models([models[j] for j in o], [1 / len(o)] * len(o), models[i])
         ts = []
         for _ in range(rounds):
             torch.cuda.synchronize()
@@ -36,7 +41,7 @@ def main():
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t)
         c = aggregate._host_cache()
-        print(json.dumps(dict(host_cache_gb=float(gb), ms_per_round=[round(1e3 * x, 1) for x in ts],
+        print(json.dumps(dict(host_pin=pin == "1", host_cache_gb=float(gb), ms_per_round=[round(1e3 * x, 1) for x in ts],
                               ms_per_call=round(1e3 * min(ts) / 64, 2),
                               params_per_s=64 * n / min(ts),
                               hits=c.hits if c else None, misses=c.misses if c else None)), flush=True)

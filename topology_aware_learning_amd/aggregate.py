@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .arena import StateLayout, bound_row
+from .arena import ModelPool, StateLayout, bound_row
 
 _tls = threading.local()
 _layout_cache: dict = {}
@@ -44,7 +44,7 @@ def layout_of_module(model: nn.Module) -> StateLayout:
 def _device_for(models: Sequence[nn.Module]) -> torch.device:
     for m in models:
         b = bound_row(m)
-        if b is not None:
+        if b is not None and b[0].device.type == "cuda":  # (pinned host rows: TAL_HOST_PIN)
             return b[0].device
     for m in models:
         for t in m.state_dict().values():
@@ -155,6 +155,53 @@ def _host_cache() -> Optional[_OperandCache]:
 _CACHE: Optional[_OperandCache] = None
 
 
+def _pin_enabled() -> bool:
+    return os.environ.get("TAL_HOST_PIN", "0") not in ("", "0")
+
+
+def _host_binding(model: nn.Module, layout: StateLayout) -> Optional[Tuple[ModelPool, int]]:
+    """(pool, row) of a model whose state lives in a pinned host row, or None.
+
+    With TAL_HOST_PIN set, a model whose state is on the CPU and not bound anywhere is bound
+    first: its state is copied once into a pinned one-row host pool and its parameters / buffers
+    become views of that row (ModelPool.bind, as for device pools).  The call then moves its
+    operands host -> device and its result device -> host as one DMA per segment straight
+    from / into the row - no packing of 320 tensors into a staging buffer and no unpacking
+    copy afterwards.  A model whose tensors are replaced later (module.to(), load_state_dict
+    into new tensors) fails the binding check and is bound again on its next call."""
+    b = bound_row(model)
+    if b is not None:
+        return b if b[0].device.type == "cpu" and b[0].layout == layout else None
+    if not _pin_enabled():
+        return None
+    sd = model.state_dict()
+    if not sd or any(t.device.type != "cpu" for t in sd.values()):
+        return None
+    try:
+        layout.check_compatible(sd, "model")
+    except ValueError:
+        return None
+
+    def pinned(rows_ld, dtype):
+        return torch.empty((1, rows_ld), dtype=dtype, pin_memory=rows_ld > 0)
+
+    pool = ModelPool(layout, 1, "cpu", f32=pinned(layout.ld_f32, torch.float32),
+                     i64=pinned(layout.ld_i64, torch.int64), b16=pinned(layout.ld_b16, torch.bfloat16))
+    pool.bind(model, 0)
+    return pool, 0
+
+
+def _pinned_signature(model: nn.Module, pool: ModelPool) -> tuple:
+    """Cache signature of a pinned-bound model: its row (binding already checked by bound_row)
+    and the version counter of every bound tensor (training steps bump them)."""
+    return (pool.f32.data_ptr(),) + tuple(table[attr]._version for table, attr in model._tal_slots)
+
+
+def _row_segments(pool: ModelPool, r: int, sizes) -> dict:
+    rows = {"f32": pool.row_f32, "b16": pool.row_b16, "i64": pool.row_i64}
+    return {g: rows[g](r) for g in sizes}
+
+
 def _stage(models: Sequence[nn.Module], layout: StateLayout, device) -> List[dict]:
     """Each non-bound model's segments as flat device tensors ({segment: [n]} per model).
 
@@ -167,6 +214,22 @@ def _stage(models: Sequence[nn.Module], layout: StateLayout, device) -> List[dic
     out: List[dict] = [None] * len(models)  # type: ignore[list-item]
     host_rows, sds, sigs = [], [], []
     for j, m in enumerate(models):
+        hb = _host_binding(m, layout)
+        if hb is not None:  # pinned row: one H2D per segment straight from it
+            sig = _pinned_signature(m, hb[0]) if cache is not None else None
+            hit = cache.get(m, sig, device) if cache is not None else None
+            if hit is not None:
+                out[j] = hit
+                continue
+            src = _row_segments(hb[0], hb[1], sizes)
+            out[j] = {g: torch.empty(n, dtype=_SEG_DTYPE[g], device=device) for g, n in sizes.items()}
+            for g in sizes:
+                out[j][g].copy_(src[g], non_blocking=True)
+            if cache is not None:
+                cache.put(m, sig, device, out[j])
+            sds.append(None)
+            sigs.append(None)
+            continue
         sd = m.state_dict()
         layout.check_compatible(sd, f"operand {j}")
         sds.append(sd)
@@ -216,16 +279,17 @@ def aggregate_models(operands: Sequence[nn.Module], weights: Sequence[float], ta
     tb = bound_row(target)
     bounds = [bound_row(m) for m in operands]
     layout = tb[0].layout if tb is not None else layout_of_module(target)
-    device = next((b[0].device for b in [tb, *bounds] if b is not None), None)
+    device = next((b[0].device for b in [tb, *bounds] if b is not None and b[0].device.type == "cuda"), None)
     if device is None:
         device = _device_for(list(operands) + [target])
+    host_target = _host_binding(target, layout) if tb is None or tb[0].device.type == "cpu" else None
     sizes = {g: n for g, n in _seg_sizes(layout).items() if n}
 
     ptrs: dict = {g: [None] * len(operands) for g in sizes}
     unbound = []
     for j, m in enumerate(operands):
         b = bounds[j]
-        if b is not None and b[0].device == device and b[0].layout == layout:
+        if b is not None and b[0].device == device and b[0].layout == layout:  # device pool row
             pool, r = b
             rows = {"f32": pool.row_f32, "b16": pool.row_b16, "i64": pool.row_i64}
             for g in sizes:
@@ -250,13 +314,23 @@ def aggregate_models(operands: Sequence[nn.Module], weights: Sequence[float], ta
     for g in sizes:
         _AGG[g](ptrs[g], w, outs[g], mode)
 
-    if not in_place:
+    if host_target is not None:  # pinned row: one D2H per segment straight into it
+        dst = _row_segments(host_target[0], host_target[1], sizes)
+        for g in sizes:
+            dst[g].copy_(outs[g], non_blocking=True)
+        torch.cuda.current_stream(device).synchronize()
+        cache = _host_cache()
+        if cache is not None:
+            cache.put(target, _pinned_signature(target, host_target[0]), device, outs)
+    elif not in_place:
         _write_back(target, layout, outs)
         cache = _host_cache()
         if cache is not None:  # the target's new state is this output: its next use copies nothing
             sd = target.state_dict()
             if not all(t.device == device for t in sd.values()):
                 cache.put(target, _OperandCache.signature(sd), device, outs)
+    elif unbound and _pin_enabled():  # H2D copies from pinned rows may still be in flight
+        torch.cuda.current_stream(device).synchronize()
     return target
 
 
