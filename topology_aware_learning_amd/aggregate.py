@@ -174,6 +174,17 @@ def _host_binding(model: nn.Module, layout: StateLayout) -> Optional[Tuple[Model
         return b if b[0].device.type == "cpu" and b[0].layout == layout else None
     if not _pin_enabled():
         return None
+    with _bind_lock:  # the reference runs two app calls at once; bind a shared operand once
+        b = bound_row(model)
+        if b is not None:
+            return b if b[0].device.type == "cpu" and b[0].layout == layout else None
+        return _bind_pinned(model, layout)
+
+
+_bind_lock = threading.Lock()
+
+
+def _bind_pinned(model: nn.Module, layout: StateLayout) -> Optional[Tuple[ModelPool, int]]:
     sd = model.state_dict()
     if not sd or any(t.device.type != "cpu" for t in sd.values()):
         return None
