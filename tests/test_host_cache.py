@@ -5,6 +5,7 @@ import gc
 
 import torch
 
+from topology_aware_learning_amd import aggregate
 from topology_aware_learning_amd.aggregate import _OperandCache
 
 
@@ -49,3 +50,17 @@ def test_lru_eviction_by_bytes():
     assert c.get(ms[2], _OperandCache.signature(ms[2].state_dict()), torch.device("cpu")) is not None
     c.put(ms[0], _OperandCache.signature(ms[0].state_dict()), torch.device("cpu"), _segs(1000))  # > cap
     assert len(c.entries) == 2
+
+
+def test_pinned_binding_is_opt_in(monkeypatch):
+    """Without TAL_HOST_PIN a CPU model is never re-pointed to pinned rows (the default host
+    path packs into staging buffers and leaves the model's tensors alone)."""
+    from topology_aware_learning_amd.arena import StateLayout
+
+    m = torch.nn.Linear(3, 2)
+    lay = StateLayout.from_state_dict(m.state_dict())
+    ptr = m.weight.data_ptr()
+    monkeypatch.delenv("TAL_HOST_PIN", raising=False)
+    assert aggregate._host_binding(m, lay) is None and m.weight.data_ptr() == ptr
+    monkeypatch.setenv("TAL_HOST_PIN", "0")
+    assert aggregate._host_binding(m, lay) is None and aggregate.bound_row(m) is None
