@@ -416,11 +416,37 @@ __device__ __forceinline__ uint32_t store_bf16x2(float a, float b) {
   return u;
 }
 
-__device__ __forceinline__ float round_bf16(float a) { return bf16_lo(cvt_bf16x2(a, 0.f)); }
+// fp32 -> nearest-even bf16, kept as the fp32 it represents: one v_cvt_pk_bf16_f32 with the value
+// in the HIGH half and +0.0 in the low half is that fp32 word as it stands (no shift or mask to
+// unpack; a pair conversion plus unpacking costs 1.5 instructions per element instead of 1)
+// (inline asm: in C++ the compiler merges two such conversions into one pair conversion plus two
+// v_perm_b32, the 1.5 instructions per element this avoids)
+__device__ __forceinline__ float round_bf16(float a) {
+  float r;
+  asm("v_cvt_pk_bf16_f32 %0, 0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
 
 __device__ __forceinline__ float4 round_bf16x4(float4 v) {
-  const uint32_t p = cvt_bf16x2(v.x, v.y), q = cvt_bf16x2(v.z, v.w);
-  return make_float4(bf16_lo(p), bf16_hi(p), bf16_lo(q), bf16_hi(q));
+  return make_float4(round_bf16(v.x), round_bf16(v.y), round_bf16(v.z), round_bf16(v.w));
+}
+
+// bf16 EXACT steps on two-element vectors, so the multiplies and adds are packed (v_pk_mul_f32,
+// v_pk_add_f32; IEEE, -ffp-contract=off) around the per-element roundings
+typedef float bf_v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bf_v2f round_bf16x2(bf_v2f a) { return bf_v2f{round_bf16(a.x), round_bf16(a.y)}; }
+
+__device__ __forceinline__ float4 bf16x_first4(float w, float4 x) {
+  const bf_v2f ww = {w, w};
+  const bf_v2f p0 = round_bf16x2(ww * bf_v2f{x.x, x.y}), p1 = round_bf16x2(ww * bf_v2f{x.z, x.w});
+  return make_float4(p0.x, p0.y, p1.x, p1.y);
+}
+
+__device__ __forceinline__ float4 bf16x_next4(float4 a, float w, float4 x) {
+  const bf_v2f ww = {w, w};
+  const bf_v2f p0 = round_bf16x2(ww * bf_v2f{x.x, x.y}), p1 = round_bf16x2(ww * bf_v2f{x.z, x.w});
+  const bf_v2f s0 = round_bf16x2(bf_v2f{a.x, a.y} + p0), s1 = round_bf16x2(bf_v2f{a.z, a.w} + p1);
+  return make_float4(s0.x, s0.y, s1.x, s1.y);
 }
 
 template <typename T>
@@ -473,13 +499,13 @@ constexpr bool kIsBf16 = std::is_same<T, uint16_t>::value;
 // result to bf16).  bf16 FMA: fp32 accumulation (fused), rounded once by the store.
 template <typename T, bool EXACT>
 __device__ __forceinline__ float4 first4t(float w, float4 x) {
-  if constexpr (kIsBf16<T> && EXACT) return round_bf16x4(mul4(w, x));
+  if constexpr (kIsBf16<T> && EXACT) return bf16x_first4(w, x);
   else return first4<EXACT>(w, x);
 }
 
 template <typename T, bool EXACT>
 __device__ __forceinline__ float4 next4t(float4 a, float w, float4 x) {
-  if constexpr (kIsBf16<T> && EXACT) return round_bf16x4(add4(a, round_bf16x4(mul4(w, x))));
+  if constexpr (kIsBf16<T> && EXACT) return bf16x_next4(a, w, x);
   else return next4<EXACT>(a, w, x);
 }
 
