@@ -910,8 +910,7 @@ __device__ __forceinline__ float4 narrow_row_tail(float4 acc, float w, uint2 e, 
     if (rem <= u) break;  // wave-uniform
     const uint32_t word = u < 2 ? e.x : e.y;
     uint32_t addr;
-    if constexpr (kIsBf16<T> && EXACT) addr = base + (((u == 1 ? word >> 16 : word) & 0xffffu) << 4);
-    else addr = u == 1 ? slot_addr_hi(word, base) : slot_addr_lo(word, base);
+    addr = u == 1 ? slot_addr_hi(word, base) : slot_addr_lo(word, base);
     acc = next4t<T, EXACT>(acc, w, lds_f4(addr));
   }
   return acc;
@@ -925,22 +924,6 @@ __device__ __forceinline__ float4 narrow_row_roww(uint4 rc, uint32_t base) {
   uint32_t q = rc.x;
   float4 acc = make_float4(-0.f, -0.f, -0.f, -0.f);
   uint2 e = lds_u2(q);
-  if constexpr (kIsBf16<T> && EXACT) {
-    // bf16 EXACT (two roundings per operand): plain extraction (the compiler's own schedule of
-    // this form measured faster than the decode below for this instantiation)
-    for (int b = 0; b < nb; ++b) {
-      float4 x[4];
-      x[0] = lds_f4(base + ((e.x & 0xffffu) << 4));
-      x[1] = lds_f4(base + ((e.x >> 16) << 4));
-      x[2] = lds_f4(base + ((e.y & 0xffffu) << 4));
-      x[3] = lds_f4(base + ((e.y >> 16) << 4));
-      q += 8;
-      e = lds_u2(q);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc = next4t<T, EXACT>(acc, w, x[u]);
-    }
-    return narrow_row_tail<T, EXACT>(acc, w, e, base, rem);
-  }
   for (int b = 0; b < nb; ++b) {
     float4 x[4];
     x[0] = lds_f4(slot_addr_lo(e.x, base));
