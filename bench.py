@@ -244,15 +244,14 @@ def main():
         trials = max(2, min(args.placement_trials, int(0.7 * torch.cuda.mem_get_info(dev)[0] // pool_bytes)))
         cand = [ModelPool(layout, rows, dev) for _ in range(trials)]
         fill_pool(cand[0], 1234)
+        tune = not (args.plan or args.stream_rows or args.no_tune or args.c4)
         if args.plan:
             plan = _ops.plan_from_spec(row_ptr, col, w, out_rows, json.loads(args.plan)).to(dev)
         elif args.stream_rows:
             plan = _ops.build_stream_plan(row_ptr, col, w, out_rows, args.stream_rows).to(dev)
-        elif args.no_tune or args.c4:
+        else:  # the model-based choice; with tuning, only for the placement calibration below
             plan = (_ops.build_plan(row_ptr, col, w, out_rows, c4=args.c4) if args.c4 else
                     _ops.default_plan(row_ptr, col, w, out_rows, bf16=bf16)).to(dev)
-        else:  # time every plan candidate on the real pools (a few rounds, once per topology)
-            plan = _ops.tune_plan(row_ptr, col, w, out_rows, seg(cand[0]), seg(cand[1]), n=n_float, mode=mode)
         ev_s, ev_e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
         def placement_score(a, b):
@@ -278,6 +277,9 @@ def main():
         del cand
         torch.cuda.empty_cache()  # the candidates not kept
         fill_pool(pin, 1234)
+        if tune:  # time every plan candidate on the pools the steps use (once per topology)
+            plan = _ops.tune_plan(row_ptr, col, w, out_rows, seg(pin), seg(pout), n=n_float, mode=mode)
+            in_place = in_place and plan.single_group
 
         def step(a, b):
             round_fn(seg(a), seg(b), plan, n=n_float, mode=mode)
