@@ -267,8 +267,9 @@ def select_pool_pair(make_pool: Callable[[], "ModelPool"], score: Callable[["Mod
     lifetime, i.e. for every round of a training run.  So the arena allocates `trials` pools
     once, times a round INTO each (`score(src, dst)`, src = the next pool), then every ordered
     pair among the three fastest destinations, keeps the pair with the fastest round trip (the
-    double-buffered round runs a -> b and b -> a in turn) and frees the others: trials + 6 timed
-    rounds instead of every ordered pair.  Returns (a, b, report); report["first_pair_ms"] is
+    double-buffered round runs a -> b and b -> a in turn; the first two allocations are a
+    candidate pair as well) and frees the others: at most trials + 8 timed rounds instead of
+    every ordered pair.  Returns (a, b, report); report["first_pair_ms"] is
     what the first two allocations run (both directions)."""
     pools = [make_pool() for _ in range(max(2, trials))]
     k = len(pools)
@@ -278,10 +279,14 @@ def select_pool_pair(make_pool: Callable[[], "ModelPool"], score: Callable[["Mod
     # than its calibration on one board, profiles/r02/final6): among the best three destinations
     # every ordered pair is timed and the pair with the fastest round trip a -> b, b -> a is kept
     top = sorted(order[:3])
-    pair_ms = {(i, j): float(score(pools[i], pools[j])) for i in top for j in top if i != j}
-    best = min(((i, j) for i in top for j in top if i < j), key=lambda q: pair_ms[q] + pair_ms[q[::-1]])
+    pairs = sorted({(i, j) for i in top for j in top if i < j} | {(0, 1)})  # the first two allocations too
+    pair_ms = {}
+    for i, j in pairs:
+        pair_ms[(i, j)] = float(score(pools[i], pools[j]))
+        pair_ms[(j, i)] = float(score(pools[j], pools[i]))
+    best = min(pairs, key=lambda q: pair_ms[q] + pair_ms[q[::-1]])
     a, b = pools[best[0]], pools[best[1]]
-    first = sum(pair_ms[q] if q in pair_ms else float(score(pools[q[0]], pools[q[1]])) for q in ((0, 1), (1, 0))) / 2
+    first = (pair_ms[(0, 1)] + pair_ms[(1, 0)]) / 2
     report = dict(pools=k, dest_ms=[round(v, 3) for v in ms], chosen=list(best),
                   pair_ms={f"{i}->{j}": round(v, 3) for (i, j), v in pair_ms.items()},
                   first_pair_ms=round(first, 3),
