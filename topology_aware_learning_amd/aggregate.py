@@ -101,7 +101,9 @@ class _OperandCache:
     def __init__(self, cap_bytes: int):
         self.cap = cap_bytes
         self.used = 0
-        self.lock = threading.Lock()
+        # re-entrant: put() allocates under the lock, which can run cyclic GC, whose collection
+        # of a cached model calls _drop on this same thread
+        self.lock = threading.RLock()
         self.entries: "OrderedDict[int, tuple]" = OrderedDict()  # id -> (wref, sig, device, segs, nbytes)
         self.hits = self.misses = 0
 
@@ -325,11 +327,13 @@ def aggregate_models(operands: Sequence[nn.Module], weights: Sequence[float], ta
     for g in sizes:
         _AGG[g](ptrs[g], w, outs[g], mode)
 
+    synced = False
     if host_target is not None:  # pinned row: one D2H per segment straight into it
         dst = _row_segments(host_target[0], host_target[1], sizes)
         for g in sizes:
             dst[g].copy_(outs[g], non_blocking=True)
         torch.cuda.current_stream(device).synchronize()
+        synced = True
         cache = _host_cache()
         if cache is not None:
             cache.put(target, _pinned_signature(target, host_target[0]), device, outs)
@@ -340,7 +344,9 @@ def aggregate_models(operands: Sequence[nn.Module], weights: Sequence[float], ta
             sd = target.state_dict()
             if not all(t.device == device for t in sd.values()):
                 cache.put(target, _OperandCache.signature(sd), device, outs)
-    elif unbound and _pin_enabled():  # H2D copies from pinned rows may still be in flight
+    if unbound and not synced and _pin_enabled():
+        # H2D copies straight from pinned rows (live model storage) may still be in flight: the
+        # caller may train that model as soon as this returns, whatever the target's placement
         torch.cuda.current_stream(device).synchronize()
     return target
 

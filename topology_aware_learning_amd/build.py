@@ -29,10 +29,9 @@ HIPCC_FLAGS = [
     # torch bundles a ROCm 7.0 HIP runtime (same soname as /opt/rocm's 7.2); code object v5
     # loads under both.
     "-mcode-object-version=5",
-    # the halo exchange's RCCL (torch's own copy, same soname, is the one loaded under torch)
-    "-L/opt/rocm/lib",
-    "-lrccl",
-    "-Wl,-rpath,/opt/rocm/lib",
+    # RCCL is not linked: the halo entry points dlopen it on first use (a host without RCCL
+    # still loads the library; under torch its already-loaded copy is found by soname)
+    "-ldl",
 ]
 
 

@@ -99,10 +99,16 @@ class HaloComm:
 
 
 def shared_halo_comm(world: int, rank: int, device, group=None) -> HaloComm:
-    """A HaloComm over the ranks of an initialised torch.distributed group: rank 0 makes the
-    unique id and broadcasts it through the group."""
+    """A HaloComm over the ranks of an initialised torch.distributed group: the group's first
+    member makes the unique id and broadcasts it through the group.
+
+    `rank` is the shard rank the communicator uses; who creates the id and where the broadcast
+    comes from are decided by group membership (a group need not contain global rank 0, and a
+    shard rank need not equal the group rank)."""
     import torch.distributed as dist
 
-    obj = [HaloComm.unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(obj, src=0, group=group)
+    grank = dist.get_rank(group) if group is not None else dist.get_rank()
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    obj = [HaloComm.unique_id() if grank == 0 else None]
+    dist.broadcast_object_list(obj, src=src, group=group)
     return HaloComm(world, rank, obj[0], device)

@@ -27,7 +27,8 @@
 #include <type_traits>
 #include <vector>
 
-#include <rccl/rccl.h>
+#include <dlfcn.h>
+#include <rccl/rccl.h>  // types only: the functions are resolved at run time (rccl())
 
 #include "../../include/tal_agg.h"
 
@@ -3178,9 +3179,65 @@ __global__ __launch_bounds__(kBlock) void k_halo_pack(const V* __restrict__ pool
     out[i] = in[i];
 }
 
-int32_t comm_fail(const char* what, ncclResult_t r) {
-  return fail(TAL_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(r));
+// RCCL is resolved at run time (dlopen / dlsym), not linked: only the halo entry points need
+// it, so a host without RCCL still loads the library (they return TAL_ERR_COMM), and under
+// torch the soname lookup finds the copy torch already loaded instead of a second instance.
+struct Rccl {
+  bool ok = false;
+  std::string why;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommCount)(const ncclComm_t, int*) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+};
+
+const Rccl& rccl() {
+  static const Rccl r = [] {
+    Rccl x;
+    void* h = nullptr;
+    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+      if ((h = dlopen(name, RTLD_NOW | RTLD_GLOBAL)) != nullptr) break;
+    if (!h) {
+      const char* e = dlerror();
+      x.why = std::string("RCCL not loadable: ") + (e ? e : "librccl.so.1 not found");
+      return x;
+    }
+    bool all = true;
+    auto sym = [&](auto& fn, const char* name) {
+      fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+      if (!fn) {
+        all = false;
+        x.why = std::string("RCCL lacks ") + name;
+      }
+    };
+    sym(x.GetErrorString, "ncclGetErrorString");
+    sym(x.GetUniqueId, "ncclGetUniqueId");
+    sym(x.CommInitRank, "ncclCommInitRank");
+    sym(x.CommDestroy, "ncclCommDestroy");
+    sym(x.CommCount, "ncclCommCount");
+    sym(x.GroupStart, "ncclGroupStart");
+    sym(x.GroupEnd, "ncclGroupEnd");
+    sym(x.Send, "ncclSend");
+    sym(x.Recv, "ncclRecv");
+    x.ok = all;
+    return x;
+  }();
+  return r;
 }
+
+int32_t comm_fail(const char* what, ncclResult_t r) {
+  return fail(TAL_ERR_COMM, std::string(what) + ": " + rccl().GetErrorString(r));
+}
+
+#define TAL_NEED_RCCL(fn)                                                      \
+  do {                                                                         \
+    if (!rccl().ok) return fail(TAL_ERR_COMM, std::string(fn ": ") + rccl().why); \
+  } while (0)
 
 }  // namespace
 
@@ -3188,8 +3245,9 @@ extern "C" {
 
 int32_t tal_comm_unique_id(void* id_out) {
   if (!id_out) return fail(TAL_ERR_INVALID, "tal_comm_unique_id: null output");
+  TAL_NEED_RCCL("tal_comm_unique_id");
   ncclUniqueId id;
-  const ncclResult_t r = ncclGetUniqueId(&id);
+  const ncclResult_t r = rccl().GetUniqueId(&id);
   if (r != ncclSuccess) return comm_fail("ncclGetUniqueId", r);
   memcpy(id_out, &id, sizeof(id));
   g_err.clear();
@@ -3199,13 +3257,14 @@ int32_t tal_comm_unique_id(void* id_out) {
 int32_t tal_comm_init(void** comm_out, int32_t world, int32_t rank, const void* id, int32_t device) {
   if (!comm_out || !id || world <= 0 || rank < 0 || rank >= world || device < 0)
     return fail(TAL_ERR_INVALID, "tal_comm_init: bad arguments");
+  TAL_NEED_RCCL("tal_comm_init");
   int prev = 0;
   if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess)
     return fail(TAL_ERR_HIP, "tal_comm_init: cannot select device " + std::to_string(device));
   ncclUniqueId uid;
   memcpy(&uid, id, sizeof(uid));
   ncclComm_t c = nullptr;
-  const ncclResult_t r = ncclCommInitRank(&c, world, uid, rank);
+  const ncclResult_t r = rccl().CommInitRank(&c, world, uid, rank);
   (void)hipSetDevice(prev);
   if (r != ncclSuccess) return comm_fail("ncclCommInitRank", r);
   *comm_out = c;
@@ -3215,7 +3274,8 @@ int32_t tal_comm_init(void** comm_out, int32_t world, int32_t rank, const void* 
 
 int32_t tal_comm_destroy(void* comm) {
   if (!comm) return fail(TAL_ERR_INVALID, "tal_comm_destroy: null communicator");
-  const ncclResult_t r = ncclCommDestroy(static_cast<ncclComm_t>(comm));
+  TAL_NEED_RCCL("tal_comm_destroy");
+  const ncclResult_t r = rccl().CommDestroy(static_cast<ncclComm_t>(comm));
   if (r != ncclSuccess) return comm_fail("ncclCommDestroy", r);
   g_err.clear();
   return TAL_OK;
@@ -3251,9 +3311,10 @@ int32_t tal_halo_exchange(void* comm, int32_t world, const void* const* send_buf
                           void* const* recv_bufs, const int64_t* recv_bytes, void* stream) {
   if (!comm || world <= 0 || !send_bytes || !recv_bytes)
     return fail(TAL_ERR_INVALID, "tal_halo_exchange: bad arguments");
+  TAL_NEED_RCCL("tal_halo_exchange");
   ncclComm_t c = static_cast<ncclComm_t>(comm);
   int n = 0;
-  ncclResult_t r = ncclCommCount(c, &n);
+  ncclResult_t r = rccl().CommCount(c, &n);
   if (r != ncclSuccess) return comm_fail("ncclCommCount", r);
   if (n != world) return fail(TAL_ERR_INVALID, "tal_halo_exchange: world differs from the communicator's size");
   for (int p = 0; p < world; ++p) {
@@ -3262,15 +3323,15 @@ int32_t tal_halo_exchange(void* comm, int32_t world, const void* const* send_buf
       return fail(TAL_ERR_INVALID, "tal_halo_exchange: bad buffer for peer " + std::to_string(p));
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
-  r = ncclGroupStart();
+  r = rccl().GroupStart();
   if (r != ncclSuccess) return comm_fail("ncclGroupStart", r);
   ncclResult_t first = ncclSuccess;
   for (int p = 0; p < world && first == ncclSuccess; ++p) {
-    if (send_bytes[p]) first = ncclSend(send_bufs[p], static_cast<size_t>(send_bytes[p]), ncclUint8, p, c, s);
+    if (send_bytes[p]) first = rccl().Send(send_bufs[p], static_cast<size_t>(send_bytes[p]), ncclUint8, p, c, s);
     if (first == ncclSuccess && recv_bytes[p])
-      first = ncclRecv(recv_bufs[p], static_cast<size_t>(recv_bytes[p]), ncclUint8, p, c, s);
+      first = rccl().Recv(recv_bufs[p], static_cast<size_t>(recv_bytes[p]), ncclUint8, p, c, s);
   }
-  r = ncclGroupEnd();
+  r = rccl().GroupEnd();
   if (first != ncclSuccess) return comm_fail("ncclSend / ncclRecv", first);
   if (r != ncclSuccess) return comm_fail("ncclGroupEnd", r);
   g_err.clear();
