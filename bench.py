@@ -126,32 +126,51 @@ def fill_pool(pool, seed: int):
 
 
 def cpu_baseline(layout_list, m: int, budget_s: float):
-    """The reference loop (clone/mul/add_/load_state_dict, oracle/torch_path.py) on host cores:
-    (i) one call at a time for ~budget_s seconds (the reported value), and (ii) the reference's
-    effective configuration, two concurrent calls (Parsl ThreadPoolExecutor(max_threads=2),
-    parsl_setup.py:75-78), for ~budget_s / 2 seconds."""
+    """The reference loop (clone/mul/add_/load_state_dict, oracle/torch_path.py) on host cores,
+    one call at a time, with torch.set_num_threads(all cores this process may run on) - SURVEY
+    §8(d)(i), the reported value - and with torch's default thread count (16 on the GPU box,
+    its OMP_NUM_THREADS); then the reference's effective configuration, two concurrent calls
+    (Parsl ThreadPoolExecutor(max_threads=2), parsl_setup.py:75-78) at the default count.
+    About budget_s seconds in all."""
     import threading
 
     import torch
 
     from oracle import torch_path
-    from topology_aware_learning_amd import synth
 
-    sds = [synth.synth_state_dict(layout_list, 100 + i) for i in range(m)]
-    targets = [synth.synth_state_dict(layout_list, 99), synth.synth_state_dict(layout_list, 98)]
+    gen = torch.Generator().manual_seed(100)
+    sds, targets = [], []
+    for k in range(m + 2):  # the values do not matter for the timing: seeded normal / counters
+        sd = {}
+        for name, shape, dt in layout_list:
+            if dt == "int64":
+                sd[name] = torch.randint(0, 1_000_000, tuple(shape), generator=gen)
+            else:
+                sd[name] = torch.randn(tuple(shape), generator=gen).to(getattr(torch, dt))
+        (sds if k < m else targets).append(sd)
     w = [1 / m] * m
-    torch_path.aggregate_call(sds, w, targets[0])  # warm-up
     n_out = sum(t.numel() for t in targets[0].values())
-    calls = 0
-    t0 = time.perf_counter()
-    while True:
-        torch_path.aggregate_call(sds, w, targets[0])
-        calls += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or calls >= 1024:
-            break
+    default_threads = torch.get_num_threads()
+    try:
+        all_threads = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover - non-Linux
+        all_threads = os.cpu_count() or default_threads
+
+    def one_at_a_time(threads: int, secs: float):
+        torch.set_num_threads(threads)
+        torch_path.aggregate_call(sds, w, targets[0])  # warm-up
+        calls, t0 = 0, time.perf_counter()
+        while True:
+            torch_path.aggregate_call(sds, w, targets[0])
+            calls += 1
+            el = time.perf_counter() - t0
+            if el >= secs or calls >= 1024:
+                return calls, el
+
+    calls_all, el_all = one_at_a_time(all_threads, 0.4 * budget_s)
+    calls_def, el_def = one_at_a_time(default_threads, 0.35 * budget_s)
     counts = [0, 0]
-    stop = time.perf_counter() + budget_s / 2
+    stop = time.perf_counter() + 0.25 * budget_s
 
     def worker(k):
         while time.perf_counter() < stop:
@@ -165,11 +184,15 @@ def cpu_baseline(layout_list, m: int, budget_s: float):
     for t in ths:
         t.join()
     el2 = time.perf_counter() - t1
-    return dict(value=calls * n_out / el, unit="params/s", cores=torch.get_num_threads(), kind="port",
-                sample=f"{calls} reference calls (M={m}, {n_out} params) one at a time in {el:.2f} s; "
+    torch.set_num_threads(default_threads)
+    return dict(value=calls_all * n_out / el_all, unit="params/s", cores=all_threads, kind="port",
+                sample=f"{calls_all} reference calls (M={m}, {n_out} params) one at a time in {el_all:.2f} s "
+                       f"with torch.set_num_threads({all_threads}) (every core this process may run on); "
                        "torch CPU clone/mul/add_/copy_ on host state_dicts",
-                ms_per_call=1e3 * el / calls,
-                os_cpu_count=os.cpu_count(), torch_threads=torch.get_num_threads(), cpu_model=cpu_model(),
+                ms_per_call=1e3 * el_all / calls_all,
+                default_threads_value=calls_def * n_out / el_def, default_threads=default_threads,
+                default_threads_ms_per_call=1e3 * el_def / calls_def,
+                os_cpu_count=os.cpu_count(), affinity_cpus=all_threads, cpu_model=cpu_model(),
                 # the reference's effective configuration: Parsl ThreadPoolExecutor(max_threads=2)
                 two_concurrent_calls_value=sum(counts) * n_out / el2, two_concurrent_calls=sum(counts),
                 two_concurrent_seconds=round(el2, 2))
@@ -285,12 +308,24 @@ def main():
             round_fn(seg(a), seg(b), plan, n=n_float, mode=mode)
             _ops.round_i64(a.i64, b.i64, plan, n=layout.n_i64)
 
-        # correctness spot check at full size: K3 row 0 == K1 on the same operands (bitwise)
+        # correctness check at full size: EVERY output row of the round (both segments) == K1
+        # on the same operands, bitwise (K1 itself is pinned to the reference's sha256 of
+        # ResNet-50 M = 9 calls; tests/test_gpu_fullsize.py pins whole rounds)
         step(pin, pout)
         chk = torch.empty(n_float, dtype=seg(pin).dtype, device=dev)
-        agg_fn([row(pin, j) for j in orders[0]], weights[0], chk, mode=mode)
-        parity_ok = bool(torch.equal(chk.view(torch.int16 if bf16 else torch.int32),
-                                     row(pout, 0).view(torch.int16 if bf16 else torch.int32)))
+        chk_i = torch.empty(layout.n_i64, dtype=torch.int64, device=dev)
+        iv = torch.int16 if bf16 else torch.int32
+        bad_rows = []
+        for r in range(rows):
+            agg_fn([row(pin, j) for j in orders[r]], weights[r], chk, mode=mode)
+            same = torch.equal(chk.view(iv), row(pout, r).view(iv))
+            if layout.n_i64:
+                _ops.agg_i64([pin.row_i64(j) for j in orders[r]], weights[r], chk_i)
+                same = same and torch.equal(chk_i, pout.row_i64(r))
+            if not same:
+                bad_rows.append(r)
+        parity_ok = not bad_rows
+        del chk, chk_i
         tol = bf16_tolerance(pin, pout, orders[0], weights[0], n_float, dev) if bf16 else None
 
         pools = [pin, pin] if in_place else [pin, pout]
@@ -318,7 +353,8 @@ def main():
                                                   lds_reads_per_column=plan.info.dense_reads,
                                                   tuned_ms=plan.tuned_ms, candidates=plan.candidates,
                                                   spec=plan.spec),
-            per_call_equivalent_GBps=per_call_bytes / (k_ms * 1e-3) / 1e9, parity_k3_vs_k1_row0=parity_ok,
+            per_call_equivalent_GBps=per_call_bytes / (k_ms * 1e-3) / 1e9,
+            parity_k3_vs_k1=dict(rows_checked=rows, rows_differing=len(bad_rows), first_bad=bad_rows[:8]),
             valu=valu_floor(len(col), rows, n_float, k_ms, mode))
         if tol is not None:
             result_extra["bf16_vs_fp32_reference_row0"] = tol
@@ -360,9 +396,24 @@ def main():
         torch.cuda.synchronize(dev)
         k_ms = float(np.mean(sr.kernel_ms()))
         bytes_round = sr.kernel_bytes
+        # DESIGN §6's model next to the measurement: per exchange kind the busiest rank's HBM
+        # bytes and the busiest GPU pair's link bytes over their peaks; the binding term
+        from topology_aware_learning_amd.distributed import partition_contiguous
+        from topology_aware_learning_amd.transposed import link_model
+
+        model = link_model(orders, partition_contiguous(n_dev_total, world), world, layout.n_f32,
+                           layout.n_i64, layout.n_b16)
+        ms_step = 1e3 * el / args.steps
+        chosen = model[sr.exchange_kind]
         result_extra = dict(kernel=",".join(sorted({ops.round_kernel_name(p) for p in sr.plans.values()})),
                             exchange=sr.exchange_kind, link_bytes_in_per_round=sr.link_bytes,
-                            link_GBps_in=sr.link_bytes / (el / args.steps) / 1e9)
+                            link_GBps_in=sr.link_bytes / (el / args.steps) / 1e9,
+                            bound_model=dict(per_exchange={k: {kk: (round(vv, 3) if isinstance(vv, float) else vv)
+                                                                for kk, vv in v.items()} for k, v in model.items()},
+                                             chosen=sr.exchange_kind, predicted_ms=round(chosen["predicted_ms"], 3),
+                                             binds=chosen["binds"], measured_ms_per_step=round(ms_step, 3),
+                                             measured_over_predicted=round(ms_step / chosen["predicted_ms"], 3),
+                                             kernel_share_of_step=round(k_ms / ms_step, 3)))
         units = n_dev_total * n_params * args.steps
         parity_ok = parity_dist
         k1 = None
@@ -448,28 +499,35 @@ def bf16_tolerance(pin, pout, order, weights, n, dev) -> dict:
 
 
 def bench_k1(layout, pool, orders, weights, mode, dev, reps: int = 20):
-    """Per-call K1 (no cross-call reuse) on row 0's operands: SURVEY §8(d) B = 4N(M+1)."""
+    """Per-call K1 (no cross-call reuse) as the per-call product path runs it: one launch over
+    the fp32 and int64 segments of a call (tal_agg_model_f32), rows rotated over the round's
+    calls; SURVEY §8(d) B = 4 N (M+1) + 8 N_i64 (M+1).  HIP events around each launch."""
     import torch
 
     from topology_aware_learning_amd import ops
 
     out = torch.empty(layout.n_f32, dtype=torch.float32, device=dev)
-    xs = [pool.row_f32(j) for j in orders[0]]
-    for _ in range(3):
-        ops.agg_f32(xs, weights[0], out, mode=mode)
+    out_i = torch.empty(layout.n_i64, dtype=torch.int64, device=dev)
+
+    def call(r):
+        o = orders[r % len(orders)]
+        ops.agg_model_f32([pool.row_f32(j) for j in o], [pool.row_i64(j) for j in o], weights[r % len(orders)],
+                          out, out_i, mode=mode)
+
+    for r in range(3):
+        call(r)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ts = []
     for r in range(reps):
-        xs = [pool.row_f32(j) for j in orders[r % len(orders)]]  # rotate rows: defeat the MALL
         s.record()
-        ops.agg_f32(xs, weights[r % len(orders)], out, mode=mode)
+        call(r)  # rotate rows: defeat the MALL
         e.record()
         e.synchronize()
         ts.append(s.elapsed_time(e))
     ms = float(np.median(ts))
     m = len(orders[0])
-    b = 4 * layout.n_f32 * (m + 1)
-    return dict(kernel="k_agg_f32_vec", ms=ms, bytes=b, GBps=b / (ms * 1e-3) / 1e9,
+    b = (4 * layout.n_f32 + 8 * layout.n_i64) * (m + 1)
+    return dict(kernel="k_agg_model", launches_per_call=1, ms=ms, bytes=b, GBps=b / (ms * 1e-3) / 1e9,
                 frac=b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, params_per_s=(layout.n_f32 + layout.n_i64) / (ms * 1e-3))
 
 

@@ -68,6 +68,16 @@ int32_t tal_agg_f32(const float* const* x_host, const double* w_host, int32_t m,
 int32_t tal_agg_i64(const int64_t* const* x_host, const double* w_host, int32_t m,
                     int64_t* out, int64_t n, void* stream);
 
+/* One call over a whole model (fp32 + int64 segments) in ONE launch: the fp32 segment as
+ * tal_agg_f32 and the int64 segment as tal_agg_i64, the same arithmetic bit for bit, but the
+ * per-call path's vector, n % 4 tail and int64 launches fused (decentralized_client.py:406-413
+ * over every state_dict entry of a ResNet: the num_batches_tracked counters ride along).
+ * xi_host may be NULL when n_i == 0.  Fused when m <= 64, n_i <= 65536 and every fp32
+ * pointer is 16-byte aligned; otherwise the two segment calls above run instead. */
+int32_t tal_agg_model_f32(const float* const* x_host, const int64_t* const* xi_host,
+                          const double* w_host, int32_t m, float* out, int64_t n,
+                          int64_t* out_i, int64_t n_i, int32_t mode, void* stream);
+
 /* bf16 buffers (uint16_t bit patterns; bf16 models).  mode TAL_MODE_EXACT: the reference's
  * own ops on bf16 tensors (decentralized_client.py:407-411 - `w * clone(v)` and `+=` each
  * round their fp32 result to bf16, nearest even), bit-identical to it; TAL_MODE_FMA: fp32

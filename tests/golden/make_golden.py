@@ -19,8 +19,13 @@ Outputs (all data, no reference source):
                                      fp32 than in exact arithmetic
   big_round_resnet18_ring32.json     BASELINE config 2 at full size: a snapshot round's outputs
                                      (sha256 per output model)
+  full_round_c3_resnet50_rr64.json   BASELINE config 3 (the benchmark's round) at full size
+  full_round_c4_resnet50_barbell.json  BASELINE config 4 (barbell(60, 8)) at full size
+  full_round_c5_vit_sbm256.json      BASELINE config 5 (SBM-256, ViT-B/16) at full size per entry
+                                     group: fp32 unweighted, fp32 degree-centrality softmax (one
+                                     group), bf16 unweighted (one group)
 
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py [generator ...]   (default: all)
 """
 from __future__ import annotations
 
@@ -342,6 +347,140 @@ def gen_big_round(dc, resnet, out):
     print("big round: resnet18 32-ring snapshot")
 
 
+def _holder(sd):
+    """An nn.Module whose state_dict is `sd`'s tensors in order (the reference apps only call
+    state_dict() / load_state_dict() on client models, decentralized_client.py:406,413)."""
+    m = nn.Module()
+    for k, v in enumerate(sd.values()):
+        m.register_buffer(f"e{k}", v.clone())
+    return m
+
+
+def _snapshot_round(dc, models, restore, orders, fn_name, kwargs, digest):
+    """One round of reference app calls in snapshot form: call i aggregates orders[i] (self
+    last) into models[i], its output is digested, then models[i] is restored to its pre-round
+    state, so every call reads the pre-round models (decentralized_app.py:605-641 with every
+    aggregation reading the train outputs)."""
+    clients = [(["r"], make_client(dc, i, m)) for i, m in enumerate(models)]
+    rows = []
+    for i, order in enumerate(orders):
+        assert order[-1] == i
+        res = getattr(dc, fn_name)(clients[i], 0, *[clients[j] for j in order], **kwargs)
+        rows.append(digest(res[1].model))
+        restore(i, models[i])
+    return rows
+
+
+def _seg_digest(model):
+    sd = sd_np(model)
+    f32 = [v.reshape(-1) for v in sd.values() if v.dtype == np.float32]
+    i64 = [v.reshape(-1) for v in sd.values() if v.dtype == np.int64]
+    out = dict(sha256_f32=sha(np.concatenate(f32)) if f32 else None)
+    if i64:
+        out["sha256_i64"] = sha(np.concatenate(i64))
+    return out
+
+
+def gen_full_round(dc, resnet, which, out):
+    """BASELINE configs 3 and 4 at full size: a snapshot round of unweighted_module_avg over
+    ResNet-50 state_dicts (reference constructor), sha256 per output model of its fp32 entries
+    and of its int64 entries (each concatenated in state_dict order).
+      config 3: nx.random_regular_graph(8, 64, seed=0), M = 9 (the benchmark's round)
+      config 4: nx.barbell_graph(60, 8), 128 devices, M = 3..61"""
+    g = nx.random_regular_graph(8, 64, seed=0) if which == "c3" else nx.barbell_graph(60, 8)
+    n = g.number_of_nodes()
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(n)]
+    base = 9300 if which == "c3" else 9400
+    seeds = [base + i for i in range(n)]
+    layout = synth.layout_of(resnet.ResNet50().state_dict())
+    models = []
+    for i in range(n):
+        m = resnet.ResNet50()
+        m.load_state_dict(synth.synth_state_dict(layout, seeds[i]))
+        models.append(m)
+
+    def restore(i, m):
+        m.load_state_dict(synth.synth_state_dict(layout, seeds[i]))
+
+    rows = _snapshot_round(dc, models, restore, orders, "unweighted_module_avg", {}, _seg_digest)
+    for r, o in zip(rows, orders):
+        r["order"] = o
+    graph = "random_regular_graph(8, 64, seed=0)" if which == "c3" else "barbell_graph(60, 8)"
+    out.write_text(json.dumps(dict(model="resnet50", graph=graph, fn="unweighted_module_avg", seeds=seeds,
+                                   semantics="snapshot (every call reads the pre-round models)",
+                                   rows=rows), indent=1))
+    print("full round", which, n)
+
+
+def _entry_groups(layout, cap):
+    """Consecutive entries in groups of at most `cap` elements (an entry larger than cap alone),
+    with each group's [start, end) in its dtype's segment."""
+    groups, cur, size, off = [], [], 0, 0
+    for k, (_, shape, _) in enumerate(layout):
+        nk = synth.numel(shape)
+        if cur and size + nk > cap:
+            groups.append(dict(entries=cur, start=off - size, end=off))
+            cur, size = [], 0
+        cur.append(k)
+        size += nk
+        off += nk
+    if cur:
+        groups.append(dict(entries=cur, start=off - size, end=off))
+    return groups
+
+
+def gen_c5_round(dc, out):
+    """BASELINE config 5 at full size, per entry group: 256 devices on the stochastic block
+    model (8 x 32, p_in = 14/31, p_out = 2/224, seed 0), ViT-B/16 layout (synthetic, not in the
+    reference).  The reference loop is per entry (decentralized_client.py:406-411), so a round
+    over a sub-state-dict of consecutive entries gives exactly those entries' bytes of the full
+    round; the 88.6 GB of models are never resident.  sha256 per (output model, group) of:
+      fp32 / unweighted_module_avg over every group (the benchmark's round),
+      fp32 / centrality_module_avg (degree, softmax, coeff 10) over the last group,
+      bf16 (model.to(torch.bfloat16)) / unweighted_module_avg over the first group."""
+    sizes = [32] * 8
+    p = [[14 / 31 if a == b else 2 / 224 for b in range(8)] for a in range(8)]
+    g = nx.stochastic_block_model(sizes, p, seed=0)
+    n = g.number_of_nodes()
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(n)]
+    seeds = [9500 + i for i in range(n)]
+    layout = synth.vit_b16_layout()
+    groups = _entry_groups(layout, 12_000_000)
+    cent = dc.create_centrality_dict(nx.to_numpy_array(g), np.random.default_rng(0))
+    runs = [("f32", "unweighted_module_avg", {}, list(range(len(groups)))),
+            ("f32", "centrality_module_avg", dict(centrality_metric="degree", centrality_dict=cent,
+                                                  softmax=True, softmax_coeff=10.0), [len(groups) - 1]),
+            ("bf16", "unweighted_module_avg", {}, [0])]
+    results = []
+    for dtype, fn, kw, gids in runs:
+        lay = layout if dtype == "f32" else synth.as_bf16(layout)
+        digests = [dict() for _ in range(n)]
+        for gi in gids:
+            ents = groups[gi]["entries"]
+            models = [_holder(synth.synth_state_dict(lay, seeds[i], entries=ents)) for i in range(n)]
+
+            def restore(i, m, ents=ents, lay=lay):
+                m.load_state_dict(_holder(synth.synth_state_dict(lay, seeds[i], entries=ents)).state_dict())
+
+            def digest(m):
+                return sha(np.concatenate([v.detach().reshape(-1).view(torch.int16 if dtype == "bf16" else torch.int32)
+                                           .numpy() for v in m.state_dict().values()]))
+
+            rows = _snapshot_round(dc, models, restore, orders, fn, kw, digest)
+            for i, d in enumerate(rows):
+                digests[i][str(gi)] = d
+            del models
+            print("c5", dtype, fn, "group", gi, flush=True)
+        results.append(dict(dtype=dtype, fn=fn, centrality_metric=kw.get("centrality_metric"),
+                            softmax=kw.get("softmax", False), softmax_coeff=kw.get("softmax_coeff"),
+                            groups=gids, sha256=digests))
+    out.write_text(json.dumps(dict(model="vit_b16 (synthetic torchvision layout)",
+                                   graph="stochastic_block_model([32]*8, p_in=14/31, p_out=2/224, seed=0)",
+                                   seeds=seeds, orders=orders, groups=groups,
+                                   semantics="snapshot (every call reads the pre-round models)",
+                                   runs=results), indent=1))
+
+
 def gen_weights(dc, out_w, out_c):
     graphs = {
         "cycle_graph(8)": nx.cycle_graph(8),
@@ -508,7 +647,8 @@ def gen_bf16(dc, out_json, out_npz):
     print(f"bf16: {len(cases)} cases")
 
 
-GENERATORS = ("layouts", "tiny", "weights", "schedulers", "round", "big", "gossip", "bf16", "big_round", "near_ties")
+GENERATORS = ("layouts", "tiny", "weights", "schedulers", "round", "big", "gossip", "bf16", "big_round", "near_ties",
+              "full_c3", "full_c4", "full_c5")
 
 
 def main(which=GENERATORS):
@@ -533,6 +673,12 @@ def main(which=GENERATORS):
         gen_near_ties(dc, HERE / "near_ties.json", HERE / "near_ties.npz")
     if "big_round" in which:
         gen_big_round(dc, resnet, HERE / "big_round_resnet18_ring32.json")
+    if "full_c3" in which:
+        gen_full_round(dc, resnet, "c3", HERE / "full_round_c3_resnet50_rr64.json")
+    if "full_c4" in which:
+        gen_full_round(dc, resnet, "c4", HERE / "full_round_c4_resnet50_barbell.json")
+    if "full_c5" in which:
+        gen_c5_round(dc, HERE / "full_round_c5_vit_sbm256.json")
 
 
 if __name__ == "__main__":

@@ -104,3 +104,42 @@ def test_bound_row_tracks_rebinding():
     assert bound_row(m) == (pool, 0)
     m.fc.bias = None  # an entry removed from its table
     assert bound_row(m) is None
+
+
+def test_bound_row_generation_hooks():
+    """The O(1) binding check (arena._GEN): every re-pointing path bumps the generation and is
+    then caught by the full check - submodule replaced, parameter / buffer set to None or
+    deleted, `.to()` of a submodule, parameter `.data` assignment, load_state_dict(assign=True);
+    an in-place load_state_dict and unrelated module construction keep the binding."""
+    import torch.nn as nn
+
+    from topology_aware_learning_amd import arena
+    from topology_aware_learning_amd.arena import ModelPool, StateLayout, bound_row
+
+    def mk():
+        m = nn.Sequential(nn.Linear(3, 4), nn.BatchNorm1d(4), nn.Linear(4, 2))
+        pool = ModelPool(StateLayout.from_state_dict(m.state_dict()), 1, "cpu")
+        pool.bind(m, 0)
+        assert bound_row(m) == (pool, 0)
+        return m, pool
+
+    cases = [
+        lambda m: m.__setitem__(0, nn.Linear(3, 4)),
+        lambda m: setattr(m[1], "running_var", None),
+        lambda m: delattr(m[2], "bias"),
+        lambda m: m[2].to(torch.float64),
+        lambda m: setattr(m[2].weight, "data", m[2].weight.data.clone()),
+        lambda m: m.load_state_dict({k: v.clone() for k, v in m.state_dict().items()}, assign=True),
+        lambda m: setattr(m[1], "running_mean", m[1].running_mean.clone()),
+    ]
+    for k, change in enumerate(cases):
+        m, _ = mk()
+        g = arena._GEN[0]
+        change(m)
+        assert arena._GEN[0] != g, k
+        assert bound_row(m) is None, k
+    m, pool = mk()
+    m.load_state_dict({k: v.clone() for k, v in m.state_dict().items()})  # copy_: still bound
+    nn.Linear(2, 2)  # a hook event elsewhere: one full check, then O(1) again
+    assert bound_row(m) == (pool, 0) and m._tal_gen == arena._GEN[0]
+    assert bound_row(m) == (pool, 0)

@@ -112,6 +112,61 @@ def test_agg_i64_truncation(cuda, m):
         assert ref[4] == 999  # nine copies of 1000 at w=1/9 come back as 999
 
 
+@pytest.mark.parametrize("m", [1, 2, 9, 17, 18, 40, 64, 65])
+@pytest.mark.parametrize("n", [1, 3, 4, 7, 1024, 1026, 4096 * 4 + 2, 262147])
+@pytest.mark.parametrize("n_i", [0, 53, 300])
+def test_agg_model_f32_one_launch(cuda, m, n, n_i):
+    """K1m (tal_agg_model_f32): fp32 segment + int64 segment of one call in one launch, bitwise
+    the oracle for every n % 4 tail, a last block full of chunks (n / 4 a multiple of 256), small
+    n, m past the fused limit (two segment launches), int64 truncation and specials."""
+    rng = np.random.default_rng(m * 7919 + n + n_i)
+    xs = [_rand_f32(rng, n, special=(i == 0)) for i in range(m)]
+    xis = [rng.integers(-(2 ** 40), 2 ** 40, size=n_i).astype(np.int64) for _ in range(m)]
+    for x in xis:
+        x[:min(n_i, 3)] = [1000, 2 ** 31 + 5, -999][:min(n_i, 3)]
+    w = list(rng.random(m))
+    dx = [torch.from_numpy(x).to(cuda) for x in xs]
+    dxi = [torch.from_numpy(x).to(cuda) for x in xis]
+    out = torch.empty(n, dtype=torch.float32, device=cuda)
+    out_i = torch.empty(n_i, dtype=torch.int64, device=cuda)
+    ops.agg_model_f32(dx, dxi, w, out, out_i)
+    assert _bits_equal(out.cpu().numpy(), oracle.agg_f32(xs, w))
+    if n_i:
+        assert np.array_equal(out_i.cpu().numpy(), oracle.agg_i64(xis, w))
+
+
+@pytest.mark.parametrize("mode", [ops.MODE_EXACT, ops.MODE_FMA])
+def test_agg_model_f32_in_place_and_fma(cuda, mode):
+    """The aggregating model is the last operand and the output (both segments), and FMA mode
+    equals agg_f32's FMA mode bit for bit."""
+    rng = np.random.default_rng(3)
+    n, n_i, m = 100003, 53, 9
+    xs = [torch.from_numpy(_rand_f32(rng, n)).to(cuda) for _ in range(m)]
+    xis = [torch.from_numpy(rng.integers(0, 10 ** 6, size=n_i)).to(cuda) for _ in range(m)]
+    w = [1 / m] * m
+    ref = torch.empty(n, device=cuda)
+    ops.agg_f32(xs, w, ref, mode=mode)
+    ref_i = torch.empty(n_i, dtype=torch.int64, device=cuda)
+    ops.agg_i64(xis, w, ref_i)
+    ops.agg_model_f32(xs, xis, w, xs[-1], xis[-1], mode=mode)
+    assert torch.equal(xs[-1].view(torch.int32), ref.view(torch.int32))
+    assert torch.equal(xis[-1], ref_i)
+
+
+def test_agg_model_f32_unaligned_falls_back(cuda):
+    rng = np.random.default_rng(8)
+    n, m = 5001, 9
+    base = [torch.from_numpy(_rand_f32(rng, n + 1)).to(cuda) for _ in range(m)]
+    xs = [b[1:] for b in base]
+    xis = [torch.from_numpy(rng.integers(0, 10 ** 6, size=20)).to(cuda) for _ in range(m)]
+    w = [1 / m] * m
+    out = torch.empty(n + 1, device=cuda)[1:]
+    out_i = torch.empty(20, dtype=torch.int64, device=cuda)
+    ops.agg_model_f32(xs, xis, w, out, out_i)
+    assert _bits_equal(out.cpu().numpy(), oracle.agg_f32([x.cpu().numpy() for x in xs], w))
+    assert np.array_equal(out_i.cpu().numpy(), oracle.agg_i64([x.cpu().numpy() for x in xis], w))
+
+
 def _graph_csr(g, weights="unweighted"):
     orders, ws = [], []
     cent = nx.degree_centrality(g)

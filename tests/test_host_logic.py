@@ -565,3 +565,37 @@ def test_auto_dense_only_for_cliques():
     rp, col, w = csr_from_lists(orders, [[1 / 40] * 40] * 40)
     p = ops.build_plan(rp, col, w, np.arange(40, dtype=np.int32), c4=64, lds_bytes=160 * 1024, dense=-1)
     assert p.info.dense_rb == 8
+
+
+# DESIGN.md §6 "Busiest-pair volumes" table (GB per round, contiguous blocks): halo / transpose
+_DESIGN_LINK_TABLE = {
+    ("barbell", 128, "resnet50"): {2: (0.09, 6.03), 4: (3.02, 1.51), 8: (1.51, 0.38)},
+    ("sbm", 256, "vit_b16"): {2: (30.13, 44.32), 4: (12.12, 11.08), 8: (4.85, 2.77)},
+    ("random", None, "resnet50"): {2: (6.03, 6.03), 4: (5.85, 3.02), 8: (4.81, 1.51)},
+}
+
+
+def test_link_model_matches_design_table():
+    """bench.py's N > 1 bound model (transposed.link_model) reproduces DESIGN §6's busiest-pair
+    table for configs 4 and 5 and the weak-scaling graph at 2 / 4 / 8 GPUs, chooses the
+    exchange with the smaller busiest pair (as choose_exchange does), and names the binding
+    term consistently with its own times."""
+    import bench
+    from topology_aware_learning_amd import synth
+    from topology_aware_learning_amd.arena import StateLayout
+    from topology_aware_learning_amd.distributed import partition_contiguous
+    from topology_aware_learning_amd.transposed import choose_exchange, link_model
+
+    for (kind, nd, model), rows in _DESIGN_LINK_TABLE.items():
+        lay = StateLayout.from_layout(synth.get_layout(model))
+        for world, (halo_gb, tr_gb) in rows.items():
+            orders, _ = bench.round_spec(nd or 64 * world, 8, kind=kind)
+            owner = partition_contiguous(len(orders), world)
+            m = link_model(orders, owner, world, lay.n_f32, lay.n_i64, lay.n_b16)
+            assert round(m["halo"]["busiest_pair_bytes"] / 1e9, 2) == halo_gb, (kind, world)
+            assert round(m["transpose"]["busiest_pair_bytes"] / 1e9, 2) == tr_gb, (kind, world)
+            for v in m.values():
+                assert v["predicted_ms"] == max(v["hbm_ms"], v["link_ms"])
+                assert v["binds"] == ("xgmi" if v["link_ms"] > v["hbm_ms"] else "hbm")
+            ch = choose_exchange(orders, owner, world, lay.n_f32, lay.n_i64, lay.n_b16)
+            assert ch == ("transpose" if tr_gb < 0.9 * halo_gb else "halo"), (kind, world)

@@ -27,13 +27,14 @@ TAL_ERR_COMM = 4
 TAL_COMM_ID_BYTES = 128
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 EXPORTED = (
     "tal_last_error",
     "tal_abi_version",
     "tal_agg_f32",
     "tal_agg_i64",
+    "tal_agg_model_f32",
     "tal_agg_bf16",
     "tal_round_plan_words",
     "tal_round_plan_build",
@@ -120,6 +121,7 @@ _SIGS = {
     "tal_abi_version": (_I32, []),
     "tal_agg_f32": (_I32, [_PP, _PD, _I32, _P, _I64, _I32, _P]),
     "tal_agg_i64": (_I32, [_PP, _PD, _I32, _P, _I64, _P]),
+    "tal_agg_model_f32": (_I32, [_PP, _PP, _PD, _I32, _P, _I64, _P, _I64, _I32, _P]),
     "tal_agg_bf16": (_I32, [_PP, _PD, _I32, _P, _I64, _I32, _P]),
     "tal_round_plan_words": (_I64, [_I32, _I64]),
     "tal_round_plan_build": (

@@ -324,8 +324,11 @@ def aggregate_models(operands: Sequence[nn.Module], weights: Sequence[float], ta
         in_place = False
 
     w = [float(x) for x in weights]
-    for g in sizes:
-        _AGG[g](ptrs[g], w, outs[g], mode)
+    if set(sizes) == {"f32", "i64"}:  # a ResNet-like model: both segments in one launch
+        ops.agg_model_f32(ptrs["f32"], ptrs["i64"], w, outs["f32"], outs["i64"], mode)
+    else:
+        for g in sizes:
+            _AGG[g](ptrs[g], w, outs[g], mode)
 
     synced = False
     if host_target is not None:  # pinned row: one D2H per segment straight into it

@@ -152,6 +152,58 @@ def by_name_offset(entries: Sequence[Entry], name: str) -> int:
     raise KeyError(name)
 
 
+# Binding generation.  A bound module's state can stop being its pool row only by being
+# re-pointed: Module._apply (module.to() / .cuda() / .float() / ..., on it or on any submodule),
+# registering a parameter / buffer / submodule (setattr, register_buffer, load_state_dict
+# (assign=True)), or assigning `.data` directly.  Hooks installed with the first bind bump this
+# counter on each of them (torch's global registration hooks, a wrapper around Module._apply,
+# and a `data` property on nn.Parameter whose setter bumps it); a binding verified entry by
+# entry at generation g stays valid while the counter is still g, so the per-call check is O(1)
+# (plus one data_ptr of the first entry) instead of one data_ptr per entry (ResNet-50: 320,
+# ~70 us per model, ten models per call).  Not hooked: `buf.data = x` on a plain-tensor buffer
+# (torch.Tensor itself is left alone); it is seen at the next full check, after any hook event.
+_GEN = [0]
+_HOOKS: list = []
+
+
+def _invalidate(*_args, **_kw) -> None:
+    _GEN[0] += 1
+
+
+def _install_hooks() -> None:
+    if _HOOKS:
+        return
+    from torch.nn.modules import module as _m
+
+    _HOOKS.append(_m.register_module_parameter_registration_hook(_invalidate))
+    _HOOKS.append(_m.register_module_buffer_registration_hook(_invalidate))
+    _HOOKS.append(_m.register_module_module_registration_hook(_invalidate))
+    orig = nn.Module._apply
+
+    def _apply(self, *args, **kwargs):
+        _invalidate()
+        return orig(self, *args, **kwargs)
+
+    _apply._tal_orig = orig  # type: ignore[attr-defined]
+    nn.Module._apply = _apply  # type: ignore[method-assign]
+    _HOOKS.append(_apply)
+    for name in ("register_parameter", "register_buffer", "__delattr__"):  # (set to None, del)
+        def wrapped(self, *args, _orig=getattr(nn.Module, name), **kwargs):
+            _invalidate()
+            return _orig(self, *args, **kwargs)
+
+        setattr(nn.Module, name, wrapped)
+        _HOOKS.append(wrapped)
+    base = torch._C.TensorBase.data
+
+    def _set_data(self, value):
+        _invalidate()
+        base.__set__(self, value)
+
+    nn.Parameter.data = property(base.__get__, _set_data, doc=base.__doc__)  # type: ignore[assignment]
+    _HOOKS.append(_set_data)
+
+
 def _resolve(module: nn.Module, name: str) -> Tuple[nn.Module, str]:
     parts = name.split(".")
     mod = module
@@ -220,30 +272,51 @@ class ModelPool:
             else:  # pragma: no cover - state_dict keys always resolve to a param or buffer
                 raise KeyError(e.name)
             slots.append((table, attr, v.data_ptr()))
+        _install_hooks()
         module._tal_pool = self  # type: ignore[attr-defined]
         module._tal_row = r  # type: ignore[attr-defined]
+        module._tal_gen = _GEN[0]  # type: ignore[attr-defined]
         module._tal_slots = [(table, attr) for table, attr, _ in slots]  # type: ignore[attr-defined]
         module._tal_ptrs = [ptr for _, _, ptr in slots]  # type: ignore[attr-defined]
         self._bound[id(module)] = r
         return module
 
     def row_of(self, module: nn.Module) -> Optional[int]:
-        """Row the module is bound to, if its state still lives there (checked per entry)."""
+        """Row the module is bound to, if its state still lives there: O(1) while no re-pointing
+        hook fired since its last full check (_GEN), else checked per entry."""
         if getattr(module, "_tal_pool", None) is not self:
             return None
         r = module._tal_row  # type: ignore[attr-defined]
-        # every state entry must still be the row view bound to it (module.to(), param.data
-        # assignment or a re-registered buffer re-point it); checked through the tables kept at
-        # bind time - no state_dict / view rebuild per call (~1 ms for ResNet-50's 320 entries)
         slots = module._tal_slots  # type: ignore[attr-defined]
+        if module._tal_gen == _GEN[0]:  # type: ignore[attr-defined]
+            # no re-pointing hook fired since the last full check (see _GEN)
+            table, attr = slots[0]
+            t = table.get(attr)
+            if t is not None and t.data_ptr() == module._tal_ptrs[0]:  # type: ignore[attr-defined]
+                return r
+            return None
+        # after a hook event: every state entry, resolved by name again (a replaced submodule
+        # keeps its old tables), must still be the row view bound to it
+        gen = _GEN[0]
+        fresh = []
+        mods = dict(module.named_modules(remove_duplicate=False))
         try:
-            ptrs = [table[attr].data_ptr() for table, attr in slots]
+            for e in self.layout.entries:
+                path, _, attr = e.name.rpartition(".")
+                mod = mods[path]
+                table = mod._parameters if attr in mod._parameters else mod._buffers
+                fresh.append((table, attr))
+            ptrs = [table[attr].data_ptr() for table, attr in fresh]
         except (KeyError, AttributeError):  # an entry removed or set to None
             return None
         if ptrs != module._tal_ptrs:  # type: ignore[attr-defined]
             return None
-        table, attr = slots[0]
-        return r if table[attr].device == self.device else None
+        table, attr = fresh[0]
+        if table[attr].device != self.device:
+            return None
+        module._tal_slots = fresh  # type: ignore[attr-defined]
+        module._tal_gen = gen  # type: ignore[attr-defined]
+        return r
 
 
 def bound_row(module: nn.Module) -> Optional[Tuple[ModelPool, int]]:

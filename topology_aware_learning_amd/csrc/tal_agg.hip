@@ -43,7 +43,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 12;
+constexpr int kAbiVersion = 13;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -256,6 +256,71 @@ __global__ __launch_bounds__(kBlock) void k_agg_i64(OpTableI64 t, int m, int64_t
     for (int k = 1; k < m; ++k)
       acc = __fadd_rn(acc, __fmul_rn(t.w[k], static_cast<float>(t.x[k][e])));
     out[e] = trunc_i64(acc);
+  }
+}
+
+// K1m: one call over a whole model in ONE launch - the fp32 segment in float4 chunks, then (last
+// block) its n % 4 tail and the int64 segment (the ~50 num_batches_tracked counters of a
+// ResNet): the per-call path's three launches (vector, tail, int64) become one.  m <= kModelOps
+// operands, 16-B aligned fp32 segments; the same element arithmetic as k_agg_f32_vec /
+// k_agg_f32_scalar / k_agg_i64, so the result is theirs bit for bit.
+constexpr int kModelOps = 64;
+constexpr int kModelI64Max = 1 << 16;  // int64 elements the last block takes (else two launches)
+
+struct OpTableModel {
+  const float* x[kModelOps];
+  const int64_t* xi[kModelOps];
+  float w[kModelOps];
+};
+
+template <int M_STATIC, bool EXACT>
+__global__ __launch_bounds__(kBlock) void k_agg_model(OpTableModel t, int m_rt, float* out, int64_t n,
+                                                      int64_t* out_i, int64_t n_i) {
+  const int m = M_STATIC > 0 ? M_STATIC : m_rt;
+  const int64_t n4 = n / 4;
+  {
+    // float4 chunks, one per lane (the last block's lanes past n4 go straight to the scalar work)
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i < n4) {
+      if constexpr (M_STATIC > 0) {
+        float4 v[M_STATIC];
+#pragma unroll
+        for (int k = 0; k < M_STATIC; ++k) v[k] = ld_stream(t.x[k], i);
+        float4 acc = first4<EXACT>(t.w[0], v[0]);
+#pragma unroll
+        for (int k = 1; k < M_STATIC; ++k) acc = next4<EXACT>(acc, t.w[k], v[k]);
+        reinterpret_cast<float4*>(out)[i] = acc;
+      } else {
+        float4 acc = first4<EXACT>(t.w[0], ld_stream(t.x[0], i));
+        for (int k = 1; k < m; k += 8) {
+          float4 v[8];
+          const int kn = min(8, m - k);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (j < kn) v[j] = ld_stream(t.x[k + j], i);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (j < kn) acc = next4<EXACT>(acc, t.w[k + j], v[j]);
+        }
+        reinterpret_cast<float4*>(out)[i] = acc;
+      }
+    }
+    if (blockIdx.x + 1 < gridDim.x) return;
+  }
+  // last block: the fp32 tail (< 4 elements) and the int64 segment, one element per lane
+  const int64_t tail = n - 4 * n4;
+  for (int64_t e = threadIdx.x; e < tail + n_i; e += kBlock) {
+    if (e < tail) {
+      const int64_t q = 4 * n4 + e;
+      float acc = first_term<EXACT>(t.w[0], t.x[0][q]);
+      for (int k = 1; k < m; ++k) acc = next_term<EXACT>(acc, t.w[k], t.x[k][q]);
+      out[q] = acc;
+    } else {
+      const int64_t q = e - tail;
+      float acc = __fmul_rn(t.w[0], static_cast<float>(t.xi[0][q]));
+      for (int k = 1; k < m; ++k) acc = __fadd_rn(acc, __fmul_rn(t.w[k], static_cast<float>(t.xi[k][q])));
+      out_i[q] = trunc_i64(acc);
+    }
   }
 }
 
@@ -2722,6 +2787,55 @@ int32_t tal_agg_i64(const int64_t* const* x_host, const double* w_host, int32_t 
   for (int i = m; i < kMaxOps; ++i) { t.x[i] = nullptr; t.w[i] = 0.f; }
   k_agg_i64<<<grid_for(n), kBlock, 0, static_cast<hipStream_t>(stream)>>>(t, m, out, n);
   return check_launch("tal_agg_i64");
+}
+
+int32_t tal_agg_model_f32(const float* const* x_host, const int64_t* const* xi_host, const double* w_host,
+                          int32_t m, float* out, int64_t n, int64_t* out_i, int64_t n_i, int32_t mode,
+                          void* stream) {
+  if (m <= 0) return fail(TAL_ERR_INVALID, "tal_agg_model_f32: m must be >= 1");
+  if (n < 0 || n_i < 0) return fail(TAL_ERR_INVALID, "tal_agg_model_f32: n < 0");
+  if (!x_host || !w_host || (n > 0 && !out) || (n_i > 0 && (!xi_host || !out_i)))
+    return fail(TAL_ERR_INVALID, "tal_agg_model_f32: null pointer");
+  bool fused = m <= kModelOps && n_i <= kModelI64Max && aligned16(out) && n > 0;
+  for (int i = 0; i < m; ++i) {
+    if ((n > 0 && !x_host[i]) || (n_i > 0 && !xi_host[i]))
+      return fail(TAL_ERR_INVALID, "tal_agg_model_f32: null operand pointer");
+    fused = fused && aligned16(x_host[i]);
+  }
+  if (!fused) {  // the segment-by-segment path (same arithmetic)
+    int32_t rc = n > 0 ? tal_agg_f32(x_host, w_host, m, out, n, mode, stream) : TAL_OK;
+    if (rc == TAL_OK && n_i > 0) rc = tal_agg_i64(xi_host, w_host, m, out_i, n_i, stream);
+    return rc;
+  }
+  OpTableModel t;
+  for (int i = 0; i < kModelOps; ++i) {
+    t.x[i] = i < m ? x_host[i] : nullptr;
+    t.xi[i] = i < m && n_i > 0 ? xi_host[i] : nullptr;
+    t.w[i] = i < m ? static_cast<float>(w_host[i]) : 0.f;
+  }
+  const int64_t n4 = n / 4;
+  // one thread per float4 chunk; the last block also takes the scalar work (an extra block
+  // when the chunks fill the last one exactly)
+  const int64_t nb = (n4 + kBlock - 1) / kBlock + (n4 % kBlock == 0 ? 1 : 0);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 g(static_cast<unsigned>(nb)), b(kBlock);
+  const bool exact = mode == TAL_MODE_EXACT;
+#define TAL_MODEL_CASE(MM)                                                                   \
+  case MM:                                                                                   \
+    if (exact) k_agg_model<MM, true><<<g, b, 0, s>>>(t, m, out, n, out_i, n_i);              \
+    else k_agg_model<MM, false><<<g, b, 0, s>>>(t, m, out, n, out_i, n_i);                   \
+    break;
+  switch (m) {
+    TAL_MODEL_CASE(1) TAL_MODEL_CASE(2) TAL_MODEL_CASE(3) TAL_MODEL_CASE(4) TAL_MODEL_CASE(5)
+    TAL_MODEL_CASE(6) TAL_MODEL_CASE(7) TAL_MODEL_CASE(8) TAL_MODEL_CASE(9) TAL_MODEL_CASE(10)
+    TAL_MODEL_CASE(11) TAL_MODEL_CASE(12) TAL_MODEL_CASE(13) TAL_MODEL_CASE(14) TAL_MODEL_CASE(15)
+    TAL_MODEL_CASE(16) TAL_MODEL_CASE(17)
+    default:
+      if (exact) k_agg_model<0, true><<<g, b, 0, s>>>(t, m, out, n, out_i, n_i);
+      else k_agg_model<0, false><<<g, b, 0, s>>>(t, m, out, n, out_i, n_i);
+  }
+#undef TAL_MODEL_CASE
+  return check_launch("tal_agg_model_f32");
 }
 
 int64_t tal_round_plan_words(int32_t rows, int64_t nnz) {

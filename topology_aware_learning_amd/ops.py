@@ -73,6 +73,21 @@ def agg_i64(xs: Sequence[torch.Tensor], weights: Sequence[float], out: torch.Ten
     return out
 
 
+def agg_model_f32(xs: Sequence[torch.Tensor], xis: Sequence[torch.Tensor], weights: Sequence[float],
+                  out: torch.Tensor, out_i: torch.Tensor, mode: int = MODE_EXACT, stream=None) -> None:
+    """K1 over a whole model in one launch: out = sum_i fp32(w_i) * xs[i] (fp32 segment) and
+    out_i = trunc(sum_i fp32(w_i) * fp32(xis[i])) (int64 segment), the arithmetic of agg_f32 and
+    agg_i64 bit for bit (decentralized_client.py:406-413 over every state_dict entry)."""
+    _require_gpu(out, "out", torch.float32)
+    _require_gpu(out_i, "out_i", torch.int64)
+    n, n_i = out.numel(), out_i.numel()
+    P, W = _ptrs_and_weights(xs, weights, n, torch.float32, out)
+    PI, _ = _ptrs_and_weights(xis, weights, n_i, torch.int64, out)
+    L = _lib.load()
+    check(L.tal_agg_model_f32(P, PI, W, len(xs), ctypes.c_void_p(out.data_ptr()), n,
+                              ctypes.c_void_p(out_i.data_ptr()), n_i, int(mode), _stream(out.device, stream)))
+
+
 def agg_bf16(xs: Sequence[torch.Tensor], weights: Sequence[float], out: torch.Tensor,
              mode: int = MODE_EXACT, stream=None) -> torch.Tensor:
     """K1 on bf16 buffers.  MODE_EXACT: the reference's torch ops on bf16 tensors (every product

@@ -78,12 +78,18 @@ def layout_counts(layout: Layout) -> Tuple[int, int]:
     return nf, ni
 
 
-def synth_state_dict(layout: Layout, seed: int) -> "OrderedDict[str, torch.Tensor]":
-    """CPU tensors for `layout`; entry values depend only on (seed, position in the layout)."""
+def synth_state_dict(layout: Layout, seed: int, entries=None) -> "OrderedDict[str, torch.Tensor]":
+    """CPU tensors for `layout`; entry values depend only on (seed, position in the layout).
+    `entries`: indices of the entries to make (default all) - a sub-state-dict with the values
+    those entries have in the whole one."""
     sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
     pos = 0
-    for name, shape, dt in layout:
+    keep = None if entries is None else set(int(e) for e in entries)
+    for k, (name, shape, dt) in enumerate(layout):
         n = numel(shape)
+        if keep is not None and k not in keep:
+            pos += n
+            continue
         if dt == "float32":
             a = counter_f32(seed, pos, n)
             if name.endswith("running_var"):
@@ -99,6 +105,64 @@ def synth_state_dict(layout: Layout, seed: int) -> "OrderedDict[str, torch.Tenso
         sd[name] = torch.from_numpy(a.reshape(shape).copy())
         pos += n
     return sd
+
+
+def _i64(u: int) -> int:
+    """uint64 constant as the int64 with the same bits (torch has no wrapping uint64 ops)."""
+    return u - (1 << 64) if u >= 1 << 63 else u
+
+
+def _srl(x: "torch.Tensor", k: int) -> "torch.Tensor":
+    """Logical right shift of int64 bit patterns."""
+    return (x >> k) & ((1 << (64 - k)) - 1)
+
+
+def counter_f32_torch(seed: int, start: int, n: int, device, out: "torch.Tensor" = None) -> "torch.Tensor":
+    """counter_f32 computed on `device` (int64 arithmetic wraps like uint64): bitwise the host
+    generator, for full-size test pools that would take minutes to generate with numpy."""
+    x = torch.arange(start, start + n, dtype=torch.int64, device=device)
+    x ^= _i64((seed & 0xFFFFFFFF) << 40 & 0xFFFFFFFFFFFFFFFF)
+    x += _i64(int(_M1))
+    x = (x ^ _srl(x, 30)) * _i64(int(_M2))
+    x = (x ^ _srl(x, 27)) * _i64(int(_M3))
+    x = x ^ _srl(x, 31)
+    mant = x & 0x7FFFFF
+    expo = 121 + (_srl(x, 23) & 7)
+    sign = _srl(x, 31) & 1
+    bits = (sign << 31) | (expo << 23) | mant
+    bits = torch.where(bits >= 1 << 31, bits - (1 << 32), bits).to(torch.int32)
+    if out is None:
+        return bits.view(torch.float32)
+    out.view(torch.int32).copy_(bits)
+    return out
+
+
+def fill_rows_torch(seg: "torch.Tensor", layout: Layout, seeds: Sequence[int], dtype: str = "float32",
+                    chunk: int = 1 << 25) -> None:
+    """seg[r, :n] = the `dtype` entries of synth_state_dict(layout, seeds[r]) concatenated in
+    state_dict order (a pool segment row), generated on seg's device.  float32, bfloat16 (the
+    bf16 of the fp32 counter value, as synth_state_dict makes it) and int64 segments."""
+    ents = []
+    pos = 0
+    for name, shape, dt in layout:
+        n = numel(shape)
+        if dt == dtype:
+            ents.append((name, pos, n))
+        pos += n
+    for r, seed in enumerate(seeds):
+        off = 0
+        for name, p0, n in ents:
+            if dtype == "int64":  # a few counters per model: host values
+                seg[r, off:off + n].copy_(torch.from_numpy(counter_i64(seed, p0, n)))
+                off += n
+                continue
+            for c0 in range(0, n, chunk):
+                c1 = min(n, c0 + chunk)
+                v = counter_f32_torch(seed, p0 + c0, c1 - c0, seg.device)
+                if dtype == "float32" and name.endswith("running_var"):  # (bf16 entries: as made)
+                    v = v.abs() + 0.5
+                seg[r, off + c0:off + c1].copy_(v)  # bfloat16: round to nearest even, as .to()
+            off += n
 
 
 # ------------------------------------------------------------------------------------------

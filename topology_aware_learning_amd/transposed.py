@@ -95,6 +95,38 @@ def exchange_bytes(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: int
                 halo_link=int(halo_link), transpose_link=int(-(-2 * own * row // world)))
 
 
+HBM_GBPS = 8000.0       # MI355X HBM3E peak per GPU (MI355X_MICROARCH.md)
+XGMI_LINK_GBPS = 153.0  # one xGMI link per GPU pair, one direction (7 links per GPU)
+
+
+def link_model(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: int = 0) -> dict:
+    """DESIGN §6's bound per exchange kind, for rank-level reporting next to a measured round:
+    local HBM bytes of the busiest rank (halo: its staged sources - own and received - read once
+    plus its own rows written; transpose: the round over every model's column block plus the
+    packing and unpacking of its own models), the busiest directed GPU pair's bytes, each over
+    its peak (HBM 8 TB/s, one xGMI link 153 GB/s), predicted_ms = the larger, and which binds."""
+    owner = np.asarray(owner)
+    row = 4 * n_f32 + 2 * n_b16 + 8 * n_i64
+    specs = [build_shard(orders, [[1.0] * len(o) for o in orders], owner, r, world) for r in range(world)]
+    vol = exchange_bytes(orders, owner, world, n_f32, n_i64, n_b16)
+    n_dev = len(orders)
+    local = {
+        "halo": max(len({j for i in s.orders_local for j in i}) + len(s.own) for s in specs) * row,
+        # K3 over [n_dev, n / world] (sources + outputs) + pack (read own, write send buffer)
+        # + unpack (read received blocks, write own rows)
+        "transpose": -(-2 * n_dev * row // world) + 4 * max(len(s.own) for s in specs) * row,
+    }
+    out = {}
+    for kind in ("halo", "transpose"):
+        pair = vol[kind + "_link"]
+        hbm_ms = local[kind] / (HBM_GBPS * 1e6)
+        link_ms = pair / (XGMI_LINK_GBPS * 1e6)
+        out[kind] = dict(local_bytes=int(local[kind]), busiest_pair_bytes=int(pair), rank_link_bytes=int(vol[kind]),
+                         hbm_ms=hbm_ms, link_ms=link_ms, predicted_ms=max(hbm_ms, link_ms),
+                         binds="xgmi" if link_ms > hbm_ms else "hbm")
+    return out
+
+
 def choose_exchange(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: int = 0) -> str:
     """'transpose' when its busiest link carries clearly fewer bytes than the halo's busiest
     link (random expanders at 4+ ranks, 60-cliques spread over 4 GPUs), else 'halo' (rings,
