@@ -151,10 +151,7 @@ def cpu_baseline(layout_list, m: int, budget_s: float):
     w = [1 / m] * m
     n_out = sum(t.numel() for t in targets[0].values())
     default_threads = torch.get_num_threads()
-    try:
-        all_threads = len(os.sched_getaffinity(0))
-    except AttributeError:  # pragma: no cover - non-Linux
-        all_threads = os.cpu_count() or default_threads
+    all_threads = usable_cpus()
 
     def one_at_a_time(threads: int, secs: float):
         torch.set_num_threads(threads)
@@ -187,7 +184,8 @@ def cpu_baseline(layout_list, m: int, budget_s: float):
     torch.set_num_threads(default_threads)
     return dict(value=calls_all * n_out / el_all, unit="params/s", cores=all_threads, kind="port",
                 sample=f"{calls_all} reference calls (M={m}, {n_out} params) one at a time in {el_all:.2f} s "
-                       f"with torch.set_num_threads({all_threads}) (every core this process may run on); "
+                       f"with torch.set_num_threads({all_threads}) (every core this process may run on: "
+                       "its affinity within the cgroup CPU quota); "
                        "torch CPU clone/mul/add_/copy_ on host state_dicts",
                 ms_per_call=1e3 * el_all / calls_all,
                 default_threads_value=calls_def * n_out / el_def, default_threads=default_threads,
@@ -196,6 +194,37 @@ def cpu_baseline(layout_list, m: int, budget_s: float):
                 # the reference's effective configuration: Parsl ThreadPoolExecutor(max_threads=2)
                 two_concurrent_calls_value=sum(counts) * n_out / el2, two_concurrent_calls=sum(counts),
                 two_concurrent_seconds=round(el2, 2))
+
+
+def usable_cpus() -> int:
+    """Cores this process may actually use: its CPU affinity, capped by a cgroup CPU quota
+    (cgroup v2 cpu.max or v1 cfs quota / period) - on a shared box os.cpu_count() shows the whole
+    machine, and that many threads on a 16-core quota would stall every parallel op."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover - non-Linux
+        n = os.cpu_count() or 1
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            if parse is not None:
+                q, per = parse(open(path).read())
+                if q != "max":
+                    n = min(n, max(1, int(int(q) / int(per))))
+            else:
+                q = int(open(path).read())
+                per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+                if q > 0:
+                    n = min(n, max(1, q // per))
+            break
+        except (OSError, ValueError):
+            continue
+    return n
+
+
+def log(msg: str) -> None:
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    print(f"bench: {msg}", file=sys.stderr, flush=True)
 
 
 def cpu_model() -> str:
@@ -265,6 +294,7 @@ def main():
         # into each candidate is timed with it and the two fastest destinations are kept
         pool_bytes = rows * (4 * layout.ld_f32 + 2 * layout.ld_b16 + 8 * layout.ld_i64)
         trials = max(2, min(args.placement_trials, int(0.7 * torch.cuda.mem_get_info(dev)[0] // pool_bytes)))
+        log(f"{rows} rows x {n_float} elements, {trials} candidate pools")
         cand = [ModelPool(layout, rows, dev) for _ in range(trials)]
         fill_pool(cand[0], 1234)
         tune = not (args.plan or args.stream_rows or args.no_tune or args.c4)
@@ -300,6 +330,7 @@ def main():
         del cand
         torch.cuda.empty_cache()  # the candidates not kept
         fill_pool(pin, 1234)
+        log(f"placement {placement}")
         if tune:  # time every plan candidate on the pools the steps use (once per topology)
             plan = _ops.tune_plan(row_ptr, col, w, out_rows, seg(pin), seg(pout), n=n_float, mode=mode)
             in_place = in_place and plan.single_group
@@ -311,6 +342,7 @@ def main():
         # correctness check at full size: EVERY output row of the round (both segments) == K1
         # on the same operands, bitwise (K1 itself is pinned to the reference's sha256 of
         # ResNet-50 M = 9 calls; tests/test_gpu_fullsize.py pins whole rounds)
+        log(f"plan {plan.spec}; checking every row against K1")
         step(pin, pout)
         chk = torch.empty(n_float, dtype=seg(pin).dtype, device=dev)
         chk_i = torch.empty(layout.n_i64, dtype=torch.int64, device=dev)
@@ -328,6 +360,7 @@ def main():
         del chk, chk_i
         tol = bf16_tolerance(pin, pout, orders[0], weights[0], n_float, dev) if bf16 else None
 
+        log(f"parity {parity_ok} ({len(bad_rows)} rows differ); timing {args.steps} steps")
         pools = [pin, pin] if in_place else [pin, pout]
         for i in range(args.warmup):
             step(pools[i % 2], pools[(i + 1) % 2])
@@ -432,6 +465,7 @@ def main():
                                            workload_key(args.graph, n_dev_total, args.model, args.dtype, args.weights)))
     cpu = None
     if not args.no_cpu_baseline and world == 1:
+        log("CPU baseline")
         cpu = cpu_baseline(lay, M, args.cpu_seconds)  # bf16 layouts: the reference's loop on bf16 tensors
     value = units / el
     out = {

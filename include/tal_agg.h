@@ -229,6 +229,24 @@ int32_t tal_agg_round_bf16(const uint16_t* pool_in, int64_t ld_in, uint16_t* poo
                            int64_t ld_out, int64_t n, const int32_t* plan_dev,
                            const tal_round_plan_info* info, int32_t mode, void* stream);
 
+/* ---- K3r: a round over register-resident source groups ----------------------------------
+ * Community graphs (BASELINE config 5's stochastic block model): the rows are grouped so that
+ * each group reads <= 64 distinct sources; one wavefront loads a group's sources for a 128-
+ * element piece of the columns into VGPRs and emits every row of the group for that piece, an
+ * operand read from the registers by the VGPR index mode (no LDS, no barrier).  Same results
+ * as tal_agg_round_f32 (EXACT: bitwise the reference; FMA: bitwise K1-FMA); bf16 pools (bf16 !=
+ * 0) in FMA mode only.  Out of place (pool_in != pool_out).  Pools 2-element aligned, even ld
+ * >= n rounded up to even.  table_dev (int32): n_groups records {first source, sources, first
+ * row, rows}; at off_src the source pool rows; at off_rows (a multiple of 4) row records {out
+ * row, operands, first operand, 0}, a group's rows consecutive; at off_ops (even) 64-bit operand
+ * records {fp32 weight bits, 2 x slot of the source in its group}, plus 8 records of padding.
+ * max_src = the largest group's sources (<= 64).  Replaces decentralized_client.py:399-413 for
+ * every row of the round at once (snapshot semantics, as tal_agg_round_f32). */
+int32_t tal_agg_round_reg(const void* pool_in, int64_t ld_in, void* pool_out, int64_t ld_out,
+                          int64_t n, int32_t bf16, const int32_t* table_dev, int32_t n_groups,
+                          int32_t off_src, int32_t off_rows, int32_t off_ops, int32_t max_src,
+                          int32_t mode, void* stream);
+
 /* ---- K2: cosine similarity of two models' parameters, bit for bit -------------------------
  * Reference: cosine_similarity, decentralized_client.py:661-681: for each parameter tensor
  * viewed as [A, I, B] (dim 1 = the reduced dim; 1-D tensors are unsqueezed to [n, 1]),

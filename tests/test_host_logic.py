@@ -599,3 +599,38 @@ def test_link_model_matches_design_table():
                 assert v["binds"] == ("xgmi" if v["link_ms"] > v["hbm_ms"] else "hbm")
             ch = choose_exchange(orders, owner, world, lay.n_f32, lay.n_i64, lay.n_b16)
             assert ch == ("transpose" if tr_gb < 0.9 * halo_gb else "halo"), (kind, world)
+
+
+def test_reg_plan_table_layout():
+    """build_reg_plan (K3r): every row in exactly one group, each group's operands among its
+    <= 64 sources, records in reference order with the fp32 weight and 2 x slot, the pair order
+    sorted by operand count, 8 read-ahead records of padding (tal_agg.h K3r layout)."""
+    import bench
+    from oracle import reference_alg as ra
+    from topology_aware_learning_amd import ops
+
+    orders, ws = bench.round_spec(256, 8, kind="sbm", weights="degcent")
+    row_ptr, col, w = ra.round_csr(orders, ws)
+    out_rows = np.arange(len(orders), dtype=np.int32)[::-1].copy()
+    p = ops.build_reg_plan(row_ptr, col, w, out_rows)
+    t = p.table
+    grp = t[: 4 * p.n_groups].reshape(-1, 4)
+    recs = t[p.off_rows: p.off_ops].reshape(-1, 4)
+    opr = t[p.off_ops:].view(np.uint32).reshape(-1, 2)
+    assert len(opr) == len(col) + 8 and p.max_src <= 64 and p.off_rows % 4 == 0 and p.off_ops % 2 == 0
+    seen = []
+    for s0, ns, r0, nr in grp:
+        srcs = t[p.off_src + s0: p.off_src + s0 + ns]
+        assert ns <= 64 and list(srcs) == sorted(set(srcs.tolist()))
+        counts = recs[r0: r0 + nr, 1]
+        assert list(counts) == sorted(counts, reverse=True)
+        for out, cnt, q0, _ in recs[r0: r0 + nr]:
+            r = int(np.flatnonzero(out_rows == out)[0])
+            seen.append(r)
+            assert cnt == len(orders[r])
+            for k in range(cnt):
+                wbits, reg = opr[q0 + k]
+                assert srcs[reg // 2] == orders[r][k] and reg % 2 == 0
+                assert wbits == np.float32(ws[r][k]).view(np.uint32)
+    assert sorted(seen) == list(range(len(orders)))
+    assert ops.build_reg_plan(row_ptr, col, w, out_rows, max_src=8) is None  # a row has 9+ sources

@@ -43,7 +43,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 13;
+constexpr int kAbiVersion = 14;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -73,6 +73,7 @@ int32_t check_launch(const char* what) {
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 inline bool aligned8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }
+inline bool aligned4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3u) == 0; }
 
 // ------------------------------------------------------------------------------------------
 // element arithmetic
@@ -1942,6 +1943,411 @@ int32_t launch_round_clique(const float* pin, int64_t ld_in, float* pout, int64_
   return TAL_OK;
 }
 
+// ------------------------------------------------------------------------------------------
+// K3r: rounds whose rows fall into groups of <= 64 distinct sources (community graphs, BASELINE
+// config 5's stochastic block model), each group's sources held in VGPRs.
+//   One wave = one item (group g, piece t): the 64 lanes load 2 elements each (fp32 8 B, bf16
+//   4 B unpacked to fp32) of every source of g at columns [128 t, 128 t + 128) straight into
+//   v[32 : 32 + 2 S) - no LDS, no barrier - then emit every row of g for that piece in
+//   reference order.  A row's operand is read from the registers by its wave-uniform slot with
+//   the VGPR index mode (s_set_gpr_idx_on / _idx / _off, SRC0): the multiply itself reads
+//   v[32 + 2 slot], so the register file stands in for K3n's LDS tile and no per-operand LDS
+//   read or extra move is issued.  The loads and the indexed arithmetic are inline asm on
+//   fixed registers (the compiler keeps the source tuples pinned there: every asm lists them
+//   as operands); rows run in pairs so that no packed instruction reads the result of the one
+//   right before it (gfx950 needs a wait state there, which the pairs fill with the other row).
+//   Items are handed to waves per XCD label (blockIdx % 8): the groups of one piece run on one
+//   XCD at the same time, so a source shared by several groups is fetched from HBM once and
+//   served to the others by that XCD's L2.
+//   Arithmetic: EXACT = fp32 multiply then fp32 add per operand from -0.0 (-0 + p = p), the
+//   reference's order; FMA = fused chains from -0.0 (fma(w, x0, -0) = fl(w x0)), bitwise K1-FMA.
+//   bf16 pools: FMA only (fp32 accumulation, one rounding at the store).
+// ------------------------------------------------------------------------------------------
+typedef float v32f __attribute__((ext_vector_type(32)));
+typedef __attribute__((address_space(4))) const uint64_t* ConstU64;
+constexpr int kRegMaxSrc = 64;
+constexpr int kRegPiece = 128;  // elements per item: 64 lanes x 2
+
+#define TAL_RLD2(a, b, k) "global_load_dwordx2 v[" #a ":" #b "], %17, %" #k " nt\n\t"
+#define TAL_RLD1(b, k) "global_load_dword v" #b ", %17, %" #k " nt\n\t"
+#define TAL_RUNP(a, b) "v_lshlrev_b32 v" #a ", 16, v" #b "\n\tv_and_b32 v" #b ", 0xffff0000, v" #b "\n\t"
+#define TAL_RF32_0 \
+  TAL_RLD2(32,33,1) TAL_RLD2(34,35,2) TAL_RLD2(36,37,3) TAL_RLD2(38,39,4) \
+  TAL_RLD2(40,41,5) TAL_RLD2(42,43,6) TAL_RLD2(44,45,7) TAL_RLD2(46,47,8) \
+  TAL_RLD2(48,49,9) TAL_RLD2(50,51,10) TAL_RLD2(52,53,11) TAL_RLD2(54,55,12) \
+  TAL_RLD2(56,57,13) TAL_RLD2(58,59,14) TAL_RLD2(60,61,15) TAL_RLD2(62,63,16)
+#define TAL_RF32_1 \
+  TAL_RLD2(64,65,1) TAL_RLD2(66,67,2) TAL_RLD2(68,69,3) TAL_RLD2(70,71,4) \
+  TAL_RLD2(72,73,5) TAL_RLD2(74,75,6) TAL_RLD2(76,77,7) TAL_RLD2(78,79,8) \
+  TAL_RLD2(80,81,9) TAL_RLD2(82,83,10) TAL_RLD2(84,85,11) TAL_RLD2(86,87,12) \
+  TAL_RLD2(88,89,13) TAL_RLD2(90,91,14) TAL_RLD2(92,93,15) TAL_RLD2(94,95,16)
+#define TAL_RF32_2 \
+  TAL_RLD2(96,97,1) TAL_RLD2(98,99,2) TAL_RLD2(100,101,3) TAL_RLD2(102,103,4) \
+  TAL_RLD2(104,105,5) TAL_RLD2(106,107,6) TAL_RLD2(108,109,7) TAL_RLD2(110,111,8) \
+  TAL_RLD2(112,113,9) TAL_RLD2(114,115,10) TAL_RLD2(116,117,11) TAL_RLD2(118,119,12) \
+  TAL_RLD2(120,121,13) TAL_RLD2(122,123,14) TAL_RLD2(124,125,15) TAL_RLD2(126,127,16)
+#define TAL_RF32_3 \
+  TAL_RLD2(128,129,1) TAL_RLD2(130,131,2) TAL_RLD2(132,133,3) TAL_RLD2(134,135,4) \
+  TAL_RLD2(136,137,5) TAL_RLD2(138,139,6) TAL_RLD2(140,141,7) TAL_RLD2(142,143,8) \
+  TAL_RLD2(144,145,9) TAL_RLD2(146,147,10) TAL_RLD2(148,149,11) TAL_RLD2(150,151,12) \
+  TAL_RLD2(152,153,13) TAL_RLD2(154,155,14) TAL_RLD2(156,157,15) TAL_RLD2(158,159,16)
+#define TAL_RB16_0 \
+  TAL_RLD1(33,1) TAL_RLD1(35,2) TAL_RLD1(37,3) TAL_RLD1(39,4) \
+  TAL_RLD1(41,5) TAL_RLD1(43,6) TAL_RLD1(45,7) TAL_RLD1(47,8) \
+  TAL_RLD1(49,9) TAL_RLD1(51,10) TAL_RLD1(53,11) TAL_RLD1(55,12) \
+  TAL_RLD1(57,13) TAL_RLD1(59,14) TAL_RLD1(61,15) TAL_RLD1(63,16)
+#define TAL_RB16_1 \
+  TAL_RLD1(65,1) TAL_RLD1(67,2) TAL_RLD1(69,3) TAL_RLD1(71,4) \
+  TAL_RLD1(73,5) TAL_RLD1(75,6) TAL_RLD1(77,7) TAL_RLD1(79,8) \
+  TAL_RLD1(81,9) TAL_RLD1(83,10) TAL_RLD1(85,11) TAL_RLD1(87,12) \
+  TAL_RLD1(89,13) TAL_RLD1(91,14) TAL_RLD1(93,15) TAL_RLD1(95,16)
+#define TAL_RB16_2 \
+  TAL_RLD1(97,1) TAL_RLD1(99,2) TAL_RLD1(101,3) TAL_RLD1(103,4) \
+  TAL_RLD1(105,5) TAL_RLD1(107,6) TAL_RLD1(109,7) TAL_RLD1(111,8) \
+  TAL_RLD1(113,9) TAL_RLD1(115,10) TAL_RLD1(117,11) TAL_RLD1(119,12) \
+  TAL_RLD1(121,13) TAL_RLD1(123,14) TAL_RLD1(125,15) TAL_RLD1(127,16)
+#define TAL_RB16_3 \
+  TAL_RLD1(129,1) TAL_RLD1(131,2) TAL_RLD1(133,3) TAL_RLD1(135,4) \
+  TAL_RLD1(137,5) TAL_RLD1(139,6) TAL_RLD1(141,7) TAL_RLD1(143,8) \
+  TAL_RLD1(145,9) TAL_RLD1(147,10) TAL_RLD1(149,11) TAL_RLD1(151,12) \
+  TAL_RLD1(153,13) TAL_RLD1(155,14) TAL_RLD1(157,15) TAL_RLD1(159,16)
+#define TAL_RUNP_0 \
+  TAL_RUNP(32,33) TAL_RUNP(34,35) TAL_RUNP(36,37) TAL_RUNP(38,39) \
+  TAL_RUNP(40,41) TAL_RUNP(42,43) TAL_RUNP(44,45) TAL_RUNP(46,47) \
+  TAL_RUNP(48,49) TAL_RUNP(50,51) TAL_RUNP(52,53) TAL_RUNP(54,55) \
+  TAL_RUNP(56,57) TAL_RUNP(58,59) TAL_RUNP(60,61) TAL_RUNP(62,63)
+#define TAL_RUNP_1 \
+  TAL_RUNP(64,65) TAL_RUNP(66,67) TAL_RUNP(68,69) TAL_RUNP(70,71) \
+  TAL_RUNP(72,73) TAL_RUNP(74,75) TAL_RUNP(76,77) TAL_RUNP(78,79) \
+  TAL_RUNP(80,81) TAL_RUNP(82,83) TAL_RUNP(84,85) TAL_RUNP(86,87) \
+  TAL_RUNP(88,89) TAL_RUNP(90,91) TAL_RUNP(92,93) TAL_RUNP(94,95)
+#define TAL_RUNP_2 \
+  TAL_RUNP(96,97) TAL_RUNP(98,99) TAL_RUNP(100,101) TAL_RUNP(102,103) \
+  TAL_RUNP(104,105) TAL_RUNP(106,107) TAL_RUNP(108,109) TAL_RUNP(110,111) \
+  TAL_RUNP(112,113) TAL_RUNP(114,115) TAL_RUNP(116,117) TAL_RUNP(118,119) \
+  TAL_RUNP(120,121) TAL_RUNP(122,123) TAL_RUNP(124,125) TAL_RUNP(126,127)
+#define TAL_RUNP_3 \
+  TAL_RUNP(128,129) TAL_RUNP(130,131) TAL_RUNP(132,133) TAL_RUNP(134,135) \
+  TAL_RUNP(136,137) TAL_RUNP(138,139) TAL_RUNP(140,141) TAL_RUNP(142,143) \
+  TAL_RUNP(144,145) TAL_RUNP(146,147) TAL_RUNP(148,149) TAL_RUNP(150,151) \
+  TAL_RUNP(152,153) TAL_RUNP(154,155) TAL_RUNP(156,157) TAL_RUNP(158,159)
+
+#define TAL_RB16(b)                                                                                 \
+  "s"(b[0]), "s"(b[1]), "s"(b[2]), "s"(b[3]), "s"(b[4]), "s"(b[5]), "s"(b[6]), "s"(b[7]), "s"(b[8]), \
+      "s"(b[9]), "s"(b[10]), "s"(b[11]), "s"(b[12]), "s"(b[13]), "s"(b[14]), "s"(b[15])
+#define TAL_RX1 "{v[32:63]}"(X0)
+#define TAL_RX2 TAL_RX1, "{v[64:95]}"(X1)
+#define TAL_RX3 TAL_RX2, "{v[96:127]}"(X2)
+#define TAL_RX4 TAL_RX3, "{v[128:159]}"(X3)
+#define TAL_UNP(...) __VA_ARGS__
+// one inline-asm statement with the NB source tuples appended to its inputs
+#define TAL_RASM(TMPL, OUTS, INS)                                                      \
+  do {                                                                                 \
+    if constexpr (NB == 1) asm volatile(TMPL : TAL_UNP OUTS : TAL_UNP INS, TAL_RX1);   \
+    else if constexpr (NB == 2) asm volatile(TMPL : TAL_UNP OUTS : TAL_UNP INS, TAL_RX2); \
+    else if constexpr (NB == 3) asm volatile(TMPL : TAL_UNP OUTS : TAL_UNP INS, TAL_RX3); \
+    else asm volatile(TMPL : TAL_UNP OUTS : TAL_UNP INS, TAL_RX4);                     \
+  } while (0)
+
+// 16 sources (block J) into v[32 + 32 J ...]: b = per-source byte addresses of the piece
+// (wave-uniform), off = the lane's byte offset in it.  No wait: reg_wait follows all blocks.
+template <int J, bool BF16>
+__device__ __forceinline__ v32f reg_load_block(const uint64_t* b, uint32_t off) {
+  v32f X;
+#define TAL_RLOAD(TM, R) asm volatile(TM : "=&{" R "}"(X) : TAL_RB16(b), "v"(off) : "memory")
+  if constexpr (!BF16) {
+    if constexpr (J == 0) TAL_RLOAD(TAL_RF32_0, "v[32:63]");
+    else if constexpr (J == 1) TAL_RLOAD(TAL_RF32_1, "v[64:95]");
+    else if constexpr (J == 2) TAL_RLOAD(TAL_RF32_2, "v[96:127]");
+    else TAL_RLOAD(TAL_RF32_3, "v[128:159]");
+  } else {  // the packed pair goes to the odd register; reg_wait unpacks it in place
+    if constexpr (J == 0) TAL_RLOAD(TAL_RB16_0, "v[32:63]");
+    else if constexpr (J == 1) TAL_RLOAD(TAL_RB16_1, "v[64:95]");
+    else if constexpr (J == 2) TAL_RLOAD(TAL_RB16_2, "v[96:127]");
+    else TAL_RLOAD(TAL_RB16_3, "v[128:159]");
+  }
+#undef TAL_RLOAD
+  return X;
+}
+
+template <int NB, bool BF16>
+__device__ __forceinline__ void reg_wait(v32f& X0, v32f& X1, v32f& X2, v32f& X3) {
+  if constexpr (!BF16) {
+    if constexpr (NB == 1) asm volatile("s_waitcnt vmcnt(0)" : "+{v[32:63]}"(X0));
+    else if constexpr (NB == 2) asm volatile("s_waitcnt vmcnt(0)" : "+{v[32:63]}"(X0), "+{v[64:95]}"(X1));
+    else if constexpr (NB == 3)
+      asm volatile("s_waitcnt vmcnt(0)" : "+{v[32:63]}"(X0), "+{v[64:95]}"(X1), "+{v[96:127]}"(X2));
+    else
+      asm volatile("s_waitcnt vmcnt(0)"
+                   : "+{v[32:63]}"(X0), "+{v[64:95]}"(X1), "+{v[96:127]}"(X2), "+{v[128:159]}"(X3));
+  } else {  // bf16 pair (lo = element 0) -> two fp32: v[2k] = lo << 16, v[2k+1] = hi & 0xffff0000
+    if constexpr (NB == 1) asm volatile("s_waitcnt vmcnt(0)\n\t" TAL_RUNP_0 : "+{v[32:63]}"(X0));
+    else if constexpr (NB == 2)
+      asm volatile("s_waitcnt vmcnt(0)\n\t" TAL_RUNP_0 TAL_RUNP_1 : "+{v[32:63]}"(X0), "+{v[64:95]}"(X1));
+    else if constexpr (NB == 3)
+      asm volatile("s_waitcnt vmcnt(0)\n\t" TAL_RUNP_0 TAL_RUNP_1 TAL_RUNP_2
+                   : "+{v[32:63]}"(X0), "+{v[64:95]}"(X1), "+{v[96:127]}"(X2));
+    else
+      asm volatile("s_waitcnt vmcnt(0)\n\t" TAL_RUNP_0 TAL_RUNP_1 TAL_RUNP_2 TAL_RUNP_3
+                   : "+{v[32:63]}"(X0), "+{v[64:95]}"(X1), "+{v[96:127]}"(X2), "+{v[128:159]}"(X3));
+  }
+}
+
+// a wave-uniform 64-bit value in an SGPR pair (the uniformity analysis does not see through the
+// per-source address arithmetic; the "s" constraints below need SGPRs)
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// An operand record is one 64-bit word: low dword = fp32 weight, high dword = register offset
+// of its source (2 x slot).  The weight is passed as that SGPR pair with op_sel_hi:[1,0] (both
+// halves of the packed multiply take the low dword); the index is its high dword.
+#define TAL_IDX(r) static_cast<uint32_t>((r) >> 32)
+
+// two rows, four operands each: A / B = this batch's operand records (SGPR tuples), pa / pb =
+// the next batch's addresses, loaded into NA / NB2 by the same asm while it computes (the scalar
+// loads' latency hides under the arithmetic; lgkmcnt is drained at the end, so the compiler
+// sees nothing pending).  The table is padded so a read-ahead past the last batch stays inside.
+typedef uint64_t u64x4 __attribute__((ext_vector_type(4)));
+#define TAL_PAIR_INS                                                                                      \
+  [w0] "s"(A[0]), [w1] "s"(A[1]), [w2] "s"(A[2]), [w3] "s"(A[3]), [v0] "s"(B[0]), [v1] "s"(B[1]),          \
+      [v2] "s"(B[2]), [v3] "s"(B[3]), [i0] "s"(TAL_IDX(A[0])), [i1] "s"(TAL_IDX(A[1])), [i2] "s"(TAL_IDX(A[2])), \
+      [i3] "s"(TAL_IDX(A[3])), [j0] "s"(TAL_IDX(B[0])), [j1] "s"(TAL_IDX(B[1])), [j2] "s"(TAL_IDX(B[2])),   \
+      [j3] "s"(TAL_IDX(B[3])), [pa] "s"(pa), [pb] "s"(pb)
+
+// EXACT: eight indexed multiplies, then the two add chains interleaved (no add reads the add
+// right before it)
+template <int NB>
+__device__ __forceinline__ void reg_pair_exact(v2f_t& ca, v2f_t& cb, const u64x4& A, const u64x4& B, u64x4& NA,
+                                               u64x4& NB2, uint64_t pa, uint64_t pb, const v32f& X0, const v32f& X1,
+                                               const v32f& X2, const v32f& X3) {
+  v2f_t t0, t1, t2, t3, t4, t5, t6, t7;
+  uint32_t m;
+  TAL_RASM("s_load_dwordx8 %[na], %[pa], 0x0\n\t"
+           "s_load_dwordx8 %[nb], %[pb], 0x0\n\t"
+           "s_mov_b32 %[m], m0\n\t"
+           "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
+           "v_pk_mul_f32 %[t0], v[32:33], %[w0] op_sel_hi:[1,0]\n\t"
+           "s_set_gpr_idx_idx %[i1]\n\t"
+           "v_pk_mul_f32 %[t1], v[32:33], %[w1] op_sel_hi:[1,0]\n\t"
+           "s_set_gpr_idx_idx %[i2]\n\t"
+           "v_pk_mul_f32 %[t2], v[32:33], %[w2] op_sel_hi:[1,0]\n\t"
+           "s_set_gpr_idx_idx %[i3]\n\t"
+           "v_pk_mul_f32 %[t3], v[32:33], %[w3] op_sel_hi:[1,0]\n\t"
+           "s_set_gpr_idx_idx %[j0]\n\t"
+           "v_pk_mul_f32 %[t4], v[32:33], %[v0] op_sel_hi:[1,0]\n\t"
+           "s_set_gpr_idx_idx %[j1]\n\t"
+           "v_pk_mul_f32 %[t5], v[32:33], %[v1] op_sel_hi:[1,0]\n\t"
+           "s_set_gpr_idx_idx %[j2]\n\t"
+           "v_pk_mul_f32 %[t6], v[32:33], %[v2] op_sel_hi:[1,0]\n\t"
+           "s_set_gpr_idx_idx %[j3]\n\t"
+           "v_pk_mul_f32 %[t7], v[32:33], %[v3] op_sel_hi:[1,0]\n\t"
+           "s_set_gpr_idx_off\n\t"
+           "s_mov_b32 m0, %[m]\n\t"
+           "v_pk_add_f32 %[ca], %[ca], %[t0]\n\t"
+           "v_pk_add_f32 %[cb], %[cb], %[t4]\n\t"
+           "v_pk_add_f32 %[ca], %[ca], %[t1]\n\t"
+           "v_pk_add_f32 %[cb], %[cb], %[t5]\n\t"
+           "v_pk_add_f32 %[ca], %[ca], %[t2]\n\t"
+           "v_pk_add_f32 %[cb], %[cb], %[t6]\n\t"
+           "v_pk_add_f32 %[ca], %[ca], %[t3]\n\t"
+           "v_pk_add_f32 %[cb], %[cb], %[t7]\n\t"
+           "s_waitcnt lgkmcnt(0)",
+           ([ca] "+v"(ca), [cb] "+v"(cb), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+            [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7), [m] "=&s"(m), [na] "=&s"(NA),
+            [nb] "=&s"(NB2)),
+           (TAL_PAIR_INS));
+}
+
+// FMA: the two fused chains alternate, an index switch between
+template <int NB>
+__device__ __forceinline__ void reg_pair_fma(v2f_t& ca, v2f_t& cb, const u64x4& A, const u64x4& B, u64x4& NA,
+                                             u64x4& NB2, uint64_t pa, uint64_t pb, const v32f& X0, const v32f& X1,
+                                             const v32f& X2, const v32f& X3) {
+  uint32_t m;
+  TAL_RASM("s_load_dwordx8 %[na], %[pa], 0x0\n\t"
+           "s_load_dwordx8 %[nb], %[pb], 0x0\n\t"
+           "s_mov_b32 %[m], m0\n\t"
+           "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
+           "v_pk_fma_f32 %[ca], v[32:33], %[w0], %[ca] op_sel_hi:[1,0,1]\n\t"
+           "s_set_gpr_idx_idx %[j0]\n\t"
+           "v_pk_fma_f32 %[cb], v[32:33], %[v0], %[cb] op_sel_hi:[1,0,1]\n\t"
+           "s_set_gpr_idx_idx %[i1]\n\t"
+           "v_pk_fma_f32 %[ca], v[32:33], %[w1], %[ca] op_sel_hi:[1,0,1]\n\t"
+           "s_set_gpr_idx_idx %[j1]\n\t"
+           "v_pk_fma_f32 %[cb], v[32:33], %[v1], %[cb] op_sel_hi:[1,0,1]\n\t"
+           "s_set_gpr_idx_idx %[i2]\n\t"
+           "v_pk_fma_f32 %[ca], v[32:33], %[w2], %[ca] op_sel_hi:[1,0,1]\n\t"
+           "s_set_gpr_idx_idx %[j2]\n\t"
+           "v_pk_fma_f32 %[cb], v[32:33], %[v2], %[cb] op_sel_hi:[1,0,1]\n\t"
+           "s_set_gpr_idx_idx %[i3]\n\t"
+           "v_pk_fma_f32 %[ca], v[32:33], %[w3], %[ca] op_sel_hi:[1,0,1]\n\t"
+           "s_set_gpr_idx_idx %[j3]\n\t"
+           "v_pk_fma_f32 %[cb], v[32:33], %[v3], %[cb] op_sel_hi:[1,0,1]\n\t"
+           "s_set_gpr_idx_off\n\t"
+           "s_mov_b32 m0, %[m]\n\t"
+           "s_waitcnt lgkmcnt(0)",
+           ([ca] "+v"(ca), [cb] "+v"(cb), [m] "=&s"(m), [na] "=&s"(NA), [nb] "=&s"(NB2)), (TAL_PAIR_INS));
+}
+
+// one operand of one row
+template <int NB, bool EXACT>
+__device__ __forceinline__ void reg_one(v2f_t& ca, uint64_t a0, const v32f& X0, const v32f& X1, const v32f& X2,
+                                        const v32f& X3) {
+  uint32_t m;
+  if constexpr (EXACT) {
+    v2f_t t0;
+    TAL_RASM("s_mov_b32 %[m], m0\n\t"
+             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
+             "v_pk_mul_f32 %[t0], v[32:33], %[w0] op_sel_hi:[1,0]\n\t"
+             "s_set_gpr_idx_off\n\t"
+             "s_mov_b32 m0, %[m]\n\t"
+             "v_pk_add_f32 %[ca], %[ca], %[t0]\n\t"
+             "s_nop 0",
+             ([ca] "+v"(ca), [t0] "=&v"(t0), [m] "=&s"(m)), ([w0] "s"(a0), [i0] "s"(TAL_IDX(a0))));
+  } else {
+    TAL_RASM("s_mov_b32 %[m], m0\n\t"
+             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
+             "v_pk_fma_f32 %[ca], v[32:33], %[w0], %[ca] op_sel_hi:[1,0,1]\n\t"
+             "s_set_gpr_idx_off\n\t"
+             "s_mov_b32 m0, %[m]",
+             ([ca] "+v"(ca), [m] "=&s"(m)), ([w0] "s"(a0), [i0] "s"(TAL_IDX(a0))));
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void reg_store(T* pout, int64_t ld_out, int32_t row, int64_t col, int64_t n, v2f_t acc) {
+  if (col >= n) return;
+  const int64_t e = static_cast<int64_t>(row) * ld_out + col;
+  if constexpr (kIsBf16<T>) {
+    uint32_t q = cvt_bf16x2(acc.x, acc.y);
+    if (__builtin_isunordered(acc.x, acc.y)) q = store_bf16x2(acc.x, acc.y);
+    if (col + 1 < n) __builtin_nontemporal_store(q, reinterpret_cast<uint32_t*>(pout + e));
+    else pout[e] = static_cast<uint16_t>(q & 0xffffu);
+  } else {
+    if (col + 1 < n) __builtin_nontemporal_store(acc, reinterpret_cast<v2f_t*>(pout + e));
+    else pout[e] = acc.x;
+  }
+}
+
+// Table (int32, device): groups [G][4] {first source, sources, first row, rows}, then source
+// rows, row records [R][4] {out row, operands, first operand, 0} (a group's rows in pair order),
+// then operand records [nnz] 64-bit {fp32 weight, 2 x slot}.
+template <int NB, typename T, bool EXACT>
+__global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, int64_t ld_in, T* __restrict__ pout,
+                                                   int64_t ld_out, int64_t n, const int32_t* __restrict__ table,
+                                                   int32_t n_groups, int32_t off_src, int32_t off_rows,
+                                                   int32_t off_ops, int32_t n_pieces, int32_t waves_per_label) {
+  constexpr bool kB = kIsBf16<T>;
+  constexpr int kEs = kB ? 2 : 4;
+  const ConstI32 tab = (ConstI32)table;
+  const ConstU64 ops = (ConstU64)(table + off_ops);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int label = static_cast<int>(blockIdx.x & 7u);
+  const int wx = static_cast<int>(blockIdx.x >> 3) * 4 + wave;
+  const int pieces_l = n_pieces > label ? (n_pieces - 1 - label) / 8 + 1 : 0;
+  const int items = pieces_l * n_groups;
+  int q = wx / n_groups, g = wx - (wx / n_groups) * n_groups;
+  const int dq = waves_per_label / n_groups, dg = waves_per_label - dq * n_groups;
+  v32f X0, X1, X2, X3;
+  for (int s = wx; s < items; s += waves_per_label) {
+    const int piece = q * 8 + label;
+    const int s0 = tab[4 * g], ns = tab[4 * g + 1], r0 = tab[4 * g + 2], nr = tab[4 * g + 3];
+    const int64_t col = static_cast<int64_t>(piece) * kRegPiece + 2 * lane;
+    const uint32_t loff = col < n ? static_cast<uint32_t>(2 * lane * kEs) : 0u;  // past n: the piece's start
+    const uint64_t pbase = reinterpret_cast<uint64_t>(pin) + static_cast<uint64_t>(piece) * (kRegPiece * kEs);
+    const uint64_t pitch = static_cast<uint64_t>(ld_in) * kEs;
+    uint64_t b[16];
+#define TAL_RBASES(J)                                                                            \
+    _Pragma("unroll") for (int k = 0; k < 16; ++k) {                                             \
+      const int sl = (J) * 16 + k;                                                               \
+      b[k] = uniform64(pbase + static_cast<uint64_t>(static_cast<uint32_t>(tab[off_src + s0 + (sl < ns ? sl : 0)])) * pitch); \
+    }
+    TAL_RBASES(0)
+    X0 = reg_load_block<0, kB>(b, loff);
+    if constexpr (NB > 1) { TAL_RBASES(1) X1 = reg_load_block<1, kB>(b, loff); }
+    if constexpr (NB > 2) { TAL_RBASES(2) X2 = reg_load_block<2, kB>(b, loff); }
+    if constexpr (NB > 3) { TAL_RBASES(3) X3 = reg_load_block<3, kB>(b, loff); }
+#undef TAL_RBASES
+    reg_wait<NB, kB>(X0, X1, X2, X3);
+    int r = 0;
+    for (; r + 1 < nr; r += 2) {
+      const int ra = 4 * (off_rows / 4 + r0 + r);  // (off_rows is a multiple of 4)
+      const int oa_row = tab[ra], na = tab[ra + 1], qa = tab[ra + 2];
+      const int ob_row = tab[ra + 4], nb = tab[ra + 5], qb = tab[ra + 6];
+      v2f_t ca = {-0.f, -0.f}, cb = {-0.f, -0.f};
+      const int common = min(na, nb) / 4;
+      if (common > 0) {
+        u64x4 A = {ops[qa], ops[qa + 1], ops[qa + 2], ops[qa + 3]};
+        u64x4 B = {ops[qb], ops[qb + 1], ops[qb + 2], ops[qb + 3]};
+        const uint64_t opsb = uniform64(reinterpret_cast<uint64_t>(table + off_ops));
+        for (int k = 0; k < common; ++k) {
+          u64x4 NA, NB2;
+          const uint64_t pa = opsb + 8ull * static_cast<uint32_t>(qa + 4 * k + 4);
+          const uint64_t pb = opsb + 8ull * static_cast<uint32_t>(qb + 4 * k + 4);
+          if constexpr (EXACT) reg_pair_exact<NB>(ca, cb, A, B, NA, NB2, pa, pb, X0, X1, X2, X3);
+          else reg_pair_fma<NB>(ca, cb, A, B, NA, NB2, pa, pb, X0, X1, X2, X3);
+          A = NA;
+          B = NB2;
+        }
+      }
+      for (int k = 4 * common; k < na; ++k) reg_one<NB, EXACT>(ca, ops[qa + k], X0, X1, X2, X3);
+      for (int k = 4 * common; k < nb; ++k) reg_one<NB, EXACT>(cb, ops[qb + k], X0, X1, X2, X3);
+      reg_store<T>(pout, ld_out, oa_row, col, n, ca);
+      reg_store<T>(pout, ld_out, ob_row, col, n, cb);
+    }
+    if (r < nr) {
+      const int ra = 4 * (off_rows / 4 + r0 + r);
+      const int oa_row = tab[ra], na = tab[ra + 1], qa = tab[ra + 2];
+      v2f_t ca = {-0.f, -0.f};
+      for (int k = 0; k < na; ++k) reg_one<NB, EXACT>(ca, ops[qa + k], X0, X1, X2, X3);
+      reg_store<T>(pout, ld_out, oa_row, col, n, ca);
+    }
+    q += dq;
+    g += dg;
+    if (g >= n_groups) {
+      g -= n_groups;
+      ++q;
+    }
+  }
+}
+
+template <int NB, typename T, bool EXACT>
+int32_t launch_round_reg_nb(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n, const int32_t* table,
+                            int32_t n_groups, int32_t off_src, int32_t off_rows, int32_t off_ops, int32_t n_pieces,
+                            hipStream_t s) {
+  static int blocks_per_cu = -1, n_cu = 0;  // per instantiation, once per process
+  if (blocks_per_cu < 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, k_round_reg<NB, T, EXACT>, 256, 0) != hipSuccess)
+      return fail(TAL_ERR_HIP, "register round: occupancy query failed");
+    blocks_per_cu = std::max(1, blocks_per_cu);
+  }
+  // persistent: every resident wave, a multiple of 8 blocks (XCD labels)
+  const int grid = std::max(8, n_cu * blocks_per_cu / 8 * 8);
+  k_round_reg<NB, T, EXACT><<<grid, 256, 0, s>>>(pin, ld_in, pout, ld_out, n, table, n_groups, off_src, off_rows,
+                                                 off_ops, n_pieces, grid / 8 * 4);
+  return check_launch("register round kernel");
+}
+
+template <typename T, bool EXACT>
+int32_t launch_round_reg(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n, const int32_t* table,
+                         int32_t n_groups, int32_t off_src, int32_t off_rows, int32_t off_ops, int32_t max_src,
+                         hipStream_t s) {
+  const int64_t n_pieces = (n + kRegPiece - 1) / kRegPiece;
+  if (n_pieces * n_groups >= (1LL << 31)) return fail(TAL_ERR_INVALID, "register round: too many items");
+  const int np = static_cast<int>(n_pieces);
+  if (max_src <= 16) return launch_round_reg_nb<1, T, EXACT>(pin, ld_in, pout, ld_out, n, table, n_groups, off_src, off_rows, off_ops, np, s);
+  if (max_src <= 32) return launch_round_reg_nb<2, T, EXACT>(pin, ld_in, pout, ld_out, n, table, n_groups, off_src, off_rows, off_ops, np, s);
+  if (max_src <= 48) return launch_round_reg_nb<3, T, EXACT>(pin, ld_in, pout, ld_out, n, table, n_groups, off_src, off_rows, off_ops, np, s);
+  return launch_round_reg_nb<4, T, EXACT>(pin, ld_in, pout, ld_out, n, table, n_groups, off_src, off_rows, off_ops, np, s);
+}
+
 template <int NT, bool EXACT>
 int32_t launch_round_stream_nt(const float* pin, int64_t ld_in, float* pout, int64_t ld_out, int64_t n4,
                                const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
@@ -3026,6 +3432,34 @@ int32_t tal_agg_round_clique_f32(const float* pool_in, int64_t ld_in, float* poo
   return mode == TAL_MODE_EXACT
              ? launch_round_clique<true>(pool_in, ld_in, pool_out, ld_out, n, table_dev, n_cliques, mmax, s)
              : launch_round_clique<false>(pool_in, ld_in, pool_out, ld_out, n, table_dev, n_cliques, mmax, s);
+}
+
+int32_t tal_agg_round_reg(const void* pool_in, int64_t ld_in, void* pool_out, int64_t ld_out, int64_t n,
+                          int32_t bf16, const int32_t* table_dev, int32_t n_groups, int32_t off_src,
+                          int32_t off_rows, int32_t off_ops, int32_t max_src, int32_t mode, void* stream) {
+  if (!pool_in || !pool_out || !table_dev) return fail(TAL_ERR_INVALID, "tal_agg_round_reg: null pointer");
+  if (pool_in == pool_out)
+    return fail(TAL_ERR_INVALID, "tal_agg_round_reg: the register round runs out of place (snapshot semantics)");
+  const int64_t n2 = n + (n & 1);  // the last lane of an odd row reads one element of padding
+  if (n < 0 || ld_in < n2 || ld_out < n2 || ld_in % 2 || ld_out % 2)
+    return fail(TAL_ERR_INVALID, "tal_agg_round_reg: need even ld >= n rounded up to even");
+  if (n_groups < 0 || max_src < 1 || max_src > kRegMaxSrc || off_src < 4 * n_groups || off_rows % 4 || off_ops % 2 ||
+      off_rows < off_src || off_ops < off_rows)
+    return fail(TAL_ERR_INVALID, "tal_agg_round_reg: bad table layout");
+  if (bf16 && mode == TAL_MODE_EXACT)
+    return fail(TAL_ERR_INVALID, "tal_agg_round_reg: bf16 rounds take FMA mode here (EXACT: tal_agg_round_bf16)");
+  if (bf16 ? !aligned4(pool_in) || !aligned4(pool_out) : !aligned8(pool_in) || !aligned8(pool_out))
+    return fail(TAL_ERR_INVALID, "tal_agg_round_reg: pools must be aligned to 2 elements");
+  if (n == 0 || n_groups == 0) { g_err.clear(); return TAL_OK; }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (bf16)
+    return launch_round_reg<uint16_t, false>(static_cast<const uint16_t*>(pool_in), ld_in, static_cast<uint16_t*>(pool_out),
+                                             ld_out, n, table_dev, n_groups, off_src, off_rows, off_ops, max_src, s);
+  if (mode == TAL_MODE_EXACT)
+    return launch_round_reg<float, true>(static_cast<const float*>(pool_in), ld_in, static_cast<float*>(pool_out), ld_out,
+                                         n, table_dev, n_groups, off_src, off_rows, off_ops, max_src, s);
+  return launch_round_reg<float, false>(static_cast<const float*>(pool_in), ld_in, static_cast<float*>(pool_out), ld_out,
+                                        n, table_dev, n_groups, off_src, off_rows, off_ops, max_src, s);
 }
 
 int32_t tal_agg_bf16(const uint16_t* const* x_host, const double* w_host, int32_t m, uint16_t* out,

@@ -332,6 +332,148 @@ def build_clique_plan(row_ptr, col, w, out_row, min_rows: int = CLIQUE_MIN_ROWS,
                       full=build_plan(row_ptr, col, w, out_row, dense=0), rows=len(out_row), rest_rows=rest)
 
 
+REG_MAX_SRC = 64   # sources per register group (v[32:160): 64 x 2 fp32 per lane)
+REG_WINDOW = 64    # rows considered when growing a group
+
+
+@dataclass
+class RegPlan:
+    """A round as register-resident source groups (K3r, tal_agg_round_reg): rows grouped so that
+    each group's operands are <= max_src distinct sources.  `full` is a sparse plan over all
+    rows for the int64 segment (and bf16 EXACT, which K3r does not take)."""
+    table: np.ndarray
+    n_groups: int
+    off_src: int
+    off_rows: int
+    off_ops: int
+    max_src: int
+    group_sources: int   # sum over groups of their sources (HBM / L2 reads per column)
+    full: RoundPlan
+    rows: int
+    device: Optional[torch.Tensor] = None
+    tuned_ms: Optional[float] = None
+    candidates: Optional[list] = None
+    spec: Optional[dict] = None
+
+    @property
+    def info(self) -> RoundPlanInfo:
+        return self.full.info
+
+    @property
+    def single_group(self) -> bool:
+        return False  # groups read other groups' outputs' rows: never in place
+
+    def staged_rows(self) -> int:
+        """Distinct sources read per column: every source once (the groups sharing a source
+        are served by L2 on the XCD their piece runs on)."""
+        return int(len(np.unique(self.table[self.off_src: self.off_rows])))
+
+    def to(self, device) -> "RegPlan":
+        self.device = torch.from_numpy(self.table).to(device)
+        self.full.to(device)
+        return self
+
+
+def reg_groups(row_ptr, col, max_src: int = REG_MAX_SRC, window: int = REG_WINDOW):
+    """Rows grouped greedily: a group starts at the first unassigned row and repeatedly takes,
+    among the next `window` unassigned rows, the one adding the fewest new sources while the
+    union stays <= max_src.  Returns [(rows, sources ascending)]."""
+    n = len(row_ptr) - 1
+    ops_ = [set(col[row_ptr[r]: row_ptr[r + 1]].tolist()) for r in range(n)]
+    left = list(range(n))
+    groups = []
+    while left:
+        r0 = left.pop(0)
+        if len(ops_[r0]) > max_src:
+            raise ValueError(f"row {r0} has {len(ops_[r0])} distinct sources > {max_src}")
+        cur, src = [r0], set(ops_[r0])
+        while True:
+            best = None
+            for r in left[:window]:
+                add = len(ops_[r] - src)
+                if len(src) + add <= max_src and (best is None or add < best[0]):
+                    best = (add, r)
+            if best is None:
+                break
+            left.remove(best[1])
+            cur.append(best[1])
+            src |= ops_[best[1]]
+        groups.append((cur, sorted(src)))
+    return groups
+
+
+def build_reg_plan(row_ptr, col, w, out_row, max_src: int = REG_MAX_SRC) -> Optional[RegPlan]:
+    """RegPlan of a round, or None when a row has more than max_src distinct sources.  Inside a
+    group the rows are ordered by operand count (descending) so the kernel's row pairs share
+    most of their batches."""
+    row_ptr, col, w, out_row = _csr(row_ptr, col, w, out_row)
+    try:
+        groups = reg_groups(row_ptr, col, max_src)
+    except ValueError:
+        return None
+    G = len(groups)
+    src_list, row_recs, op_recs = [], [], []
+    grp = np.zeros((G, 4), np.int32)
+    for g, (rows, srcs) in enumerate(groups):
+        slot = {s_: k for k, s_ in enumerate(srcs)}
+        rows = sorted(rows, key=lambda r: -(row_ptr[r + 1] - row_ptr[r]))
+        grp[g] = (len(src_list), len(srcs), len(row_recs), len(rows))
+        src_list.extend(srcs)
+        for r in rows:
+            q0, q1 = int(row_ptr[r]), int(row_ptr[r + 1])
+            row_recs.append((int(out_row[r]), q1 - q0, len(op_recs), 0))
+            w32 = w[q0:q1].astype(np.float32).view(np.uint32)
+            for k in range(q0, q1):
+                op_recs.append((int(w32[k - q0]), 2 * slot[int(col[k])]))
+    off_src = 4 * G
+    off_rows = (off_src + len(src_list) + 3) // 4 * 4
+    off_ops = off_rows + 4 * len(row_recs)
+    words = off_ops + 2 * (len(op_recs) + 8)  # + 8 records of read-ahead padding
+    table = np.zeros(words, np.int32)
+    table[:off_src] = grp.reshape(-1)
+    table[off_src: off_src + len(src_list)] = src_list
+    table[off_rows: off_ops] = np.asarray(row_recs, np.int32).reshape(-1)
+    if op_recs:
+        table[off_ops: off_ops + 2 * len(op_recs)] = np.asarray(op_recs, np.uint32).view(np.int32).reshape(-1)
+    return RegPlan(table=table, n_groups=G, off_src=off_src, off_rows=off_rows, off_ops=off_ops,
+                   max_src=max(len(s_) for _, s_ in groups), group_sources=len(src_list),
+                   full=build_plan(row_ptr, col, w, out_row, dense=0), rows=len(out_row))
+
+
+def _round_reg(pool_in, pool_out, plan: RegPlan, n, dtype, mode, stream):
+    _require_gpu(pool_in, "pool_in", dtype)
+    _require_gpu(pool_out, "pool_out", dtype)
+    if pool_in.dim() != 2 or pool_out.dim() != 2:
+        raise ValueError("pools must be 2-D [models, ld]")
+    if pool_in.device != pool_out.device:
+        raise ValueError("pools on different devices")
+    if pool_in.data_ptr() == pool_out.data_ptr():
+        raise ValueError("a register round runs out of place (snapshot semantics)")
+    n = pool_in.shape[1] if n is None else int(n)
+    bf16 = dtype == torch.bfloat16
+    esz = pool_in.element_size()
+    pad = n + (n & 1)
+    if (bf16 and mode == MODE_EXACT) or pool_in.stride(0) % 2 or pool_out.stride(0) % 2 \
+            or pool_in.shape[1] < pad or pool_out.shape[1] < pad \
+            or (pool_in.data_ptr() | pool_out.data_ptr()) % (2 * esz):
+        # K3r reads and writes 2-element pairs and runs bf16 in FMA mode only: other pools and
+        # bf16 EXACT take the full plan
+        return _round(pool_in, pool_out, plan.full, n, dtype, mode, stream)
+    if plan.device is None or plan.device.device != pool_in.device:
+        plan.to(pool_in.device)
+    t = plan.table
+    if t[plan.off_src: plan.off_rows].max(initial=-1) >= pool_in.shape[0]:
+        raise ValueError("plan reads a pool row beyond pool_in")
+    if t[plan.off_rows: plan.off_ops].reshape(-1, 4)[:, 0].max(initial=-1) >= pool_out.shape[0]:
+        raise ValueError("plan writes a pool row beyond pool_out")
+    L = _lib.load()
+    check(L.tal_agg_round_reg(ctypes.c_void_p(pool_in.data_ptr()), pool_in.stride(0),
+                              ctypes.c_void_p(pool_out.data_ptr()), pool_out.stride(0), n, int(bf16),
+                              ctypes.c_void_p(plan.device.data_ptr()), plan.n_groups, plan.off_src,
+                              plan.off_rows, plan.off_ops, plan.max_src, int(mode), _stream(pool_in.device, stream)))
+    return pool_out
+
+
 def _sub_csr(row_ptr, col, w, out_row, rows):
     """The CSR of a subset of a round's rows."""
     rp = np.concatenate([[0], np.cumsum([row_ptr[r + 1] - row_ptr[r] for r in rows])]).astype(np.int32)
@@ -420,6 +562,11 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
                 cp.rest = tune_plan(r_rp, r_col, r_w, r_out, pool_in, pool_out, n=n, reps=reps, mode=mode)
                 cp.spec["rest"] = cp.rest.spec
             cands.append((("clique", cp.n_cliques, cp.staged_rows(), 0, cp.mmax, 0), cp))
+    if not bf16 or mode == MODE_FMA:  # register-resident groups (K3r; bf16 in FMA mode only)
+        rp = build_reg_plan(row_ptr, col, w, out_row)
+        if rp is not None:
+            rp.spec = dict(reg=1)
+            cands.append((("reg", rp.n_groups, rp.group_sources, 0, rp.max_src, 0), rp))
     if not cands:
         return build_plan(row_ptr, col, w, out_row, dense=0)
     if len(cands) == 1:
@@ -460,6 +607,12 @@ def plan_from_spec(row_ptr, col, w, out_row, spec: dict) -> RoundPlan:
             raise ValueError("plan spec asks for clique blocks but the round has none")
         p.spec = dict(spec)
         return p
+    if spec.get("reg"):
+        p = build_reg_plan(row_ptr, col, w, out_row, int(spec.get("max_src", REG_MAX_SRC)))
+        if p is None:
+            raise ValueError("plan spec asks for register groups but a row has too many sources")
+        p.spec = dict(spec)
+        return p
     if "stream_rows" in spec:
         p = build_stream_plan(row_ptr, col, w, out_row, int(spec["stream_rows"]), int(spec["stream_src"]))
     else:
@@ -488,6 +641,8 @@ def round_kernel_name(plan) -> str:
     launch_round_vec); clique plans name the K3c kernel (their rest rows run a second one)."""
     if isinstance(plan, CliquePlan):
         return "k_round_clique"
+    if isinstance(plan, RegPlan):
+        return "k_round_reg"
     info = plan.info if isinstance(plan, RoundPlan) else plan
     if info.stream_cs:
         return "k_round_stream"
@@ -522,6 +677,8 @@ def round_f32(pool_in: torch.Tensor, pool_out: torch.Tensor, plan, n: Optional[i
     its clique blocks with K3c and its other rows with their regular plan (out of place)."""
     if isinstance(plan, CliquePlan):
         return _round_clique(pool_in, pool_out, plan, n, mode, stream)
+    if isinstance(plan, RegPlan):
+        return _round_reg(pool_in, pool_out, plan, n, torch.float32, mode, stream)
     return _round(pool_in, pool_out, plan, n, torch.float32, mode, stream)
 
 
@@ -559,7 +716,7 @@ def _round_clique(pool_in, pool_out, plan: CliquePlan, n, mode, stream):
 
 def round_i64(pool_in: torch.Tensor, pool_out: torch.Tensor, plan: RoundPlan, n: Optional[int] = None,
               stream=None) -> torch.Tensor:
-    if isinstance(plan, CliquePlan):
+    if isinstance(plan, (CliquePlan, RegPlan)):
         plan = plan.full
     return _round(pool_in, pool_out, plan, n, torch.int64, MODE_EXACT, stream)
 
@@ -569,6 +726,8 @@ def round_bf16(pool_in: torch.Tensor, pool_out: torch.Tensor, plan: RoundPlan, n
     """K3 on [models, ld] bf16 pools (sparse or narrow plans; modes as agg_bf16)."""
     if isinstance(plan, CliquePlan):
         plan = plan.full
+    if isinstance(plan, RegPlan):
+        return _round_reg(pool_in, pool_out, plan, n, torch.bfloat16, mode, stream)
     return _round(pool_in, pool_out, plan, n, torch.bfloat16, mode, stream)
 
 
