@@ -76,7 +76,8 @@ def parse():
                         "with softmax(10 x degree centrality): per-operand weights")
     p.add_argument("--halo-transport", default="device", choices=["device", "cabi"],
                    help="N > 1, halo exchange over nccl: torch.distributed's RCCL (device) or the "
-                        "library's own communicator and gather kernel (cabi, include/tal_agg.h)")
+                        "library's own communicator and gather kernel (cabi, include/tal_agg.h; "
+                        "experimental: not yet run across GPUs)")
     p.add_argument("--exchange", default="auto", choices=["auto", "halo", "transpose"],
                    help="N > 1: neighbor models by RCCL P2P (halo) or column blocks by all-to-all "
                         "(transpose); auto = fewer link bytes (transposed.choose_exchange)")

@@ -98,3 +98,57 @@ def test_sharded_round_through_cabi_transport(cuda, tmp_path):
         sr.comm.close()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("graph,world,dtype", [("regular", 2, "f32"), ("sbm256", 8, "f32"), ("barbell60", 8, "bf16"),
+                                               ("ring", 2, "bf16")])
+def test_virtual_ranks_messages_from_cabi_pack(cuda, graph, world, dtype):
+    """The multi-rank 'cabi' transport's messages without a second GPU: `world` ShardedRounds
+    in one process, each peer's message built exactly as post_exchange_cabi builds it (the
+    library's gather kernel into the HaloPacker buffers, or the consecutive-row view) and copied
+    into the receiver's halo block, two rounds, bitwise the oracle.  (RCCL refuses two ranks on
+    one GPU, so the exchange itself runs across ranks only on the driver's node.)"""
+    from test_gpu_distributed import _get_rows, _graph, _put_row, _seg_setup
+
+    from oracle import reference_alg as ra
+    from topology_aware_learning_amd import ops
+    from topology_aware_learning_amd.distributed import ShardedRound, recv_range
+
+    g = _graph(graph)
+    n = g.number_of_nodes()
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(n)]
+    ws = [ra.unweighted_weights(len(o)) for o in orders]
+    layout, pool, ipool = _seg_setup(dtype, n, 2)
+    srs = [ShardedRound(layout, orders, ws, r, world, cuda, exchange=lambda sr: []) for r in range(world)]
+    for sr in srs:
+        for k, gid in enumerate(sr.spec.own):
+            _put_row(sr.pool_a, k, dtype, pool[gid], ipool[gid], cuda)
+    packed = 0
+    rp, col, w = ra.round_csr(orders, ws)
+    ref, iref = pool, ipool
+    for _ in range(2):
+        for sr in srs:  # post_exchange_cabi's message construction, peer by peer
+            for peer in sr.spec.recv:
+                r0, r1 = recv_range(sr.spec, peer)
+                src = srs[peer]
+                for si, (_, t, _) in enumerate(sr.pool_a.segments()):
+                    ts = src.pool_a.segments()[si][1]
+                    pk = src.packers[si]
+                    if sr.spec.rank in pk.idx32:
+                        msg = HaloComm.pack(ts, pk.idx32[sr.spec.rank], pk.bufs[sr.spec.rank])
+                        packed += 1
+                    else:
+                        rows = src.spec.send[sr.spec.rank]
+                        msg = ts[rows[0]: rows[0] + len(rows)]
+                    t[r0:r1].copy_(msg)
+        for sr in srs:
+            sr.step()
+        ref = (oracle.round_f32(ref, rp, col, w, np.arange(n)) if dtype == "f32"
+               else oracle.round_bf16(ref, rp, col, w, np.arange(n)))
+        iref = oracle.round_i64(iref, rp, col, w, np.arange(n))
+    torch.cuda.synchronize()
+    assert packed > 0 or graph == "ring"
+    for sr in srs:
+        got = _get_rows(sr.own_rows(), len(sr.spec.own), dtype)
+        assert np.array_equal(got, ref[sr.spec.own].view(got.dtype))
+        assert np.array_equal(sr.own_rows().i64[: len(sr.spec.own), :1].cpu().numpy(), iref[sr.spec.own])

@@ -634,3 +634,28 @@ def test_reg_plan_table_layout():
                 assert wbits == np.float32(ws[r][k]).view(np.uint32)
     assert sorted(seen) == list(range(len(orders)))
     assert ops.build_reg_plan(row_ptr, col, w, out_rows, max_src=8) is None  # a row has 9+ sources
+
+
+def test_select_pool_pair_keeps_first_unless_clearly_faster():
+    """Placement calibration (arena.select_pool_pair): a pair is chosen by its best-of-two round
+    trip; the first two allocations stay unless another pair beats them by more than 2 % (on
+    a VALU-bound round all placements run alike and the minimum is noise)."""
+    from topology_aware_learning_amd.arena import select_pool_pair
+
+    def run(dest_ms, noise=0.0):
+        made = iter(range(len(dest_ms)))
+        calls = []
+
+        def score(a, b):
+            calls.append((a, b))
+            return dest_ms[b] * (1 + noise * (len(calls) % 3 - 1))
+
+        a, b, rep = select_pool_pair(lambda: next(made), score, len(dest_ms))
+        return (a, b), rep
+
+    # pools 2 and 3 write 20 % faster: kept
+    pair, rep = run([2.4, 2.4, 2.0, 2.0, 2.4, 2.4])
+    assert set(pair) == {2, 3} and rep["first_pair_ms"] == 2.4 and rep["chosen_pair_ms"] == 2.0
+    # all alike within 1 % (noise): the first two stay
+    pair, _ = run([4.20, 4.21, 4.17, 4.18, 4.19, 4.22], noise=0.004)
+    assert pair == (0, 1)

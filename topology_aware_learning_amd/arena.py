@@ -341,8 +341,9 @@ def select_pool_pair(make_pool: Callable[[], "ModelPool"], score: Callable[["Mod
     once, times a round INTO each (`score(src, dst)`, src = the next pool), then every ordered
     pair among the three fastest destinations, keeps the pair with the fastest round trip (the
     double-buffered round runs a -> b and b -> a in turn; the first two allocations are a
-    candidate pair as well) and frees the others: at most trials + 8 timed rounds instead of
-    every ordered pair.  Returns (a, b, report); report["first_pair_ms"] is
+    candidate pair as well, and are kept unless another pair is more than 2 % faster; pairs are
+    timed twice, interleaved, best of two) and frees the others: at most trials + 16 timed
+    rounds instead of every ordered pair.  Returns (a, b, report); report["first_pair_ms"] is
     what the first two allocations run (both directions)."""
     pools = [make_pool() for _ in range(max(2, trials))]
     k = len(pools)
@@ -354,10 +355,18 @@ def select_pool_pair(make_pool: Callable[[], "ModelPool"], score: Callable[["Mod
     top = sorted(order[:3])
     pairs = sorted({(i, j) for i in top for j in top if i < j} | {(0, 1)})  # the first two allocations too
     pair_ms = {}
-    for i, j in pairs:
-        pair_ms[(i, j)] = float(score(pools[i], pools[j]))
-        pair_ms[(j, i)] = float(score(pools[j], pools[i]))
+    for _ in range(2):  # two passes, interleaved: the lower of two times per direction
+        for i, j in pairs:
+            for a, b in ((i, j), (j, i)):
+                t = float(score(pools[a], pools[b]))
+                pair_ms[(a, b)] = min(t, pair_ms.get((a, b), t))
     best = min(pairs, key=lambda q: pair_ms[q] + pair_ms[q[::-1]])
+    # keep the first two allocations unless another pair is clearly faster: on a vector-ALU-bound
+    # round every placement runs alike and the minimum is noise (config 4 once kept a pair
+    # slower than the first)
+    rt = {q: pair_ms[q] + pair_ms[q[::-1]] for q in pairs}
+    if rt[best] > 0.98 * rt[(0, 1)]:
+        best = (0, 1)
     a, b = pools[best[0]], pools[best[1]]
     first = (pair_ms[(0, 1)] + pair_ms[(1, 0)]) / 2
     report = dict(pools=k, dest_ms=[round(v, 3) for v in ms], chosen=list(best),

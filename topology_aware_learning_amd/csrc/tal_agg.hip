@@ -2264,7 +2264,7 @@ __global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, in
 #define TAL_RBASES(J)                                                                            \
     _Pragma("unroll") for (int k = 0; k < 16; ++k) {                                             \
       const int sl = (J) * 16 + k;                                                               \
-      b[k] = uniform64(pbase + static_cast<uint64_t>(static_cast<uint32_t>(tab[off_src + s0 + (sl < ns ? sl : 0)])) * pitch); \
+      b[k] = pbase + static_cast<uint64_t>(static_cast<uint32_t>(tab[off_src + s0 + (sl < ns ? sl : 0)])) * pitch; \
     }
     TAL_RBASES(0)
     X0 = reg_load_block<0, kB>(b, loff);

@@ -278,8 +278,10 @@ class ShardedRound:
         self.group = group
         # exchange(self) -> requests; default: RCCL/gloo P2P.  Tests may pass an in-process copy.
         # transport "host": the exchange is staged through host memory (gloo rehearsal runs);
-        # "cabi": the library's own RCCL communicator and gather kernel (comm.HaloComm) on a
-        # side stream, the unique id broadcast through the torch.distributed group
+        # "cabi" (experimental: its RCCL exchange has run with one rank only - RCCL refuses two
+        # ranks on one GPU - while its messages are tested across virtual ranks,
+        # tests/test_gpu_comm.py): the library's own RCCL communicator and gather kernel
+        # (comm.HaloComm) on a side stream, the unique id broadcast through the torch.distributed group
         if transport not in ("device", "host", "cabi"):
             raise ValueError(f"unknown transport {transport!r}")
         self.transport = transport
