@@ -96,7 +96,7 @@ def test_reg_round_groups_use_every_register_block():
 def test_reg_round_each_block_count(cuda, cap):
     """The same round built with groups of <= cap sources (NB = cap / 16 register blocks) is
     bitwise the oracle for each kernel instantiation."""
-    orders, ws, row_ptr, col, w = _csr(_GRAPHS["regular40"]())
+    orders, ws, row_ptr, col, w = _csr(_GRAPHS["regular40" if cap < 64 else "sbm64"]())
     rows = len(orders)
     out_rows = np.arange(rows, dtype=np.int32)
     plan = ops.build_reg_plan(row_ptr, col, w, out_rows, max_src=cap)
