@@ -2266,16 +2266,33 @@ __global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, in
       const int sl = (J) * 16 + k;                                                               \
       b[k] = pbase + static_cast<uint64_t>(static_cast<uint32_t>(tab[off_src + s0 + (sl < ns ? sl : 0)])) * pitch; \
     }
+#ifdef TAL_PROBE_REG_NOLOAD  // A/B probe: sources loaded for a wave's first item only
+    if (s == wx) {
+#endif
     TAL_RBASES(0)
     X0 = reg_load_block<0, kB>(b, loff);
     if constexpr (NB > 1) { TAL_RBASES(1) X1 = reg_load_block<1, kB>(b, loff); }
     if constexpr (NB > 2) { TAL_RBASES(2) X2 = reg_load_block<2, kB>(b, loff); }
     if constexpr (NB > 3) { TAL_RBASES(3) X3 = reg_load_block<3, kB>(b, loff); }
+#ifdef TAL_PROBE_REG_NOLOAD
+    }
+#endif
 #undef TAL_RBASES
     reg_wait<NB, kB>(X0, X1, X2, X3);
+#ifdef TAL_PROBE_REG_HOTSQC  // A/B probe: every item walks group 0's row and operand tables
+    const int g_rows = 0;
+#else
+    const int g_rows = g;
+#endif
+    const int r0t = tab[4 * g_rows + 2], nrt = tab[4 * g_rows + 3];
+    (void)r0;
+    (void)nr;
     int r = 0;
-    for (; r + 1 < nr; r += 2) {
-      const int ra = 4 * (off_rows / 4 + r0 + r);  // (off_rows is a multiple of 4)
+#ifdef TAL_PROBE_REG_NOCOMP  // A/B probe: the stores without the row arithmetic
+    for (; r < nrt; ++r) reg_store<T>(pout, ld_out, tab[4 * (off_rows / 4 + r0t + r)], col, n, v2f_t{0.f, 0.f});
+#endif
+    for (; r + 1 < nrt; r += 2) {
+      const int ra = 4 * (off_rows / 4 + r0t + r);  // (off_rows is a multiple of 4)
       const int oa_row = tab[ra], na = tab[ra + 1], qa = tab[ra + 2];
       const int ob_row = tab[ra + 4], nb = tab[ra + 5], qb = tab[ra + 6];
       v2f_t ca = {-0.f, -0.f}, cb = {-0.f, -0.f};
@@ -2299,8 +2316,8 @@ __global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, in
       reg_store<T>(pout, ld_out, oa_row, col, n, ca);
       reg_store<T>(pout, ld_out, ob_row, col, n, cb);
     }
-    if (r < nr) {
-      const int ra = 4 * (off_rows / 4 + r0 + r);
+    if (r < nrt) {
+      const int ra = 4 * (off_rows / 4 + r0t + r);
       const int oa_row = tab[ra], na = tab[ra + 1], qa = tab[ra + 2];
       v2f_t ca = {-0.f, -0.f};
       for (int k = 0; k < na; ++k) reg_one<NB, EXACT>(ca, ops[qa + k], X0, X1, X2, X3);
