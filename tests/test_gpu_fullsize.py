@@ -121,15 +121,15 @@ def _check_resnet_round(cuda, name, spec):
 @pytest.mark.parametrize("spec", [None, {"c4": 64, "lds": 81920, "dense": 0}, {"c4": 128, "lds": 163840, "dense": 0},
                                   {"c4": 128, "lds": 81920, "dense": 0}, {"c4": 32, "lds": 81920, "dense": 0},
                                   {"c4": 16, "lds": 81920, "dense": 0}, {"c4": 64, "lds": 81920, "dense": 8},
-                                  {"stream_rows": 64, "stream_src": 0}])
+                                  {"stream_rows": 64, "stream_src": 0}, {"reg": 1}])
 def test_config3_full_round_vs_reference(cuda, spec):
     """The benchmark's round (64-device random 8-regular graph, ResNet-50, M = 9) at full size:
     all 64 output models bitwise the reference's, for every plan form the tuner can pick."""
     _check_resnet_round(cuda, "full_round_c3_resnet50_rr64.json", spec)
 
 
-@pytest.mark.parametrize("spec", [None, {"c4": 128, "lds": 81920, "dense": 0}, {"c4": 64, "lds": 163840, "dense": 8},
-                                  {"c4": 16, "lds": 81920, "dense": 0}])
+@pytest.mark.parametrize("spec", [None, {"c4": 128, "lds": 163840, "dense": 0}, {"c4": 64, "lds": 163840, "dense": 8},
+                                  {"c4": 16, "lds": 81920, "dense": 0}, {"reg": 1}])
 def test_config4_full_round_vs_reference(cuda, spec):
     """barbell(60, 8), 128 x ResNet-50 at full size: the K3c clique blocks with their attached
     bridge rows (default plan) and the LDS-tiled forms, all 128 output models bitwise the
@@ -177,17 +177,18 @@ def _check_c5(cuda, dtype, fn, spec, mode=ops.MODE_EXACT):
     assert not bad, f"{len(bad)} (model, entry group) outputs differ from the reference, first {bad[:8]}"
 
 
-@pytest.mark.parametrize("spec", [None, {"c4": 32, "lds": 163840, "dense": 0}])
+@pytest.mark.parametrize("spec", [None, {"c4": 32, "lds": 163840, "dense": 0}, {"reg": 1}])
 def test_config5_full_round_vs_reference(cuda, spec):
     """SBM-256 x ViT-B/16 fp32 at full size (88.6 GB of models): every (output model, entry
     group) bitwise the reference's unweighted_module_avg."""
     _check_c5(cuda, "f32", "unweighted_module_avg", spec)
 
 
-def test_config5_degree_centrality_vs_reference(cuda):
+@pytest.mark.parametrize("spec", [None, {"reg": 1}])
+def test_config5_degree_centrality_vs_reference(cuda, spec):
     """The per-operand-weight form (centrality_module_avg, degree, softmax coeff 10) of config 5
     at full width: the last entry group of every output model bitwise the reference's."""
-    _check_c5(cuda, "f32", "centrality_module_avg", None)
+    _check_c5(cuda, "f32", "centrality_module_avg", spec)
 
 
 def test_config5_bf16_exact_vs_reference(cuda):
