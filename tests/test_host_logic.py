@@ -603,36 +603,45 @@ def test_link_model_matches_design_table():
 
 def test_reg_plan_table_layout():
     """build_reg_plan (K3r): every row in exactly one group, each group's operands among its
-    <= 64 sources, records in reference order with the fp32 weight and 2 x slot, the pair order
-    sorted by operand count, 8 read-ahead records of padding (tal_agg.h K3r layout)."""
+    <= 64 sources (the list padded to 16 x NB entries with its first source), records in
+    reference order as 2 x slot with the fp32 weights alongside, rows in pair order (operand
+    count descending), each row's operands 4-aligned, 8 dwords of padding after each array, the
+    per-operand flag exactly on rows whose weights differ (tal_agg.h K3r layout)."""
     import bench
     from oracle import reference_alg as ra
     from topology_aware_learning_amd import ops
 
-    orders, ws = bench.round_spec(256, 8, kind="sbm", weights="degcent")
-    row_ptr, col, w = ra.round_csr(orders, ws)
-    out_rows = np.arange(len(orders), dtype=np.int32)[::-1].copy()
-    p = ops.build_reg_plan(row_ptr, col, w, out_rows)
-    t = p.table
-    grp = t[: 4 * p.n_groups].reshape(-1, 4)
-    recs = t[p.off_rows: p.off_ops].reshape(-1, 4)
-    opr = t[p.off_ops:].view(np.uint32).reshape(-1, 2)
-    assert len(opr) == len(col) + 8 and p.max_src <= 64 and p.off_rows % 4 == 0 and p.off_ops % 2 == 0
-    seen = []
-    for s0, ns, r0, nr in grp:
-        srcs = t[p.off_src + s0: p.off_src + s0 + ns]
-        assert ns <= 64 and list(srcs) == sorted(set(srcs.tolist()))
-        counts = recs[r0: r0 + nr, 1]
-        assert list(counts) == sorted(counts, reverse=True)
-        for out, cnt, q0, _ in recs[r0: r0 + nr]:
-            r = int(np.flatnonzero(out_rows == out)[0])
-            seen.append(r)
-            assert cnt == len(orders[r])
-            for k in range(cnt):
-                wbits, reg = opr[q0 + k]
-                assert srcs[reg // 2] == orders[r][k] and reg % 2 == 0
-                assert wbits == np.float32(ws[r][k]).view(np.uint32)
-    assert sorted(seen) == list(range(len(orders)))
+    for weights in ("unweighted", "degcent"):
+        orders, ws = bench.round_spec(256, 8, kind="sbm", weights=weights)
+        row_ptr, col, w = ra.round_csr(orders, ws)
+        out_rows = np.arange(len(orders), dtype=np.int32)[::-1].copy()
+        p = ops.build_reg_plan(row_ptr, col, w, out_rows)
+        t = p.table
+        span = 16 * ((p.max_src + 15) // 16)
+        grp = t[: 4 * p.n_groups].reshape(-1, 4)
+        recs = t[p.off_rows: p.off_idx].reshape(-1, 4).view(np.uint32)
+        assert p.max_src <= 64 and p.off_rows % 4 == 0 and p.off_idx % 4 == 0 and p.off_w % 4 == 0
+        assert p.off_w - p.off_idx >= 8 and len(t) - p.off_w >= 8
+        seen = []
+        for g, (s0, ns, r0, nr) in enumerate(grp):
+            assert s0 == g * span and ns <= 64
+            srcs = t[p.off_src + s0: p.off_src + s0 + ns]
+            assert list(srcs) == sorted(set(srcs.tolist()))
+            assert np.all(t[p.off_src + s0 + ns: p.off_src + s0 + span] == srcs[0])
+            counts = recs[r0: r0 + nr, 1] & ~np.uint32(ops.REG_PER_OP)
+            assert list(counts) == sorted(counts, reverse=True)
+            for out, flag, q0, wrow in recs[r0: r0 + nr]:
+                r = int(np.flatnonzero(out_rows == out)[0])
+                seen.append(r)
+                cnt = flag & ~np.uint32(ops.REG_PER_OP)
+                assert cnt == len(orders[r]) and q0 % 4 == 0
+                w32 = np.float32(ws[r]).view(np.uint32)
+                assert bool(flag & ops.REG_PER_OP) == bool(np.any(w32 != w32[0])) and wrow == w32[0]
+                for k in range(cnt):
+                    reg = t[p.off_idx + q0 + k]
+                    assert reg % 2 == 0 and srcs[reg // 2] == orders[r][k]
+                    assert t[p.off_w + q0 + k].view(np.uint32) == w32[k]
+        assert sorted(seen) == list(range(len(orders)))
     assert ops.build_reg_plan(row_ptr, col, w, out_rows, max_src=8) is None  # a row has 9+ sources
 
 

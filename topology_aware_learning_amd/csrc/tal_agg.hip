@@ -43,7 +43,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 14;
+constexpr int kAbiVersion = 16;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -1968,8 +1968,11 @@ typedef __attribute__((address_space(4))) const uint64_t* ConstU64;
 constexpr int kRegMaxSrc = 64;
 constexpr int kRegPiece = 128;  // elements per item: 64 lanes x 2
 
-#define TAL_RLD2(a, b, k) "global_load_dwordx2 v[" #a ":" #b "], %17, %" #k " nt\n\t"
-#define TAL_RLD1(b, k) "global_load_dword v" #b ", %17, %" #k " nt\n\t"
+// plain (temporal) loads: a source shared by several groups of a piece is served to the others
+// by the XCD's L2 (non-temporal loads were measured fetching every group's sources from HBM:
+// 4.1x the bytes on config 5)
+#define TAL_RLD2(a, b, k) "global_load_dwordx2 v[" #a ":" #b "], %17, %" #k "\n\t"
+#define TAL_RLD1(b, k) "global_load_dword v" #b ", %17, %" #k "\n\t"
 #define TAL_RUNP(a, b) "v_lshlrev_b32 v" #a ", 16, v" #b "\n\tv_and_b32 v" #b ", 0xffff0000, v" #b "\n\t"
 #define TAL_RF32_0 \
   TAL_RLD2(32,33,1) TAL_RLD2(34,35,2) TAL_RLD2(36,37,3) TAL_RLD2(38,39,4) \
@@ -2093,127 +2096,129 @@ __device__ __forceinline__ void reg_wait(v32f& X0, v32f& X1, v32f& X2, v32f& X3)
   }
 }
 
-// a wave-uniform 64-bit value in an SGPR pair (the uniformity analysis does not see through the
-// per-source address arithmetic; the "s" constraints below need SGPRs)
-__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
-  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
-  return (static_cast<uint64_t>(hi) << 32) | lo;
-}
+// Operands: a row's sources as register offsets (2 x slot, one dword each) in `idx`, its
+// weights either one per row (row record) or one per operand in `wts` (fp32 bits, parallel to
+// idx).  A weight reaches the packed multiply as a 64-bit SGPR pair: op_sel_hi:[1,0] makes both
+// halves take its low dword, op_sel:[0,1] op_sel_hi:[1,1] its high dword (so one aligned pair
+// serves two operands' weights).  The asm blocks also read the NEXT batch's operand dwords
+// (s_load with a byte offset from the table base) while they compute and drain lgkmcnt at the
+// end; a batch is four operands of each of two rows, the two rows' chains interleaved so no
+// packed instruction reads the result of the one right before it (gfx950 needs a wait state
+// there).  M0, which the index mode writes, is used by nothing else in this kernel (no LDS).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
-// An operand record is one 64-bit word: low dword = fp32 weight, high dword = register offset
-// of its source (2 x slot).  The weight is passed as that SGPR pair with op_sel_hi:[1,0] (both
-// halves of the packed multiply take the low dword); the index is its high dword.
-#define TAL_IDX(r) static_cast<uint32_t>((r) >> 32)
+#define TAL_MUL(T, I, W, SEL) "s_set_gpr_idx_idx %[" I "]\n\tv_pk_mul_f32 %[" T "], v[32:33], %[" W "] " SEL "\n\t"
+#define TAL_FMA(C, I, W, SEL) "s_set_gpr_idx_idx %[" I "]\n\tv_pk_fma_f32 %[" C "], v[32:33], %[" W "], %[" C "] " SEL "\n\t"
+#define TAL_LO "op_sel_hi:[1,0]"
+#define TAL_HI "op_sel:[0,1] op_sel_hi:[1,1]"
+#define TAL_LO3 "op_sel_hi:[1,0,1]"
+#define TAL_HI3 "op_sel:[0,1,0] op_sel_hi:[1,1,1]"
+#define TAL_ADDS                                                                            \
+  "v_pk_add_f32 %[ca], %[ca], %[t0]\n\tv_pk_add_f32 %[cb], %[cb], %[t4]\n\t"                \
+  "v_pk_add_f32 %[ca], %[ca], %[t1]\n\tv_pk_add_f32 %[cb], %[cb], %[t5]\n\t"                \
+  "v_pk_add_f32 %[ca], %[ca], %[t2]\n\tv_pk_add_f32 %[cb], %[cb], %[t6]\n\t"                \
+  "v_pk_add_f32 %[ca], %[ca], %[t3]\n\tv_pk_add_f32 %[cb], %[cb], %[t7]\n\t"
+#define TAL_IDX_INS                                                                                     \
+  [i0] "s"(A[0]), [i1] "s"(A[1]), [i2] "s"(A[2]), [i3] "s"(A[3]), [j0] "s"(B[0]), [j1] "s"(B[1]),        \
+      [j2] "s"(B[2]), [j3] "s"(B[3]), [base] "s"(base), [oa] "s"(oa), [ob] "s"(ob)
 
-// two rows, four operands each: A / B = this batch's operand records (SGPR tuples), pa / pb =
-// the next batch's addresses, loaded into NA / NB2 by the same asm while it computes (the scalar
-// loads' latency hides under the arithmetic; lgkmcnt is drained at the end, so the compiler
-// sees nothing pending).  The table is padded so a read-ahead past the last batch stays inside.
-typedef uint64_t u64x4 __attribute__((ext_vector_type(4)));
-#define TAL_PAIR_INS                                                                                      \
-  [w0] "s"(A[0]), [w1] "s"(A[1]), [w2] "s"(A[2]), [w3] "s"(A[3]), [v0] "s"(B[0]), [v1] "s"(B[1]),          \
-      [v2] "s"(B[2]), [v3] "s"(B[3]), [i0] "s"(TAL_IDX(A[0])), [i1] "s"(TAL_IDX(A[1])), [i2] "s"(TAL_IDX(A[2])), \
-      [i3] "s"(TAL_IDX(A[3])), [j0] "s"(TAL_IDX(B[0])), [j1] "s"(TAL_IDX(B[1])), [j2] "s"(TAL_IDX(B[2])),   \
-      [j3] "s"(TAL_IDX(B[3])), [pa] "s"(pa), [pb] "s"(pb)
-
-// EXACT: eight indexed multiplies, then the two add chains interleaved (no add reads the add
-// right before it)
-template <int NB>
-__device__ __forceinline__ void reg_pair_exact(v2f_t& ca, v2f_t& cb, const u64x4& A, const u64x4& B, u64x4& NA,
-                                               u64x4& NB2, uint64_t pa, uint64_t pb, const v32f& X0, const v32f& X1,
-                                               const v32f& X2, const v32f& X3) {
-  v2f_t t0, t1, t2, t3, t4, t5, t6, t7;
-  uint32_t m;
-  TAL_RASM("s_load_dwordx8 %[na], %[pa], 0x0\n\t"
-           "s_load_dwordx8 %[nb], %[pb], 0x0\n\t"
-           "s_mov_b32 %[m], m0\n\t"
-           "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
-           "v_pk_mul_f32 %[t0], v[32:33], %[w0] op_sel_hi:[1,0]\n\t"
-           "s_set_gpr_idx_idx %[i1]\n\t"
-           "v_pk_mul_f32 %[t1], v[32:33], %[w1] op_sel_hi:[1,0]\n\t"
-           "s_set_gpr_idx_idx %[i2]\n\t"
-           "v_pk_mul_f32 %[t2], v[32:33], %[w2] op_sel_hi:[1,0]\n\t"
-           "s_set_gpr_idx_idx %[i3]\n\t"
-           "v_pk_mul_f32 %[t3], v[32:33], %[w3] op_sel_hi:[1,0]\n\t"
-           "s_set_gpr_idx_idx %[j0]\n\t"
-           "v_pk_mul_f32 %[t4], v[32:33], %[v0] op_sel_hi:[1,0]\n\t"
-           "s_set_gpr_idx_idx %[j1]\n\t"
-           "v_pk_mul_f32 %[t5], v[32:33], %[v1] op_sel_hi:[1,0]\n\t"
-           "s_set_gpr_idx_idx %[j2]\n\t"
-           "v_pk_mul_f32 %[t6], v[32:33], %[v2] op_sel_hi:[1,0]\n\t"
-           "s_set_gpr_idx_idx %[j3]\n\t"
-           "v_pk_mul_f32 %[t7], v[32:33], %[v3] op_sel_hi:[1,0]\n\t"
-           "s_set_gpr_idx_off\n\t"
-           "s_mov_b32 m0, %[m]\n\t"
-           "v_pk_add_f32 %[ca], %[ca], %[t0]\n\t"
-           "v_pk_add_f32 %[cb], %[cb], %[t4]\n\t"
-           "v_pk_add_f32 %[ca], %[ca], %[t1]\n\t"
-           "v_pk_add_f32 %[cb], %[cb], %[t5]\n\t"
-           "v_pk_add_f32 %[ca], %[ca], %[t2]\n\t"
-           "v_pk_add_f32 %[cb], %[cb], %[t6]\n\t"
-           "v_pk_add_f32 %[ca], %[ca], %[t3]\n\t"
-           "v_pk_add_f32 %[cb], %[cb], %[t7]\n\t"
-           "s_waitcnt lgkmcnt(0)",
-           ([ca] "+v"(ca), [cb] "+v"(cb), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
-            [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7), [m] "=&s"(m), [na] "=&s"(NA),
-            [nb] "=&s"(NB2)),
-           (TAL_PAIR_INS));
-}
-
-// FMA: the two fused chains alternate, an index switch between
-template <int NB>
-__device__ __forceinline__ void reg_pair_fma(v2f_t& ca, v2f_t& cb, const u64x4& A, const u64x4& B, u64x4& NA,
-                                             u64x4& NB2, uint64_t pa, uint64_t pb, const v32f& X0, const v32f& X1,
-                                             const v32f& X2, const v32f& X3) {
-  uint32_t m;
-  TAL_RASM("s_load_dwordx8 %[na], %[pa], 0x0\n\t"
-           "s_load_dwordx8 %[nb], %[pb], 0x0\n\t"
-           "s_mov_b32 %[m], m0\n\t"
-           "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
-           "v_pk_fma_f32 %[ca], v[32:33], %[w0], %[ca] op_sel_hi:[1,0,1]\n\t"
-           "s_set_gpr_idx_idx %[j0]\n\t"
-           "v_pk_fma_f32 %[cb], v[32:33], %[v0], %[cb] op_sel_hi:[1,0,1]\n\t"
-           "s_set_gpr_idx_idx %[i1]\n\t"
-           "v_pk_fma_f32 %[ca], v[32:33], %[w1], %[ca] op_sel_hi:[1,0,1]\n\t"
-           "s_set_gpr_idx_idx %[j1]\n\t"
-           "v_pk_fma_f32 %[cb], v[32:33], %[v1], %[cb] op_sel_hi:[1,0,1]\n\t"
-           "s_set_gpr_idx_idx %[i2]\n\t"
-           "v_pk_fma_f32 %[ca], v[32:33], %[w2], %[ca] op_sel_hi:[1,0,1]\n\t"
-           "s_set_gpr_idx_idx %[j2]\n\t"
-           "v_pk_fma_f32 %[cb], v[32:33], %[v2], %[cb] op_sel_hi:[1,0,1]\n\t"
-           "s_set_gpr_idx_idx %[i3]\n\t"
-           "v_pk_fma_f32 %[ca], v[32:33], %[w3], %[ca] op_sel_hi:[1,0,1]\n\t"
-           "s_set_gpr_idx_idx %[j3]\n\t"
-           "v_pk_fma_f32 %[cb], v[32:33], %[v3], %[cb] op_sel_hi:[1,0,1]\n\t"
-           "s_set_gpr_idx_off\n\t"
-           "s_mov_b32 m0, %[m]\n\t"
-           "s_waitcnt lgkmcnt(0)",
-           ([ca] "+v"(ca), [cb] "+v"(cb), [m] "=&s"(m), [na] "=&s"(NA), [nb] "=&s"(NB2)), (TAL_PAIR_INS));
-}
-
-// one operand of one row
+// one batch, row weights (uniform per row): wa / wb = the rows' weights in the low dword
 template <int NB, bool EXACT>
-__device__ __forceinline__ void reg_one(v2f_t& ca, uint64_t a0, const v32f& X0, const v32f& X1, const v32f& X2,
-                                        const v32f& X3) {
-  uint32_t m;
+__device__ __forceinline__ void reg_pair_u(v2f_t& ca, v2f_t& cb, const u32x4& A, const u32x4& B, u32x4& NA,
+                                           u32x4& NB2, uint64_t wa, uint64_t wb, uint64_t base, uint32_t oa,
+                                           uint32_t ob, const v32f& X0, const v32f& X1, const v32f& X2,
+                                           const v32f& X3) {
+  if constexpr (EXACT) {
+    v2f_t t0, t1, t2, t3, t4, t5, t6, t7;
+    TAL_RASM("s_load_dwordx4 %[na], %[base], %[oa]\n\t"
+             "s_load_dwordx4 %[nb], %[base], %[ob]\n\t"
+             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
+             "v_pk_mul_f32 %[t0], v[32:33], %[wa] " TAL_LO "\n\t"
+             TAL_MUL("t1", "i1", "wa", TAL_LO) TAL_MUL("t2", "i2", "wa", TAL_LO) TAL_MUL("t3", "i3", "wa", TAL_LO)
+             TAL_MUL("t4", "j0", "wb", TAL_LO) TAL_MUL("t5", "j1", "wb", TAL_LO) TAL_MUL("t6", "j2", "wb", TAL_LO)
+             TAL_MUL("t7", "j3", "wb", TAL_LO)
+             "s_set_gpr_idx_off\n\t" TAL_ADDS
+             "s_waitcnt lgkmcnt(0)",
+             ([ca] "+v"(ca), [cb] "+v"(cb), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+              [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7), [na] "=&s"(NA), [nb] "=&s"(NB2)),
+             (TAL_IDX_INS, [wa] "s"(wa), [wb] "s"(wb)));
+  } else {
+    TAL_RASM("s_load_dwordx4 %[na], %[base], %[oa]\n\t"
+             "s_load_dwordx4 %[nb], %[base], %[ob]\n\t"
+             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
+             "v_pk_fma_f32 %[ca], v[32:33], %[wa], %[ca] " TAL_LO3 "\n\t"
+             TAL_FMA("cb", "j0", "wb", TAL_LO3) TAL_FMA("ca", "i1", "wa", TAL_LO3) TAL_FMA("cb", "j1", "wb", TAL_LO3)
+             TAL_FMA("ca", "i2", "wa", TAL_LO3) TAL_FMA("cb", "j2", "wb", TAL_LO3) TAL_FMA("ca", "i3", "wa", TAL_LO3)
+             TAL_FMA("cb", "j3", "wb", TAL_LO3)
+             "s_set_gpr_idx_off\n\t"
+             "s_waitcnt lgkmcnt(0)",
+             ([ca] "+v"(ca), [cb] "+v"(cb), [na] "=&s"(NA), [nb] "=&s"(NB2)), (TAL_IDX_INS, [wa] "s"(wa), [wb] "s"(wb)));
+  }
+}
+
+// one batch, a weight per operand: WA / WB = the rows' four weights as two pairs each; their
+// next batch (at byte offsets ow from the table base, the weights' array) loads alongside
+template <int NB, bool EXACT>
+__device__ __forceinline__ void reg_pair_w(v2f_t& ca, v2f_t& cb, const u32x4& A, const u32x4& B, u32x4& NA,
+                                           u32x4& NB2, const u64x2& WA, const u64x2& WB, u64x2& NWA, u64x2& NWB,
+                                           uint64_t base, uint32_t oa, uint32_t ob, uint32_t owa, uint32_t owb,
+                                           const v32f& X0, const v32f& X1, const v32f& X2, const v32f& X3) {
+  const uint64_t wa01 = WA[0], wa23 = WA[1], wb01 = WB[0], wb23 = WB[1];
+  if constexpr (EXACT) {
+    v2f_t t0, t1, t2, t3, t4, t5, t6, t7;
+    TAL_RASM("s_load_dwordx4 %[na], %[base], %[oa]\n\t"
+             "s_load_dwordx4 %[nb], %[base], %[ob]\n\t"
+             "s_load_dwordx4 %[nwa], %[base], %[owa]\n\t"
+             "s_load_dwordx4 %[nwb], %[base], %[owb]\n\t"
+             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
+             "v_pk_mul_f32 %[t0], v[32:33], %[wa01] " TAL_LO "\n\t"
+             TAL_MUL("t1", "i1", "wa01", TAL_HI) TAL_MUL("t2", "i2", "wa23", TAL_LO) TAL_MUL("t3", "i3", "wa23", TAL_HI)
+             TAL_MUL("t4", "j0", "wb01", TAL_LO) TAL_MUL("t5", "j1", "wb01", TAL_HI) TAL_MUL("t6", "j2", "wb23", TAL_LO)
+             TAL_MUL("t7", "j3", "wb23", TAL_HI)
+             "s_set_gpr_idx_off\n\t" TAL_ADDS
+             "s_waitcnt lgkmcnt(0)",
+             ([ca] "+v"(ca), [cb] "+v"(cb), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+              [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7), [na] "=&s"(NA), [nb] "=&s"(NB2),
+              [nwa] "=&s"(NWA), [nwb] "=&s"(NWB)),
+             (TAL_IDX_INS, [wa01] "s"(wa01), [wa23] "s"(wa23), [wb01] "s"(wb01), [wb23] "s"(wb23), [owa] "s"(owa),
+              [owb] "s"(owb)));
+  } else {
+    TAL_RASM("s_load_dwordx4 %[na], %[base], %[oa]\n\t"
+             "s_load_dwordx4 %[nb], %[base], %[ob]\n\t"
+             "s_load_dwordx4 %[nwa], %[base], %[owa]\n\t"
+             "s_load_dwordx4 %[nwb], %[base], %[owb]\n\t"
+             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
+             "v_pk_fma_f32 %[ca], v[32:33], %[wa01], %[ca] " TAL_LO3 "\n\t"
+             TAL_FMA("cb", "j0", "wb01", TAL_LO3) TAL_FMA("ca", "i1", "wa01", TAL_HI3) TAL_FMA("cb", "j1", "wb01", TAL_HI3)
+             TAL_FMA("ca", "i2", "wa23", TAL_LO3) TAL_FMA("cb", "j2", "wb23", TAL_LO3) TAL_FMA("ca", "i3", "wa23", TAL_HI3)
+             TAL_FMA("cb", "j3", "wb23", TAL_HI3)
+             "s_set_gpr_idx_off\n\t"
+             "s_waitcnt lgkmcnt(0)",
+             ([ca] "+v"(ca), [cb] "+v"(cb), [na] "=&s"(NA), [nb] "=&s"(NB2), [nwa] "=&s"(NWA), [nwb] "=&s"(NWB)),
+             (TAL_IDX_INS, [wa01] "s"(wa01), [wa23] "s"(wa23), [wb01] "s"(wb01), [wb23] "s"(wb23), [owa] "s"(owa),
+              [owb] "s"(owb)));
+  }
+}
+
+// one operand of one row (the rows' tails past their common batches, a lone last row): weight
+// in the low dword of w
+template <int NB, bool EXACT>
+__device__ __forceinline__ void reg_one(v2f_t& ca, uint32_t idx, uint64_t w, const v32f& X0, const v32f& X1,
+                                        const v32f& X2, const v32f& X3) {
   if constexpr (EXACT) {
     v2f_t t0;
-    TAL_RASM("s_mov_b32 %[m], m0\n\t"
-             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
-             "v_pk_mul_f32 %[t0], v[32:33], %[w0] op_sel_hi:[1,0]\n\t"
+    TAL_RASM("s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
+             "v_pk_mul_f32 %[t0], v[32:33], %[w0] " TAL_LO "\n\t"
              "s_set_gpr_idx_off\n\t"
-             "s_mov_b32 m0, %[m]\n\t"
              "v_pk_add_f32 %[ca], %[ca], %[t0]\n\t"
              "s_nop 0",
-             ([ca] "+v"(ca), [t0] "=&v"(t0), [m] "=&s"(m)), ([w0] "s"(a0), [i0] "s"(TAL_IDX(a0))));
+             ([ca] "+v"(ca), [t0] "=&v"(t0)), ([w0] "s"(w), [i0] "s"(idx)));
   } else {
-    TAL_RASM("s_mov_b32 %[m], m0\n\t"
-             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
-             "v_pk_fma_f32 %[ca], v[32:33], %[w0], %[ca] op_sel_hi:[1,0,1]\n\t"
-             "s_set_gpr_idx_off\n\t"
-             "s_mov_b32 m0, %[m]",
-             ([ca] "+v"(ca), [m] "=&s"(m)), ([w0] "s"(a0), [i0] "s"(TAL_IDX(a0))));
+    TAL_RASM("s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
+             "v_pk_fma_f32 %[ca], v[32:33], %[w0], %[ca] " TAL_LO3 "\n\t"
+             "s_set_gpr_idx_off",
+             ([ca] "+v"(ca)), ([w0] "s"(w), [i0] "s"(idx)));
   }
 }
 
@@ -2232,18 +2237,25 @@ __device__ __forceinline__ void reg_store(T* pout, int64_t ld_out, int32_t row, 
   }
 }
 
-// Table (int32, device): groups [G][4] {first source, sources, first row, rows}, then source
-// rows, row records [R][4] {out row, operands, first operand, 0} (a group's rows in pair order),
-// then operand records [nnz] 64-bit {fp32 weight, 2 x slot}.
+constexpr uint32_t kRegPerOp = 0x40000000u;  // row record word 1: the row's weights are per operand
+
+// Table (int32, device): groups [G][4] {first source, sources, first row, rows}; at off_src the
+// source pool rows; at off_rows (a multiple of 4) row records [R][4] {out row, operands |
+// kRegPerOp, first operand, fp32 row weight}, a group's rows consecutive (pair order); at
+// off_idx (a multiple of 4) the operands' register offsets (2 x slot), at off_w (a multiple of
+// 4) their fp32 weights (rows with kRegPerOp), each array followed by 8 dwords of padding.
 template <int NB, typename T, bool EXACT>
 __global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, int64_t ld_in, T* __restrict__ pout,
                                                    int64_t ld_out, int64_t n, const int32_t* __restrict__ table,
-                                                   int32_t n_groups, int32_t off_src, int32_t off_rows,
-                                                   int32_t off_ops, int32_t n_pieces, int32_t waves_per_label) {
+                                                   const int64_t* __restrict__ src_off, int32_t n_groups,
+                                                   int32_t off_rows, int32_t off_idx, int32_t off_w,
+                                                   int32_t n_pieces, int32_t waves_per_label) {
   constexpr bool kB = kIsBf16<T>;
   constexpr int kEs = kB ? 2 : 4;
   const ConstI32 tab = (ConstI32)table;
-  const ConstU64 ops = (ConstU64)(table + off_ops);
+  const ConstU64 tab64 = (ConstU64)table;
+  const ConstU64 soff = (ConstU64)src_off;
+  const uint64_t base = reinterpret_cast<uint64_t>(table);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int label = static_cast<int>(blockIdx.x & 7u);
@@ -2259,13 +2271,14 @@ __global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, in
     const int64_t col = static_cast<int64_t>(piece) * kRegPiece + 2 * lane;
     const uint32_t loff = col < n ? static_cast<uint32_t>(2 * lane * kEs) : 0u;  // past n: the piece's start
     const uint64_t pbase = reinterpret_cast<uint64_t>(pin) + static_cast<uint64_t>(piece) * (kRegPiece * kEs);
-    const uint64_t pitch = static_cast<uint64_t>(ld_in) * kEs;
+    (void)ns;
+    (void)ld_in;
     uint64_t b[16];
+    // the group's source list is padded to 16 x NB entries (src_off: their byte offsets in the
+    // pool), so each block's 16 offsets come in two 8-dword scalar loads, one wait
 #define TAL_RBASES(J)                                                                            \
-    _Pragma("unroll") for (int k = 0; k < 16; ++k) {                                             \
-      const int sl = (J) * 16 + k;                                                               \
-      b[k] = pbase + static_cast<uint64_t>(static_cast<uint32_t>(tab[off_src + s0 + (sl < ns ? sl : 0)])) * pitch; \
-    }
+    _Pragma("unroll") for (int k = 0; k < 16; ++k)                                               \
+      b[k] = pbase + static_cast<uint64_t>(soff[s0 + (J) * 16 + k]);
 #ifdef TAL_PROBE_REG_NOLOAD  // A/B probe: sources loaded for a wave's first item only
     if (s == wx) {
 #endif
@@ -2279,48 +2292,80 @@ __global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, in
 #endif
 #undef TAL_RBASES
     reg_wait<NB, kB>(X0, X1, X2, X3);
-#ifdef TAL_PROBE_REG_HOTSQC  // A/B probe: every item walks group 0's row and operand tables
-    const int g_rows = 0;
-#else
-    const int g_rows = g;
-#endif
-    const int r0t = tab[4 * g_rows + 2], nrt = tab[4 * g_rows + 3];
-    (void)r0;
-    (void)nr;
     int r = 0;
 #ifdef TAL_PROBE_REG_NOCOMP  // A/B probe: the stores without the row arithmetic
-    for (; r < nrt; ++r) reg_store<T>(pout, ld_out, tab[4 * (off_rows / 4 + r0t + r)], col, n, v2f_t{0.f, 0.f});
+    for (; r < nr; ++r) reg_store<T>(pout, ld_out, tab[off_rows + 4 * (r0 + r)], col, n, v2f_t{0.f, 0.f});
 #endif
-    for (; r + 1 < nrt; r += 2) {
-      const int ra = 4 * (off_rows / 4 + r0t + r);  // (off_rows is a multiple of 4)
-      const int oa_row = tab[ra], na = tab[ra + 1], qa = tab[ra + 2];
-      const int ob_row = tab[ra + 4], nb = tab[ra + 5], qb = tab[ra + 6];
+    for (; r + 1 < nr; r += 2) {
+      const int ra = off_rows + 4 * (r0 + r);
+      const int oa_row = tab[ra], fa = tab[ra + 1], qa = tab[ra + 2];
+      const int ob_row = tab[ra + 4], fb = tab[ra + 5], qb = tab[ra + 6];
+      const uint64_t wa = static_cast<uint32_t>(tab[ra + 3]), wb = static_cast<uint32_t>(tab[ra + 7]);
+      const bool per_op = ((fa | fb) & static_cast<int>(kRegPerOp)) != 0;
+      const int na = fa & ~static_cast<int>(kRegPerOp), nb = fb & ~static_cast<int>(kRegPerOp);
       v2f_t ca = {-0.f, -0.f}, cb = {-0.f, -0.f};
       const int common = min(na, nb) / 4;
       if (common > 0) {
-        u64x4 A = {ops[qa], ops[qa + 1], ops[qa + 2], ops[qa + 3]};
-        u64x4 B = {ops[qb], ops[qb + 1], ops[qb + 2], ops[qb + 3]};
-        const uint64_t opsb = uniform64(reinterpret_cast<uint64_t>(table + off_ops));
-        for (int k = 0; k < common; ++k) {
-          u64x4 NA, NB2;
-          const uint64_t pa = opsb + 8ull * static_cast<uint32_t>(qa + 4 * k + 4);
-          const uint64_t pb = opsb + 8ull * static_cast<uint32_t>(qb + 4 * k + 4);
-          if constexpr (EXACT) reg_pair_exact<NB>(ca, cb, A, B, NA, NB2, pa, pb, X0, X1, X2, X3);
-          else reg_pair_fma<NB>(ca, cb, A, B, NA, NB2, pa, pb, X0, X1, X2, X3);
-          A = NA;
-          B = NB2;
+        // dword offsets stay 4-aligned only when qa, qb are: the table pads every row's
+        // operand list to a multiple of 4 dwords
+        u32x4 A = {static_cast<uint32_t>(tab[off_idx + qa]), static_cast<uint32_t>(tab[off_idx + qa + 1]),
+                   static_cast<uint32_t>(tab[off_idx + qa + 2]), static_cast<uint32_t>(tab[off_idx + qa + 3])};
+        u32x4 B = {static_cast<uint32_t>(tab[off_idx + qb]), static_cast<uint32_t>(tab[off_idx + qb + 1]),
+                   static_cast<uint32_t>(tab[off_idx + qb + 2]), static_cast<uint32_t>(tab[off_idx + qb + 3])};
+        uint32_t oa = 4u * static_cast<uint32_t>(off_idx + qa + 4), ob = 4u * static_cast<uint32_t>(off_idx + qb + 4);
+        if (!per_op) {
+          // two batches per trip, the operand registers ping-ponging between A/B and NA/NB2
+          // (a one-batch loop copied NA -> A with eight s_mov per batch)
+          int k = 0;
+          for (; k + 2 <= common; k += 2) {
+            u32x4 NA, NB2;
+            reg_pair_u<NB, EXACT>(ca, cb, A, B, NA, NB2, wa, wb, base, oa, ob, X0, X1, X2, X3);
+            reg_pair_u<NB, EXACT>(ca, cb, NA, NB2, A, B, wa, wb, base, oa + 16u, ob + 16u, X0, X1, X2, X3);
+            oa += 32u;
+            ob += 32u;
+          }
+          if (k < common) {
+            u32x4 NA, NB2;
+            reg_pair_u<NB, EXACT>(ca, cb, A, B, NA, NB2, wa, wb, base, oa, ob, X0, X1, X2, X3);
+          }
+        } else {  // row weights replicated per operand by the plan when only one row is per-op
+          u64x2 WA = {tab64[(off_w + qa) / 2], tab64[(off_w + qa) / 2 + 1]};
+          u64x2 WB = {tab64[(off_w + qb) / 2], tab64[(off_w + qb) / 2 + 1]};
+          uint32_t owa = 4u * static_cast<uint32_t>(off_w + qa + 4), owb = 4u * static_cast<uint32_t>(off_w + qb + 4);
+          for (int k = 0; k < common; ++k) {
+            u32x4 NA, NB2;
+            u64x2 NWA, NWB;
+            reg_pair_w<NB, EXACT>(ca, cb, A, B, NA, NB2, WA, WB, NWA, NWB, base, oa, ob, owa, owb, X0, X1, X2, X3);
+            A = NA;
+            B = NB2;
+            WA = NWA;
+            WB = NWB;
+            oa += 16u;
+            ob += 16u;
+            owa += 16u;
+            owb += 16u;
+          }
         }
       }
-      for (int k = 4 * common; k < na; ++k) reg_one<NB, EXACT>(ca, ops[qa + k], X0, X1, X2, X3);
-      for (int k = 4 * common; k < nb; ++k) reg_one<NB, EXACT>(cb, ops[qb + k], X0, X1, X2, X3);
+      for (int k = 4 * common; k < na; ++k)
+        reg_one<NB, EXACT>(ca, static_cast<uint32_t>(tab[off_idx + qa + k]),
+                           per_op ? static_cast<uint32_t>(tab[off_w + qa + k]) : wa, X0, X1, X2, X3);
+      for (int k = 4 * common; k < nb; ++k)
+        reg_one<NB, EXACT>(cb, static_cast<uint32_t>(tab[off_idx + qb + k]),
+                           per_op ? static_cast<uint32_t>(tab[off_w + qb + k]) : wb, X0, X1, X2, X3);
       reg_store<T>(pout, ld_out, oa_row, col, n, ca);
       reg_store<T>(pout, ld_out, ob_row, col, n, cb);
     }
-    if (r < nrt) {
-      const int ra = 4 * (off_rows / 4 + r0t + r);
-      const int oa_row = tab[ra], na = tab[ra + 1], qa = tab[ra + 2];
+    if (r < nr) {
+      const int ra = off_rows + 4 * (r0 + r);
+      const int oa_row = tab[ra], fa = tab[ra + 1], qa = tab[ra + 2];
+      const bool per_op = (fa & static_cast<int>(kRegPerOp)) != 0;
+      const int na = fa & ~static_cast<int>(kRegPerOp);
+      const uint64_t wa = static_cast<uint32_t>(tab[ra + 3]);
       v2f_t ca = {-0.f, -0.f};
-      for (int k = 0; k < na; ++k) reg_one<NB, EXACT>(ca, ops[qa + k], X0, X1, X2, X3);
+      for (int k = 0; k < na; ++k)
+        reg_one<NB, EXACT>(ca, static_cast<uint32_t>(tab[off_idx + qa + k]),
+                           per_op ? static_cast<uint32_t>(tab[off_w + qa + k]) : wa, X0, X1, X2, X3);
       reg_store<T>(pout, ld_out, oa_row, col, n, ca);
     }
     q += dq;
@@ -2334,8 +2379,8 @@ __global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, in
 
 template <int NB, typename T, bool EXACT>
 int32_t launch_round_reg_nb(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n, const int32_t* table,
-                            int32_t n_groups, int32_t off_src, int32_t off_rows, int32_t off_ops, int32_t n_pieces,
-                            hipStream_t s) {
+                            const int64_t* src_off, int32_t n_groups, int32_t off_rows, int32_t off_idx,
+                            int32_t off_w, int32_t n_pieces, hipStream_t s) {
   static int blocks_per_cu = -1, n_cu = 0;  // per instantiation, once per process
   if (blocks_per_cu < 0) {
     int dev = 0;
@@ -2347,22 +2392,25 @@ int32_t launch_round_reg_nb(const T* pin, int64_t ld_in, T* pout, int64_t ld_out
   }
   // persistent: every resident wave, a multiple of 8 blocks (XCD labels)
   const int grid = std::max(8, n_cu * blocks_per_cu / 8 * 8);
-  k_round_reg<NB, T, EXACT><<<grid, 256, 0, s>>>(pin, ld_in, pout, ld_out, n, table, n_groups, off_src, off_rows,
-                                                 off_ops, n_pieces, grid / 8 * 4);
+  k_round_reg<NB, T, EXACT><<<grid, 256, 0, s>>>(pin, ld_in, pout, ld_out, n, table, src_off, n_groups, off_rows,
+                                                 off_idx, off_w, n_pieces, grid / 8 * 4);
   return check_launch("register round kernel");
 }
 
 template <typename T, bool EXACT>
 int32_t launch_round_reg(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n, const int32_t* table,
-                         int32_t n_groups, int32_t off_src, int32_t off_rows, int32_t off_ops, int32_t max_src,
-                         hipStream_t s) {
+                         const int64_t* src_off, int32_t n_groups, int32_t off_rows, int32_t off_idx, int32_t off_w,
+                         int32_t max_src, hipStream_t s) {
   const int64_t n_pieces = (n + kRegPiece - 1) / kRegPiece;
   if (n_pieces * n_groups >= (1LL << 31)) return fail(TAL_ERR_INVALID, "register round: too many items");
   const int np = static_cast<int>(n_pieces);
-  if (max_src <= 16) return launch_round_reg_nb<1, T, EXACT>(pin, ld_in, pout, ld_out, n, table, n_groups, off_src, off_rows, off_ops, np, s);
-  if (max_src <= 32) return launch_round_reg_nb<2, T, EXACT>(pin, ld_in, pout, ld_out, n, table, n_groups, off_src, off_rows, off_ops, np, s);
-  if (max_src <= 48) return launch_round_reg_nb<3, T, EXACT>(pin, ld_in, pout, ld_out, n, table, n_groups, off_src, off_rows, off_ops, np, s);
-  return launch_round_reg_nb<4, T, EXACT>(pin, ld_in, pout, ld_out, n, table, n_groups, off_src, off_rows, off_ops, np, s);
+#define TAL_REG_NB(NBV) \
+  launch_round_reg_nb<NBV, T, EXACT>(pin, ld_in, pout, ld_out, n, table, src_off, n_groups, off_rows, off_idx, off_w, np, s)
+  if (max_src <= 16) return TAL_REG_NB(1);
+  if (max_src <= 32) return TAL_REG_NB(2);
+  if (max_src <= 48) return TAL_REG_NB(3);
+  return TAL_REG_NB(4);
+#undef TAL_REG_NB
 }
 
 template <int NT, bool EXACT>
@@ -3452,16 +3500,18 @@ int32_t tal_agg_round_clique_f32(const float* pool_in, int64_t ld_in, float* poo
 }
 
 int32_t tal_agg_round_reg(const void* pool_in, int64_t ld_in, void* pool_out, int64_t ld_out, int64_t n,
-                          int32_t bf16, const int32_t* table_dev, int32_t n_groups, int32_t off_src,
-                          int32_t off_rows, int32_t off_ops, int32_t max_src, int32_t mode, void* stream) {
-  if (!pool_in || !pool_out || !table_dev) return fail(TAL_ERR_INVALID, "tal_agg_round_reg: null pointer");
+                          int32_t bf16, const int32_t* table_dev, const int64_t* src_off_dev, int32_t n_groups,
+                          int32_t off_src, int32_t off_rows, int32_t off_idx, int32_t off_w, int32_t max_src,
+                          int32_t mode, void* stream) {
+  if (!pool_in || !pool_out || !table_dev || !src_off_dev)
+    return fail(TAL_ERR_INVALID, "tal_agg_round_reg: null pointer");
   if (pool_in == pool_out)
     return fail(TAL_ERR_INVALID, "tal_agg_round_reg: the register round runs out of place (snapshot semantics)");
   const int64_t n2 = n + (n & 1);  // the last lane of an odd row reads one element of padding
   if (n < 0 || ld_in < n2 || ld_out < n2 || ld_in % 2 || ld_out % 2)
     return fail(TAL_ERR_INVALID, "tal_agg_round_reg: need even ld >= n rounded up to even");
-  if (n_groups < 0 || max_src < 1 || max_src > kRegMaxSrc || off_src < 4 * n_groups || off_rows % 4 || off_ops % 2 ||
-      off_rows < off_src || off_ops < off_rows)
+  if (n_groups < 0 || max_src < 1 || max_src > kRegMaxSrc || off_src < 4 * n_groups || off_rows % 4 || off_idx % 4 ||
+      off_w % 4 || off_rows < off_src || off_idx < off_rows || off_w < off_idx)
     return fail(TAL_ERR_INVALID, "tal_agg_round_reg: bad table layout");
   if (bf16 && mode == TAL_MODE_EXACT)
     return fail(TAL_ERR_INVALID, "tal_agg_round_reg: bf16 rounds take FMA mode here (EXACT: tal_agg_round_bf16)");
@@ -3471,12 +3521,12 @@ int32_t tal_agg_round_reg(const void* pool_in, int64_t ld_in, void* pool_out, in
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (bf16)
     return launch_round_reg<uint16_t, false>(static_cast<const uint16_t*>(pool_in), ld_in, static_cast<uint16_t*>(pool_out),
-                                             ld_out, n, table_dev, n_groups, off_src, off_rows, off_ops, max_src, s);
+                                             ld_out, n, table_dev, src_off_dev, n_groups, off_rows, off_idx, off_w, max_src, s);
   if (mode == TAL_MODE_EXACT)
     return launch_round_reg<float, true>(static_cast<const float*>(pool_in), ld_in, static_cast<float*>(pool_out), ld_out,
-                                         n, table_dev, n_groups, off_src, off_rows, off_ops, max_src, s);
+                                         n, table_dev, src_off_dev, n_groups, off_rows, off_idx, off_w, max_src, s);
   return launch_round_reg<float, false>(static_cast<const float*>(pool_in), ld_in, static_cast<float*>(pool_out), ld_out,
-                                        n, table_dev, n_groups, off_src, off_rows, off_ops, max_src, s);
+                                        n, table_dev, src_off_dev, n_groups, off_rows, off_idx, off_w, max_src, s);
 }
 
 int32_t tal_agg_bf16(const uint16_t* const* x_host, const double* w_host, int32_t m, uint16_t* out,

@@ -345,9 +345,10 @@ class RegPlan:
     n_groups: int
     off_src: int
     off_rows: int
-    off_ops: int
+    off_idx: int
+    off_w: int
     max_src: int
-    group_sources: int   # sum over groups of their sources (HBM / L2 reads per column)
+    group_sources: int   # sum over groups of their sources (L2 reads per column)
     full: RoundPlan
     rows: int
     device: Optional[torch.Tensor] = None
@@ -361,7 +362,7 @@ class RegPlan:
 
     @property
     def single_group(self) -> bool:
-        return False  # groups read other groups' outputs' rows: never in place
+        return False  # groups read other groups' output rows: never in place
 
     def staged_rows(self) -> int:
         """Distinct sources read per column: every source once (the groups sharing a source
@@ -371,7 +372,22 @@ class RegPlan:
     def to(self, device) -> "RegPlan":
         self.device = torch.from_numpy(self.table).to(device)
         self.full.to(device)
+        self._src_off = {}
         return self
+
+    def src_offsets(self, pitch_bytes: int, device) -> torch.Tensor:
+        """Device int64 byte offsets (row x pitch) of the source list's entries, once per pool
+        pitch: the kernel adds them to the piece's base instead of multiplying per source."""
+        cache = self.__dict__.setdefault("_src_off", {})
+        key = (int(pitch_bytes), str(device))
+        t = cache.get(key)
+        if t is None:
+            rows = self.table[self.off_src: self.off_src + 16 * ((self.max_src + 15) // 16) * self.n_groups]
+            t = cache[key] = torch.from_numpy(rows.astype(np.int64) * int(pitch_bytes)).to(device)
+        return t
+
+
+REG_PER_OP = 0x40000000  # row record: weights per operand (tal_agg.hip kRegPerOp)
 
 
 def reg_groups(row_ptr, col, max_src: int = REG_MAX_SRC, window: int = REG_WINDOW):
@@ -403,40 +419,49 @@ def reg_groups(row_ptr, col, max_src: int = REG_MAX_SRC, window: int = REG_WINDO
 
 
 def build_reg_plan(row_ptr, col, w, out_row, max_src: int = REG_MAX_SRC) -> Optional[RegPlan]:
-    """RegPlan of a round, or None when a row has more than max_src distinct sources.  Inside a
-    group the rows are ordered by operand count (descending) so the kernel's row pairs share
-    most of their batches."""
+    """RegPlan of a round (table layout: tal_agg.h K3r), or None when a row has more than
+    max_src distinct sources.  Inside a group the rows are ordered by operand count
+    (descending) so the kernel's row pairs share most of their batches; a row whose fp32
+    weights are not all equal is flagged per-operand (its weights are read per operand)."""
+    row_ptr, col, w = row_ptr.astype(np.int32), col.astype(np.int32), np.asarray(w, np.float64)
     row_ptr, col, w, out_row = _csr(row_ptr, col, w, out_row)
     try:
         groups = reg_groups(row_ptr, col, max_src)
     except ValueError:
         return None
     G = len(groups)
-    src_list, row_recs, op_recs = [], [], []
+    src_list, row_recs, idx, wts = [], [], [], []
     grp = np.zeros((G, 4), np.int32)
+    w32all = w.astype(np.float32).view(np.uint32)
+    span = 16 * ((max(len(s_) for _, s_ in groups) + 15) // 16)  # the kernel's 16 x NB loads
     for g, (rows, srcs) in enumerate(groups):
         slot = {s_: k for k, s_ in enumerate(srcs)}
         rows = sorted(rows, key=lambda r: -(row_ptr[r + 1] - row_ptr[r]))
         grp[g] = (len(src_list), len(srcs), len(row_recs), len(rows))
-        src_list.extend(srcs)
+        src_list.extend(srcs + [srcs[0]] * (span - len(srcs)))  # padding reloads the first source
         for r in rows:
             q0, q1 = int(row_ptr[r]), int(row_ptr[r + 1])
-            row_recs.append((int(out_row[r]), q1 - q0, len(op_recs), 0))
-            w32 = w[q0:q1].astype(np.float32).view(np.uint32)
-            for k in range(q0, q1):
-                op_recs.append((int(w32[k - q0]), 2 * slot[int(col[k])]))
+            w32 = w32all[q0:q1]
+            per_op = bool(np.any(w32 != w32[0]))
+            row_recs.append((int(out_row[r]), (q1 - q0) | (REG_PER_OP if per_op else 0), len(idx), int(w32[0])))
+            idx.extend(2 * slot[int(c)] for c in col[q0:q1])
+            wts.extend(int(x) for x in w32)
+            pad = -len(idx) % 4  # every row's list starts 4-dword aligned
+            idx.extend([0] * pad)
+            wts.extend([0] * pad)
     off_src = 4 * G
     off_rows = (off_src + len(src_list) + 3) // 4 * 4
-    off_ops = off_rows + 4 * len(row_recs)
-    words = off_ops + 2 * (len(op_recs) + 8)  # + 8 records of read-ahead padding
+    off_idx = off_rows + 4 * len(row_recs)
+    off_w = off_idx + len(idx) + 8
+    words = off_w + len(wts) + 8  # + 8 dwords of read-ahead padding after each operand array
     table = np.zeros(words, np.int32)
     table[:off_src] = grp.reshape(-1)
     table[off_src: off_src + len(src_list)] = src_list
-    table[off_rows: off_ops] = np.asarray(row_recs, np.int32).reshape(-1)
-    if op_recs:
-        table[off_ops: off_ops + 2 * len(op_recs)] = np.asarray(op_recs, np.uint32).view(np.int32).reshape(-1)
-    return RegPlan(table=table, n_groups=G, off_src=off_src, off_rows=off_rows, off_ops=off_ops,
-                   max_src=max(len(s_) for _, s_ in groups), group_sources=len(src_list),
+    table[off_rows: off_idx] = np.asarray(row_recs, np.uint32).view(np.int32).reshape(-1)
+    table[off_idx: off_idx + len(idx)] = idx
+    table[off_w: off_w + len(wts)] = np.asarray(wts, np.uint32).view(np.int32)
+    return RegPlan(table=table, n_groups=G, off_src=off_src, off_rows=off_rows, off_idx=off_idx, off_w=off_w,
+                   max_src=max(len(s_) for _, s_ in groups), group_sources=sum(len(s_) for _, s_ in groups),
                    full=build_plan(row_ptr, col, w, out_row, dense=0), rows=len(out_row))
 
 
@@ -464,13 +489,16 @@ def _round_reg(pool_in, pool_out, plan: RegPlan, n, dtype, mode, stream):
     t = plan.table
     if t[plan.off_src: plan.off_rows].max(initial=-1) >= pool_in.shape[0]:
         raise ValueError("plan reads a pool row beyond pool_in")
-    if t[plan.off_rows: plan.off_ops].reshape(-1, 4)[:, 0].max(initial=-1) >= pool_out.shape[0]:
+    if t[plan.off_rows: plan.off_idx].reshape(-1, 4)[:, 0].max(initial=-1) >= pool_out.shape[0]:
         raise ValueError("plan writes a pool row beyond pool_out")
     L = _lib.load()
+    offs = plan.src_offsets(pool_in.stride(0) * esz, pool_in.device)
     check(L.tal_agg_round_reg(ctypes.c_void_p(pool_in.data_ptr()), pool_in.stride(0),
                               ctypes.c_void_p(pool_out.data_ptr()), pool_out.stride(0), n, int(bf16),
-                              ctypes.c_void_p(plan.device.data_ptr()), plan.n_groups, plan.off_src,
-                              plan.off_rows, plan.off_ops, plan.max_src, int(mode), _stream(pool_in.device, stream)))
+                              ctypes.c_void_p(plan.device.data_ptr()), ctypes.c_void_p(offs.data_ptr()),
+                              plan.n_groups, plan.off_src,
+                              plan.off_rows, plan.off_idx, plan.off_w, plan.max_src, int(mode),
+                              _stream(pool_in.device, stream)))
     return pool_out
 
 
