@@ -37,11 +37,12 @@ def main():
     torch.cuda.synchronize()
     per_call = (time.perf_counter() - t) / calls * 1e3
     rows = [pool.row_f32(i) for i in range(9)]
-    out = pool.row_f32(8)
+    irows = [pool.row_i64(i) for i in range(9)]
+    out, out_i = pool.row_f32(8), pool.row_i64(8)
     torch.cuda.synchronize()
     t = time.perf_counter()
     for _ in range(calls):
-        ops.agg_f32(rows, w, out)
+        ops.agg_model_f32(rows, irows, w, out, out_i)  # the call's one launch (both segments)
     torch.cuda.synchronize()
     k1 = (time.perf_counter() - t) / calls * 1e3
     print(json.dumps(dict(aggregate_models_ms=round(per_call, 4), bare_k1_ms=round(k1, 4))), flush=True)

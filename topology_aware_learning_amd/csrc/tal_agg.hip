@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -2222,6 +2223,9 @@ __device__ __forceinline__ void reg_one(v2f_t& ca, uint32_t idx, uint64_t w, con
   }
 }
 
+// Output stores with sc1: the line leaves the XCD's L2 instead of staying there (plain / nt
+// stores keep it), so the outputs do not push the sources the other groups of the piece are
+// about to read out of L2 (MI355X_MICROARCH.md, store flavours).
 template <typename T>
 __device__ __forceinline__ void reg_store(T* pout, int64_t ld_out, int32_t row, int64_t col, int64_t n, v2f_t acc) {
   if (col >= n) return;
@@ -2229,10 +2233,10 @@ __device__ __forceinline__ void reg_store(T* pout, int64_t ld_out, int32_t row, 
   if constexpr (kIsBf16<T>) {
     uint32_t q = cvt_bf16x2(acc.x, acc.y);
     if (__builtin_isunordered(acc.x, acc.y)) q = store_bf16x2(acc.x, acc.y);
-    if (col + 1 < n) __builtin_nontemporal_store(q, reinterpret_cast<uint32_t*>(pout + e));
+    if (col + 1 < n) asm volatile("global_store_dword %0, %1, off sc1" : : "v"(pout + e), "v"(q) : "memory");
     else pout[e] = static_cast<uint16_t>(q & 0xffffu);
   } else {
-    if (col + 1 < n) __builtin_nontemporal_store(acc, reinterpret_cast<v2f_t*>(pout + e));
+    if (col + 1 < n) asm volatile("global_store_dwordx2 %0, %1, off sc1" : : "v"(pout + e), "v"(acc) : "memory");
     else pout[e] = acc.x;
   }
 }
@@ -2390,8 +2394,11 @@ int32_t launch_round_reg_nb(const T* pin, int64_t ld_in, T* pout, int64_t ld_out
       return fail(TAL_ERR_HIP, "register round: occupancy query failed");
     blocks_per_cu = std::max(1, blocks_per_cu);
   }
-  // persistent: every resident wave, a multiple of 8 blocks (XCD labels)
-  const int grid = std::max(8, n_cu * blocks_per_cu / 8 * 8);
+  // persistent: every resident wave (TAL_REG_BLOCKS_PER_CU caps it: A/B probes of how many
+  // pieces are in flight per XCD), a multiple of 8 blocks (XCD labels)
+  int bpc = blocks_per_cu;
+  if (const char* e = getenv("TAL_REG_BLOCKS_PER_CU")) bpc = std::max(1, std::min(bpc, atoi(e)));
+  const int grid = std::max(8, n_cu * bpc / 8 * 8);
   k_round_reg<NB, T, EXACT><<<grid, 256, 0, s>>>(pin, ld_in, pout, ld_out, n, table, src_off, n_groups, off_rows,
                                                  off_idx, off_w, n_pieces, grid / 8 * 4);
   return check_launch("register round kernel");
