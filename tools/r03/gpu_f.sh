@@ -11,7 +11,7 @@ for bpc in 3 2 1; do
   timeout -k 10 300 python bench.py $B --plan '{"reg":1}' > $OUT/c5_bpc$bpc.log 2>&1 || { echo FAIL; tail -3 $OUT/c5_bpc$bpc.log; exit 1; }
   python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; print('bpc', sys.argv[2], round(d['roofline']['kernel_ms'],3), d['parity'])" $OUT/c5_bpc$bpc.log $bpc
   cd /tmp
-  timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE WRITE_SIZE --output-format csv -d $OUT/pmc_bpc$bpc -o pmc -- python3 $GRAFT_REPO_ROOT/bench.py $B --plan '{"reg":1}' > $OUT/pmc_bpc$bpc.log 2>&1 || { echo FAIL pmc; exit 1; }
+  timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_bpc$bpc -o pmc -- python3 $GRAFT_REPO_ROOT/bench.py $B --plan '{"reg":1}' > $OUT/pmc_bpc$bpc.log 2>&1 || { echo FAIL pmc; exit 1; }
   f=$(find $OUT/pmc_bpc$bpc -name '*counter_collection.csv' | head -1); python3 $GRAFT_REPO_ROOT/tools/pmc_summary.py "$f" k_round_reg
   cd $GRAFT_REPO_ROOT
 done
