@@ -2202,6 +2202,76 @@ __device__ __forceinline__ void reg_pair_w(v2f_t& ca, v2f_t& cb, const u32x4& A,
   }
 }
 
+// one batch of four operands of ONE row (a pair's longer row past the shorter one's batches, a
+// lone last row): EXACT spaces its dependent adds with s_nop; FMA has an index switch between
+template <int NB, bool EXACT>
+__device__ __forceinline__ void reg_row_u(v2f_t& ca, const u32x4& A, u32x4& NA, uint64_t wa, uint64_t base,
+                                          uint32_t oa, const v32f& X0, const v32f& X1, const v32f& X2,
+                                          const v32f& X3) {
+  if constexpr (EXACT) {
+    v2f_t t0, t1, t2, t3;
+    TAL_RASM("s_load_dwordx4 %[na], %[base], %[oa]\n\t"
+             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
+             "v_pk_mul_f32 %[t0], v[32:33], %[wa] " TAL_LO "\n\t"
+             TAL_MUL("t1", "i1", "wa", TAL_LO) TAL_MUL("t2", "i2", "wa", TAL_LO) TAL_MUL("t3", "i3", "wa", TAL_LO)
+             "s_set_gpr_idx_off\n\t"
+             "v_pk_add_f32 %[ca], %[ca], %[t0]\n\ts_nop 0\n\t"
+             "v_pk_add_f32 %[ca], %[ca], %[t1]\n\ts_nop 0\n\t"
+             "v_pk_add_f32 %[ca], %[ca], %[t2]\n\ts_nop 0\n\t"
+             "v_pk_add_f32 %[ca], %[ca], %[t3]\n\t"
+             "s_waitcnt lgkmcnt(0)",
+             ([ca] "+v"(ca), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [na] "=&s"(NA)),
+             ([i0] "s"(A[0]), [i1] "s"(A[1]), [i2] "s"(A[2]), [i3] "s"(A[3]), [base] "s"(base), [oa] "s"(oa),
+              [wa] "s"(wa)));
+  } else {
+    TAL_RASM("s_load_dwordx4 %[na], %[base], %[oa]\n\t"
+             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
+             "v_pk_fma_f32 %[ca], v[32:33], %[wa], %[ca] " TAL_LO3 "\n\t"
+             TAL_FMA("ca", "i1", "wa", TAL_LO3) TAL_FMA("ca", "i2", "wa", TAL_LO3) TAL_FMA("ca", "i3", "wa", TAL_LO3)
+             "s_set_gpr_idx_off\n\t"
+             "s_waitcnt lgkmcnt(0)",
+             ([ca] "+v"(ca), [na] "=&s"(NA)),
+             ([i0] "s"(A[0]), [i1] "s"(A[1]), [i2] "s"(A[2]), [i3] "s"(A[3]), [base] "s"(base), [oa] "s"(oa),
+              [wa] "s"(wa)));
+  }
+}
+
+template <int NB, bool EXACT>
+__device__ __forceinline__ void reg_row_w(v2f_t& ca, const u32x4& A, u32x4& NA, const u64x2& WA, u64x2& NWA,
+                                          uint64_t base, uint32_t oa, uint32_t owa, const v32f& X0, const v32f& X1,
+                                          const v32f& X2, const v32f& X3) {
+  const uint64_t wa01 = WA[0], wa23 = WA[1];
+  if constexpr (EXACT) {
+    v2f_t t0, t1, t2, t3;
+    TAL_RASM("s_load_dwordx4 %[na], %[base], %[oa]\n\t"
+             "s_load_dwordx4 %[nwa], %[base], %[owa]\n\t"
+             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
+             "v_pk_mul_f32 %[t0], v[32:33], %[wa01] " TAL_LO "\n\t"
+             TAL_MUL("t1", "i1", "wa01", TAL_HI) TAL_MUL("t2", "i2", "wa23", TAL_LO) TAL_MUL("t3", "i3", "wa23", TAL_HI)
+             "s_set_gpr_idx_off\n\t"
+             "v_pk_add_f32 %[ca], %[ca], %[t0]\n\ts_nop 0\n\t"
+             "v_pk_add_f32 %[ca], %[ca], %[t1]\n\ts_nop 0\n\t"
+             "v_pk_add_f32 %[ca], %[ca], %[t2]\n\ts_nop 0\n\t"
+             "v_pk_add_f32 %[ca], %[ca], %[t3]\n\t"
+             "s_waitcnt lgkmcnt(0)",
+             ([ca] "+v"(ca), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [na] "=&s"(NA),
+              [nwa] "=&s"(NWA)),
+             ([i0] "s"(A[0]), [i1] "s"(A[1]), [i2] "s"(A[2]), [i3] "s"(A[3]), [base] "s"(base), [oa] "s"(oa),
+              [owa] "s"(owa), [wa01] "s"(wa01), [wa23] "s"(wa23)));
+  } else {
+    TAL_RASM("s_load_dwordx4 %[na], %[base], %[oa]\n\t"
+             "s_load_dwordx4 %[nwa], %[base], %[owa]\n\t"
+             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
+             "v_pk_fma_f32 %[ca], v[32:33], %[wa01], %[ca] " TAL_LO3 "\n\t"
+             TAL_FMA("ca", "i1", "wa01", TAL_HI3) TAL_FMA("ca", "i2", "wa23", TAL_LO3) TAL_FMA("ca", "i3", "wa23", TAL_HI3)
+             "s_set_gpr_idx_off\n\t"
+             "s_waitcnt lgkmcnt(0)",
+             ([ca] "+v"(ca), [na] "=&s"(NA), [nwa] "=&s"(NWA)),
+             ([i0] "s"(A[0]), [i1] "s"(A[1]), [i2] "s"(A[2]), [i3] "s"(A[3]), [base] "s"(base), [oa] "s"(oa),
+              [owa] "s"(owa), [wa01] "s"(wa01), [wa23] "s"(wa23)));
+  }
+}
+
 // one operand of one row (the rows' tails past their common batches, a lone last row): weight
 // in the low dword of w
 template <int NB, bool EXACT>
@@ -2300,77 +2370,89 @@ __global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, in
 #ifdef TAL_PROBE_REG_NOCOMP  // A/B probe: the stores without the row arithmetic
     for (; r < nr; ++r) reg_store<T>(pout, ld_out, tab[off_rows + 4 * (r0 + r)], col, n, v2f_t{0.f, 0.f});
 #endif
-    for (; r + 1 < nr; r += 2) {
+    // rows in pairs (the plan sorts a group's rows by operand count, descending: A >= B);
+    // every operand list is read 4 dwords at a time, the next 4 prefetched by the batch that
+    // consumes the current ones, so after the batches the registers hold the 1-3 operand tail
+    for (; r < nr; r += 2) {
+      const bool pair = r + 1 < nr;
       const int ra = off_rows + 4 * (r0 + r);
       const int oa_row = tab[ra], fa = tab[ra + 1], qa = tab[ra + 2];
-      const int ob_row = tab[ra + 4], fb = tab[ra + 5], qb = tab[ra + 6];
-      const uint64_t wa = static_cast<uint32_t>(tab[ra + 3]), wb = static_cast<uint32_t>(tab[ra + 7]);
+      const int ob_row = pair ? tab[ra + 4] : -1, fb = pair ? tab[ra + 5] : 0, qb = pair ? tab[ra + 6] : qa;
+      const uint64_t wa = static_cast<uint32_t>(tab[ra + 3]), wb = pair ? static_cast<uint32_t>(tab[ra + 7]) : 0u;
       const bool per_op = ((fa | fb) & static_cast<int>(kRegPerOp)) != 0;
       const int na = fa & ~static_cast<int>(kRegPerOp), nb = fb & ~static_cast<int>(kRegPerOp);
       v2f_t ca = {-0.f, -0.f}, cb = {-0.f, -0.f};
-      const int common = min(na, nb) / 4;
-      if (common > 0) {
-        // dword offsets stay 4-aligned only when qa, qb are: the table pads every row's
-        // operand list to a multiple of 4 dwords
-        u32x4 A = {static_cast<uint32_t>(tab[off_idx + qa]), static_cast<uint32_t>(tab[off_idx + qa + 1]),
-                   static_cast<uint32_t>(tab[off_idx + qa + 2]), static_cast<uint32_t>(tab[off_idx + qa + 3])};
-        u32x4 B = {static_cast<uint32_t>(tab[off_idx + qb]), static_cast<uint32_t>(tab[off_idx + qb + 1]),
-                   static_cast<uint32_t>(tab[off_idx + qb + 2]), static_cast<uint32_t>(tab[off_idx + qb + 3])};
-        uint32_t oa = 4u * static_cast<uint32_t>(off_idx + qa + 4), ob = 4u * static_cast<uint32_t>(off_idx + qb + 4);
-        if (!per_op) {
-          // two batches per trip, the operand registers ping-ponging between A/B and NA/NB2
-          // (a one-batch loop copied NA -> A with eight s_mov per batch)
-          int k = 0;
-          for (; k + 2 <= common; k += 2) {
-            u32x4 NA, NB2;
-            reg_pair_u<NB, EXACT>(ca, cb, A, B, NA, NB2, wa, wb, base, oa, ob, X0, X1, X2, X3);
-            reg_pair_u<NB, EXACT>(ca, cb, NA, NB2, A, B, wa, wb, base, oa + 16u, ob + 16u, X0, X1, X2, X3);
-            oa += 32u;
-            ob += 32u;
-          }
-          if (k < common) {
-            u32x4 NA, NB2;
-            reg_pair_u<NB, EXACT>(ca, cb, A, B, NA, NB2, wa, wb, base, oa, ob, X0, X1, X2, X3);
-          }
-        } else {  // row weights replicated per operand by the plan when only one row is per-op
-          u64x2 WA = {tab64[(off_w + qa) / 2], tab64[(off_w + qa) / 2 + 1]};
-          u64x2 WB = {tab64[(off_w + qb) / 2], tab64[(off_w + qb) / 2 + 1]};
-          uint32_t owa = 4u * static_cast<uint32_t>(off_w + qa + 4), owb = 4u * static_cast<uint32_t>(off_w + qb + 4);
-          for (int k = 0; k < common; ++k) {
-            u32x4 NA, NB2;
-            u64x2 NWA, NWB;
-            reg_pair_w<NB, EXACT>(ca, cb, A, B, NA, NB2, WA, WB, NWA, NWB, base, oa, ob, owa, owb, X0, X1, X2, X3);
-            A = NA;
-            B = NB2;
-            WA = NWA;
-            WB = NWB;
-            oa += 16u;
-            ob += 16u;
-            owa += 16u;
-            owb += 16u;
-          }
+      u32x4 A = {static_cast<uint32_t>(tab[off_idx + qa]), static_cast<uint32_t>(tab[off_idx + qa + 1]),
+                 static_cast<uint32_t>(tab[off_idx + qa + 2]), static_cast<uint32_t>(tab[off_idx + qa + 3])};
+      u32x4 B = {static_cast<uint32_t>(tab[off_idx + qb]), static_cast<uint32_t>(tab[off_idx + qb + 1]),
+                 static_cast<uint32_t>(tab[off_idx + qb + 2]), static_cast<uint32_t>(tab[off_idx + qb + 3])};
+      uint32_t oa = 4u * static_cast<uint32_t>(off_idx + qa + 4), ob = 4u * static_cast<uint32_t>(off_idx + qb + 4);
+      const int common = nb / 4, extra = na / 4 - common;
+      u64x2 WA = {0, 0}, WB = {0, 0};
+      uint32_t owa = 4u * static_cast<uint32_t>(off_w + qa + 4), owb = 4u * static_cast<uint32_t>(off_w + qb + 4);
+      if (!per_op) {
+        // two batches per trip, the operand registers ping-ponging between A/B and NA/NB2
+        // (a one-batch loop copied NA -> A with eight s_mov per batch)
+        int k = 0;
+        for (; k + 2 <= common; k += 2) {
+          u32x4 NA, NB2;
+          reg_pair_u<NB, EXACT>(ca, cb, A, B, NA, NB2, wa, wb, base, oa, ob, X0, X1, X2, X3);
+          reg_pair_u<NB, EXACT>(ca, cb, NA, NB2, A, B, wa, wb, base, oa + 16u, ob + 16u, X0, X1, X2, X3);
+          oa += 32u;
+          ob += 32u;
+        }
+        if (k < common) {
+          u32x4 NA, NB2;
+          reg_pair_u<NB, EXACT>(ca, cb, A, B, NA, NB2, wa, wb, base, oa, ob, X0, X1, X2, X3);
+          A = NA;
+          B = NB2;
+          oa += 16u;
+          ob += 16u;
+        }
+        for (k = 0; k < extra; ++k) {
+          u32x4 NA;
+          reg_row_u<NB, EXACT>(ca, A, NA, wa, base, oa, X0, X1, X2, X3);
+          A = NA;
+          oa += 16u;
+        }
+      } else {
+        WA = u64x2{tab64[(off_w + qa) / 2], tab64[(off_w + qa) / 2 + 1]};
+        WB = u64x2{tab64[(off_w + qb) / 2], tab64[(off_w + qb) / 2 + 1]};
+        for (int k = 0; k < common; ++k) {
+          u32x4 NA, NB2;
+          u64x2 NWA, NWB;
+          reg_pair_w<NB, EXACT>(ca, cb, A, B, NA, NB2, WA, WB, NWA, NWB, base, oa, ob, owa, owb, X0, X1, X2, X3);
+          A = NA;
+          B = NB2;
+          WA = NWA;
+          WB = NWB;
+          oa += 16u;
+          ob += 16u;
+          owa += 16u;
+          owb += 16u;
+        }
+        for (int k = 0; k < extra; ++k) {
+          u32x4 NA;
+          u64x2 NWA;
+          reg_row_w<NB, EXACT>(ca, A, NA, WA, NWA, base, oa, owa, X0, X1, X2, X3);
+          A = NA;
+          WA = NWA;
+          oa += 16u;
+          owa += 16u;
         }
       }
-      for (int k = 4 * common; k < na; ++k)
-        reg_one<NB, EXACT>(ca, static_cast<uint32_t>(tab[off_idx + qa + k]),
-                           per_op ? static_cast<uint32_t>(tab[off_w + qa + k]) : wa, X0, X1, X2, X3);
-      for (int k = 4 * common; k < nb; ++k)
-        reg_one<NB, EXACT>(cb, static_cast<uint32_t>(tab[off_idx + qb + k]),
-                           per_op ? static_cast<uint32_t>(tab[off_w + qb + k]) : wb, X0, X1, X2, X3);
+      // tails (uniform trip counts, constant register indices): a weight per operand sits in
+      // the low (even operand) or high (odd) dword of its pair
+#define TAL_TAIL(C, R, W, REM)                                                                         \
+      if ((REM) > 0) reg_one<NB, EXACT>(C, R[0], per_op ? (W[0] & 0xffffffffull) : w##C, X0, X1, X2, X3); \
+      if ((REM) > 1) reg_one<NB, EXACT>(C, R[1], per_op ? (W[0] >> 32) : w##C, X0, X1, X2, X3);          \
+      if ((REM) > 2) reg_one<NB, EXACT>(C, R[2], per_op ? (W[1] & 0xffffffffull) : w##C, X0, X1, X2, X3);
+      const uint64_t wca = wa, wcb = wb;
+      TAL_TAIL(ca, A, WA, na % 4)
+      TAL_TAIL(cb, B, WB, nb % 4)
+#undef TAL_TAIL
       reg_store<T>(pout, ld_out, oa_row, col, n, ca);
-      reg_store<T>(pout, ld_out, ob_row, col, n, cb);
-    }
-    if (r < nr) {
-      const int ra = off_rows + 4 * (r0 + r);
-      const int oa_row = tab[ra], fa = tab[ra + 1], qa = tab[ra + 2];
-      const bool per_op = (fa & static_cast<int>(kRegPerOp)) != 0;
-      const int na = fa & ~static_cast<int>(kRegPerOp);
-      const uint64_t wa = static_cast<uint32_t>(tab[ra + 3]);
-      v2f_t ca = {-0.f, -0.f};
-      for (int k = 0; k < na; ++k)
-        reg_one<NB, EXACT>(ca, static_cast<uint32_t>(tab[off_idx + qa + k]),
-                           per_op ? static_cast<uint32_t>(tab[off_w + qa + k]) : wa, X0, X1, X2, X3);
-      reg_store<T>(pout, ld_out, oa_row, col, n, ca);
+      if (pair) reg_store<T>(pout, ld_out, ob_row, col, n, cb);
     }
     q += dq;
     g += dg;
