@@ -1,6 +1,6 @@
 # GPU A/B of a library experiment switch: parity tests with the switch on, then config-3 benches
 # (c4 = 32 and 16 narrow plans) with it off / on, twice, and config 5 off / on.
-# Usage: bash tools/gpu_ab_env.sh <tag> <VAR> <value>   (uses the in-tree library built on the CPU host)
+# Usage: bash profiles/scripts_r01_r02/gpu_ab_env.sh <tag> <VAR> <value>   (uses the in-tree library built on the CPU host)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p $OUT; TAG=$1; VAR=$2; VAL=$3

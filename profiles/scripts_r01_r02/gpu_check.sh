@@ -1,4 +1,4 @@
-# GPU check: kernel parity tests, smoke, bench (short).  Usage: bash tools/gpu_check.sh [tag]
+# GPU check: kernel parity tests, smoke, bench (short).  Usage: bash profiles/scripts_r01_r02/gpu_check.sh [tag]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo BUILD FAILED; exit 1; }

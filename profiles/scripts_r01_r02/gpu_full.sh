@@ -1,5 +1,5 @@
 # Full GPU pass: tests, smoke, bench, rocprofv3 kernel trace + PMC (FETCH_SIZE / WRITE_SIZE).
-# Usage: bash tools/gpu_full.sh <tag>
+# Usage: bash profiles/scripts_r01_r02/gpu_full.sh <tag>
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo BUILD FAILED; exit 1; }

@@ -1,5 +1,5 @@
 # GPU A/B: config-3 round out of place (ping-pong between two pools) vs in place on one pool.
-# Usage: bash tools/gpu_inplace_ab.sh <tag>
+# Usage: bash profiles/scripts_r01_r02/gpu_inplace_ab.sh <tag>
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p $OUT; TAG=${1:-ip}

@@ -1,5 +1,5 @@
 # GPU: kernel parity tests, then config 3 (tuned) and config 5 fp32 / bf16 benches.
-# Usage: bash tools/gpu_k3n_check.sh <tag>   (uses the in-tree library built on the CPU host)
+# Usage: bash profiles/scripts_r01_r02/gpu_k3n_check.sh <tag>   (uses the in-tree library built on the CPU host)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p $OUT; TAG=${1:-k3n}

@@ -1,5 +1,5 @@
 # Config 5 narrow-kernel decomposition: base vs no-arithmetic vs no-HBM-load vs neither (probe
-# builds from tools/build_probe_libs.sh), fp32 exact and bf16 FMA.  Usage: bash tools/gpu_k3n_probe.sh <tag>
+# builds from tools/build_probe_libs.sh), fp32 exact and bf16 FMA.  Usage: bash profiles/scripts_r01_r02/gpu_k3n_probe.sh <tag>
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${1:-k3n}

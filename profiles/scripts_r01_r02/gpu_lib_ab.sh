@@ -1,6 +1,6 @@
 # GPU A/B of two library builds on one box: parity tests with the in-tree library, then config 3
 # and config 5 (fp32, bf16) with the in-tree library and with tools/tune/libtal_agg_base.so
-# swapped in, interleaved.  Usage: bash tools/gpu_lib_ab.sh <tag>
+# swapped in, interleaved.  Usage: bash profiles/scripts_r01_r02/gpu_lib_ab.sh <tag>
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p $OUT; TAG=${1:-lib}

@@ -1,6 +1,6 @@
 # GPU A/B of two library builds on config 5 bf16, EXACT and FMA (in-tree library vs
 # tools/tune/libtal_agg_base.so), interleaved, after the kernel parity tests.
-# Usage: bash tools/gpu_lib_ab_bf16x.sh <tag>
+# Usage: bash profiles/scripts_r01_r02/gpu_lib_ab_bf16x.sh <tag>
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p $OUT; TAG=${1:-libx}

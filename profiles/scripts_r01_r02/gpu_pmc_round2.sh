@@ -1,4 +1,4 @@
-# Activity PMC pass (one run) over one round-plan form: bash tools/gpu_pmc_round2.sh <tag> <run_round.py args...>
+# Activity PMC pass (one run) over one round-plan form: bash profiles/scripts_r01_r02/gpu_pmc_round2.sh <tag> <run_round.py args...>
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p $OUT; TAG=$1; shift

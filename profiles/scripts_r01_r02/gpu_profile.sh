@@ -1,6 +1,6 @@
 # Profiling pass (round 2): the driver's bench command under rocprofv3 --kernel-trace --stats
 # (bench line + kernel trace from ONE process), then FETCH_SIZE / WRITE_SIZE passes per plan
-# spec the tuner can pick, for tools/summarize_r02.py.   Usage: bash tools/gpu_profile.sh <tag>
+# spec the tuner can pick, for tools/summarize_r02.py.   Usage: bash profiles/scripts_r01_r02/gpu_profile.sh <tag>
 set -o pipefail
 TAG=${1:-r02prof}
 R=$GRAFT_REPO_ROOT

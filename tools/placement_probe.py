@@ -2,7 +2,7 @@
 on which allocation it writes?  One input pool and K output pools of config 3's size; the round
 (c4 = 64 sparse plan) is timed into each, `reps` launches per pool in a fixed order, and each
 launch's time is printed as one JSON line so a rocprofv3 --pmc pass of this same process
-(same allocations) can be matched launch by launch (tools/gpu_placement.sh).
+(same allocations) can be matched launch by launch (profiles/scripts_r01_r02/gpu_placement.sh).
 
 Usage: python tools/placement_probe.py [K] [reps]"""
 import json

@@ -1,4 +1,4 @@
-"""Summarize a round-2 profiling pass (tools/gpu_profile.sh) into profiles/<sub>/ and
+"""Summarize a round-2 profiling pass (profiles/scripts_r01_r02/gpu_profile.sh) into profiles/<sub>/ and
 profiles/traffic.json.
 
 Inputs under gpurun_out/<tag>/:
