@@ -2323,7 +2323,8 @@ __global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, in
                                                    int64_t ld_out, int64_t n, const int32_t* __restrict__ table,
                                                    const int64_t* __restrict__ src_off, int32_t n_groups,
                                                    int32_t off_rows, int32_t off_idx, int32_t off_w,
-                                                   int32_t n_pieces, int32_t waves_per_label) {
+                                                   int32_t n_pieces, int32_t waves_per_label,
+                                                   int32_t* __restrict__ ticket) {
   constexpr bool kB = kIsBf16<T>;
   constexpr int kEs = kB ? 2 : 4;
   const ConstI32 tab = (ConstI32)table;
@@ -2336,10 +2337,25 @@ __global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, in
   const int wx = static_cast<int>(blockIdx.x >> 3) * 4 + wave;
   const int pieces_l = n_pieces > label ? (n_pieces - 1 - label) / 8 + 1 : 0;
   const int items = pieces_l * n_groups;
-  int q = wx / n_groups, g = wx - (wx / n_groups) * n_groups;
-  const int dq = waves_per_label / n_groups, dg = waves_per_label - dq * n_groups;
+  // Items are dealt in order by a per-label ticket counter (one atomic per item, fetched one item
+  // ahead), so the items in flight on an XCD stay a window of consecutive pieces: with a static
+  // round-robin the waves drift apart over thousands of items and the groups of one piece no
+  // longer meet in L2.
+  int32_t* my_ticket = ticket + 16 * label;  // 64 B apart
+  auto take = [&]() {
+    int t = 0;
+    if (lane == 0) t = __hip_atomic_fetch_add(my_ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readfirstlane(t);
+  };
+  (void)wx;
+  (void)waves_per_label;
+  int s_next = take();
   v32f X0, X1, X2, X3;
-  for (int s = wx; s < items; s += waves_per_label) {
+  for (;;) {
+    const int s = s_next;
+    if (s >= items) break;
+    s_next = take();
+    const int q = s / n_groups, g = s - q * n_groups;
     const int piece = q * 8 + label;
     const int s0 = tab[4 * g], ns = tab[4 * g + 1], r0 = tab[4 * g + 2], nr = tab[4 * g + 3];
     const int64_t col = static_cast<int64_t>(piece) * kRegPiece + 2 * lane;
@@ -2454,13 +2470,27 @@ __global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, in
       reg_store<T>(pout, ld_out, oa_row, col, n, ca);
       if (pair) reg_store<T>(pout, ld_out, ob_row, col, n, cb);
     }
-    q += dq;
-    g += dg;
-    if (g >= n_groups) {
-      g -= n_groups;
-      ++q;
-    }
   }
+}
+
+// The register round's item tickets: eight counters 64 B apart, one per XCD label, reset on the
+// stream before each launch.  The library's only device allocation: 512 B per device, made once.
+constexpr size_t kRegTicketBytes = 8 * 64;
+
+int32_t reg_tickets(int32_t** out) {
+  static std::mutex mu;
+  static std::vector<int32_t*> per_dev;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(TAL_ERR_HIP, "register round: no current device");
+  std::lock_guard<std::mutex> lk(mu);
+  if (per_dev.size() <= static_cast<size_t>(dev)) per_dev.resize(dev + 1, nullptr);
+  if (!per_dev[dev]) {
+    void* p = nullptr;
+    if (hipMalloc(&p, kRegTicketBytes) != hipSuccess) return fail(TAL_ERR_HIP, "register round: ticket allocation failed");
+    per_dev[dev] = static_cast<int32_t*>(p);
+  }
+  *out = per_dev[dev];
+  return TAL_OK;
 }
 
 template <int NB, typename T, bool EXACT>
@@ -2481,8 +2511,12 @@ int32_t launch_round_reg_nb(const T* pin, int64_t ld_in, T* pout, int64_t ld_out
   int bpc = blocks_per_cu;
   if (const char* e = getenv("TAL_REG_BLOCKS_PER_CU")) bpc = std::max(1, std::min(bpc, atoi(e)));
   const int grid = std::max(8, n_cu * bpc / 8 * 8);
+  int32_t* ticket = nullptr;
+  if (int32_t rc = reg_tickets(&ticket)) return rc;
+  if (hipMemsetAsync(ticket, 0, kRegTicketBytes, s) != hipSuccess)
+    return fail(TAL_ERR_HIP, "register round: ticket reset failed");
   k_round_reg<NB, T, EXACT><<<grid, 256, 0, s>>>(pin, ld_in, pout, ld_out, n, table, src_off, n_groups, off_rows,
-                                                 off_idx, off_w, n_pieces, grid / 8 * 4);
+                                                 off_idx, off_w, n_pieces, grid / 8 * 4, ticket);
   return check_launch("register round kernel");
 }
 
