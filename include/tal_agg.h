@@ -236,19 +236,22 @@ int32_t tal_agg_round_bf16(const uint16_t* pool_in, int64_t ld_in, uint16_t* poo
  * operand read from the registers by the VGPR index mode (no LDS, no barrier).  Same results
  * as tal_agg_round_f32 (EXACT: bitwise the reference; FMA: bitwise K1-FMA); bf16 pools (bf16 !=
  * 0) in FMA mode only.  Out of place (pool_in != pool_out).  Pools 2-element aligned, even ld
- * >= n rounded up to even.  table_dev (int32): n_groups records {first source, sources, first
- * row, rows}; at off_src the source pool rows, every group's list padded to 16 x ceil(max_src /
- * 16) entries (src_off_dev: int64 byte offsets of those entries, row x ld_in x element size); at off_rows (a multiple of 4) row records {out
- * row, operands | 0x40000000 when the row's weights are per operand, first operand, fp32 row
- * weight}, a group's rows consecutive; at off_idx (a multiple of 4) every operand's register
- * offset (2 x slot of its source in the group), at off_w (a multiple of 4) every operand's fp32
- * weight; each row's operands start 4-aligned; each array is followed by 8 dwords of padding.
- * max_src = the largest group's sources (<= 64).  Replaces decentralized_client.py:399-413 for
- * every row of the round at once (snapshot semantics, as tal_agg_round_f32). */
+ * >= n rounded up to even; table_dev 64-B aligned.  table_dev (int32): n_groups records {first
+ * source, sources, first pair, pairs}; at off_src the source pool rows, every group's list
+ * padded to 16 x NB entries, NB = ceil(max_src / 16) (src_off_dev: int64 byte offsets of those
+ * entries, row x ld_in x element size); at off_pairs (a multiple of 4) row-pair records {out
+ * row A, out row B or -1, trips, byte offset from table_dev of the pair's first trip record}, a
+ * group's pairs consecutive; at off_rec (a multiple of 16) trip records of 16 dwords {A's four
+ * operand register offsets (2 x the source's slot in the group), B's four, A's four fp32
+ * weights, B's four}, a row padded to its pair's trips with the neutral operand (offset 32 x
+ * NB, weight +0.0: a -0.0 product that leaves the sum unchanged), followed by one record of
+ * padding.  max_src = the largest group's sources (<= 64).  Replaces
+ * decentralized_client.py:399-413 for every row of the round at once (snapshot semantics, as
+ * tal_agg_round_f32). */
 int32_t tal_agg_round_reg(const void* pool_in, int64_t ld_in, void* pool_out, int64_t ld_out,
                           int64_t n, int32_t bf16, const int32_t* table_dev, const int64_t* src_off_dev,
-                          int32_t n_groups, int32_t off_src, int32_t off_rows, int32_t off_idx,
-                          int32_t off_w, int32_t max_src, int32_t mode, void* stream);
+                          int32_t n_groups, int32_t off_src, int32_t off_pairs, int32_t off_rec,
+                          int32_t max_src, int32_t mode, void* stream);
 
 /* ---- K2: cosine similarity of two models' parameters, bit for bit -------------------------
  * Reference: cosine_similarity, decentralized_client.py:661-681: for each parameter tensor

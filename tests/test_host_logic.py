@@ -603,10 +603,11 @@ def test_link_model_matches_design_table():
 
 def test_reg_plan_table_layout():
     """build_reg_plan (K3r): every row in exactly one group, each group's operands among its
-    <= 64 sources (the list padded to 16 x NB entries with its first source), records in
-    reference order as 2 x slot with the fp32 weights alongside, rows in pair order (operand
-    count descending), each row's operands 4-aligned, 8 dwords of padding after each array, the
-    per-operand flag exactly on rows whose weights differ (tal_agg.h K3r layout)."""
+    <= 64 sources (the list padded to 16 x NB entries with its first source), rows paired in
+    operand-count order, each pair's trip records {A idx x4, B idx x4, A w x4, B w x4} holding
+    the rows' operands in reference order as 2 x slot with their fp32 weights, the rest of a
+    pair's trips the neutral operand (offset 32 x NB, weight +0.0), one record of read-ahead
+    padding after the last (tal_agg.h K3r layout)."""
     import bench
     from oracle import reference_alg as ra
     from topology_aware_learning_amd import ops
@@ -617,30 +618,40 @@ def test_reg_plan_table_layout():
         out_rows = np.arange(len(orders), dtype=np.int32)[::-1].copy()
         p = ops.build_reg_plan(row_ptr, col, w, out_rows)
         t = p.table
-        span = 16 * ((p.max_src + 15) // 16)
+        nb = (p.max_src + 15) // 16
+        span, neutral = 16 * nb, 32 * nb
         grp = t[: 4 * p.n_groups].reshape(-1, 4)
-        recs = t[p.off_rows: p.off_idx].reshape(-1, 4).view(np.uint32)
-        assert p.max_src <= 64 and p.off_rows % 4 == 0 and p.off_idx % 4 == 0 and p.off_w % 4 == 0
-        assert p.off_w - p.off_idx >= 8 and len(t) - p.off_w >= 8
+        pairs = p.pair_records()
+        assert p.max_src <= 64 and p.off_pairs % 4 == 0 and p.off_rec % 16 == 0
+        assert len(t) == p.off_rec + 16 * (p.trips + 1)
         seen = []
-        for g, (s0, ns, r0, nr) in enumerate(grp):
+        for g, (s0, ns, p0, npair) in enumerate(grp):
             assert s0 == g * span and ns <= 64
             srcs = t[p.off_src + s0: p.off_src + s0 + ns]
             assert list(srcs) == sorted(set(srcs.tolist()))
             assert np.all(t[p.off_src + s0 + ns: p.off_src + s0 + span] == srcs[0])
-            counts = recs[r0: r0 + nr, 1] & ~np.uint32(ops.REG_PER_OP)
-            assert list(counts) == sorted(counts, reverse=True)
-            for out, flag, q0, wrow in recs[r0: r0 + nr]:
-                r = int(np.flatnonzero(out_rows == out)[0])
-                seen.append(r)
-                cnt = flag & ~np.uint32(ops.REG_PER_OP)
-                assert cnt == len(orders[r]) and q0 % 4 == 0
-                w32 = np.float32(ws[r]).view(np.uint32)
-                assert bool(flag & ops.REG_PER_OP) == bool(np.any(w32 != w32[0])) and wrow == w32[0]
-                for k in range(cnt):
-                    reg = t[p.off_idx + q0 + k]
-                    assert reg % 2 == 0 and srcs[reg // 2] == orders[r][k]
-                    assert t[p.off_w + q0 + k].view(np.uint32) == w32[k]
+            counts = []
+            for k, (oa, ob, trips, boff) in enumerate(pairs[p0: p0 + npair]):
+                assert boff % 64 == 0 and trips >= 1
+                rec = t[boff // 4: boff // 4 + 16 * trips].reshape(trips, 16)
+                idx_a, idx_b = rec[:, 0:4].reshape(-1), rec[:, 4:8].reshape(-1)
+                w_a, w_b = rec[:, 8:12].reshape(-1).view(np.uint32), rec[:, 12:16].reshape(-1).view(np.uint32)
+                assert ob >= 0 or k == npair - 1
+                lens = []
+                for out, idx, wv in ((oa, idx_a, w_a), (ob, idx_b, w_b)):
+                    if out < 0:
+                        assert np.all(idx == neutral) and np.all(wv == 0)
+                        continue
+                    r = int(np.flatnonzero(out_rows == out)[0])
+                    seen.append(r)
+                    m = len(orders[r])
+                    lens.append(m)
+                    assert [srcs[i // 2] for i in idx[:m]] == list(orders[r]) and np.all(idx[:m] % 2 == 0)
+                    assert np.array_equal(wv[:m], np.float32(ws[r]).view(np.uint32))
+                    assert np.all(idx[m:] == neutral) and np.all(wv[m:] == 0)
+                assert trips == (max(lens) + 3) // 4
+                counts.extend(lens)
+            assert counts == sorted(counts, reverse=True)
         assert sorted(seen) == list(range(len(orders)))
     assert ops.build_reg_plan(row_ptr, col, w, out_rows, max_src=8) is None  # a row has 9+ sources
 

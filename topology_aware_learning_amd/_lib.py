@@ -27,7 +27,7 @@ TAL_ERR_COMM = 4
 TAL_COMM_ID_BYTES = 128
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 EXPORTED = (
     "tal_last_error",
@@ -137,7 +137,7 @@ _SIGS = {
     "tal_agg_round_i64": (_I32, [_P, _I64, _P, _I64, _I64, _P, ctypes.POINTER(RoundPlanInfo), _P]),
     "tal_agg_round_bf16": (_I32, [_P, _I64, _P, _I64, _I64, _P, ctypes.POINTER(RoundPlanInfo), _I32, _P]),
     "tal_agg_round_clique_f32": (_I32, [_P, _I64, _P, _I64, _I64, _P, _I32, _I32, _I32, _P]),
-    "tal_agg_round_reg": (_I32, [_P, _I64, _P, _I64, _I64, _I32, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _P]),
+    "tal_agg_round_reg": (_I32, [_P, _I64, _P, _I64, _I64, _I32, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P]),
     "tal_cosine_plan_words": (_I64, [_PI64, _I32]),
     "tal_cosine_plan_build": (_I32, [_PI64, _I32, _PI64, _I64, _PI32]),
     "tal_cosine_scratch_bytes": (_I64, [_PI64, _I32]),

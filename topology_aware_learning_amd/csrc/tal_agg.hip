@@ -44,7 +44,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 16;
+constexpr int kAbiVersion = 17;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -2097,200 +2097,116 @@ __device__ __forceinline__ void reg_wait(v32f& X0, v32f& X1, v32f& X2, v32f& X3)
   }
 }
 
-// Operands: a row's sources as register offsets (2 x slot, one dword each) in `idx`, its
-// weights either one per row (row record) or one per operand in `wts` (fp32 bits, parallel to
-// idx).  A weight reaches the packed multiply as a 64-bit SGPR pair: op_sel_hi:[1,0] makes both
-// halves take its low dword, op_sel:[0,1] op_sel_hi:[1,1] its high dword (so one aligned pair
-// serves two operands' weights).  The asm blocks also read the NEXT batch's operand dwords
-// (s_load with a byte offset from the table base) while they compute and drain lgkmcnt at the
-// end; a batch is four operands of each of two rows, the two rows' chains interleaved so no
+// Operands come in RECORDS of 16 dwords, one per trip of a row pair (A, B): {A's four register
+// offsets, B's four, A's four fp32 weights, B's four}; a register offset is 2 x the source's slot
+// in the group, and a row with fewer operands than its trips hold is padded with the NEUTRAL
+// operand (offset 32 x NB: the register pair held at -0.0 past the sources, weight +0.0), whose
+// product -0.0 leaves any accumulator unchanged (x + -0 = x, also for x = +0 and NaN; fma(0,
+// -0, x) = x).  A pair's trips run as ONE inline-asm loop: the next record is read into the
+// other half of s[40:71] (s_load_dwordx16) while the current one computes, so a trip is one
+// scalar load, the index switch per operand and four loop instructions — no copies, no address
+// arithmetic per operand (v3's per-operand SALU stream was the kernel's limit).  A weight
+// reaches the packed multiply as a 64-bit SGPR pair: op_sel_hi:[1,0] broadcasts its low dword,
+// op_sel:[0,1] op_sel_hi:[1,1] its high dword.  The two rows' chains are interleaved, so no
 // packed instruction reads the result of the one right before it (gfx950 needs a wait state
 // there).  M0, which the index mode writes, is used by nothing else in this kernel (no LDS).
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
-#define TAL_MUL(T, I, W, SEL) "s_set_gpr_idx_idx %[" I "]\n\tv_pk_mul_f32 %[" T "], v[32:33], %[" W "] " SEL "\n\t"
-#define TAL_FMA(C, I, W, SEL) "s_set_gpr_idx_idx %[" I "]\n\tv_pk_fma_f32 %[" C "], v[32:33], %[" W "], %[" C "] " SEL "\n\t"
-#define TAL_LO "op_sel_hi:[1,0]"
-#define TAL_HI "op_sel:[0,1] op_sel_hi:[1,1]"
-#define TAL_LO3 "op_sel_hi:[1,0,1]"
-#define TAL_HI3 "op_sel:[0,1,0] op_sel_hi:[1,1,1]"
-#define TAL_ADDS                                                                            \
-  "v_pk_add_f32 %[ca], %[ca], %[t0]\n\tv_pk_add_f32 %[cb], %[cb], %[t4]\n\t"                \
-  "v_pk_add_f32 %[ca], %[ca], %[t1]\n\tv_pk_add_f32 %[cb], %[cb], %[t5]\n\t"                \
-  "v_pk_add_f32 %[ca], %[ca], %[t2]\n\tv_pk_add_f32 %[cb], %[cb], %[t6]\n\t"                \
+// one trip: i* / j* = A's / B's index SGPRs, wa* / wb* = their weight pairs
+#define TAL_TRIP_E(i0, i1, i2, i3, j0, j1, j2, j3, wa01, wa23, wb01, wb23)                            \
+  "s_set_gpr_idx_on " i0 ", gpr_idx(SRC0)\n\t"                                                          \
+  "v_pk_mul_f32 %[t0], v[32:33], " wa01 " op_sel_hi:[1,0]\n\t"                                          \
+  "s_set_gpr_idx_idx " j0 "\n\tv_pk_mul_f32 %[t4], v[32:33], " wb01 " op_sel_hi:[1,0]\n\t"              \
+  "s_set_gpr_idx_idx " i1 "\n\tv_pk_mul_f32 %[t1], v[32:33], " wa01 " op_sel:[0,1] op_sel_hi:[1,1]\n\t" \
+  "s_set_gpr_idx_idx " j1 "\n\tv_pk_mul_f32 %[t5], v[32:33], " wb01 " op_sel:[0,1] op_sel_hi:[1,1]\n\t" \
+  "s_set_gpr_idx_idx " i2 "\n\tv_pk_mul_f32 %[t2], v[32:33], " wa23 " op_sel_hi:[1,0]\n\t"              \
+  "s_set_gpr_idx_idx " j2 "\n\tv_pk_mul_f32 %[t6], v[32:33], " wb23 " op_sel_hi:[1,0]\n\t"              \
+  "s_set_gpr_idx_idx " i3 "\n\tv_pk_mul_f32 %[t3], v[32:33], " wa23 " op_sel:[0,1] op_sel_hi:[1,1]\n\t" \
+  "s_set_gpr_idx_idx " j3 "\n\tv_pk_mul_f32 %[t7], v[32:33], " wb23 " op_sel:[0,1] op_sel_hi:[1,1]\n\t" \
+  "s_set_gpr_idx_off\n\t"                                                                               \
+  "v_pk_add_f32 %[ca], %[ca], %[t0]\n\tv_pk_add_f32 %[cb], %[cb], %[t4]\n\t"                            \
+  "v_pk_add_f32 %[ca], %[ca], %[t1]\n\tv_pk_add_f32 %[cb], %[cb], %[t5]\n\t"                            \
+  "v_pk_add_f32 %[ca], %[ca], %[t2]\n\tv_pk_add_f32 %[cb], %[cb], %[t6]\n\t"                            \
   "v_pk_add_f32 %[ca], %[ca], %[t3]\n\tv_pk_add_f32 %[cb], %[cb], %[t7]\n\t"
-#define TAL_IDX_INS                                                                                     \
-  [i0] "s"(A[0]), [i1] "s"(A[1]), [i2] "s"(A[2]), [i3] "s"(A[3]), [j0] "s"(B[0]), [j1] "s"(B[1]),        \
-      [j2] "s"(B[2]), [j3] "s"(B[3]), [base] "s"(base), [oa] "s"(oa), [ob] "s"(ob)
+#define TAL_TRIP_F(i0, i1, i2, i3, j0, j1, j2, j3, wa01, wa23, wb01, wb23)                                          \
+  "s_set_gpr_idx_on " i0 ", gpr_idx(SRC0)\n\t"                                                                        \
+  "v_pk_fma_f32 %[ca], v[32:33], " wa01 ", %[ca] op_sel_hi:[1,0,1]\n\t"                                               \
+  "s_set_gpr_idx_idx " j0 "\n\tv_pk_fma_f32 %[cb], v[32:33], " wb01 ", %[cb] op_sel_hi:[1,0,1]\n\t"                   \
+  "s_set_gpr_idx_idx " i1 "\n\tv_pk_fma_f32 %[ca], v[32:33], " wa01 ", %[ca] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"    \
+  "s_set_gpr_idx_idx " j1 "\n\tv_pk_fma_f32 %[cb], v[32:33], " wb01 ", %[cb] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"    \
+  "s_set_gpr_idx_idx " i2 "\n\tv_pk_fma_f32 %[ca], v[32:33], " wa23 ", %[ca] op_sel_hi:[1,0,1]\n\t"                   \
+  "s_set_gpr_idx_idx " j2 "\n\tv_pk_fma_f32 %[cb], v[32:33], " wb23 ", %[cb] op_sel_hi:[1,0,1]\n\t"                   \
+  "s_set_gpr_idx_idx " i3 "\n\tv_pk_fma_f32 %[ca], v[32:33], " wa23 ", %[ca] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"    \
+  "s_set_gpr_idx_idx " j3 "\n\tv_pk_fma_f32 %[cb], v[32:33], " wb23 ", %[cb] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"    \
+  "s_set_gpr_idx_off\n\t"
+#define TAL_TRIP_P(TRIP) TRIP("s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s[48:49]", "s[50:51]", "s[52:53]", "s[54:55]")
+#define TAL_TRIP_Q(TRIP) TRIP("s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s[64:65]", "s[66:67]", "s[68:69]", "s[70:71]")
+// the pair loop over records at byte offsets off, off + 64, ... (from the table base), last =
+// off + 64 x trips: after a trip the offset register points one past the record being loaded,
+// i.e. at off + 64 (k + 2) after record k, and record k + 1 exists iff that is <= last
+#define TAL_PAIR_LOOP(TRIP)                                     \
+  "s_load_dwordx16 s[40:55], %[base], %[off]\n\t"                \
+  "s_add_u32 %[off], %[off], 64\n\t"                             \
+  "s_waitcnt lgkmcnt(0)\n"                                       \
+  "1:\n\t"                                                       \
+  "s_load_dwordx16 s[56:71], %[base], %[off]\n\t"                \
+  "s_add_u32 %[off], %[off], 64\n\t" TAL_TRIP_P(TRIP)           \
+  "s_cmp_le_u32 %[off], %[last]\n\t"                             \
+  "s_waitcnt lgkmcnt(0)\n\t"                                     \
+  "s_cbranch_scc0 2f\n\t"                                        \
+  "s_load_dwordx16 s[40:55], %[base], %[off]\n\t"                \
+  "s_add_u32 %[off], %[off], 64\n\t" TAL_TRIP_Q(TRIP)           \
+  "s_cmp_le_u32 %[off], %[last]\n\t"                             \
+  "s_waitcnt lgkmcnt(0)\n\t"                                     \
+  "s_cbranch_scc1 1b\n"                                          \
+  "2:"
+#define TAL_REC_CLOBBERS                                                                                    \
+  "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", \
+      "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68",     \
+      "s69", "s70", "s71", "scc"
 
-// one batch, row weights (uniform per row): wa / wb = the rows' weights in the low dword
 template <int NB, bool EXACT>
-__device__ __forceinline__ void reg_pair_u(v2f_t& ca, v2f_t& cb, const u32x4& A, const u32x4& B, u32x4& NA,
-                                           u32x4& NB2, uint64_t wa, uint64_t wb, uint64_t base, uint32_t oa,
-                                           uint32_t ob, const v32f& X0, const v32f& X1, const v32f& X2,
-                                           const v32f& X3) {
+__device__ __forceinline__ void reg_pair(v2f_t& ca, v2f_t& cb, uint64_t base, uint32_t off, uint32_t last,
+                                         const v32f& X0, const v32f& X1, const v32f& X2, const v32f& X3,
+                                         const v2f_t& Z) {
+#define TAL_PASM(TMPL, OUTS, ZR)                                                                             \
+  do {                                                                                                       \
+    if constexpr (NB == 1)                                                                                   \
+      asm volatile(TMPL : TAL_UNP OUTS : [base] "s"(base), [last] "s"(last), TAL_RX1, ZR(Z) : TAL_REC_CLOBBERS); \
+    else if constexpr (NB == 2)                                                                              \
+      asm volatile(TMPL : TAL_UNP OUTS : [base] "s"(base), [last] "s"(last), TAL_RX2, ZR(Z) : TAL_REC_CLOBBERS); \
+    else if constexpr (NB == 3)                                                                              \
+      asm volatile(TMPL : TAL_UNP OUTS : [base] "s"(base), [last] "s"(last), TAL_RX3, ZR(Z) : TAL_REC_CLOBBERS); \
+    else                                                                                                     \
+      asm volatile(TMPL : TAL_UNP OUTS : [base] "s"(base), [last] "s"(last), TAL_RX4, ZR(Z) : TAL_REC_CLOBBERS); \
+  } while (0)
+#define TAL_Z1 "{v[64:65]}"
+#define TAL_Z2 "{v[96:97]}"
+#define TAL_Z3 "{v[128:129]}"
+#define TAL_Z4 "{v[160:161]}"
   if constexpr (EXACT) {
     v2f_t t0, t1, t2, t3, t4, t5, t6, t7;
-    TAL_RASM("s_load_dwordx4 %[na], %[base], %[oa]\n\t"
-             "s_load_dwordx4 %[nb], %[base], %[ob]\n\t"
-             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
-             "v_pk_mul_f32 %[t0], v[32:33], %[wa] " TAL_LO "\n\t"
-             TAL_MUL("t1", "i1", "wa", TAL_LO) TAL_MUL("t2", "i2", "wa", TAL_LO) TAL_MUL("t3", "i3", "wa", TAL_LO)
-             TAL_MUL("t4", "j0", "wb", TAL_LO) TAL_MUL("t5", "j1", "wb", TAL_LO) TAL_MUL("t6", "j2", "wb", TAL_LO)
-             TAL_MUL("t7", "j3", "wb", TAL_LO)
-             "s_set_gpr_idx_off\n\t" TAL_ADDS
-             "s_waitcnt lgkmcnt(0)",
-             ([ca] "+v"(ca), [cb] "+v"(cb), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
-              [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7), [na] "=&s"(NA), [nb] "=&s"(NB2)),
-             (TAL_IDX_INS, [wa] "s"(wa), [wb] "s"(wb)));
+#define TAL_OUTS_E                                                                                          \
+  ([ca] "+v"(ca), [cb] "+v"(cb), [off] "+s"(off), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2),           \
+   [t3] "=&v"(t3), [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7))
+    if constexpr (NB == 1) TAL_PASM(TAL_PAIR_LOOP(TAL_TRIP_E), TAL_OUTS_E, TAL_Z1);
+    else if constexpr (NB == 2) TAL_PASM(TAL_PAIR_LOOP(TAL_TRIP_E), TAL_OUTS_E, TAL_Z2);
+    else if constexpr (NB == 3) TAL_PASM(TAL_PAIR_LOOP(TAL_TRIP_E), TAL_OUTS_E, TAL_Z3);
+    else TAL_PASM(TAL_PAIR_LOOP(TAL_TRIP_E), TAL_OUTS_E, TAL_Z4);
+#undef TAL_OUTS_E
   } else {
-    TAL_RASM("s_load_dwordx4 %[na], %[base], %[oa]\n\t"
-             "s_load_dwordx4 %[nb], %[base], %[ob]\n\t"
-             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
-             "v_pk_fma_f32 %[ca], v[32:33], %[wa], %[ca] " TAL_LO3 "\n\t"
-             TAL_FMA("cb", "j0", "wb", TAL_LO3) TAL_FMA("ca", "i1", "wa", TAL_LO3) TAL_FMA("cb", "j1", "wb", TAL_LO3)
-             TAL_FMA("ca", "i2", "wa", TAL_LO3) TAL_FMA("cb", "j2", "wb", TAL_LO3) TAL_FMA("ca", "i3", "wa", TAL_LO3)
-             TAL_FMA("cb", "j3", "wb", TAL_LO3)
-             "s_set_gpr_idx_off\n\t"
-             "s_waitcnt lgkmcnt(0)",
-             ([ca] "+v"(ca), [cb] "+v"(cb), [na] "=&s"(NA), [nb] "=&s"(NB2)), (TAL_IDX_INS, [wa] "s"(wa), [wb] "s"(wb)));
+#define TAL_OUTS_F ([ca] "+v"(ca), [cb] "+v"(cb), [off] "+s"(off))
+    if constexpr (NB == 1) TAL_PASM(TAL_PAIR_LOOP(TAL_TRIP_F), TAL_OUTS_F, TAL_Z1);
+    else if constexpr (NB == 2) TAL_PASM(TAL_PAIR_LOOP(TAL_TRIP_F), TAL_OUTS_F, TAL_Z2);
+    else if constexpr (NB == 3) TAL_PASM(TAL_PAIR_LOOP(TAL_TRIP_F), TAL_OUTS_F, TAL_Z3);
+    else TAL_PASM(TAL_PAIR_LOOP(TAL_TRIP_F), TAL_OUTS_F, TAL_Z4);
+#undef TAL_OUTS_F
   }
-}
-
-// one batch, a weight per operand: WA / WB = the rows' four weights as two pairs each; their
-// next batch (at byte offsets ow from the table base, the weights' array) loads alongside
-template <int NB, bool EXACT>
-__device__ __forceinline__ void reg_pair_w(v2f_t& ca, v2f_t& cb, const u32x4& A, const u32x4& B, u32x4& NA,
-                                           u32x4& NB2, const u64x2& WA, const u64x2& WB, u64x2& NWA, u64x2& NWB,
-                                           uint64_t base, uint32_t oa, uint32_t ob, uint32_t owa, uint32_t owb,
-                                           const v32f& X0, const v32f& X1, const v32f& X2, const v32f& X3) {
-  const uint64_t wa01 = WA[0], wa23 = WA[1], wb01 = WB[0], wb23 = WB[1];
-  if constexpr (EXACT) {
-    v2f_t t0, t1, t2, t3, t4, t5, t6, t7;
-    TAL_RASM("s_load_dwordx4 %[na], %[base], %[oa]\n\t"
-             "s_load_dwordx4 %[nb], %[base], %[ob]\n\t"
-             "s_load_dwordx4 %[nwa], %[base], %[owa]\n\t"
-             "s_load_dwordx4 %[nwb], %[base], %[owb]\n\t"
-             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
-             "v_pk_mul_f32 %[t0], v[32:33], %[wa01] " TAL_LO "\n\t"
-             TAL_MUL("t1", "i1", "wa01", TAL_HI) TAL_MUL("t2", "i2", "wa23", TAL_LO) TAL_MUL("t3", "i3", "wa23", TAL_HI)
-             TAL_MUL("t4", "j0", "wb01", TAL_LO) TAL_MUL("t5", "j1", "wb01", TAL_HI) TAL_MUL("t6", "j2", "wb23", TAL_LO)
-             TAL_MUL("t7", "j3", "wb23", TAL_HI)
-             "s_set_gpr_idx_off\n\t" TAL_ADDS
-             "s_waitcnt lgkmcnt(0)",
-             ([ca] "+v"(ca), [cb] "+v"(cb), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
-              [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7), [na] "=&s"(NA), [nb] "=&s"(NB2),
-              [nwa] "=&s"(NWA), [nwb] "=&s"(NWB)),
-             (TAL_IDX_INS, [wa01] "s"(wa01), [wa23] "s"(wa23), [wb01] "s"(wb01), [wb23] "s"(wb23), [owa] "s"(owa),
-              [owb] "s"(owb)));
-  } else {
-    TAL_RASM("s_load_dwordx4 %[na], %[base], %[oa]\n\t"
-             "s_load_dwordx4 %[nb], %[base], %[ob]\n\t"
-             "s_load_dwordx4 %[nwa], %[base], %[owa]\n\t"
-             "s_load_dwordx4 %[nwb], %[base], %[owb]\n\t"
-             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
-             "v_pk_fma_f32 %[ca], v[32:33], %[wa01], %[ca] " TAL_LO3 "\n\t"
-             TAL_FMA("cb", "j0", "wb01", TAL_LO3) TAL_FMA("ca", "i1", "wa01", TAL_HI3) TAL_FMA("cb", "j1", "wb01", TAL_HI3)
-             TAL_FMA("ca", "i2", "wa23", TAL_LO3) TAL_FMA("cb", "j2", "wb23", TAL_LO3) TAL_FMA("ca", "i3", "wa23", TAL_HI3)
-             TAL_FMA("cb", "j3", "wb23", TAL_HI3)
-             "s_set_gpr_idx_off\n\t"
-             "s_waitcnt lgkmcnt(0)",
-             ([ca] "+v"(ca), [cb] "+v"(cb), [na] "=&s"(NA), [nb] "=&s"(NB2), [nwa] "=&s"(NWA), [nwb] "=&s"(NWB)),
-             (TAL_IDX_INS, [wa01] "s"(wa01), [wa23] "s"(wa23), [wb01] "s"(wb01), [wb23] "s"(wb23), [owa] "s"(owa),
-              [owb] "s"(owb)));
-  }
-}
-
-// one batch of four operands of ONE row (a pair's longer row past the shorter one's batches, a
-// lone last row): EXACT spaces its dependent adds with s_nop; FMA has an index switch between
-template <int NB, bool EXACT>
-__device__ __forceinline__ void reg_row_u(v2f_t& ca, const u32x4& A, u32x4& NA, uint64_t wa, uint64_t base,
-                                          uint32_t oa, const v32f& X0, const v32f& X1, const v32f& X2,
-                                          const v32f& X3) {
-  if constexpr (EXACT) {
-    v2f_t t0, t1, t2, t3;
-    TAL_RASM("s_load_dwordx4 %[na], %[base], %[oa]\n\t"
-             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
-             "v_pk_mul_f32 %[t0], v[32:33], %[wa] " TAL_LO "\n\t"
-             TAL_MUL("t1", "i1", "wa", TAL_LO) TAL_MUL("t2", "i2", "wa", TAL_LO) TAL_MUL("t3", "i3", "wa", TAL_LO)
-             "s_set_gpr_idx_off\n\t"
-             "v_pk_add_f32 %[ca], %[ca], %[t0]\n\ts_nop 0\n\t"
-             "v_pk_add_f32 %[ca], %[ca], %[t1]\n\ts_nop 0\n\t"
-             "v_pk_add_f32 %[ca], %[ca], %[t2]\n\ts_nop 0\n\t"
-             "v_pk_add_f32 %[ca], %[ca], %[t3]\n\t"
-             "s_waitcnt lgkmcnt(0)",
-             ([ca] "+v"(ca), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [na] "=&s"(NA)),
-             ([i0] "s"(A[0]), [i1] "s"(A[1]), [i2] "s"(A[2]), [i3] "s"(A[3]), [base] "s"(base), [oa] "s"(oa),
-              [wa] "s"(wa)));
-  } else {
-    TAL_RASM("s_load_dwordx4 %[na], %[base], %[oa]\n\t"
-             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
-             "v_pk_fma_f32 %[ca], v[32:33], %[wa], %[ca] " TAL_LO3 "\n\t"
-             TAL_FMA("ca", "i1", "wa", TAL_LO3) TAL_FMA("ca", "i2", "wa", TAL_LO3) TAL_FMA("ca", "i3", "wa", TAL_LO3)
-             "s_set_gpr_idx_off\n\t"
-             "s_waitcnt lgkmcnt(0)",
-             ([ca] "+v"(ca), [na] "=&s"(NA)),
-             ([i0] "s"(A[0]), [i1] "s"(A[1]), [i2] "s"(A[2]), [i3] "s"(A[3]), [base] "s"(base), [oa] "s"(oa),
-              [wa] "s"(wa)));
-  }
-}
-
-template <int NB, bool EXACT>
-__device__ __forceinline__ void reg_row_w(v2f_t& ca, const u32x4& A, u32x4& NA, const u64x2& WA, u64x2& NWA,
-                                          uint64_t base, uint32_t oa, uint32_t owa, const v32f& X0, const v32f& X1,
-                                          const v32f& X2, const v32f& X3) {
-  const uint64_t wa01 = WA[0], wa23 = WA[1];
-  if constexpr (EXACT) {
-    v2f_t t0, t1, t2, t3;
-    TAL_RASM("s_load_dwordx4 %[na], %[base], %[oa]\n\t"
-             "s_load_dwordx4 %[nwa], %[base], %[owa]\n\t"
-             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
-             "v_pk_mul_f32 %[t0], v[32:33], %[wa01] " TAL_LO "\n\t"
-             TAL_MUL("t1", "i1", "wa01", TAL_HI) TAL_MUL("t2", "i2", "wa23", TAL_LO) TAL_MUL("t3", "i3", "wa23", TAL_HI)
-             "s_set_gpr_idx_off\n\t"
-             "v_pk_add_f32 %[ca], %[ca], %[t0]\n\ts_nop 0\n\t"
-             "v_pk_add_f32 %[ca], %[ca], %[t1]\n\ts_nop 0\n\t"
-             "v_pk_add_f32 %[ca], %[ca], %[t2]\n\ts_nop 0\n\t"
-             "v_pk_add_f32 %[ca], %[ca], %[t3]\n\t"
-             "s_waitcnt lgkmcnt(0)",
-             ([ca] "+v"(ca), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [na] "=&s"(NA),
-              [nwa] "=&s"(NWA)),
-             ([i0] "s"(A[0]), [i1] "s"(A[1]), [i2] "s"(A[2]), [i3] "s"(A[3]), [base] "s"(base), [oa] "s"(oa),
-              [owa] "s"(owa), [wa01] "s"(wa01), [wa23] "s"(wa23)));
-  } else {
-    TAL_RASM("s_load_dwordx4 %[na], %[base], %[oa]\n\t"
-             "s_load_dwordx4 %[nwa], %[base], %[owa]\n\t"
-             "s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
-             "v_pk_fma_f32 %[ca], v[32:33], %[wa01], %[ca] " TAL_LO3 "\n\t"
-             TAL_FMA("ca", "i1", "wa01", TAL_HI3) TAL_FMA("ca", "i2", "wa23", TAL_LO3) TAL_FMA("ca", "i3", "wa23", TAL_HI3)
-             "s_set_gpr_idx_off\n\t"
-             "s_waitcnt lgkmcnt(0)",
-             ([ca] "+v"(ca), [na] "=&s"(NA), [nwa] "=&s"(NWA)),
-             ([i0] "s"(A[0]), [i1] "s"(A[1]), [i2] "s"(A[2]), [i3] "s"(A[3]), [base] "s"(base), [oa] "s"(oa),
-              [owa] "s"(owa), [wa01] "s"(wa01), [wa23] "s"(wa23)));
-  }
-}
-
-// one operand of one row (the rows' tails past their common batches, a lone last row): weight
-// in the low dword of w
-template <int NB, bool EXACT>
-__device__ __forceinline__ void reg_one(v2f_t& ca, uint32_t idx, uint64_t w, const v32f& X0, const v32f& X1,
-                                        const v32f& X2, const v32f& X3) {
-  if constexpr (EXACT) {
-    v2f_t t0;
-    TAL_RASM("s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
-             "v_pk_mul_f32 %[t0], v[32:33], %[w0] " TAL_LO "\n\t"
-             "s_set_gpr_idx_off\n\t"
-             "v_pk_add_f32 %[ca], %[ca], %[t0]\n\t"
-             "s_nop 0",
-             ([ca] "+v"(ca), [t0] "=&v"(t0)), ([w0] "s"(w), [i0] "s"(idx)));
-  } else {
-    TAL_RASM("s_set_gpr_idx_on %[i0], gpr_idx(SRC0)\n\t"
-             "v_pk_fma_f32 %[ca], v[32:33], %[w0], %[ca] " TAL_LO3 "\n\t"
-             "s_set_gpr_idx_off",
-             ([ca] "+v"(ca)), ([w0] "s"(w), [i0] "s"(idx)));
-  }
+#undef TAL_Z1
+#undef TAL_Z2
+#undef TAL_Z3
+#undef TAL_Z4
+#undef TAL_PASM
 }
 
 // Output stores with sc1: the line leaves the XCD's L2 instead of staying there (plain / nt
@@ -2311,66 +2227,63 @@ __device__ __forceinline__ void reg_store(T* pout, int64_t ld_out, int32_t row, 
   }
 }
 
-constexpr uint32_t kRegPerOp = 0x40000000u;  // row record word 1: the row's weights are per operand
-
-// Table (int32, device): groups [G][4] {first source, sources, first row, rows}; at off_src the
-// source pool rows; at off_rows (a multiple of 4) row records [R][4] {out row, operands |
-// kRegPerOp, first operand, fp32 row weight}, a group's rows consecutive (pair order); at
-// off_idx (a multiple of 4) the operands' register offsets (2 x slot), at off_w (a multiple of
-// 4) their fp32 weights (rows with kRegPerOp), each array followed by 8 dwords of padding.
+// Table (int32, device): groups [G][4] {first source, sources, first pair, pairs}; at off_src
+// the source pool rows (each group's list padded to 16 x NB entries; src_off = their byte
+// offsets in the pool); at off_pairs (a multiple of 4) pair records [P][4] {out row A, out row
+// B or -1, trips, byte offset of the first trip record}, a group's pairs consecutive; at off_rec
+// (a multiple of 16) the trip records [T][16], followed by one record of padding (the loop reads
+// one record ahead).
 template <int NB, typename T, bool EXACT>
-__global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, int64_t ld_in, T* __restrict__ pout,
-                                                   int64_t ld_out, int64_t n, const int32_t* __restrict__ table,
+__global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, T* __restrict__ pout, int64_t ld_out,
+                                                   int64_t n, const int32_t* __restrict__ table,
                                                    const int64_t* __restrict__ src_off, int32_t n_groups,
-                                                   int32_t off_rows, int32_t off_idx, int32_t off_w,
-                                                   int32_t n_pieces, int32_t waves_per_label,
+                                                   int32_t off_pairs, int32_t n_pieces,
                                                    int32_t* __restrict__ ticket) {
   constexpr bool kB = kIsBf16<T>;
   constexpr int kEs = kB ? 2 : 4;
   const ConstI32 tab = (ConstI32)table;
-  const ConstU64 tab64 = (ConstU64)table;
   const ConstU64 soff = (ConstU64)src_off;
   const uint64_t base = reinterpret_cast<uint64_t>(table);
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int label = static_cast<int>(blockIdx.x & 7u);
-  const int wx = static_cast<int>(blockIdx.x >> 3) * 4 + wave;
   const int pieces_l = n_pieces > label ? (n_pieces - 1 - label) / 8 + 1 : 0;
   const int items = pieces_l * n_groups;
-  // Items are dealt in order by a per-label ticket counter (one atomic per item, fetched one item
-  // ahead), so the items in flight on an XCD stay a window of consecutive pieces: with a static
-  // round-robin the waves drift apart over thousands of items and the groups of one piece no
-  // longer meet in L2.
+  // Items are dealt in order by a per-label ticket counter (one atomic per item), so the items in
+  // flight on an XCD stay a window of consecutive pieces: with a static round-robin the waves
+  // drift apart over thousands of items and the groups of one piece no longer meet in L2
+  // (profiles/r03/k3r: HBM reads 3.9x -> 1.0-1.5x the algorithmic bytes).  The next ticket is
+  // taken once the current item's sources have arrived, not when the item starts: a ticket held
+  // for a whole item spreads a piece's groups over two item times, and the window (pieces whose
+  // sources must stay in L2) doubles past the 4 MB L2.
   int32_t* my_ticket = ticket + 16 * label;  // 64 B apart
   auto take = [&]() {
     int t = 0;
     if (lane == 0) t = __hip_atomic_fetch_add(my_ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return __builtin_amdgcn_readfirstlane(t);
   };
-  (void)wx;
-  (void)waves_per_label;
+  const v2f_t zn = {-0.f, -0.f};  // the neutral operand's register pair
   int s_next = take();
   v32f X0, X1, X2, X3;
+#ifdef TAL_PROBE_REG_NOLOAD
+  bool loaded = false;
+#endif
   for (;;) {
     const int s = s_next;
     if (s >= items) break;
-    s_next = take();
     const int q = s / n_groups, g = s - q * n_groups;
     const int piece = q * 8 + label;
-    const int s0 = tab[4 * g], ns = tab[4 * g + 1], r0 = tab[4 * g + 2], nr = tab[4 * g + 3];
+    const int s0 = tab[4 * g], p0 = tab[4 * g + 2], np = tab[4 * g + 3];
     const int64_t col = static_cast<int64_t>(piece) * kRegPiece + 2 * lane;
     const uint32_t loff = col < n ? static_cast<uint32_t>(2 * lane * kEs) : 0u;  // past n: the piece's start
     const uint64_t pbase = reinterpret_cast<uint64_t>(pin) + static_cast<uint64_t>(piece) * (kRegPiece * kEs);
-    (void)ns;
-    (void)ld_in;
     uint64_t b[16];
-    // the group's source list is padded to 16 x NB entries (src_off: their byte offsets in the
-    // pool), so each block's 16 offsets come in two 8-dword scalar loads, one wait
+    // each block's 16 source offsets come in two 8-dword scalar loads, one wait
 #define TAL_RBASES(J)                                                                            \
     _Pragma("unroll") for (int k = 0; k < 16; ++k)                                               \
       b[k] = pbase + static_cast<uint64_t>(soff[s0 + (J) * 16 + k]);
 #ifdef TAL_PROBE_REG_NOLOAD  // A/B probe: sources loaded for a wave's first item only
-    if (s == wx) {
+    if (!loaded) {
+      loaded = true;
 #endif
     TAL_RBASES(0)
     X0 = reg_load_block<0, kB>(b, loff);
@@ -2382,93 +2295,19 @@ __global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, in
 #endif
 #undef TAL_RBASES
     reg_wait<NB, kB>(X0, X1, X2, X3);
-    int r = 0;
-#ifdef TAL_PROBE_REG_NOCOMP  // A/B probe: the stores without the row arithmetic
-    for (; r < nr; ++r) reg_store<T>(pout, ld_out, tab[off_rows + 4 * (r0 + r)], col, n, v2f_t{0.f, 0.f});
-#endif
-    // rows in pairs (the plan sorts a group's rows by operand count, descending: A >= B);
-    // every operand list is read 4 dwords at a time, the next 4 prefetched by the batch that
-    // consumes the current ones, so after the batches the registers hold the 1-3 operand tail
-    for (; r < nr; r += 2) {
-      const bool pair = r + 1 < nr;
-      const int ra = off_rows + 4 * (r0 + r);
-      const int oa_row = tab[ra], fa = tab[ra + 1], qa = tab[ra + 2];
-      const int ob_row = pair ? tab[ra + 4] : -1, fb = pair ? tab[ra + 5] : 0, qb = pair ? tab[ra + 6] : qa;
-      const uint64_t wa = static_cast<uint32_t>(tab[ra + 3]), wb = pair ? static_cast<uint32_t>(tab[ra + 7]) : 0u;
-      const bool per_op = ((fa | fb) & static_cast<int>(kRegPerOp)) != 0;
-      const int na = fa & ~static_cast<int>(kRegPerOp), nb = fb & ~static_cast<int>(kRegPerOp);
+    s_next = take();
+    for (int p = 0; p < np; ++p) {
+      const u32x4 pr = ((const __attribute__((address_space(4))) u32x4*)(tab + off_pairs))[p0 + p];
       v2f_t ca = {-0.f, -0.f}, cb = {-0.f, -0.f};
-      u32x4 A = {static_cast<uint32_t>(tab[off_idx + qa]), static_cast<uint32_t>(tab[off_idx + qa + 1]),
-                 static_cast<uint32_t>(tab[off_idx + qa + 2]), static_cast<uint32_t>(tab[off_idx + qa + 3])};
-      u32x4 B = {static_cast<uint32_t>(tab[off_idx + qb]), static_cast<uint32_t>(tab[off_idx + qb + 1]),
-                 static_cast<uint32_t>(tab[off_idx + qb + 2]), static_cast<uint32_t>(tab[off_idx + qb + 3])};
-      uint32_t oa = 4u * static_cast<uint32_t>(off_idx + qa + 4), ob = 4u * static_cast<uint32_t>(off_idx + qb + 4);
-      const int common = nb / 4, extra = na / 4 - common;
-      u64x2 WA = {0, 0}, WB = {0, 0};
-      uint32_t owa = 4u * static_cast<uint32_t>(off_w + qa + 4), owb = 4u * static_cast<uint32_t>(off_w + qb + 4);
-      if (!per_op) {
-        // two batches per trip, the operand registers ping-ponging between A/B and NA/NB2
-        // (a one-batch loop copied NA -> A with eight s_mov per batch)
-        int k = 0;
-        for (; k + 2 <= common; k += 2) {
-          u32x4 NA, NB2;
-          reg_pair_u<NB, EXACT>(ca, cb, A, B, NA, NB2, wa, wb, base, oa, ob, X0, X1, X2, X3);
-          reg_pair_u<NB, EXACT>(ca, cb, NA, NB2, A, B, wa, wb, base, oa + 16u, ob + 16u, X0, X1, X2, X3);
-          oa += 32u;
-          ob += 32u;
-        }
-        if (k < common) {
-          u32x4 NA, NB2;
-          reg_pair_u<NB, EXACT>(ca, cb, A, B, NA, NB2, wa, wb, base, oa, ob, X0, X1, X2, X3);
-          A = NA;
-          B = NB2;
-          oa += 16u;
-          ob += 16u;
-        }
-        for (k = 0; k < extra; ++k) {
-          u32x4 NA;
-          reg_row_u<NB, EXACT>(ca, A, NA, wa, base, oa, X0, X1, X2, X3);
-          A = NA;
-          oa += 16u;
-        }
-      } else {
-        WA = u64x2{tab64[(off_w + qa) / 2], tab64[(off_w + qa) / 2 + 1]};
-        WB = u64x2{tab64[(off_w + qb) / 2], tab64[(off_w + qb) / 2 + 1]};
-        for (int k = 0; k < common; ++k) {
-          u32x4 NA, NB2;
-          u64x2 NWA, NWB;
-          reg_pair_w<NB, EXACT>(ca, cb, A, B, NA, NB2, WA, WB, NWA, NWB, base, oa, ob, owa, owb, X0, X1, X2, X3);
-          A = NA;
-          B = NB2;
-          WA = NWA;
-          WB = NWB;
-          oa += 16u;
-          ob += 16u;
-          owa += 16u;
-          owb += 16u;
-        }
-        for (int k = 0; k < extra; ++k) {
-          u32x4 NA;
-          u64x2 NWA;
-          reg_row_w<NB, EXACT>(ca, A, NA, WA, NWA, base, oa, owa, X0, X1, X2, X3);
-          A = NA;
-          WA = NWA;
-          oa += 16u;
-          owa += 16u;
-        }
-      }
-      // tails (uniform trip counts, constant register indices): a weight per operand sits in
-      // the low (even operand) or high (odd) dword of its pair
-#define TAL_TAIL(C, R, W, REM)                                                                         \
-      if ((REM) > 0) reg_one<NB, EXACT>(C, R[0], per_op ? (W[0] & 0xffffffffull) : w##C, X0, X1, X2, X3); \
-      if ((REM) > 1) reg_one<NB, EXACT>(C, R[1], per_op ? (W[0] >> 32) : w##C, X0, X1, X2, X3);          \
-      if ((REM) > 2) reg_one<NB, EXACT>(C, R[2], per_op ? (W[1] & 0xffffffffull) : w##C, X0, X1, X2, X3);
-      const uint64_t wca = wa, wcb = wb;
-      TAL_TAIL(ca, A, WA, na % 4)
-      TAL_TAIL(cb, B, WB, nb % 4)
-#undef TAL_TAIL
-      reg_store<T>(pout, ld_out, oa_row, col, n, ca);
-      if (pair) reg_store<T>(pout, ld_out, ob_row, col, n, cb);
+      const uint32_t off = pr[3];
+      const uint32_t last = off + 64u * pr[2];  // the loop goes on while (next record's offset + 64) <= last
+#ifndef TAL_PROBE_REG_NOCOMP  // A/B probe: the stores without the row arithmetic
+      reg_pair<NB, EXACT>(ca, cb, base, off, last, X0, X1, X2, X3, zn);
+#else
+      (void)last;
+#endif
+      reg_store<T>(pout, ld_out, static_cast<int32_t>(pr[0]), col, n, ca);
+      if (static_cast<int32_t>(pr[1]) >= 0) reg_store<T>(pout, ld_out, static_cast<int32_t>(pr[1]), col, n, cb);
     }
   }
 }
@@ -2494,9 +2333,9 @@ int32_t reg_tickets(int32_t** out) {
 }
 
 template <int NB, typename T, bool EXACT>
-int32_t launch_round_reg_nb(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n, const int32_t* table,
-                            const int64_t* src_off, int32_t n_groups, int32_t off_rows, int32_t off_idx,
-                            int32_t off_w, int32_t n_pieces, hipStream_t s) {
+int32_t launch_round_reg_nb(const T* pin, T* pout, int64_t ld_out, int64_t n, const int32_t* table,
+                            const int64_t* src_off, int32_t n_groups, int32_t off_pairs, int32_t n_pieces,
+                            hipStream_t s) {
   static int blocks_per_cu = -1, n_cu = 0;  // per instantiation, once per process
   if (blocks_per_cu < 0) {
     int dev = 0;
@@ -2515,20 +2354,18 @@ int32_t launch_round_reg_nb(const T* pin, int64_t ld_in, T* pout, int64_t ld_out
   if (int32_t rc = reg_tickets(&ticket)) return rc;
   if (hipMemsetAsync(ticket, 0, kRegTicketBytes, s) != hipSuccess)
     return fail(TAL_ERR_HIP, "register round: ticket reset failed");
-  k_round_reg<NB, T, EXACT><<<grid, 256, 0, s>>>(pin, ld_in, pout, ld_out, n, table, src_off, n_groups, off_rows,
-                                                 off_idx, off_w, n_pieces, grid / 8 * 4, ticket);
+  k_round_reg<NB, T, EXACT><<<grid, 256, 0, s>>>(pin, pout, ld_out, n, table, src_off, n_groups, off_pairs, n_pieces,
+                                                 ticket);
   return check_launch("register round kernel");
 }
 
 template <typename T, bool EXACT>
-int32_t launch_round_reg(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n, const int32_t* table,
-                         const int64_t* src_off, int32_t n_groups, int32_t off_rows, int32_t off_idx, int32_t off_w,
-                         int32_t max_src, hipStream_t s) {
+int32_t launch_round_reg(const T* pin, T* pout, int64_t ld_out, int64_t n, const int32_t* table,
+                         const int64_t* src_off, int32_t n_groups, int32_t off_pairs, int32_t max_src, hipStream_t s) {
   const int64_t n_pieces = (n + kRegPiece - 1) / kRegPiece;
   if (n_pieces * n_groups >= (1LL << 31)) return fail(TAL_ERR_INVALID, "register round: too many items");
   const int np = static_cast<int>(n_pieces);
-#define TAL_REG_NB(NBV) \
-  launch_round_reg_nb<NBV, T, EXACT>(pin, ld_in, pout, ld_out, n, table, src_off, n_groups, off_rows, off_idx, off_w, np, s)
+#define TAL_REG_NB(NBV) launch_round_reg_nb<NBV, T, EXACT>(pin, pout, ld_out, n, table, src_off, n_groups, off_pairs, np, s)
   if (max_src <= 16) return TAL_REG_NB(1);
   if (max_src <= 32) return TAL_REG_NB(2);
   if (max_src <= 48) return TAL_REG_NB(3);
@@ -3624,8 +3461,8 @@ int32_t tal_agg_round_clique_f32(const float* pool_in, int64_t ld_in, float* poo
 
 int32_t tal_agg_round_reg(const void* pool_in, int64_t ld_in, void* pool_out, int64_t ld_out, int64_t n,
                           int32_t bf16, const int32_t* table_dev, const int64_t* src_off_dev, int32_t n_groups,
-                          int32_t off_src, int32_t off_rows, int32_t off_idx, int32_t off_w, int32_t max_src,
-                          int32_t mode, void* stream) {
+                          int32_t off_src, int32_t off_pairs, int32_t off_rec, int32_t max_src, int32_t mode,
+                          void* stream) {
   if (!pool_in || !pool_out || !table_dev || !src_off_dev)
     return fail(TAL_ERR_INVALID, "tal_agg_round_reg: null pointer");
   if (pool_in == pool_out)
@@ -3633,23 +3470,25 @@ int32_t tal_agg_round_reg(const void* pool_in, int64_t ld_in, void* pool_out, in
   const int64_t n2 = n + (n & 1);  // the last lane of an odd row reads one element of padding
   if (n < 0 || ld_in < n2 || ld_out < n2 || ld_in % 2 || ld_out % 2)
     return fail(TAL_ERR_INVALID, "tal_agg_round_reg: need even ld >= n rounded up to even");
-  if (n_groups < 0 || max_src < 1 || max_src > kRegMaxSrc || off_src < 4 * n_groups || off_rows % 4 || off_idx % 4 ||
-      off_w % 4 || off_rows < off_src || off_idx < off_rows || off_w < off_idx)
+  if (n_groups < 0 || max_src < 1 || max_src > kRegMaxSrc || off_src < 4 * n_groups || off_pairs % 4 ||
+      off_rec % 16 || off_pairs < off_src || off_rec < off_pairs)
     return fail(TAL_ERR_INVALID, "tal_agg_round_reg: bad table layout");
   if (bf16 && mode == TAL_MODE_EXACT)
     return fail(TAL_ERR_INVALID, "tal_agg_round_reg: bf16 rounds take FMA mode here (EXACT: tal_agg_round_bf16)");
   if (bf16 ? !aligned4(pool_in) || !aligned4(pool_out) : !aligned8(pool_in) || !aligned8(pool_out))
     return fail(TAL_ERR_INVALID, "tal_agg_round_reg: pools must be aligned to 2 elements");
+  if (reinterpret_cast<uintptr_t>(table_dev) % 64)
+    return fail(TAL_ERR_INVALID, "tal_agg_round_reg: table must be 64-B aligned");
   if (n == 0 || n_groups == 0) { g_err.clear(); return TAL_OK; }
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (bf16)
-    return launch_round_reg<uint16_t, false>(static_cast<const uint16_t*>(pool_in), ld_in, static_cast<uint16_t*>(pool_out),
-                                             ld_out, n, table_dev, src_off_dev, n_groups, off_rows, off_idx, off_w, max_src, s);
+    return launch_round_reg<uint16_t, false>(static_cast<const uint16_t*>(pool_in), static_cast<uint16_t*>(pool_out),
+                                             ld_out, n, table_dev, src_off_dev, n_groups, off_pairs, max_src, s);
   if (mode == TAL_MODE_EXACT)
-    return launch_round_reg<float, true>(static_cast<const float*>(pool_in), ld_in, static_cast<float*>(pool_out), ld_out,
-                                         n, table_dev, src_off_dev, n_groups, off_rows, off_idx, off_w, max_src, s);
-  return launch_round_reg<float, false>(static_cast<const float*>(pool_in), ld_in, static_cast<float*>(pool_out), ld_out,
-                                        n, table_dev, src_off_dev, n_groups, off_rows, off_idx, off_w, max_src, s);
+    return launch_round_reg<float, true>(static_cast<const float*>(pool_in), static_cast<float*>(pool_out), ld_out, n,
+                                         table_dev, src_off_dev, n_groups, off_pairs, max_src, s);
+  return launch_round_reg<float, false>(static_cast<const float*>(pool_in), static_cast<float*>(pool_out), ld_out, n,
+                                        table_dev, src_off_dev, n_groups, off_pairs, max_src, s);
 }
 
 int32_t tal_agg_bf16(const uint16_t* const* x_host, const double* w_host, int32_t m, uint16_t* out,

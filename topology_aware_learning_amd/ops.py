@@ -339,18 +339,19 @@ REG_WINDOW = 64    # rows considered when growing a group
 @dataclass
 class RegPlan:
     """A round as register-resident source groups (K3r, tal_agg_round_reg): rows grouped so that
-    each group's operands are <= max_src distinct sources.  `full` is a sparse plan over all
-    rows for the int64 segment (and bf16 EXACT, which K3r does not take)."""
+    each group's operands are <= max_src distinct sources, a group's rows run in pairs whose
+    operands come in trip records of four per row.  `full` is a sparse plan over all rows for
+    the int64 segment (and bf16 EXACT, which K3r does not take)."""
     table: np.ndarray
     n_groups: int
     off_src: int
-    off_rows: int
-    off_idx: int
-    off_w: int
+    off_pairs: int
+    off_rec: int
     max_src: int
     group_sources: int   # sum over groups of their sources (L2 reads per column)
     full: RoundPlan
     rows: int
+    trips: int = 0       # trip records (16 dwords each; 8 operand slots, padding included)
     device: Optional[torch.Tensor] = None
     tuned_ms: Optional[float] = None
     candidates: Optional[list] = None
@@ -367,7 +368,16 @@ class RegPlan:
     def staged_rows(self) -> int:
         """Distinct sources read per column: every source once (the groups sharing a source
         are served by L2 on the XCD their piece runs on)."""
-        return int(len(np.unique(self.table[self.off_src: self.off_rows])))
+        return int(len(np.unique(self.table[self.off_src: self.off_pairs])))
+
+    def pair_records(self) -> np.ndarray:
+        """[P, 4] {out row A, out row B or -1, trips, byte offset of the first trip record}."""
+        return self.table[self.off_pairs: self.off_rec].reshape(-1, 4)[:self.n_pairs]
+
+    @property
+    def n_pairs(self) -> int:
+        g = self.table[: 4 * self.n_groups].reshape(-1, 4)
+        return int(g[:, 3].sum())
 
     def to(self, device) -> "RegPlan":
         self.device = torch.from_numpy(self.table).to(device)
@@ -387,7 +397,8 @@ class RegPlan:
         return t
 
 
-REG_PER_OP = 0x40000000  # row record: weights per operand (tal_agg.hip kRegPerOp)
+REG_TRIP = 4        # operands of each row per trip record
+REG_REC_WORDS = 16  # {A idx x4, B idx x4, A w x4, B w x4}
 
 
 def reg_groups(row_ptr, col, max_src: int = REG_MAX_SRC, window: int = REG_WINDOW):
@@ -421,8 +432,9 @@ def reg_groups(row_ptr, col, max_src: int = REG_MAX_SRC, window: int = REG_WINDO
 def build_reg_plan(row_ptr, col, w, out_row, max_src: int = REG_MAX_SRC) -> Optional[RegPlan]:
     """RegPlan of a round (table layout: tal_agg.h K3r), or None when a row has more than
     max_src distinct sources.  Inside a group the rows are ordered by operand count
-    (descending) so the kernel's row pairs share most of their batches; a row whose fp32
-    weights are not all equal is flagged per-operand (its weights are read per operand)."""
+    (descending) and paired in that order, so a pair's rows need about the same number of
+    trips; the shorter row (and a lone last row's partner) is padded with the neutral operand
+    (register offset 32 x NB, weight +0.0)."""
     row_ptr, col, w = row_ptr.astype(np.int32), col.astype(np.int32), np.asarray(w, np.float64)
     row_ptr, col, w, out_row = _csr(row_ptr, col, w, out_row)
     try:
@@ -430,39 +442,50 @@ def build_reg_plan(row_ptr, col, w, out_row, max_src: int = REG_MAX_SRC) -> Opti
     except ValueError:
         return None
     G = len(groups)
-    src_list, row_recs, idx, wts = [], [], [], []
-    grp = np.zeros((G, 4), np.int32)
+    nb = (max(len(s_) for _, s_ in groups) + 15) // 16
+    span, neutral = 16 * nb, 32 * nb
     w32all = w.astype(np.float32).view(np.uint32)
-    span = 16 * ((max(len(s_) for _, s_ in groups) + 15) // 16)  # the kernel's 16 x NB loads
+    src_list, pairs, recs = [], [], []
+    grp = np.zeros((G, 4), np.int32)
+
+    def lists(r, slot):
+        if r is None:
+            return [], []
+        q0, q1 = int(row_ptr[r]), int(row_ptr[r + 1])
+        return [2 * slot[int(c)] for c in col[q0:q1]], [int(x) for x in w32all[q0:q1]]
+
     for g, (rows, srcs) in enumerate(groups):
         slot = {s_: k for k, s_ in enumerate(srcs)}
         rows = sorted(rows, key=lambda r: -(row_ptr[r + 1] - row_ptr[r]))
-        grp[g] = (len(src_list), len(srcs), len(row_recs), len(rows))
+        grp[g] = (len(src_list), len(srcs), len(pairs), (len(rows) + 1) // 2)
         src_list.extend(srcs + [srcs[0]] * (span - len(srcs)))  # padding reloads the first source
-        for r in rows:
-            q0, q1 = int(row_ptr[r]), int(row_ptr[r + 1])
-            w32 = w32all[q0:q1]
-            per_op = bool(np.any(w32 != w32[0]))
-            row_recs.append((int(out_row[r]), (q1 - q0) | (REG_PER_OP if per_op else 0), len(idx), int(w32[0])))
-            idx.extend(2 * slot[int(c)] for c in col[q0:q1])
-            wts.extend(int(x) for x in w32)
-            pad = -len(idx) % 4  # every row's list starts 4-dword aligned
-            idx.extend([0] * pad)
-            wts.extend([0] * pad)
+        for k in range(0, len(rows), 2):
+            ra, rb = rows[k], rows[k + 1] if k + 1 < len(rows) else None
+            ia, wa = lists(ra, slot)
+            ib, wb = lists(rb, slot)
+            trips = (max(len(ia), len(ib)) + REG_TRIP - 1) // REG_TRIP
+            pad = REG_TRIP * trips
+            ia, wa = ia + [neutral] * (pad - len(ia)), wa + [0] * (pad - len(wa))
+            ib, wb = ib + [neutral] * (pad - len(ib)), wb + [0] * (pad - len(wb))
+            pairs.append([int(out_row[ra]), -1 if rb is None else int(out_row[rb]), trips, len(recs)])
+            for t in range(trips):
+                sl = slice(REG_TRIP * t, REG_TRIP * (t + 1))
+                recs.append(ia[sl] + ib[sl] + wa[sl] + wb[sl])
     off_src = 4 * G
-    off_rows = (off_src + len(src_list) + 3) // 4 * 4
-    off_idx = off_rows + 4 * len(row_recs)
-    off_w = off_idx + len(idx) + 8
-    words = off_w + len(wts) + 8  # + 8 dwords of read-ahead padding after each operand array
+    off_pairs = (off_src + len(src_list) + 3) // 4 * 4
+    off_rec = (off_pairs + 4 * len(pairs) + 15) // 16 * 16
+    words = off_rec + REG_REC_WORDS * (len(recs) + 1)  # + one record read ahead by the loop
     table = np.zeros(words, np.int32)
     table[:off_src] = grp.reshape(-1)
     table[off_src: off_src + len(src_list)] = src_list
-    table[off_rows: off_idx] = np.asarray(row_recs, np.uint32).view(np.int32).reshape(-1)
-    table[off_idx: off_idx + len(idx)] = idx
-    table[off_w: off_w + len(wts)] = np.asarray(wts, np.uint32).view(np.int32)
-    return RegPlan(table=table, n_groups=G, off_src=off_src, off_rows=off_rows, off_idx=off_idx, off_w=off_w,
+    pr = np.asarray(pairs, np.int64)
+    pr[:, 3] = 4 * (off_rec + REG_REC_WORDS * pr[:, 3])  # byte offsets from the table base
+    table[off_pairs: off_pairs + 4 * len(pairs)] = pr.astype(np.int32).reshape(-1)
+    table[off_rec: off_rec + REG_REC_WORDS * len(recs)] = \
+        np.asarray(recs, np.uint32).view(np.int32).reshape(-1)
+    return RegPlan(table=table, n_groups=G, off_src=off_src, off_pairs=off_pairs, off_rec=off_rec,
                    max_src=max(len(s_) for _, s_ in groups), group_sources=sum(len(s_) for _, s_ in groups),
-                   full=build_plan(row_ptr, col, w, out_row, dense=0), rows=len(out_row))
+                   full=build_plan(row_ptr, col, w, out_row, dense=0), rows=len(out_row), trips=len(recs))
 
 
 def _round_reg(pool_in, pool_out, plan: RegPlan, n, dtype, mode, stream):
@@ -487,9 +510,9 @@ def _round_reg(pool_in, pool_out, plan: RegPlan, n, dtype, mode, stream):
     if plan.device is None or plan.device.device != pool_in.device:
         plan.to(pool_in.device)
     t = plan.table
-    if t[plan.off_src: plan.off_rows].max(initial=-1) >= pool_in.shape[0]:
+    if t[plan.off_src: plan.off_pairs].max(initial=-1) >= pool_in.shape[0]:
         raise ValueError("plan reads a pool row beyond pool_in")
-    if t[plan.off_rows: plan.off_idx].reshape(-1, 4)[:, 0].max(initial=-1) >= pool_out.shape[0]:
+    if plan.pair_records()[:, :2].max(initial=-1) >= pool_out.shape[0]:
         raise ValueError("plan writes a pool row beyond pool_out")
     L = _lib.load()
     offs = plan.src_offsets(pool_in.stride(0) * esz, pool_in.device)
@@ -497,7 +520,7 @@ def _round_reg(pool_in, pool_out, plan: RegPlan, n, dtype, mode, stream):
                               ctypes.c_void_p(pool_out.data_ptr()), pool_out.stride(0), n, int(bf16),
                               ctypes.c_void_p(plan.device.data_ptr()), ctypes.c_void_p(offs.data_ptr()),
                               plan.n_groups, plan.off_src,
-                              plan.off_rows, plan.off_idx, plan.off_w, plan.max_src, int(mode),
+                              plan.off_pairs, plan.off_rec, plan.max_src, int(mode),
                               _stream(pool_in.device, stream)))
     return pool_out
 
