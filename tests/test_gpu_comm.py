@@ -100,8 +100,8 @@ def test_sharded_round_through_cabi_transport(cuda, tmp_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("graph,world,dtype", [("regular", 2, "f32"), ("sbm256", 8, "f32"), ("barbell60", 8, "bf16"),
-                                               ("ring", 2, "bf16")])
+@pytest.mark.parametrize("graph,world,dtype", [("regular", 4, "f32"), ("sbm256", 8, "f32"), ("sbm256", 8, "bf16"),
+                                               ("barbell60", 8, "bf16"), ("ring", 2, "bf16")])
 def test_virtual_ranks_messages_from_cabi_pack(cuda, graph, world, dtype):
     """The multi-rank 'cabi' transport's messages without a second GPU: `world` ShardedRounds
     in one process, each peer's message built exactly as post_exchange_cabi builds it (the
@@ -147,7 +147,9 @@ def test_virtual_ranks_messages_from_cabi_pack(cuda, graph, world, dtype):
                else oracle.round_bf16(ref, rp, col, w, np.arange(n)))
         iref = oracle.round_i64(iref, rp, col, w, np.arange(n))
     torch.cuda.synchronize()
-    assert packed > 0 or graph == "ring"
+    # the gather kernel ran (regular at world 2 or 3, barbell60 at 8 and rings send consecutive
+    # rows: views only)
+    assert packed > 0 or graph in ("ring", "barbell60")
     for sr in srs:
         got = _get_rows(sr.own_rows(), len(sr.spec.own), dtype)
         assert np.array_equal(got, ref[sr.spec.own].view(got.dtype))
