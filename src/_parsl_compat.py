@@ -44,11 +44,9 @@ except Exception:  # noqa: BLE001
         def deco(fn):
             def submit(*args, **kwargs):
                 out: Future = Future()
-                deps = [a for a in list(args) + list(kwargs.values()) if isinstance(a, Future)]
-                pending = [len(deps)]
-                plock = threading.Lock()
 
                 def run():
+                    # a failed dependency's exception surfaces here, through result()
                     try:
                         res = fn(*[_resolve(a) for a in args], **{k: _resolve(v) for k, v in kwargs.items()})
                     except BaseException as exc:  # noqa: BLE001 - propagated into the future
@@ -56,23 +54,26 @@ except Exception:  # noqa: BLE001
                     else:
                         out.set_result(res)
 
-                def launch():
-                    for d in deps:
-                        if d.exception() is not None:
-                            out.set_exception(d.exception())
-                            return
+                # one callback per distinct dependency still running (a round's apps share most
+                # of their futures: ten neighbor futures per aggregation, mostly done already)
+                deps = {}
+                for a in (*args, *kwargs.values()):
+                    if isinstance(a, Future) and not a.done():
+                        deps[id(a)] = a
+                if not deps:
                     _executor(label).submit(run)
+                    return out
+                pending = [len(deps)]
+                plock = threading.Lock()
 
                 def on_done(_):
                     with plock:
                         pending[0] -= 1
                         ready = pending[0] == 0
                     if ready:
-                        launch()
+                        _executor(label).submit(run)
 
-                if not deps:
-                    launch()
-                for d in deps:
+                for d in deps.values():
                     d.add_done_callback(on_done)
                 return out
 

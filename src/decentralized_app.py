@@ -24,7 +24,7 @@ import torch
 
 from src.aggregation_scheduler import (BaseScheduler, CosineAnnealingWarmRestarts, ExponentialScheduler,
                                        OscilateScheduler)
-from src.decentralized_client import (DecentralClient, centrality_module_avg, create_centrality_dict,  # noqa: F401
+from src.decentralized_client import (DecentralClient, centrality_module_avg, create_centrality_dict, draw_neighbors,  # noqa: F401
                                       create_clients, scale_agg, sim_centrality_module_avg, test_agg,
                                       unweighted_module_avg, update_random_agg_coeffs, weighted_module_avg)
 from src.modules import create_model, load_data
@@ -215,12 +215,16 @@ class DecentrallearnApp:
         batch = [] if self.batched_round else None
         nxt = self.round_states[round_idx + 1] = {}
         cur = self.round_states[round_idx]
+        sel = set(selected)
+        # the selected clients' neighbor draws of each loop in one RNG call (same stream as
+        # one get_neighbors() per client in client order, draw_neighbors)
+        draws = iter(draw_neighbors([c for c in self.clients if c.idx in sel]))
         for client in self.clients:
             train_input = cur[client.idx]["agg"]
-            if client.idx not in selected:
+            if client.idx not in sel:
                 nxt[client.idx] = {"train": train_input}
                 continue
-            prox_neighbors = [cur[i]["agg"] for i in client.get_neighbors()]
+            prox_neighbors = [cur[i]["agg"] for i in next(draws)]
             nxt[client.idx] = {"train": job(train_input, round_idx, self.epochs, self.batch_size, self.lr,
                                             self.momentum, self.prox_coeff, self.seed, self.backdoor, self.dataset,
                                             self.optimizer, self.weight_decay, self.beta_1, self.beta_2,
@@ -229,13 +233,14 @@ class DecentrallearnApp:
             self.centrality_dict = update_random_agg_coeffs(seed=self.seed, round_idx=round_idx,
                                                             num_clients=len(self.clients),
                                                             centrality_dict=self.centrality_dict)
+        draws = iter(draw_neighbors([c for c in self.clients if c.idx in sel]))
         for client in self.clients:
             agg_client = nxt[client.idx]["train"]
-            if client.idx not in selected:
+            if client.idx not in sel:
                 nxt[client.idx]["agg"] = agg_client
                 futures.append(agg_client)
                 continue
-            neighbor_idxs = client.get_neighbors()  # second, independent draw (:616)
+            neighbor_idxs = next(draws)  # second, independent draw (:616)
             if len(neighbor_idxs) == 0:
                 nxt[client.idx]["agg"] = agg_client
                 futures.append(agg_client)

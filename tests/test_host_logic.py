@@ -105,6 +105,32 @@ def test_get_neighbors_drop_out():
     assert c.get_neighbors() == [1, 3]
 
 
+def test_draw_neighbors_is_the_sequential_stream():
+    """The driver's one-call draw per loop gives the lists and the global RNG state of one
+    get_neighbors() per client in order (reference decentralized_client.py:63-71)."""
+    from src.decentralized_client import DecentralClient, draw_neighbors
+    from torch.utils.data import TensorDataset
+
+    ds = TensorDataset(torch.zeros(2, 1))
+    rng = np.random.default_rng(11)
+    clients = []
+    for i in range(40):
+        k = int(rng.integers(0, 10))
+        nb = sorted(rng.choice(100, size=k, replace=False).tolist())
+        pr = rng.choice([0.0, 0.3, 0.5, 0.999, 1.0], size=k).tolist()
+        clients.append(DecentralClient(idx=i, prox_coeff=0.0, model=torch.nn.Linear(1, 1), train_data=None,
+                                       test_data=None, valid_data=None, global_test_data=ds,
+                                       global_backdoor_test_data=None, neighbors=nb, neighbor_probs=pr))
+    for sub in (clients, clients[::3], clients[:1], []):
+        np.random.seed(4)
+        seq = [c.get_neighbors() for c in sub]
+        st = np.random.get_state()
+        np.random.seed(4)
+        assert draw_neighbors(sub) == seq
+        st2 = np.random.get_state()
+        assert np.array_equal(st[1], st2[1]) and st[2] == st2[2]
+
+
 def test_layouts_match_reference_models():
     ref = json.loads((GOLDEN / "layouts.json").read_text())
     for name in ("cifar10", "resnet18", "resnet50"):

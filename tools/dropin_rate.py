@@ -11,8 +11,9 @@ Python plus the aggregation.  Also
 times RoundExecutor(pool).run directly on the round (its default plan, in place) against the
 bench's K1 floor (64 x one K1 call).  One JSON line per measurement.
 
-usage: python tools/dropin_rate.py [rounds] [--profile]   (--profile: cProfile of the batched
-rounds only, top functions by cumulative time)"""
+usage: python tools/dropin_rate.py [rounds] [--profile[=per_call]]   (--profile: cProfile of the
+batched rounds only, or of the per-call rounds with =per_call; top functions by cumulative and by
+own time)"""
 import json
 import os
 import sys
@@ -33,7 +34,9 @@ import torch  # noqa: E402
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     rounds = int(args[0]) if args else 5
-    profile = "--profile" in sys.argv
+    prof_arg = [a for a in sys.argv[1:] if a.startswith("--profile")]
+    profile = bool(prof_arg)
+    prof_mode = prof_arg[0].split("=", 1)[1] if prof_arg and "=" in prof_arg[0] else "batched"
     from src.decentralized_app import DecentrallearnApp
     from topology_aware_learning_amd import ops
     from topology_aware_learning_amd.round import RoundExecutor
@@ -62,7 +65,7 @@ def main():
         import io
         import pstats
 
-        app.batched_round = True
+        app.batched_round = prof_mode == "batched"
         for _ in range(2):  # warm: plan build, pools
             for f in app._federated_round(r):
                 f.result()
@@ -80,6 +83,7 @@ def main():
         pr.disable()
         out = io.StringIO()
         pstats.Stats(pr, stream=out).sort_stats("cumulative").print_stats(45)
+        pstats.Stats(pr, stream=out).sort_stats("tottime").print_stats(30)
         print(out.getvalue(), flush=True)
         return
     for mode in ("per_call", "batched", "per_call", "batched"):

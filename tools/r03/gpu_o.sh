@@ -1,0 +1,9 @@
+# Round 3 (o): the full -m gpu suite and smoke on the round-3 code
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r03o}; mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/ --durations=25 > $OUT/tests.log 2>&1; rc=$?
+tail -30 $OUT/tests.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" $OUT/tests.log | head -20; exit $rc; }
+timeout -k 10 150 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
+cat $OUT/smoke.log

@@ -890,7 +890,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)p));
 }
 
-template <int C4, int CB = 16>
+template <int C4>
 __device__ __forceinline__ NarrowLds stage_narrow_roww(const PlanView& p, int g, float4* s_data, int nthreads) {
   NarrowLds L;
   const int r_beg = p.grp_row_ptr[g];
@@ -903,18 +903,12 @@ __device__ __forceinline__ NarrowLds stage_narrow_roww(const PlanView& p, int g,
   // offsets in 32-bit words from s_data (index arithmetic keeps the LDS address space: a
   // pointer rebuilt from an integer would become a generic one and every read a flat load)
   int32_t* base32 = reinterpret_cast<int32_t*>(s_data);
-  int32_t* rec = base32 + (ns + 2) * C4 * (CB / 4);
+  int32_t* rec = base32 + (ns + 2) * C4 * 4;
   uint32_t* slots = reinterpret_cast<uint32_t*>(rec + 4 * nrec);
   const uint32_t slots_addr = lds_addr(slots);
-  if constexpr (CB == 16) {
-    for (int k = threadIdx.x; k < 2 * C4; k += nthreads)  // zero tiles: slot ns = -0.0, ns + 1 = +0.0
-      s_data[static_cast<size_t>(ns) * C4 + k] = k < C4 ? make_float4(-0.f, -0.f, -0.f, -0.f)
-                                                        : make_float4(0.f, 0.f, 0.f, 0.f);
-  } else {  // bf16 image: -0.0 is 0x8000 per element
-    u32x2* s2 = reinterpret_cast<u32x2*>(s_data);
-    for (int k = threadIdx.x; k < 2 * C4; k += nthreads)
-      s2[static_cast<size_t>(ns) * C4 + k] = k < C4 ? u32x2{0x80008000u, 0x80008000u} : u32x2{0u, 0u};
-  }
+  for (int k = threadIdx.x; k < 2 * C4; k += nthreads)  // zero tiles: slot ns = -0.0, ns + 1 = +0.0
+    s_data[static_cast<size_t>(ns) * C4 + k] = k < C4 ? make_float4(-0.f, -0.f, -0.f, -0.f)
+                                                      : make_float4(0.f, 0.f, 0.f, 0.f);
   for (int k = threadIdx.x; k < nrec; k += nthreads) {
     const int row = k < L.nr ? k : k / kRpw * kRpw;  // padding rows: their pass's first row
     const int q0 = p.nrow_ptr[r_beg + row] - e_beg, q1 = p.nrow_ptr[r_beg + row + 1] - e_beg;
@@ -953,17 +947,6 @@ __device__ __forceinline__ uint32_t slot_addr_hi(uint32_t word, uint32_t base) {
   asm("v_mad_u32_u16 %0, %1, 16, %2 op_sel:[1,0,0,0]" : "=v"(a) : "v"(word), "v"(base));
   return a;
 }
-// bf16 LDS image (8-B chunks): slot * 8 + base
-__device__ __forceinline__ uint32_t slot_addr8_lo(uint32_t word, uint32_t base) {
-  uint32_t a;
-  asm("v_mad_u32_u16 %0, %1, 8, %2" : "=v"(a) : "v"(word), "v"(base));
-  return a;
-}
-__device__ __forceinline__ uint32_t slot_addr8_hi(uint32_t word, uint32_t base) {
-  uint32_t a;
-  asm("v_mad_u32_u16 %0, %1, 8, %2 op_sel:[1,0,0,0]" : "=v"(a) : "v"(word), "v"(base));
-  return a;
-}
 __device__ __forceinline__ uint2 lds_u2(uint32_t addr) {
   typedef unsigned int u32x2_lds __attribute__((ext_vector_type(2)));
   const u32x2_lds q = *reinterpret_cast<__attribute__((address_space(3))) const u32x2_lds*>(static_cast<uintptr_t>(addr));
@@ -986,18 +969,7 @@ __device__ __forceinline__ uint4 lds_u4(uint32_t addr) {
 // row of the pass (host padding), so the loop counts on the scalar unit: per batch 4 address +
 // 16 (EXACT) or 8 (FMA) arithmetic VALU and one cursor add.  (Before the tail, rows padded to
 // whole batches of four read 9.6 % zero-tile slots on config 5.)
-// one operand's chunk from the data tile: fp32 image (16-B chunks) or bf16 image (8-B chunks,
-// unpacked after the read: half the LDS bytes, four more VALU per chunk)
-template <int CB>
-__device__ __forceinline__ float4 narrow_x(uint32_t word, uint32_t base, bool hi) {
-  if constexpr (CB == 16) return lds_f4(hi ? slot_addr_hi(word, base) : slot_addr_lo(word, base));
-  else {
-    const uint2 q = lds_u2(hi ? slot_addr8_hi(word, base) : slot_addr8_lo(word, base));
-    return Io<uint16_t>::f4(u32x2{q.x, q.y});
-  }
-}
-
-template <typename T, bool EXACT, int CB = 16>
+template <typename T, bool EXACT>
 __device__ __forceinline__ float4 narrow_row_tail(float4 acc, float w, uint2 e, uint32_t base, int rem) {
   // one operand at a time (a 1-3 long tail per row; read and use back to back keeps the
   // register budget of two workgroups per CU)
@@ -1005,12 +977,14 @@ __device__ __forceinline__ float4 narrow_row_tail(float4 acc, float w, uint2 e, 
   for (int u = 0; u < 3; ++u) {
     if (rem <= u) break;  // wave-uniform
     const uint32_t word = u < 2 ? e.x : e.y;
-    acc = next4t<T, EXACT>(acc, w, narrow_x<CB>(word, base, u == 1));
+    uint32_t addr;
+    addr = u == 1 ? slot_addr_hi(word, base) : slot_addr_lo(word, base);
+    acc = next4t<T, EXACT>(acc, w, lds_f4(addr));
   }
   return acc;
 }
 
-template <typename T, bool EXACT, int CB = 16>
+template <typename T, bool EXACT>
 __device__ __forceinline__ float4 narrow_row_roww(uint4 rc, uint32_t base) {
   const int nb = __builtin_amdgcn_readfirstlane(static_cast<int>(rc.y & 0xffffu));
   const int rem = __builtin_amdgcn_readfirstlane(static_cast<int>(rc.y >> 16));
@@ -1020,20 +994,10 @@ __device__ __forceinline__ float4 narrow_row_roww(uint4 rc, uint32_t base) {
   uint2 e = lds_u2(q);
   for (int b = 0; b < nb; ++b) {
     float4 x[4];
-    if constexpr (CB == 16) {
-      x[0] = lds_f4(slot_addr_lo(e.x, base));
-      x[1] = lds_f4(slot_addr_hi(e.x, base));
-      x[2] = lds_f4(slot_addr_lo(e.y, base));
-      x[3] = lds_f4(slot_addr_hi(e.y, base));
-    } else {  // the four 8-B reads first, then the unpacking
-      uint2 r[4];
-      r[0] = lds_u2(slot_addr8_lo(e.x, base));
-      r[1] = lds_u2(slot_addr8_hi(e.x, base));
-      r[2] = lds_u2(slot_addr8_lo(e.y, base));
-      r[3] = lds_u2(slot_addr8_hi(e.y, base));
-#pragma unroll
-      for (int u = 0; u < 4; ++u) x[u] = Io<uint16_t>::f4(u32x2{r[u].x, r[u].y});
-    }
+    x[0] = lds_f4(slot_addr_lo(e.x, base));
+    x[1] = lds_f4(slot_addr_hi(e.x, base));
+    x[2] = lds_f4(slot_addr_lo(e.y, base));
+    x[3] = lds_f4(slot_addr_hi(e.y, base));
     asm("v_add_u32 %0, 8, %0" : "+v"(q));
     e = lds_u2(q);  // next batch (or the read-ahead pad), in flight with this batch's data reads
 #pragma unroll
@@ -1042,7 +1006,7 @@ __device__ __forceinline__ float4 narrow_row_roww(uint4 rc, uint32_t base) {
     // read to the loop head and waits on it before the data reads
     asm volatile("" : "+v"(e.x), "+v"(e.y));
   }
-  return narrow_row_tail<T, EXACT, CB>(acc, w, e, base, rem);
+  return narrow_row_tail<T, EXACT>(acc, w, e, base, rem);
 }
 
 template <int C4>
@@ -1119,22 +1083,17 @@ __device__ __forceinline__ int narrow_set(int p, int wave, int nwaves) {
 
 // NP = row sets held in registers: kNarrowPasses for one resident workgroup per CU (128 VGPRs),
 // 0 for two (64 VGPRs: the extents are then read from LDS each pass).
-// B16I (bf16 pools, ROWW plans): the data tile holds the staged chunks as loaded (8-B bf16
-// chunks, no unpacking at staging) and every operand read unpacks its chunk: half the LDS bytes
-// of the fp32 image per (row, operand, column), four more VALU per chunk.
-template <int C4, int NT, int J, int NP, bool EXACT, typename T = float, bool ROWW = false, bool B16I = false>
+template <int C4, int NT, int J, int NP, bool EXACT, typename T = float, bool ROWW = false>
 __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round_f32_narrow(
     const T* __restrict__ pin, int64_t ld_in4, T* __restrict__ pout, int64_t ld_out4, int64_t n4,
     PlanView p, int64_t n_tiles) {
   static_assert(C4 == 16 || C4 == 32, "narrow tiles are 16 or 32 float4 wide");
-  static_assert(!B16I || (ROWW && kIsBf16<T>), "the bf16 image is for bf16 pools under ROWW plans");
-  constexpr int kCB = B16I ? 8 : 16;  // LDS bytes per staged chunk
   static_assert(NT % C4 == 0, "a block stages whole source tiles");
   constexpr int kRpw = 64 / C4;
   constexpr int kW = NT / 64;
   extern __shared__ float4 s_data[];
   const int g = blockIdx.y;
-  const NarrowLds L = ROWW ? stage_narrow_roww<C4, kCB>(p, g, s_data, NT) : stage_narrow<C4>(p, g, s_data, NT);
+  const NarrowLds L = ROWW ? stage_narrow_roww<C4>(p, g, s_data, NT) : stage_narrow<C4>(p, g, s_data, NT);
   const int s_beg = p.grp_src_ptr[g];
   const int ns = p.grp_src_ptr[g + 1] - s_beg;
   const int c = threadIdx.x % C4;
@@ -1170,7 +1129,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   }
   const int n_sets = (L.nr + kRpw - 1) / kRpw;
   // ROWW: this lane's column base in the data tile, and its record offset within a pass
-  const uint32_t col_base = lds_addr(s_data) + static_cast<uint32_t>(cl * kCB);
+  const uint32_t col_base = lds_addr(s_data + cl);
   const uint32_t rec_lane = L.rec + 16u * static_cast<uint32_t>(sub);
   typename Io<T>::raw_t v[J];  // converted to fp32 when written to LDS, not when loaded
   auto load_tile = [&](int64_t tt) {
@@ -1194,8 +1153,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const int k = j * NT + static_cast<int>(threadIdx.x);
-      if constexpr (B16I) reinterpret_cast<u32x2*>(s_data)[k < staged ? k : c] = v[j];
-      else s_data[k < staged ? k : c] = Io<T>::f4(v[j]);
+      s_data[k < staged ? k : c] = Io<T>::f4(v[j]);
     }
     __syncthreads();
     if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
@@ -1208,7 +1166,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
 #ifdef TAL_PROBE_NOCOMP  // A/B probe (tools/gpu_k3n_probe.sh): stores without the row arithmetic
         const float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #else
-        const float4 acc = narrow_row_roww<T, EXACT, kCB>(rc, col_base);
+        const float4 acc = narrow_row_roww<T, EXACT>(rc, col_base);
 #endif
         if (static_cast<int32_t>(rc.w) >= 0 && col < n4)
           Io<T>::st(pout, static_cast<int64_t>(static_cast<int32_t>(rc.w)) * ld_out4 + col, acc);
@@ -1712,18 +1670,10 @@ int resident_per_cu(const void* kernel, int threads, size_t lds) {
   return nb;
 }
 
-bool narrow_b16_image() {
-  static const int on = [] {
-    const char* e = getenv("TAL_NARROW_B16_IMAGE");
-    return e && atoi(e) > 0 ? 1 : 0;
-  }();
-  return on != 0;
-}
-
 template <int C4, int J, bool EXACT, typename T = float, bool ROWW = false>
 int32_t launch_round_narrow_jr(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
                                const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
-  size_t lds = static_cast<size_t>(in.lds_bytes);
+  const size_t lds = static_cast<size_t>(in.lds_bytes);
   // two workgroups per CU when their LDS allows it (registers capped at 64), else one with the
   // row extents in registers
   constexpr int kNP = J >= 12 ? kNarrowPasses / 2 : kNarrowPasses;  // J = 12: VGPRs for the staging
@@ -1732,15 +1682,6 @@ int32_t launch_round_narrow_jr(const T* pin, int64_t ld_in, T* pout, int64_t ld_
   if constexpr (J <= 4)
     if (2 * lds <= 160 * 1024) k = k_round_f32_narrow<C4, kNarrowThreads, J, 0, EXACT, T, ROWW>;
 #endif
-  if constexpr (ROWW && kIsBf16<T> && J <= 4) {
-    if (narrow_b16_image()) {
-      // the plan's LDS size counts 16-B chunks; the bf16 image needs 8 B of each data chunk
-      // (exact for one group; a multi-group plan keeps the larger carve: its largest group need
-      // not be the one with the most sources)
-      if (in.n_groups == 1) lds -= static_cast<size_t>(in.max_src + 2) * C4 * 8;
-      k = k_round_f32_narrow<C4, kNarrowThreads, J, 0, EXACT, T, ROWW, true>;
-    }
-  }
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;
   const int64_t tiles = (n4 + C4 - 1) / C4;
