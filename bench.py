@@ -65,7 +65,7 @@ def parse():
                         "elements (int64 buffers kept); the config names the reduced layout")
     p.add_argument("--no-k1", action="store_true", help="skip the per-call K1 side measurement")
     p.add_argument("--host-path", action="store_true", help="also time the H2D+K1+D2H per-call path")
-    p.add_argument("--placement-trials", type=int, default=8,
+    p.add_argument("--placement-trials", type=int, default=16,
                    help="N = 1: candidate pools for the placement calibration (arena.select_pool_pair); "
                         "2 = none (the first two allocations)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],

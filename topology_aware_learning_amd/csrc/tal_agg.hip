@@ -462,6 +462,7 @@ __device__ __forceinline__ void st_stream(float* base, int64_t i, float4 v) {
 // ------------------------------------------------------------------------------------------
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
@@ -541,7 +542,7 @@ struct Io<uint16_t> {
   static __device__ __forceinline__ float4 f4(raw_t q) {
     return make_float4(bf16_lo(q.x), bf16_hi(q.x), bf16_lo(q.y), bf16_hi(q.y));
   }
-  static __device__ __forceinline__ void st(uint16_t* b, int64_t i4, float4 v) {
+  static __device__ __forceinline__ u32x2 pack(float4 v) {
     u32x2 q = {cvt_bf16x2(v.x, v.y), cvt_bf16x2(v.z, v.w)};
     // NaN canonicalisation (store_bf16x2) only where a lane holds one: two unordered compares
     // on the common path instead of four compare-and-selects
@@ -549,7 +550,10 @@ struct Io<uint16_t> {
       q.x = store_bf16x2(v.x, v.y);
       q.y = store_bf16x2(v.z, v.w);
     }
-    __builtin_nontemporal_store(q, reinterpret_cast<u32x2*>(b) + i4);
+    return q;
+  }
+  static __device__ __forceinline__ void st(uint16_t* b, int64_t i4, float4 v) {
+    __builtin_nontemporal_store(pack(v), reinterpret_cast<u32x2*>(b) + i4);
   }
   static __device__ __forceinline__ float ld1(const uint16_t* b, int64_t e) {
     return __uint_as_float(static_cast<uint32_t>(b[e]) << 16);
@@ -807,15 +811,17 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const T* __restrict
   // lane-fixed staging slots: slot k = j*NT + tid holds column c = tid % C4 (NT is a multiple
   // of C4) of staged source k / C4; only the source's pool row is kept per slot (-1 = unused)
   static_assert(NT % C4 == 0, "a block stages whole source tiles");
+  constexpr int kLd = J, kLps = C4;  // staging as k_round_f32_narrow without its 16-B bf16 lanes
+  constexpr bool W16 = false;
   // Branch-free staging (see k_round_f32_narrow): a slot past the group's sources reloads source
   // 0's chunk of its column and writes it where source 0's own slot does (the same value).
   // The write index and (dense form, whose registers are tight) the load addresses are recomputed
   // per tile behind an empty asm, so the compiler does not hoist them into more registers.
   const int c = threadIdx.x % C4;
-  int srow[J];
+  int srow[kLd];
 #pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int src = (j * NT + threadIdx.x) / C4;
+  for (int j = 0; j < kLd; ++j) {
+    const int src = (j * NT + threadIdx.x) / kLps;
     srow[j] = p.src_row[s_beg + (src < ns ? src : 0)];
   }
   typename Io<T>::raw_t v[J];
@@ -832,12 +838,18 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const T* __restrict
   if (t < n_tiles) load_tile(t);
   for (; t < n_tiles; t += gridDim.x) {
     __syncthreads();  // the previous tile's readers are done with s_data
-    int staged = ns * C4;  // float4 slots of real sources
+    int staged = ns * kLps;  // staging units (float4 slots; W16: slot pairs) of real sources
     asm volatile("" : "+s"(staged));
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
+    for (int j = 0; j < kLd; ++j) {
       const int k = j * NT + static_cast<int>(threadIdx.x);
-      s_data[k < staged ? k : c] = Io<T>::f4(v[j]);
+      if constexpr (W16) {
+        const int q = 2 * (k < staged ? k : c);
+        s_data[q] = Io<T>::f4(u32x2{v[j].x, v[j].y});
+        s_data[q + 1] = Io<T>::f4(u32x2{v[j].z, v[j].w});
+      } else {
+        s_data[k < staged ? k : c] = Io<T>::f4(v[j]);
+      }
     }
     __syncthreads();
     if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
@@ -1083,12 +1095,20 @@ __device__ __forceinline__ int narrow_set(int p, int wave, int nwaves) {
 
 // NP = row sets held in registers: kNarrowPasses for one resident workgroup per CU (128 VGPRs),
 // 0 for two (64 VGPRs: the extents are then read from LDS each pass).
-template <int C4, int NT, int J, int NP, bool EXACT, typename T = float, bool ROWW = false>
+// W16 (bf16 pools): staging loads are 16 B per lane (two 4-element chunks, C4/2 lanes per source
+// and tile, J/2 loads per lane) instead of 8 B; each lane writes its two chunks to LDS as two
+// adjacent fp32 float4.  Needs a row stride of an even number of chunks and a 16-B aligned base
+// (the launcher checks); a row's last, odd chunk then reads the first chunk of its padding,
+// which no store uses.
+template <int C4, int NT, int J, int NP, bool EXACT, typename T = float, bool ROWW = false, bool W16 = false>
 __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round_f32_narrow(
     const T* __restrict__ pin, int64_t ld_in4, T* __restrict__ pout, int64_t ld_out4, int64_t n4,
     PlanView p, int64_t n_tiles) {
   static_assert(C4 == 16 || C4 == 32, "narrow tiles are 16 or 32 float4 wide");
   static_assert(NT % C4 == 0, "a block stages whole source tiles");
+  static_assert(!W16 || (kIsBf16<T> && J % 2 == 0), "16-B staging lanes: bf16 pools, even J");
+  constexpr int kLd = W16 ? J / 2 : J;       // staging loads per lane
+  constexpr int kLps = W16 ? C4 / 2 : C4;    // staging lanes per source and tile
   constexpr int kRpw = 64 / C4;
   constexpr int kW = NT / 64;
   extern __shared__ float4 s_data[];
@@ -1096,7 +1116,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   const NarrowLds L = ROWW ? stage_narrow_roww<C4>(p, g, s_data, NT) : stage_narrow<C4>(p, g, s_data, NT);
   const int s_beg = p.grp_src_ptr[g];
   const int ns = p.grp_src_ptr[g + 1] - s_beg;
-  const int c = threadIdx.x % C4;
+  const int c = threadIdx.x % kLps;  // staging: the lane's chunk (W16: chunk pair) of its source
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int sub = lane / C4;
@@ -1108,10 +1128,10 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   // The write index and (pairs form, whose registers are tight) the load addresses are
   // recomputed per tile behind an empty asm, so the compiler does not hoist them into J more
   // registers each (it spilled).
-  int srow[J];
+  int srow[kLd];
 #pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int src = (j * NT + threadIdx.x) / C4;
+  for (int j = 0; j < kLd; ++j) {
+    const int src = (j * NT + threadIdx.x) / kLps;
     srow[j] = p.src_row[s_beg + (src < ns ? src : 0)];
   }
   __syncthreads();  // plan slice staged
@@ -1131,29 +1151,45 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   // ROWW: this lane's column base in the data tile, and its record offset within a pass
   const uint32_t col_base = lds_addr(s_data + cl);
   const uint32_t rec_lane = L.rec + 16u * static_cast<uint32_t>(sub);
-  typename Io<T>::raw_t v[J];  // converted to fp32 when written to LDS, not when loaded
+  // converted to fp32 when written to LDS, not when loaded
+  typedef typename std::conditional<W16, u32x4, typename Io<T>::raw_t>::type raw_t;
+  raw_t v[kLd];
   auto load_tile = [&](int64_t tt) {
 #ifdef TAL_PROBE_NOLOAD  // A/B probe: no HBM reads (the tile keeps the first tile's values)
     if (tt != blockIdx.x) return;
 #endif
-    const int64_t col = min(tt * C4 + c, n4 - 1);  // past the end: a duplicate (cache hit)
+    if constexpr (W16) {  // 16-B units: chunk pair tt * C4 / 2 + c of each row
+      const int64_t col = min(tt * kLps + c, (n4 - 1) / 2);  // past the end: a duplicate
+      const u32x4* b = reinterpret_cast<const u32x4*>(pin);
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-      int r = srow[j];
-      if constexpr (!ROWW) asm volatile("" : "+v"(r));
-      v[j] = Io<T>::ld_raw(pin, static_cast<int64_t>(r) * ld_in4 + col);
+      for (int j = 0; j < kLd; ++j)
+        v[j] = __builtin_nontemporal_load(b + static_cast<int64_t>(srow[j]) * (ld_in4 / 2) + col);
+    } else {
+      const int64_t col = min(tt * C4 + c, n4 - 1);  // past the end: a duplicate (cache hit)
+#pragma unroll
+      for (int j = 0; j < kLd; ++j) {
+        int r = srow[j];
+        if constexpr (!ROWW) asm volatile("" : "+v"(r));
+        v[j] = Io<T>::ld_raw(pin, static_cast<int64_t>(r) * ld_in4 + col);
+      }
     }
   };
   int64_t t = blockIdx.x;
   if (t < n_tiles) load_tile(t);
   for (; t < n_tiles; t += gridDim.x) {
     __syncthreads();  // the previous tile's readers are done with s_data
-    int staged = ns * C4;  // float4 slots of real sources
+    int staged = ns * kLps;  // staging units (float4 slots; W16: slot pairs) of real sources
     asm volatile("" : "+s"(staged));
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
+    for (int j = 0; j < kLd; ++j) {
       const int k = j * NT + static_cast<int>(threadIdx.x);
-      s_data[k < staged ? k : c] = Io<T>::f4(v[j]);
+      if constexpr (W16) {
+        const int q = 2 * (k < staged ? k : c);
+        s_data[q] = Io<T>::f4(u32x2{v[j].x, v[j].y});
+        s_data[q + 1] = Io<T>::f4(u32x2{v[j].z, v[j].w});
+      } else {
+        s_data[k < staged ? k : c] = Io<T>::f4(v[j]);
+      }
     }
     __syncthreads();
     if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
@@ -1168,8 +1204,9 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
 #else
         const float4 acc = narrow_row_roww<T, EXACT>(rc, col_base);
 #endif
-        if (static_cast<int32_t>(rc.w) >= 0 && col < n4)
+        if (static_cast<int32_t>(rc.w) >= 0 && col < n4) {
           Io<T>::st(pout, static_cast<int64_t>(static_cast<int32_t>(rc.w)) * ld_out4 + col, acc);
+        }
       }
       continue;
     }
@@ -1670,6 +1707,15 @@ int resident_per_cu(const void* kernel, int threads, size_t lds) {
   return nb;
 }
 
+// 16-B staging lanes for bf16 pools (W16 in k_round_f32_narrow): on unless TAL_NARROW_W16=0 (A/B)
+bool narrow_w16_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("TAL_NARROW_W16");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <int C4, int J, bool EXACT, typename T = float, bool ROWW = false>
 int32_t launch_round_narrow_jr(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
                                const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
@@ -1682,6 +1728,12 @@ int32_t launch_round_narrow_jr(const T* pin, int64_t ld_in, T* pout, int64_t ld_
   if constexpr (J <= 4)
     if (2 * lds <= 160 * 1024) k = k_round_f32_narrow<C4, kNarrowThreads, J, 0, EXACT, T, ROWW>;
 #endif
+  if constexpr (kIsBf16<T> && J >= 2 && J <= 4) {
+    // whole chunk pairs per row (even stride in chunks) from a 16-B aligned base
+    if (narrow_w16_enabled() && (ld_in / 4) % 2 == 0 && (reinterpret_cast<uintptr_t>(pin) & 15) == 0)
+      k = 2 * lds <= 160 * 1024 ? k_round_f32_narrow<C4, kNarrowThreads, J, 0, EXACT, T, ROWW, true>
+                                : k_round_f32_narrow<C4, kNarrowThreads, J, kNP, EXACT, T, ROWW, true>;
+  }
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;
   const int64_t tiles = (n4 + C4 - 1) / C4;
@@ -2110,7 +2162,6 @@ __device__ __forceinline__ void reg_wait(v32f& X0, v32f& X1, v32f& X2, v32f& X3)
 // op_sel:[0,1] op_sel_hi:[1,1] its high dword.  The two rows' chains are interleaved, so no
 // packed instruction reads the result of the one right before it (gfx950 needs a wait state
 // there).  M0, which the index mode writes, is used by nothing else in this kernel (no LDS).
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // one trip: i* / j* = A's / B's index SGPRs, wa* / wb* = their weight pairs
 #define TAL_TRIP_E(i0, i1, i2, i3, j0, j1, j2, j3, wa01, wa23, wb01, wb23)                            \
