@@ -71,3 +71,41 @@ def test_strategy_dispatch_and_unweighted_fl_topology(tmp_path, monkeypatch, rec
     assert np.array_equal(app.topology, np.ones((4, 4)) - np.eye(4))
     app.run()
     assert len(recorder) == 4 and all(len(c["ids"]) == 4 for c in recorder)
+
+
+def test_parsl_standin_dependencies():
+    """The in-process Parsl stand-in: an app waits for every distinct future among its args and
+    kwargs (the same future passed ten times counts once), runs once, and a failed dependency's
+    exception becomes the app's (reference apps take AppFutures, decentralized_app.py:605-641)."""
+    import threading
+    from concurrent.futures import Future
+
+    from src import _parsl_compat as pc
+
+    if pc.HAVE_PARSL:
+        pytest.skip("real Parsl installed")
+    runs = []
+
+    @pc.python_app(executors=["threadpool_executor"])
+    def app(a, *rest, k=None):
+        runs.append(threading.get_ident())
+        return a + sum(rest) + (k or 0)
+
+    f = Future()
+    g = Future()
+    out = app(f, f, f, 1, k=g)  # same future three times + a kwarg future
+    assert not out.done()
+    f.set_result(10)
+    assert not out.done()
+    g.set_result(5)
+    assert out.result(timeout=10) == 10 * 3 + 1 + 5
+    assert len(runs) == 1
+    done = Future()
+    done.set_result(2)
+    assert app(done, done).result(timeout=10) == 4  # dependencies already resolved
+    bad = Future()
+    chained = app(bad, f)
+    bad.set_exception(ValueError("upstream"))
+    with pytest.raises(ValueError, match="upstream"):
+        chained.result(timeout=10)
+    assert app(app(done, 1), 1).result(timeout=10) == 4  # app futures chain
