@@ -68,6 +68,10 @@ def parse():
     p.add_argument("--placement-trials", type=int, default=16,
                    help="N = 1: candidate pools for the placement calibration (arena.select_pool_pair); "
                         "2 = none (the first two allocations)")
+    p.add_argument("--sharded", action="store_true",
+                   help="run the sharded (N > 1) path at N = 1 as well: a one-rank process group, the "
+                        "exchange's collectives on RCCL with nothing to move (a check of that code path "
+                        "on one GPU, never the benchmark)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="N > 1: nccl (RCCL over xGMI, the benchmark); gloo = rehearsal of the same "
                         "code path with the exchange staged through host memory, ranks may share a GPU")
@@ -256,7 +260,8 @@ def main():
         local %= torch.cuda.device_count()  # rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    sharded = world > 1 or args.sharded
+    if sharded:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -280,7 +285,7 @@ def main():
     n_dev_total = len(orders)
     M = max(len(o) for o in orders)
 
-    if world == 1:
+    if not sharded:
         from topology_aware_learning_amd import ops as _ops
 
         rows = n_dev_total
@@ -454,18 +459,18 @@ def main():
         hostp = None
 
     if rank != 0:
-        if world > 1:
+        if sharded:
             dist.barrier()
             dist.destroy_process_group()
         return
 
     achieved = bytes_round / (k_ms * 1e-3) / 1e9
     traffic = None
-    if world == 1:  # PMC bytes of exactly this kernel + plan spec + workload, when profiled
+    if not sharded:  # PMC bytes of exactly this kernel + plan spec + workload, when profiled
         traffic = load_traffic(traffic_key(result_extra["kernel"], result_extra["plan"]["spec"],
                                            workload_key(args.graph, n_dev_total, args.model, args.dtype, args.weights)))
     cpu = None
-    if not args.no_cpu_baseline and world == 1:
+    if not args.no_cpu_baseline and not sharded:
         log("CPU baseline")
         cpu = cpu_baseline(lay, M, args.cpu_seconds)  # bf16 layouts: the reference's loop on bf16 tensors
     value = units / el
@@ -489,7 +494,7 @@ def main():
                                + "one full aggregation round per step, snapshot semantics",
                    "model_layout": args.model + (f" (first {args.max_params} float params: rehearsal)"
                                                  if args.max_params else ""), "devices": n_dev_total, "devices_per_gpu": args.devices_per_gpu,
-                   "params_per_model": n_params, "parallelism": f"{result_extra.get('exchange', '')}-sharded x{world}" if world > 1 else "1 GPU"},
+                   "params_per_model": n_params, "parallelism": f"{result_extra.get('exchange', '')}-sharded x{world}" if sharded else "1 GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                      "bytes_per_launch": bytes_round, "kernel_ms": k_ms},
@@ -502,7 +507,7 @@ def main():
     if hostp is not None:
         out["host_path_per_call"] = hostp
     print(json.dumps(out), flush=True)
-    if world > 1:
+    if sharded:
         dist.barrier()
         dist.destroy_process_group()
 

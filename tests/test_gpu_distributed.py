@@ -217,3 +217,31 @@ def test_bench_world8_rehearsal(cuda, tmp_path, graph, model, dtype, exchange):
     assert d["value"] > 0 and d["link_bytes_in_per_round"] > 0
     if exchange != "auto":
         assert d["exchange"] == exchange
+
+
+@pytest.mark.parametrize("exchange", ["halo", "transpose"])
+def test_bench_sharded_one_rank_rccl(cuda, tmp_path, exchange):
+    """bench.py's sharded branch on a one-rank RCCL (backend "nccl") process group: the
+    exchange's collectives (batched P2P group / all_to_all_single on device tensors, the
+    spot-check all-reduce, barriers) on the real transport with nothing to move — the RCCL
+    calls of the 8-GPU run, on one GPU (RCCL refuses two ranks on one device)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    port = 28700 + (os.getpid() % 400) + (0 if exchange == "halo" else 3)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", str(ROOT / "bench.py"), "--gpus", "1",
+           "--sharded", "--dist-backend", "nccl", "--exchange", exchange, "--model", "cifar10",
+           "--devices-per-gpu", "16", "--degree", "4", "--steps", "2", "--warmup", "1", "--no-tune"]
+    out = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1, out.stdout[-2000:]
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 1 and d["parity"] is True and d["exchange"] == exchange
+    assert d["config"]["parallelism"] == f"{exchange}-sharded x1"

@@ -92,7 +92,8 @@ def exchange_bytes(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: int
     halo_link = max([len(v) for s in specs for v in list(s.send.values()) + list(s.recv.values())] or [0]) * row
     own = max(len(s.own) for s in specs)
     return dict(halo=int(halo), transpose=int(2 * own * row * (world - 1) // world),
-                halo_link=int(halo_link), transpose_link=int(-(-2 * own * row // world)))
+                halo_link=int(halo_link),
+                transpose_link=int(-(-2 * own * row // world)) if world > 1 else 0)  # one rank: no link
 
 
 HBM_GBPS = 8000.0       # MI355X HBM3E peak per GPU (MI355X_MICROARCH.md)
