@@ -538,37 +538,43 @@ def bf16_tolerance(pin, pout, order, weights, n, dev) -> dict:
                 bound="|d| <= 2^-8 |ref| + M 2^-24 sum|w x| (SURVEY §8(a) bf16 run)")
 
 
-def bench_k1(layout, pool, orders, weights, mode, dev, reps: int = 20):
+def bench_k1(layout, pool, orders, weights, mode, dev, reps: int = 64):
     """Per-call K1 (no cross-call reuse) as the per-call product path runs it: one launch over
     the fp32 and int64 segments of a call (tal_agg_model_f32), rows rotated over the round's
-    calls; SURVEY §8(d) B = 4 N (M+1) + 8 N_i64 (M+1).  HIP events around each launch."""
+    calls; SURVEY §8(d) B = 4 N (M+1) + 8 N_i64 (M+1).  HIP events around `reps` calls issued
+    back to back (operand lists built beforehand), so the time is the kernels' and not the
+    Python between an event and its launch (an event pair around each single call measured
+    0.198 ms for a 0.157 ms kernel)."""
     import torch
 
     from topology_aware_learning_amd import ops
 
     out = torch.empty(layout.n_f32, dtype=torch.float32, device=dev)
     out_i = torch.empty(layout.n_i64, dtype=torch.int64, device=dev)
+    calls = [([pool.row_f32(j) for j in orders[r % len(orders)]], [pool.row_i64(j) for j in orders[r % len(orders)]],
+              weights[r % len(orders)]) for r in range(reps)]
 
-    def call(r):
-        o = orders[r % len(orders)]
-        ops.agg_model_f32([pool.row_f32(j) for j in o], [pool.row_i64(j) for j in o], weights[r % len(orders)],
-                          out, out_i, mode=mode)
+    def call(c):
+        ops.agg_model_f32(c[0], c[1], c[2], out, out_i, mode=mode)
 
-    for r in range(3):
-        call(r)
+    for c in calls[:3]:
+        call(c)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ts = []
-    for r in range(reps):
+    for _ in range(3):
+        torch.cuda.synchronize(dev)
         s.record()
-        call(r)  # rotate rows: defeat the MALL
+        for c in calls:  # rotate rows: defeat the MALL
+            call(c)
         e.record()
         e.synchronize()
-        ts.append(s.elapsed_time(e))
+        ts.append(s.elapsed_time(e) / len(calls))
     ms = float(np.median(ts))
     m = len(orders[0])
     b = (4 * layout.n_f32 + 8 * layout.n_i64) * (m + 1)
-    return dict(kernel="k_agg_model", launches_per_call=1, ms=ms, bytes=b, GBps=b / (ms * 1e-3) / 1e9,
-                frac=b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, params_per_s=(layout.n_f32 + layout.n_i64) / (ms * 1e-3))
+    return dict(kernel="k_agg_model", launches_per_call=1, ms=ms, calls_timed=len(calls), bytes=b,
+                GBps=b / (ms * 1e-3) / 1e9, frac=b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                params_per_s=(layout.n_f32 + layout.n_i64) / (ms * 1e-3))
 
 
 def bench_host_path(lay, m, dev, reps: int = 5):
