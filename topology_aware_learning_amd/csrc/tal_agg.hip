@@ -291,7 +291,11 @@ __global__ __launch_bounds__(kBlock) void k_agg_model(OpTableModel t, int m_rt, 
         float4 acc = first4<EXACT>(t.w[0], v[0]);
 #pragma unroll
         for (int k = 1; k < M_STATIC; ++k) acc = next4<EXACT>(acc, t.w[k], v[k]);
+#ifdef TAL_PROBE_K1_NTSTORE  // A/B probe: non-temporal output store
+        __builtin_nontemporal_store(v4f{acc.x, acc.y, acc.z, acc.w}, reinterpret_cast<v4f*>(out) + i);
+#else
         reinterpret_cast<float4*>(out)[i] = acc;
+#endif
       } else {
         float4 acc = first4<EXACT>(t.w[0], ld_stream(t.x[0], i));
         for (int k = 1; k < m; k += 8) {
@@ -1097,9 +1101,8 @@ __device__ __forceinline__ int narrow_set(int p, int wave, int nwaves) {
 // 0 for two (64 VGPRs: the extents are then read from LDS each pass).
 // W16 (bf16 pools): staging loads are 16 B per lane (two 4-element chunks, C4/2 lanes per source
 // and tile, J/2 loads per lane) instead of 8 B; each lane writes its two chunks to LDS as two
-// adjacent fp32 float4.  Needs a row stride of an even number of chunks and a 16-B aligned base
-// (the launcher checks); a row's last, odd chunk then reads the first chunk of its padding,
-// which no store uses.
+// adjacent fp32 float4.  Needs an even chunk count, a row stride of an even number of chunks and
+// a 16-B aligned base (the launcher checks), so every pair lies inside its row.
 template <int C4, int NT, int J, int NP, bool EXACT, typename T = float, bool ROWW = false, bool W16 = false>
 __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round_f32_narrow(
     const T* __restrict__ pin, int64_t ld_in4, T* __restrict__ pout, int64_t ld_out4, int64_t n4,
@@ -1729,8 +1732,9 @@ int32_t launch_round_narrow_jr(const T* pin, int64_t ld_in, T* pout, int64_t ld_
     if (2 * lds <= 160 * 1024) k = k_round_f32_narrow<C4, kNarrowThreads, J, 0, EXACT, T, ROWW>;
 #endif
   if constexpr (kIsBf16<T> && J >= 2 && J <= 4) {
-    // whole chunk pairs per row (even stride in chunks) from a 16-B aligned base
-    if (narrow_w16_enabled() && (ld_in / 4) % 2 == 0 && (reinterpret_cast<uintptr_t>(pin) & 15) == 0)
+    // whole chunk pairs per row (an even chunk count and stride) from a 16-B aligned base: no
+    // pair reaches past a row's last chunk
+    if (narrow_w16_enabled() && n4 % 2 == 0 && (ld_in / 4) % 2 == 0 && (reinterpret_cast<uintptr_t>(pin) & 15) == 0)
       k = 2 * lds <= 160 * 1024 ? k_round_f32_narrow<C4, kNarrowThreads, J, 0, EXACT, T, ROWW, true>
                                 : k_round_f32_narrow<C4, kNarrowThreads, J, kNP, EXACT, T, ROWW, true>;
   }
