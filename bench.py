@@ -57,7 +57,7 @@ def parse():
     p.add_argument("--in-place", action="store_true",
                    help="N = 1, single-group plans: every round in place on one pool (RoundExecutor's own form)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=4.0,
+    p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bound of the CPU baseline sample (one call at a time; the two-concurrent-calls "
                         "configuration runs half as long)")
     p.add_argument("--max-params", type=int, default=0,
@@ -159,18 +159,22 @@ def cpu_baseline(layout_list, m: int, budget_s: float):
     all_threads = usable_cpus()
 
     def one_at_a_time(threads: int, secs: float):
+        """(calls, seconds, median seconds per call): the GPU box's host is shared, so a call's
+        time varies with other tenants; the median per call is the reported rate."""
         torch.set_num_threads(threads)
         torch_path.aggregate_call(sds, w, targets[0])  # warm-up
-        calls, t0 = 0, time.perf_counter()
+        calls, t0, per = 0, time.perf_counter(), []
         while True:
+            t = time.perf_counter()
             torch_path.aggregate_call(sds, w, targets[0])
+            per.append(time.perf_counter() - t)
             calls += 1
             el = time.perf_counter() - t0
             if el >= secs or calls >= 1024:
-                return calls, el
+                return calls, el, float(np.median(per))
 
-    calls_all, el_all = one_at_a_time(all_threads, 0.4 * budget_s)
-    calls_def, el_def = one_at_a_time(default_threads, 0.35 * budget_s)
+    calls_all, el_all, med_all = one_at_a_time(all_threads, 0.4 * budget_s)
+    calls_def, el_def, med_def = one_at_a_time(default_threads, 0.35 * budget_s)
     counts = [0, 0]
     stop = time.perf_counter() + 0.25 * budget_s
 
@@ -187,14 +191,14 @@ def cpu_baseline(layout_list, m: int, budget_s: float):
         t.join()
     el2 = time.perf_counter() - t1
     torch.set_num_threads(default_threads)
-    return dict(value=calls_all * n_out / el_all, unit="params/s", cores=all_threads, kind="port",
+    return dict(value=n_out / med_all, unit="params/s", cores=all_threads, kind="port",
                 sample=f"{calls_all} reference calls (M={m}, {n_out} params) one at a time in {el_all:.2f} s "
                        f"with torch.set_num_threads({all_threads}) (every core this process may run on: "
-                       "its affinity within the cgroup CPU quota); "
+                       "its affinity within the cgroup CPU quota), value from the median call; "
                        "torch CPU clone/mul/add_/copy_ on host state_dicts",
-                ms_per_call=1e3 * el_all / calls_all,
-                default_threads_value=calls_def * n_out / el_def, default_threads=default_threads,
-                default_threads_ms_per_call=1e3 * el_def / calls_def,
+                ms_per_call=1e3 * med_all, window_value=calls_all * n_out / el_all,
+                default_threads_value=n_out / med_def, default_threads=default_threads,
+                default_threads_ms_per_call=1e3 * med_def,
                 os_cpu_count=os.cpu_count(), affinity_cpus=all_threads, cpu_model=cpu_model(),
                 # the reference's effective configuration: Parsl ThreadPoolExecutor(max_threads=2)
                 two_concurrent_calls_value=sum(counts) * n_out / el2, two_concurrent_calls=sum(counts),
