@@ -216,9 +216,13 @@ class DecentrallearnApp:
         nxt = self.round_states[round_idx + 1] = {}
         cur = self.round_states[round_idx]
         sel = set(selected)
-        # the selected clients' neighbor draws of each loop in one RNG call (same stream as
-        # one get_neighbors() per client in client order, draw_neighbors)
-        draws = iter(draw_neighbors([c for c in self.clients if c.idx in sel]))
+        # both loops' neighbor draws (one get_neighbors() per selected client in client order,
+        # loop 1 then loop 2: nothing between them draws from NumPy's global RNG) in one RNG call
+        # made before any app is submitted: the same stream (draw_neighbors), and no GIL
+        # hand-off to the app threads in the middle of the round
+        picked = [c for c in self.clients if c.idx in sel]
+        both = draw_neighbors(picked + picked)
+        draws, draws2 = iter(both[:len(picked)]), iter(both[len(picked):])
         for client in self.clients:
             train_input = cur[client.idx]["agg"]
             if client.idx not in sel:
@@ -233,14 +237,13 @@ class DecentrallearnApp:
             self.centrality_dict = update_random_agg_coeffs(seed=self.seed, round_idx=round_idx,
                                                             num_clients=len(self.clients),
                                                             centrality_dict=self.centrality_dict)
-        draws = iter(draw_neighbors([c for c in self.clients if c.idx in sel]))
         for client in self.clients:
             agg_client = nxt[client.idx]["train"]
             if client.idx not in sel:
                 nxt[client.idx]["agg"] = agg_client
                 futures.append(agg_client)
                 continue
-            neighbor_idxs = next(draws)  # second, independent draw (:616)
+            neighbor_idxs = next(draws2)  # second, independent draw (:616)
             if len(neighbor_idxs) == 0:
                 nxt[client.idx]["agg"] = agg_client
                 futures.append(agg_client)
@@ -273,8 +276,15 @@ class DecentrallearnApp:
 
         from src.decentralized_client import aggregation_weights
 
+        done_of: dict = {}  # id(future) -> its result: each distinct future resolved once per round
+
         def res(x):
-            return x.result() if isinstance(x, Future) else x
+            if not isinstance(x, Future):
+                return x
+            r = done_of.get(id(x))
+            if r is None:
+                r = done_of[id(x)] = x.result()
+            return r
 
         orders, weights, out_rows, done = [], [], [], []
         row_of: dict = {}  # id(model) -> pool row: each model's binding is checked once per round
