@@ -158,11 +158,13 @@ def test_virtual_ranks_transposed_two_rounds(cuda, graph, world, dtype, mode, ch
         assert np.array_equal(sr.own_rows().i64[: sr.local_rows, :1].cpu().numpy(), iref[sr.own])
 
 
-@pytest.mark.parametrize("exchange,world", [("halo", 2), ("transpose", 2), ("transpose", 3), ("halo", 3)])
-def test_bench_multi_rank_rehearsal(cuda, tmp_path, exchange, world):
-    """bench.py's N > 1 branch end to end (make_round, tuning, exchange, spot check, timing, JSON)
-    with `world` ranks sharing this GPU over gloo (exchange staged through host memory): the
-    same code the 8-GPU RCCL run executes, except the transport."""
+@pytest.mark.parametrize("exchange,world,tune", [("halo", 2, False), ("transpose", 2, False), ("transpose", 3, False),
+                                                ("halo", 3, False), ("halo", 2, True), ("transpose", 2, True)])
+def test_bench_multi_rank_rehearsal(cuda, tmp_path, exchange, world, tune):
+    """bench.py's N > 1 branch end to end (make_round, exchange, spot check, timing, JSON) with
+    `world` ranks sharing this GPU over gloo (exchange staged through host memory): the same
+    code the 8-GPU RCCL run executes, except the transport; tune=True is the driver's default
+    command (every rank tunes its plans on its own buffers)."""
     import json
     import os
     import subprocess
@@ -171,11 +173,11 @@ def test_bench_multi_rank_rehearsal(cuda, tmp_path, exchange, world):
     from conftest import ROOT
 
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
-    port = 29500 + (os.getpid() % 400) + world * 7 + (0 if exchange == "halo" else 3)
+    port = 29500 + (os.getpid() % 400) + world * 7 + (0 if exchange == "halo" else 3) + (50 if tune else 0)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", str(ROOT / "bench.py"), "--gpus", str(world),
            "--dist-backend", "gloo", "--exchange", exchange, "--model", "cifar10", "--devices-per-gpu", "16",
-           "--degree", "4", "--steps", "2", "--warmup", "1", "--no-tune"]
+           "--degree", "4", "--steps", "2", "--warmup", "1"] + ([] if tune else ["--no-tune"])
     out = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-3000:]
     line = [l for l in out.stdout.splitlines() if l.startswith("{")]
@@ -219,8 +221,8 @@ def test_bench_world8_rehearsal(cuda, tmp_path, graph, model, dtype, exchange):
         assert d["exchange"] == exchange
 
 
-@pytest.mark.parametrize("exchange", ["halo", "transpose"])
-def test_bench_sharded_one_rank_rccl(cuda, tmp_path, exchange):
+@pytest.mark.parametrize("exchange,tune", [("halo", False), ("transpose", False), ("transpose", True)])
+def test_bench_sharded_one_rank_rccl(cuda, tmp_path, exchange, tune):
     """bench.py's sharded branch on a one-rank RCCL (backend "nccl") process group: the
     exchange's collectives (batched P2P group / all_to_all_single on device tensors, the
     spot-check all-reduce, barriers) on the real transport with nothing to move — the RCCL
@@ -233,11 +235,11 @@ def test_bench_sharded_one_rank_rccl(cuda, tmp_path, exchange):
     from conftest import ROOT
 
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
-    port = 28700 + (os.getpid() % 400) + (0 if exchange == "halo" else 3)
+    port = 28700 + (os.getpid() % 400) + (0 if exchange == "halo" else 3) + (20 if tune else 0)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
            "--master-addr", "127.0.0.1", f"--master-port={port}", str(ROOT / "bench.py"), "--gpus", "1",
            "--sharded", "--dist-backend", "nccl", "--exchange", exchange, "--model", "cifar10",
-           "--devices-per-gpu", "16", "--degree", "4", "--steps", "2", "--warmup", "1", "--no-tune"]
+           "--devices-per-gpu", "16", "--degree", "4", "--steps", "2", "--warmup", "1"] + ([] if tune else ["--no-tune"])
     out = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-3000:]
     line = [l for l in out.stdout.splitlines() if l.startswith("{")]
