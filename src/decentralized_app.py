@@ -179,7 +179,7 @@ class DecentrallearnApp:
         layout = layout_of_module(self.clients[0].model)
         # the pool the models live in for the whole run, placed where in-place rounds are fast
         pool = calibrated_pool(layout, len(self.clients), torch.device("cuda", torch.cuda.current_device()),
-                               trials=int(os.environ.get("TAL_POOL_PLACEMENT_TRIALS", "3")))
+                               trials=int(os.environ.get("TAL_POOL_PLACEMENT_TRIALS", "8")))
         for c in self.clients:
             c.model.to(pool.device)
             pool.bind(c.model, c.idx)

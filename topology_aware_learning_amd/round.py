@@ -129,7 +129,7 @@ class RoundExecutor:
             t.index_copy_(0, idx, src.index_select(0, idx))
 
 
-def calibrated_pool(layout, rows: int, device, trials: int = 3, degree: int = 8) -> ModelPool:
+def calibrated_pool(layout, rows: int, device, trials: int = 8, degree: int = 8) -> ModelPool:
     """A ModelPool placed where an in-place round runs fast.
 
     The HBM placement of the pool a round writes changes its time bimodally (config 3: ~2.05
