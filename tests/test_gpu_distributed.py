@@ -190,12 +190,14 @@ def test_bench_multi_rank_rehearsal(cuda, tmp_path, exchange, world, tune):
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("graph,model,dtype,exchange", [("barbell", "resnet50", "f32", "auto"),
                                                         ("sbm", "vit_b16", "bf16", "auto"),
-                                                        ("sbm", "vit_b16", "bf16", "transpose")])
+                                                        ("sbm", "vit_b16", "bf16", "transpose"),
+                                                        ("random", "resnet50", "f32", "auto")])
 def test_bench_world8_rehearsal(cuda, tmp_path, graph, model, dtype, exchange):
-    """bench.py --gpus 8 on BASELINE config 4 (barbell(60, 8), ResNet-50 layout) and config 5
-    (SBM 8 x 32, ViT-B/16 layout, bf16) with 8 gloo ranks sharing this GPU: the driver's 8-GPU
-    command with the exchange staged through host memory and the layouts cut to their first
-    131,072 float params (--max-params)."""
+    """bench.py --gpus 8 on BASELINE config 4 (barbell(60, 8), ResNet-50 layout), config 5
+    (SBM 8 x 32, ViT-B/16 layout, bf16) and the weak-scaling default (random 8-regular graph over
+    64 x 8 devices, ResNet-50 layout, plans tuned per rank: the driver's SCALE command) with 8
+    gloo ranks sharing this GPU: the exchange staged through host memory and the layouts cut to
+    their first 131,072 float params (--max-params)."""
     import json
     import os
     import subprocess
@@ -204,18 +206,20 @@ def test_bench_world8_rehearsal(cuda, tmp_path, graph, model, dtype, exchange):
     from conftest import ROOT
 
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
-    port = 29900 + (os.getpid() % 300) + (0 if graph == "barbell" else 11) + (0 if exchange == "auto" else 5)
+    port = 29900 + (os.getpid() % 300) + {"barbell": 0, "sbm": 11, "random": 23}[graph] + (0 if exchange == "auto" else 5)
+    devices = {"sbm": ["--devices", "256"], "barbell": ["--devices", "128"], "random": []}[graph]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
            "--master-addr", "127.0.0.1", f"--master-port={port}", str(ROOT / "bench.py"), "--gpus", "8",
-           "--dist-backend", "gloo", "--graph", graph, "--model", model, "--dtype", dtype, "--devices", "256"
-           if graph == "sbm" else "128", "--exchange", exchange, "--max-params", "131072",
-           "--steps", "2", "--warmup", "1", "--no-tune"]
+           "--dist-backend", "gloo", "--graph", graph, "--model", model, "--dtype", dtype, *devices,
+           "--exchange", exchange, "--max-params", "131072", "--steps", "2", "--warmup", "1"] + \
+        ([] if graph == "random" else ["--no-tune"])
     out = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=280)
     assert out.returncode == 0, out.stderr[-3000:]
     line = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(line) == 1, out.stdout[-2000:]
     d = json.loads(line[0])
-    assert d["n_gpus"] == 8 and d["parity"] is True and d["config"]["devices"] == (256 if graph == "sbm" else 128)
+    assert d["n_gpus"] == 8 and d["parity"] is True
+    assert d["config"]["devices"] == {"sbm": 256, "barbell": 128, "random": 512}[graph]
     assert d["value"] > 0 and d["link_bytes_in_per_round"] > 0
     if exchange != "auto":
         assert d["exchange"] == exchange
