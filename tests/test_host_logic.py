@@ -625,6 +625,12 @@ def test_link_model_matches_design_table():
                 assert v["binds"] == ("xgmi" if v["link_ms"] > v["hbm_ms"] else "hbm")
             ch = choose_exchange(orders, owner, world, lay.n_f32, lay.n_i64, lay.n_b16)
             assert ch == ("transpose" if tr_gb < 0.9 * halo_gb else "halo"), (kind, world)
+    # one rank (bench.py --sharded): no link at all, both exchanges bound by HBM
+    orders, _ = bench.round_spec(64, 8, kind="random")
+    lay = StateLayout.from_layout(synth.get_layout("resnet50"))
+    m = link_model(orders, partition_contiguous(64, 1), 1, lay.n_f32, lay.n_i64, lay.n_b16)
+    for v in m.values():
+        assert v["busiest_pair_bytes"] == 0 and v["binds"] == "hbm" and v["predicted_ms"] > 0
 
 
 def test_reg_plan_table_layout():
