@@ -314,7 +314,7 @@ def main():
             plan = _ops.build_stream_plan(row_ptr, col, w, out_rows, args.stream_rows).to(dev)
         else:  # the model-based choice; with tuning, only for the placement calibration below
             plan = (_ops.build_plan(row_ptr, col, w, out_rows, c4=args.c4) if args.c4 else
-                    _ops.default_plan(row_ptr, col, w, out_rows, bf16=bf16)).to(dev)
+                    _ops.default_plan(row_ptr, col, w, out_rows, bf16=bf16, mode=mode)).to(dev)
         ev_s, ev_e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
         def placement_score(a, b):

@@ -177,3 +177,32 @@ def test_reg_plan_spec_roundtrip_and_i64(cuda):
     iout = torch.zeros_like(iin)
     ops.round_i64(iin, iout, plan)
     assert np.array_equal(iout.cpu().numpy(), oracle.round_i64(xi, row_ptr, col, w, out_rows))
+
+
+def test_round_executor_bf16_fma_per_operand_weights(cuda):
+    """The product's untimed default for a bf16 FMA round with per-operand (degree-centrality)
+    weights is K3r (ops.default_plan): RoundExecutor on bf16 model rows of the SBM-256 topology,
+    every row bitwise the bf16 FMA oracle (fp32 fused chain, one rounding), the int64 segment
+    through the plan's full form, bitwise the oracle's truncation."""
+    from topology_aware_learning_amd.arena import ModelPool, StateLayout
+    from topology_aware_learning_amd.round import RoundExecutor
+
+    orders, ws, row_ptr, col, w = _csr(_GRAPHS["sbm256"](), weights="degcent")
+    rows = len(orders)
+    lay = StateLayout.from_layout([("w", [1003], "bfloat16"), ("n", [3], "int64")])
+    pool = ModelPool(lay, rows, cuda)
+    rng = np.random.default_rng(5)
+    x = torch.from_numpy(_pool(rng, rows, lay.n_b16)).to(torch.bfloat16)
+    xi = torch.from_numpy(rng.integers(0, 10 ** 6, (rows, lay.n_i64)))
+    pool.b16[:, :lay.n_b16].copy_(x.to(cuda))
+    pool.i64[:, :lay.n_i64].copy_(xi.to(cuda))
+    ex = RoundExecutor(pool, mode=ops.MODE_FMA)
+    assert isinstance(ex.plan(orders, ws, list(range(rows))), ops.RegPlan)
+    bits = x.view(torch.int16).numpy().view(np.uint16)
+    ref = oracle.round_bf16(bits, row_ptr, col, w, np.arange(rows, dtype=np.int32), exact=False)
+    iref = oracle.round_i64(xi.numpy(), row_ptr, col, w, np.arange(rows, dtype=np.int32))
+    ex.run(orders, ws)
+    torch.cuda.synchronize(cuda)
+    got = pool.b16[:, :lay.n_b16].cpu().view(torch.int16).numpy().view(np.uint16)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(pool.i64[:, :lay.n_i64].cpu().numpy(), iref)

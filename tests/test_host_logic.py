@@ -579,6 +579,27 @@ def test_default_plan_forms(kind, n, deg, form):
         assert p.info.c4 == 16 and p.info.n_groups == 1 and p.staged_rows() == 256
 
 
+def test_default_plan_bf16_per_operand_weights():
+    """Config 5 with degree-centrality softmax weights: bf16 FMA rounds default to register-
+    resident groups (K3r won the round-3 closing table, 29.8 vs 33.1 ms); fp32 and bf16 EXACT
+    keep the narrow pairs form, and unweighted bf16 FMA the narrow ROWW form."""
+    import bench
+    from topology_aware_learning_amd.round import csr_from_lists
+
+    orders, ws = bench.round_spec(256, 8, kind="sbm", weights="degcent")
+    rp, col, w = csr_from_lists(orders, ws)
+    rows = np.arange(len(orders), dtype=np.int32)
+    p = ops.default_plan(rp, col, w, rows, bf16=True, mode=ops.MODE_FMA)
+    assert isinstance(p, ops.RegPlan) and p.spec == {"reg": 1}
+    for kw in (dict(bf16=False, mode=ops.MODE_FMA), dict(bf16=True, mode=ops.MODE_EXACT), dict(bf16=True)):
+        q = ops.default_plan(rp, col, w, rows, **kw)
+        assert isinstance(q, ops.RoundPlan) and q.info.c4 == 16 and not q.info.narrow_roww
+    orders, ws = bench.round_spec(256, 8, kind="sbm")
+    rp, col, w = csr_from_lists(orders, ws)
+    q = ops.default_plan(rp, col, w, rows, bf16=True, mode=ops.MODE_FMA)
+    assert isinstance(q, ops.RoundPlan) and q.info.narrow_roww
+
+
 def test_auto_dense_only_for_cliques():
     """dense_rb = -1 (library's choice) keeps random graphs sparse and takes dense row blocks on
     a complete graph (one LDS read serves every row of a block)."""

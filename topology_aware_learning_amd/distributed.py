@@ -312,7 +312,7 @@ class ShardedRound:
                 self.plans[name] = (
                     ops.tune_plan(rp, col, w, out, _pool_segs(self.pool_a)[tg], _pool_segs(self.pool_b)[tg],
                                   n=getattr(layout, "n_" + tg), mode=mode)
-                    if tune else ops.default_plan(rp, col, w, out, bf16=bool(layout.n_b16)).to(self.device))
+                    if tune else ops.default_plan(rp, col, w, out, bf16=bool(layout.n_b16), mode=mode).to(self.device))
         if exchange is None and dist.is_available() and dist.is_initialized():
             # a collective over the whole group first: RCCL then builds the communicator with
             # every rank, so the first batched P2P does not depend on which ranks have halos

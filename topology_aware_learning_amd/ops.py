@@ -673,18 +673,27 @@ def plan_from_spec(row_ptr, col, w, out_row, spec: dict) -> RoundPlan:
     return p
 
 
-def default_plan(row_ptr, col, w, out_row, bf16: bool = False):
+def default_plan(row_ptr, col, w, out_row, bf16: bool = False, mode: int = MODE_EXACT):
     """The plan the round components build when they do not time candidates (tune=False):
     the round's uniform-weight clique blocks by K3c when it has any (fp32 pools; the other rows
     by their own sparse plan), else build_plan's sparse form at the tile width and LDS budget
     its cost model picks.  On the round-1 A/B tables this is the measured winner's form for
-    configs 2-5 (tests/test_host_logic.py::test_default_plan_forms)."""
+    configs 2-5 (tests/test_host_logic.py::test_default_plan_forms).  One exception, from the
+    round-3 closing table: a bf16 round in FMA mode whose narrow plan needs per-operand weights
+    (the pairs form: centrality weights on a graph whose degrees differ) runs as register-
+    resident groups (K3r, 29.8 vs 33.1 ms on config 5 with degree-centrality weights)."""
     if not bf16:
         cp = build_clique_plan(row_ptr, col, w, out_row)
         if cp is not None:
             cp.spec = dict(clique=1, rest=cp.rest.spec if cp.rest is not None else None)
             return cp
-    return build_plan(row_ptr, col, w, out_row, dense=0)
+    p = build_plan(row_ptr, col, w, out_row, dense=0)
+    if bf16 and mode == MODE_FMA and p.info.c4 < 64 and not p.info.narrow_roww:
+        rp = build_reg_plan(row_ptr, col, w, out_row)
+        if rp is not None:
+            rp.spec = {"reg": 1}
+            return rp
+    return p
 
 
 def round_kernel_name(plan) -> str:

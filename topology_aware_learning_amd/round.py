@@ -85,7 +85,7 @@ class RoundExecutor:
         if p is None:
             row_ptr, col, w = csr_from_lists(orders, weights)
             p = ops.default_plan(row_ptr, col, w, np.asarray(out_rows, np.int32),
-                                 bf16=bool(self.pool.layout.n_b16)).to(self.pool.device)
+                                 bf16=bool(self.pool.layout.n_b16), mode=self.mode).to(self.pool.device)
             if len(self._plans) > 64:
                 self._plans.clear()
             self._plans[key] = p

@@ -213,7 +213,7 @@ class TransposedRound:
         if tune and w0:
             self.plan = ops.tune_plan(rp, col, w, out_rows, f.work_in[0], f.work_out[0], n=w0, mode=mode)
         else:
-            self.plan = ops.default_plan(rp, col, w, out_rows, bf16=bool(layout.n_b16)).to(self.device)
+            self.plan = ops.default_plan(rp, col, w, out_rows, bf16=bool(layout.n_b16), mode=mode).to(self.device)
         self.plans = {"round": self.plan}
         self.staged_sources = self.plan.staged_rows()
         self.exchange_kind = "transpose"
