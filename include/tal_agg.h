@@ -24,7 +24,9 @@
  *     thread-local message for the last failure on the calling thread.
  *   - all data pointers are DEVICE pointers owned by the caller; host arrays are named *_host.
  *   - `stream` is a hipStream_t (NULL = the default stream); calls are stream-ordered and
- *     never synchronize the device; the library allocates no device memory.
+ *     never synchronize the device; the library allocates no device memory except 512 B of
+ *     item counters per (device, stream) that tal_agg_round_reg launches on (made on first use,
+ *     kept for the process: launches on different streams never share counters).
  *   - weights arrive as float64 (Python floats / numpy float64 in the reference) and are
  *     rounded to fp32 exactly as torch does for `python_float * fp32_tensor`.
  *   - mode: TAL_MODE_EXACT reproduces the reference bit for bit (ordered i=0..M-1,
@@ -157,6 +159,25 @@ typedef struct tal_round_plan_info {
   int32_t narrow_roww;
   int32_t off_nrow_w;       /* [rows] fp32 weight bits (narrow_roww) */
   int32_t scalar_lds_bytes; /* LDS of the staged scalar tail kernel (the largest group) */
+  /* broadcast form (narrow_bcast > 0, built by tal_round_plan_build_bcast; c4 16 / 32): the
+   * LDS holds only the group's data tile and one -0.0 tile (slot max_src).  Each wavefront of
+   * a workgroup runs a fixed program over the group's passes (64 / c4 rows computed together,
+   * rows ordered by operand count, descending), kept in VGPRs for the whole launch: a record
+   * is 64 lanes x {LDS byte offset of the operand's tile column 0, fp32 weight bits} holding
+   * operands 16c .. 16c+15 of every row of the pass (lane L: row L / c4, operand 16c + L % 16;
+   * past a row's count: the -0.0 tile with weight 1.0, an exact identity); the kernel hands
+   * operand u to the row's lanes by a DPP row broadcast from lane u, so no per-operand plan
+   * read touches LDS.  Program of wavefront w of group g at word off_bc_prog[g * narrow_bcast +
+   * w] (even): {n_rec, n_pass, data offset (words from the program, even), 5 x 0},
+   * bc_rec_max descriptors {operands in the record (1..16) | last of its pass << 8 | pass << 16},
+   * 4 output rows per pass (-1: none), then the n_rec records (128 words each). */
+  int32_t narrow_bcast;     /* wavefronts per workgroup (8 or 16); 0 = not this form */
+  int32_t bc_rec_max;       /* records per wavefront (128 / narrow_bcast) */
+  int32_t off_bc_prog;      /* [n_groups * narrow_bcast] program offsets */
+  int32_t bc_records;       /* records over all programs */
+  int32_t bc_wg_per_cu;     /* resident workgroups per CU the launch sizes registers for (1: 128
+                             * VGPRs at 1024 threads, deeper read pipelining; 2: two groups' tiles
+                             * overlap one's staging with the other's arithmetic) */
 } tal_round_plan_info;
 
 /* Blob size in int32 words of the sparse or narrow form for `rows` rows / `nnz` operands (an upper
@@ -177,6 +198,17 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
                              const double* w_host, const int32_t* out_row_host, int32_t c4,
                              int32_t lds_bytes, int32_t dense_rb, int32_t* plan_host,
                              int64_t plan_capacity_words, tal_round_plan_info* info);
+
+/* Broadcast-form narrow plan (see narrow_bcast above): as tal_round_plan_build at c4 16 / 32,
+ * with waves (8 or 16) wavefronts per workgroup and wg_per_cu (1 or 2) resident workgroups per CU
+ * (2 caps lds_bytes at 80 KiB); a group also needs every wavefront's program
+ * to fit 128 / waves records (TAL_ERR_CAPACITY for a row no group can take).  Per-operand
+ * weights cost no LDS reads in this form (the centrality strategies on graphs whose degrees
+ * differ: decentralized_client.py:572-611). */
+int32_t tal_round_plan_build_bcast(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host,
+                                   const double* w_host, const int32_t* out_row_host, int32_t c4,
+                                   int32_t lds_bytes, int32_t waves, int32_t wg_per_cu, int32_t* plan_host,
+                                   int64_t plan_capacity_words, tal_round_plan_info* info);
 
 /* Streamed plan (see stream_cs above).  Rows keep their order; consecutive rows share a group
  * while the group has at most max_group_rows rows (<= 128) and, if max_group_src > 0, at
@@ -305,6 +337,20 @@ int32_t tal_prox_grad(const float* w, const float* const* wt_host, int32_t k,
                       const int64_t* plan_dev, int32_t n_chunks, int32_t n_seg,
                       const float* norms, const float* scale_dev, float* gw,
                       float* const* gwt_host, void* stream);
+
+/* ---- Host reduction: processes that see no GPU ------------------------------------------
+ * BASELINE config 1 runs the reference's driver with CPU models and no GPU
+ * (decentralized_client.py:399-413 on CPU tensors).  These compute the same arithmetic as
+ * tal_agg_f32 / tal_agg_i64 / tal_agg_bf16 (EXACT: bitwise the reference; FMA as documented
+ * there) on HOST pointers, elementwise in operand order, on up to 16 host threads.  out may
+ * alias any x[i].  The package calls them only when torch sees no GPU; with a GPU visible
+ * every aggregation runs the kernels above. */
+int32_t tal_host_agg_f32(const float* const* x_host, const double* w_host, int32_t m, float* out,
+                         int64_t n, int32_t mode);
+int32_t tal_host_agg_i64(const int64_t* const* x_host, const double* w_host, int32_t m, int64_t* out,
+                         int64_t n);
+int32_t tal_host_agg_bf16(const uint16_t* const* x_host, const double* w_host, int32_t m, uint16_t* out,
+                          int64_t n, int32_t mode);
 
 /* ---- Multi-GPU halo exchange (SURVEY §8(b) tal_halo_exchange, §8(e)) ---------------------
  * Reference: the models that cross workers are shipped by Parsl as Python objects

@@ -22,8 +22,8 @@ Outputs (all data, no reference source):
   full_round_c3_resnet50_rr64.json   BASELINE config 3 (the benchmark's round) at full size
   full_round_c4_resnet50_barbell.json  BASELINE config 4 (barbell(60, 8)) at full size
   full_round_c5_vit_sbm256.json      BASELINE config 5 (SBM-256, ViT-B/16) at full size per entry
-                                     group: fp32 unweighted, fp32 degree-centrality softmax (one
-                                     group), bf16 unweighted (one group)
+                                     group: fp32 unweighted, fp32 degree-centrality softmax and
+                                     bf16 unweighted, every group (round 4; one group before)
 
 Usage:  python tests/golden/make_golden.py [generator ...]   (default: all)
 """
@@ -436,8 +436,9 @@ def gen_c5_round(dc, out):
     over a sub-state-dict of consecutive entries gives exactly those entries' bytes of the full
     round; the 88.6 GB of models are never resident.  sha256 per (output model, group) of:
       fp32 / unweighted_module_avg over every group (the benchmark's round),
-      fp32 / centrality_module_avg (degree, softmax, coeff 10) over the last group,
-      bf16 (model.to(torch.bfloat16)) / unweighted_module_avg over the first group."""
+      fp32 / centrality_module_avg (degree, softmax, coeff 10) over every group,
+      bf16 (model.to(torch.bfloat16)) / unweighted_module_avg over every group
+    (rounds 1-3 pinned the last / first group of the latter two; round 4 pins every group)."""
     sizes = [32] * 8
     p = [[14 / 31 if a == b else 2 / 224 for b in range(8)] for a in range(8)]
     g = nx.stochastic_block_model(sizes, p, seed=0)
@@ -449,8 +450,8 @@ def gen_c5_round(dc, out):
     cent = dc.create_centrality_dict(nx.to_numpy_array(g), np.random.default_rng(0))
     runs = [("f32", "unweighted_module_avg", {}, list(range(len(groups)))),
             ("f32", "centrality_module_avg", dict(centrality_metric="degree", centrality_dict=cent,
-                                                  softmax=True, softmax_coeff=10.0), [len(groups) - 1]),
-            ("bf16", "unweighted_module_avg", {}, [0])]
+                                                  softmax=True, softmax_coeff=10.0), list(range(len(groups)))),
+            ("bf16", "unweighted_module_avg", {}, list(range(len(groups))))]
     results = []
     for dtype, fn, kw, gids in runs:
         lay = layout if dtype == "f32" else synth.as_bf16(layout)

@@ -1,32 +1,34 @@
 """BASELINE config 1 plumbing: 8-device ring, CIFAR-10 CNN, one round through
 src/experiments/decentralized_main.py on the CPU.
 
-There is no GPU here, so the test swaps the device reduction for a recorder that checks what
-the driver hands it (operands in reference order, self last, weights) and applies the
-reference's own CPU loop (oracle/torch_path.py) — test infrastructure only.  The same run
-goes through the HIP library in tests/test_gpu_interface.py."""
+There is no GPU here, so every aggregation runs the product's host reduction (the library's
+tal_host_agg_*, aggregate.py's no-GPU dispatch).  The recorder only observes: it calls the
+product's aggregate_models straight through and notes what the driver handed it (operands in
+reference order, self last, weights) and the result.  The results are checked bitwise against
+the reference's CPU loop in tests/test_host_backend.py; the same run goes through the HIP
+library in tests/test_gpu_interface.py."""
 import numpy as np
 import networkx as nx
 import pytest
 import torch
 
-from oracle import torch_path
-
 
 @pytest.fixture()
 def recorder(monkeypatch):
     import src.decentralized_client as dc
+    from topology_aware_learning_amd import aggregate
 
+    assert dc.aggregate_models is aggregate.aggregate_models
+    real = aggregate.aggregate_models
     calls = []
 
-    def fake_aggregate(operands, weights, target, mode=None):
-        sds = [{k: v.detach().clone() for k, v in m.state_dict().items()} for m in operands]
-        torch_path.aggregate_call(sds, weights, target.state_dict())
+    def observe(operands, weights, target, mode=aggregate.ops.MODE_EXACT):
+        out = real(operands, weights, target, mode)
         calls.append(dict(ids=[id(m) for m in operands], target=id(target), weights=list(weights),
                           out={k: v.detach().clone() for k, v in target.state_dict().items()}))
-        return target
+        return out
 
-    monkeypatch.setattr(dc, "aggregate_models", fake_aggregate)
+    monkeypatch.setattr(dc, "aggregate_models", observe)
     return calls
 
 

@@ -297,3 +297,22 @@ def test_round_executor_scratch_placement(cuda):
     rp, col, w = ra.round_csr(orders, ws)
     ref = oracle.round_f32(x, rp, col, w, np.arange(1000))
     assert bits_equal(pool.f32[:, :4093].cpu().numpy(), ref)
+
+
+def test_host_reduction_unused_with_a_gpu(cuda, monkeypatch):
+    """With a GPU visible the package never runs the host reduction (tal_host_agg_*, the
+    no-GPU path of BASELINE config 1): CPU-resident models go through the HIP kernels."""
+    import src.decentralized_client as dc
+    from topology_aware_learning_amd import ops
+
+    def refuse(*a, **k):
+        raise AssertionError("host reduction called with a GPU visible")
+
+    monkeypatch.setattr(ops, "host_agg", refuse)
+    case = next(c for c in TINY["cases"] if c["fn"] == "unweighted_module_avg")
+    clients, _ = build_clients(case, "cpu", cuda)
+    res = dc.unweighted_module_avg(clients[-1], 0, *clients).result()
+    sd = res[1].model.state_dict()
+    for name, _, _ in LAYOUT:
+        assert sd[name].device.type == "cpu"
+        assert bits_equal(sd[name].detach().numpy(), TINYZ[f"c{case['case']}_out_{name}"]), name

@@ -99,11 +99,21 @@ def test_missing_library_fails_loudly(tmp_path):
         _lib.load(tmp_path / "libtal_agg.so")
 
 
-def test_aggregate_without_gpu_fails_loudly():
+def test_aggregate_without_gpu_runs_the_library_or_fails_loudly(monkeypatch):
+    """No GPU visible: the aggregation is the library's host reduction (native code, the
+    kernels' arithmetic; tests/test_host_backend.py pins it bitwise), and without the library
+    it raises TalLibraryError - there is no Python arithmetic path."""
     if torch.cuda.is_available():
         pytest.skip("GPU present")
+    from topology_aware_learning_amd import _lib
     from topology_aware_learning_amd.aggregate import aggregate_models
 
-    m = torch.nn.Linear(2, 2)
-    with pytest.raises(RuntimeError, match="GPU"):
-        aggregate_models([m, m], [0.5, 0.5], m)
+    a, b = torch.nn.Linear(2, 2), torch.nn.Linear(2, 2)
+    want = {k: (0.5 * a.state_dict()[k] + 0.5 * b.state_dict()[k]) for k in a.state_dict()}
+    aggregate_models([a, b], [0.5, 0.5], b)
+    for k, v in b.state_dict().items():
+        assert torch.equal(v, want[k])
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", _lib.LIB_PATH.with_name("missing_libtal_agg.so"))
+    with pytest.raises(_lib.TalLibraryError):
+        aggregate_models([a, b], [0.5, 0.5], b)

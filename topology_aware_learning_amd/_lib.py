@@ -27,7 +27,7 @@ TAL_ERR_COMM = 4
 TAL_COMM_ID_BYTES = 128
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 EXPORTED = (
     "tal_last_error",
@@ -38,6 +38,7 @@ EXPORTED = (
     "tal_agg_bf16",
     "tal_round_plan_words",
     "tal_round_plan_build",
+    "tal_round_plan_build_bcast",
     "tal_round_plan_build_stream",
     "tal_agg_round_f32",
     "tal_agg_round_i64",
@@ -58,6 +59,9 @@ EXPORTED = (
     "tal_comm_destroy",
     "tal_halo_pack",
     "tal_halo_exchange",
+    "tal_host_agg_f32",
+    "tal_host_agg_i64",
+    "tal_host_agg_bf16",
 )
 
 
@@ -106,6 +110,11 @@ class RoundPlanInfo(ctypes.Structure):
         ("narrow_roww", ctypes.c_int32),
         ("off_nrow_w", ctypes.c_int32),
         ("scalar_lds_bytes", ctypes.c_int32),
+        ("narrow_bcast", ctypes.c_int32),
+        ("bc_rec_max", ctypes.c_int32),
+        ("off_bc_prog", ctypes.c_int32),
+        ("bc_records", ctypes.c_int32),
+        ("bc_wg_per_cu", ctypes.c_int32),
     ]
 
 
@@ -128,6 +137,10 @@ _SIGS = {
     "tal_round_plan_build": (
         _I32,
         [_I32, _PI32, _PI32, _PD, _PI32, _I32, _I32, _I32, _PI32, _I64, ctypes.POINTER(RoundPlanInfo)],
+    ),
+    "tal_round_plan_build_bcast": (
+        _I32,
+        [_I32, _PI32, _PI32, _PD, _PI32, _I32, _I32, _I32, _I32, _PI32, _I64, ctypes.POINTER(RoundPlanInfo)],
     ),
     "tal_round_plan_build_stream": (
         _I32,
@@ -152,6 +165,9 @@ _SIGS = {
     "tal_comm_destroy": (_I32, [_P]),
     "tal_halo_pack": (_I32, [_P, _I64, _I64, _P, _I32, _I64, _P, _P]),
     "tal_halo_exchange": (_I32, [_P, _I32, _PP, _PI64, _PP, _PI64, _P]),
+    "tal_host_agg_f32": (_I32, [_PP, _PD, _I32, _P, _I64, _I32]),
+    "tal_host_agg_i64": (_I32, [_PP, _PD, _I32, _P, _I64]),
+    "tal_host_agg_bf16": (_I32, [_PP, _PD, _I32, _P, _I64, _I32]),
 }
 
 _lock = threading.Lock()

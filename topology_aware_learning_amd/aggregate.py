@@ -11,7 +11,10 @@ Operands and target may be
   * any other models (CPU — as the reference leaves them after training, tasks.py:342 — or
     GPU): their state is packed into one pinned host buffer, copied H2D once, aggregated, and
     the result copied back into the target's own tensors, as load_state_dict would.
-There is no CPU arithmetic path.
+A process that sees no GPU (BASELINE config 1: the reference's driver on CPU models, no GPU)
+runs the library's host reduction instead (tal_host_agg_*, native code with the kernels'
+arithmetic); with a GPU visible every call runs the HIP kernels.  Without the library either
+way raises TalLibraryError.
 """
 from __future__ import annotations
 
@@ -287,6 +290,8 @@ def aggregate_models(operands: Sequence[nn.Module], weights: Sequence[float], ta
         raise ValueError("no operands")
     if len(weights) != len(operands):
         raise ValueError("one weight per operand is required")
+    if not torch.cuda.is_available():
+        return _aggregate_host(operands, weights, target, mode)
     # pool-bound models are checked once each (bound_row: every entry still a view of its
     # row); the target's pool then gives the layout without rebuilding its state_dict
     tb = bound_row(target)
@@ -394,3 +399,30 @@ def _write_back(target: nn.Module, layout: StateLayout, outs: dict) -> None:
         for e in layout.entries:  # tied keys share storage; copy_ as load_state_dict would
             if e.alias_of is not None:
                 sd[e.name].copy_(views[e.name])
+
+
+def _aggregate_host(operands: Sequence[nn.Module], weights: Sequence[float], target: nn.Module,
+                    mode: int) -> nn.Module:
+    """No GPU visible: each operand's segments packed into flat CPU tensors, the library's host
+    reduction (ops.host_agg), and the result copied into the target's own tensors as
+    load_state_dict(avg) would (decentralized_client.py:399-413 on CPU models)."""
+    layout = layout_of_module(target)
+    sizes = {g: n for g, n in _seg_sizes(layout).items() if n}
+    flats = []
+    for j, m in enumerate(operands):
+        sd = m.state_dict()
+        layout.check_compatible(sd, f"operand {j}")
+        if any(t.device.type != "cpu" for t in sd.values()):
+            raise RuntimeError("no GPU is visible, but an operand has tensors off the CPU")
+        flats.append({g: torch.cat([t.detach() for t in layout.flatten_cat(sd, g)]) for g in sizes})
+    w = [float(x) for x in weights]
+    outs = {g: torch.empty(n, dtype=_SEG_DTYPE[g]) for g, n in sizes.items()}
+    for g in sizes:
+        ops.host_agg([f[g] for f in flats], w, outs[g], mode)
+    empty = {g: torch.empty(0, dtype=_SEG_DTYPE[g]) for g in _SEG_DTYPE}
+    views = layout.views(outs.get("f32", empty["f32"]), outs.get("i64", empty["i64"]), outs.get("b16", empty["b16"]))
+    sd = target.state_dict()
+    with torch.no_grad():
+        for name, t in sd.items():
+            t.copy_(views[name])
+    return target

@@ -24,6 +24,7 @@
 #include <cmath>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <type_traits>
 #include <vector>
@@ -44,7 +45,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 17;
+constexpr int kAbiVersion = 18;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -394,6 +395,7 @@ struct PlanView {
   const int32_t* nrow_ptr;     // narrow form only
   const int32_t* npairs;
   const int32_t* nrow_w;       // narrow_roww only
+  const int32_t* bc_prog;      // narrow_bcast only: [n_groups * waves] word offset of each wave's program
 };
 
 PlanView make_view(const int32_t* plan, const tal_round_plan_info& in) {
@@ -411,6 +413,7 @@ PlanView make_view(const int32_t* plan, const tal_round_plan_info& in) {
   v.nrow_ptr = plan + in.off_nrow_ptr;
   v.npairs = plan + in.off_npairs;
   v.nrow_w = plan + in.off_nrow_w;
+  v.bc_prog = plan + in.off_bc_prog;
   return v;
 }
 
@@ -1021,6 +1024,120 @@ __device__ __forceinline__ float4 narrow_row_roww(uint4 rc, uint32_t base) {
   return narrow_row_tail<T, EXACT>(acc, w, e, base, rem);
 }
 
+// ---- broadcast form (narrow_bcast, tal_round_plan_build_bcast) ---------------------------
+// A wavefront's plan is a program of records held in VGPRs for the whole launch: record lane L
+// = {LDS byte offset, fp32 weight bits} of operand 16c + L % 16 of row L / C4 of a pass.  Operand
+// u reaches the 16 lanes of its DPP row (a C4 = 16 row group; half of one at C4 = 32, whose two
+// halves hold the same record) by `row_newbcast:u`, a VALU move, so the row loop reads only
+// data from LDS: no slot or weight read and no LDS round trip between a batch's slot word and
+// its data reads (the addresses of a whole record are known when the record is).
+constexpr int kBcRecPerWg = 128;  // records per workgroup; a wavefront holds 128 / waves of them
+constexpr int kBcHdr = 8;         // program header words
+
+template <int NT>
+constexpr int bc_rec_max() { return kBcRecPerWg / (NT / 64); }
+
+// lane U of each 16-lane row, to the row (row_newbcast:U).  As update_dpp with bound_ctrl and
+// old = 0 the backend folds it into the consuming v_add_u32 (v_add_u32_dpp: the address costs
+// one VALU, as the ROWW form's v_mad_u32_u16); a plain mov_dpp stays a separate v_mov_b32_dpp.
+template <int U>
+__device__ __forceinline__ uint32_t bc_lane(uint32_t v) {
+  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x150 + U, 0xf, 0xf, true));
+}
+
+template <int U>
+__device__ __forceinline__ float4 bc_x(int2 e, uint32_t base) { return lds_f4(bc_lane<U>(static_cast<uint32_t>(e.x)) + base); }
+
+template <int U>
+__device__ __forceinline__ float bc_w(int2 e) { return __uint_as_float(bc_lane<U>(static_cast<uint32_t>(e.y))); }
+
+// One record: its first `cnt` (1..16) operands, in order, for this lane's row and column, as
+// ceil(cnt / 4) batches of four data reads and their arithmetic (a partial last batch computes
+// its identity pads: lanes past a pass's count hold the -0.0 tile with weight 1.0).  With PIPE
+// the next batch's reads are issued before this batch's arithmetic (8 reads in flight: the
+// 512-thread form's registers), else each batch reads, then computes (the 1024-thread form's
+// 64-VGPR budget).  The scheduling barriers keep the compiler from hoisting all 16 reads at
+// once (64 VGPRs, then spills).
+template <int B>
+__device__ __forceinline__ void bc_read4(float4 (&x)[4], int2 e, uint32_t base) {
+  x[0] = bc_x<4 * B>(e, base);
+  x[1] = bc_x<4 * B + 1>(e, base);
+  x[2] = bc_x<4 * B + 2>(e, base);
+  x[3] = bc_x<4 * B + 3>(e, base);
+}
+
+// fp32 EXACT: the four products first, then the ordered adds (each add then has independent
+// work between it and the multiply it consumes: no s_nop); the other modes chain next4t.
+template <typename T, bool EXACT, int B>
+__device__ __forceinline__ float4 bc_math4(float4 acc, const float4 (&x)[4], int2 e) {
+  if constexpr (EXACT && !kIsBf16<T>) {
+    const float4 p0 = mul4(bc_w<4 * B>(e), x[0]), p1 = mul4(bc_w<4 * B + 1>(e), x[1]),
+                 p2 = mul4(bc_w<4 * B + 2>(e), x[2]), p3 = mul4(bc_w<4 * B + 3>(e), x[3]);
+    return add4(add4(add4(add4(acc, p0), p1), p2), p3);
+  } else {
+    acc = next4t<T, EXACT>(acc, bc_w<4 * B>(e), x[0]);
+    acc = next4t<T, EXACT>(acc, bc_w<4 * B + 1>(e), x[1]);
+    acc = next4t<T, EXACT>(acc, bc_w<4 * B + 2>(e), x[2]);
+    return next4t<T, EXACT>(acc, bc_w<4 * B + 3>(e), x[3]);
+  }
+}
+
+template <typename T, bool EXACT, bool PIPE>
+__device__ __forceinline__ float4 bc_record(float4 acc, int2 e, uint32_t base, int cnt) {
+  const int nb = (cnt + 3) >> 2;  // wave-uniform
+  float4 xa[4], xb[4];
+  if constexpr (PIPE) {
+    bc_read4<0>(xa, e, base);
+    if (nb > 1) bc_read4<1>(xb, e, base);
+    __builtin_amdgcn_sched_barrier(0);
+    acc = bc_math4<T, EXACT, 0>(acc, xa, e);
+    if (nb > 1) {
+      if (nb > 2) bc_read4<2>(xa, e, base);
+      __builtin_amdgcn_sched_barrier(0);
+      acc = bc_math4<T, EXACT, 1>(acc, xb, e);
+    }
+    if (nb > 2) {
+      if (nb > 3) bc_read4<3>(xb, e, base);
+      __builtin_amdgcn_sched_barrier(0);
+      acc = bc_math4<T, EXACT, 2>(acc, xa, e);
+    }
+    if (nb > 3) acc = bc_math4<T, EXACT, 3>(acc, xb, e);
+  } else {
+    bc_read4<0>(xa, e, base);
+    acc = bc_math4<T, EXACT, 0>(acc, xa, e);
+    if (nb > 1) {
+      __builtin_amdgcn_sched_barrier(0);
+      bc_read4<1>(xb, e, base);
+      acc = bc_math4<T, EXACT, 1>(acc, xb, e);
+    }
+    if (nb > 2) {
+      __builtin_amdgcn_sched_barrier(0);
+      bc_read4<2>(xa, e, base);
+      acc = bc_math4<T, EXACT, 2>(acc, xa, e);
+    }
+    if (nb > 3) {
+      __builtin_amdgcn_sched_barrier(0);
+      bc_read4<3>(xb, e, base);
+      acc = bc_math4<T, EXACT, 3>(acc, xb, e);
+    }
+  }
+  return acc;
+}
+
+template <int C4>
+__device__ __forceinline__ NarrowLds stage_narrow_bc(const PlanView& p, int g, float4* s_data, int nthreads) {
+  NarrowLds L;
+  L.nr = p.grp_row_ptr[g + 1] - p.grp_row_ptr[g];
+  const int ns = p.grp_src_ptr[g + 1] - p.grp_src_ptr[g];
+  for (int k = threadIdx.x; k < C4; k += nthreads)  // the identity pads' tile of -0.0 (slot ns)
+    s_data[static_cast<size_t>(ns) * C4 + k] = make_float4(-0.f, -0.f, -0.f, -0.f);
+  L.rowptr = nullptr;
+  L.pairs = nullptr;
+  L.out = nullptr;
+  L.rec = 0;
+  return L;
+}
+
 template <int C4>
 __device__ __forceinline__ NarrowLds stage_narrow(const PlanView& p, int g, float4* s_data, int nthreads) {
   NarrowLds L;
@@ -1099,7 +1216,9 @@ __device__ __forceinline__ int narrow_set(int p, int wave, int nwaves) {
 // and tile, J/2 loads per lane) instead of 8 B; each lane writes its two chunks to LDS as two
 // adjacent fp32 float4.  Needs an even chunk count, a row stride of an even number of chunks and
 // a 16-B aligned base (the launcher checks), so every pair lies inside its row.
-template <int C4, int NT, int J, int NP, bool EXACT, typename T = float, bool ROWW = false, bool W16 = false>
+// BC: the broadcast form (narrow_bcast plans; NT = 64 x the plan's waves per workgroup).
+template <int C4, int NT, int J, int NP, bool EXACT, typename T = float, bool ROWW = false, bool W16 = false,
+          bool BC = false>
 __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round_f32_narrow(
     const T* __restrict__ pin, int64_t ld_in4, T* __restrict__ pout, int64_t ld_out4, int64_t n4,
     PlanView p, int64_t n_tiles) {
@@ -1112,7 +1231,8 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   constexpr int kW = NT / 64;
   extern __shared__ float4 s_data[];
   const int g = blockIdx.y;
-  const NarrowLds L = ROWW ? stage_narrow_roww<C4>(p, g, s_data, NT) : stage_narrow<C4>(p, g, s_data, NT);
+  const NarrowLds L = BC ? stage_narrow_bc<C4>(p, g, s_data, NT)
+                          : ROWW ? stage_narrow_roww<C4>(p, g, s_data, NT) : stage_narrow<C4>(p, g, s_data, NT);
   const int s_beg = p.grp_src_ptr[g];
   const int ns = p.grp_src_ptr[g + 1] - s_beg;
   const int c = threadIdx.x % kLps;  // staging: the lane's chunk (W16: chunk pair) of its source
@@ -1150,6 +1270,22 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   // ROWW: this lane's column base in the data tile, and its record offset within a pass
   const uint32_t col_base = lds_addr(s_data + cl);
   const uint32_t rec_lane = L.rec + 16u * static_cast<uint32_t>(sub);
+  // BC: this wavefront's program (wave-uniform: scalar loads) and its records, loaded once
+  // before the first staging loads (the records never wait behind them)
+  constexpr int kR = BC ? bc_rec_max<NT>() : 1;
+  // BC read depth: 8 data reads in flight where the registers allow it (one workgroup per CU:
+  // NP = 1, 128 VGPRs at 1024 threads; 512 threads except fp32 EXACT, whose separate products
+  // and the 8-VGPR staging of 8 loads per lane fill 128), else 4
+  constexpr bool kBcPipe = NP == 1 || (NT <= 512 && !(EXACT && !kIsBf16<T>));
+  const int bc_off = BC ? ((ConstI32)p.bc_prog)[g * kW + wave] : 0;
+  const ConstI32 prog = (ConstI32)(p.base + bc_off);
+  const int bc_n = BC ? prog[0] : 0;
+  int2 bc_rec[kR];
+  if constexpr (BC) {
+    const int2* recs = reinterpret_cast<const int2*>(p.base + (bc_off + prog[2])) + lane;
+#pragma unroll
+    for (int r = 0; r < kR; ++r) bc_rec[r] = r < bc_n ? recs[64 * r] : make_int2(0, 0);
+  }
   // converted to fp32 when written to LDS, not when loaded
   typedef typename std::conditional<W16, u32x4, typename Io<T>::raw_t>::type raw_t;
   raw_t v[kLd];
@@ -1177,7 +1313,9 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   if (t < n_tiles) load_tile(t);
   for (; t < n_tiles; t += gridDim.x) {
     __syncthreads();  // the previous tile's readers are done with s_data
-    int staged = ns * kLps;  // staging units (float4 slots; W16: slot pairs) of real sources
+    // staging units (float4 slots; W16: slot pairs) of real sources (readfirstlane: the broadcast
+    // form's control flow otherwise leaves the compiler unsure that ns is uniform here)
+    int staged = __builtin_amdgcn_readfirstlane(ns * kLps);
     asm volatile("" : "+s"(staged));
 #pragma unroll
     for (int j = 0; j < kLd; ++j) {
@@ -1193,6 +1331,32 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
     __syncthreads();
     if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
     const int64_t col = t * C4 + cl;
+    if constexpr (BC) {
+      // the records are loop-invariant: without this the compiler hoists every broadcast and
+      // address of the tile loop out of it (hundreds of VGPRs, then spills)
+#pragma unroll
+      for (int r = 0; r < kR; ++r) asm volatile("" : "+v"(bc_rec[r].x), "+v"(bc_rec[r].y));
+      float4 acc = make_float4(-0.f, -0.f, -0.f, -0.f);
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        if (r >= bc_n) continue;  // wave-uniform (a constant trip count keeps the loop unrolled,
+                                  // so the records stay in registers)
+        const uint32_t d = static_cast<uint32_t>(prog[kBcHdr + r]);
+#ifdef TAL_PROBE_NOCOMP
+        (void)d;
+#else
+        acc = bc_record<T, EXACT, kBcPipe>(acc, bc_rec[r], col_base, static_cast<int>(d & 0xffu));
+#endif
+        if (d & 0x100u) {  // the pass's last record: store its rows
+          const ConstI32 orow = prog + kBcHdr + kR + 4 * static_cast<int>(d >> 16);
+          const int o0 = orow[0], o1 = orow[1], o2 = orow[2], o3 = orow[3];
+          const int o = sub == 0 ? o0 : sub == 1 ? o1 : sub == 2 ? o2 : o3;
+          if (o >= 0 && col < n4) Io<T>::st(pout, static_cast<int64_t>(o) * ld_out4 + col, acc);
+          acc = make_float4(-0.f, -0.f, -0.f, -0.f);
+        }
+      }
+      continue;
+    }
     if constexpr (ROWW) {
       for (int k = 0; k * kW < n_sets; ++k) {  // passes: row sets in snake order
         const int set = narrow_set(k, wave, kW);
@@ -1637,6 +1801,11 @@ int32_t validate_info(const tal_round_plan_info* info) {
     return fail(TAL_ERR_INVALID, "plan c4 must be 16, 32, 64 or 128");
   if (info->c4 < 64 && info->dense_rb != 0)
     return fail(TAL_ERR_INVALID, "narrow plans (c4 16 / 32) are sparse");
+  if (info->narrow_bcast != 0 &&
+      (info->c4 >= 64 || (info->narrow_bcast != 8 && info->narrow_bcast != 16) ||
+       info->bc_rec_max != kBcRecPerWg / info->narrow_bcast || info->bc_wg_per_cu < 1 || info->bc_wg_per_cu > 2))
+    return fail(TAL_ERR_INVALID, "broadcast-form plan: c4 16 / 32, 8 or 16 wavefronts, 128 / waves records, "
+                                 "1 or 2 workgroups per CU");
   if (info->dense_rb != 0 && info->dense_rb != kDenseRb)
     return fail(TAL_ERR_INVALID, "plan dense_rb must be 0 or 8");
   if (info->stream_cs != 0 && info->stream_cs != 8 * kStreamPerWave && info->stream_cs != 16 * kStreamPerWave)
@@ -1752,9 +1921,54 @@ int32_t launch_round_narrow_j(const T* pin, int64_t ld_in, T* pout, int64_t ld_o
                         : launch_round_narrow_jr<C4, J, EXACT, T, false>(pin, ld_in, pout, ld_out, n4, v, in, s);
 }
 
+// Broadcast form: NT = 64 x the plan's waves; J staging loads per lane cover the largest group.
+template <int C4, int NT, int J, bool EXACT, typename T>
+int32_t launch_round_bcast_j(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
+                             const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
+  const size_t lds = static_cast<size_t>(in.lds_bytes);
+  const bool one = in.bc_wg_per_cu == 1;  // one workgroup per CU: 128 VGPRs at 1024 threads
+  const bool w16 = kIsBf16<T> && J % 2 == 0 && narrow_w16_enabled() && n4 % 2 == 0 && (ld_in / 4) % 2 == 0 &&
+                   (reinterpret_cast<uintptr_t>(pin) & 15) == 0;
+  auto k = one ? k_round_f32_narrow<C4, NT, J, 1, EXACT, T, false, false, true>
+               : k_round_f32_narrow<C4, NT, J, 0, EXACT, T, false, false, true>;
+  if constexpr (kIsBf16<T> && J % 2 == 0) {
+    if (w16)
+      k = one ? k_round_f32_narrow<C4, NT, J, 1, EXACT, T, false, true, true>
+              : k_round_f32_narrow<C4, NT, J, 0, EXACT, T, false, true, true>;
+  }
+  int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
+  if (rc) return rc;
+  const int64_t tiles = (n4 + C4 - 1) / C4;
+  const int64_t per_cu = resident_per_cu(reinterpret_cast<const void*>(k), NT, lds);
+  int64_t gx = std::max<int64_t>(1, 256 * per_cu / in.n_groups);
+  gx = std::min<int64_t>(gx, tiles);
+  const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(in.n_groups));
+  k<<<grid, NT, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles);
+  return check_launch("round kernel (narrow tiles, broadcast form)");
+}
+
+template <int C4, int NT, bool EXACT, typename T>
+int32_t launch_round_bcast_nt(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
+                              const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
+  const int64_t loads = static_cast<int64_t>(in.max_src) * C4;  // float4 staging loads per tile
+  if (loads <= 2LL * NT) return launch_round_bcast_j<C4, NT, 2, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  if (loads <= 4LL * NT) return launch_round_bcast_j<C4, NT, 4, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  if constexpr (NT <= 512)
+    if (loads <= 8LL * NT) return launch_round_bcast_j<C4, NT, 8, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  return fail(TAL_ERR_CAPACITY, "broadcast-form round plan: group tile too large for the workgroup");
+}
+
+template <int C4, bool EXACT, typename T>
+int32_t launch_round_bcast(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
+                           const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
+  return in.narrow_bcast == 8 ? launch_round_bcast_nt<C4, 512, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s)
+                              : launch_round_bcast_nt<C4, 1024, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
+}
+
 template <int C4, bool EXACT, typename T = float>
 int32_t launch_round_narrow(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
                             const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
+  if (in.narrow_bcast) return launch_round_bcast<C4, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
   const int64_t loads = static_cast<int64_t>(in.max_src) * C4;  // float4 staging loads per tile
   if (loads <= 1LL * kNarrowThreads) return launch_round_narrow_j<C4, 1, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
   if (loads <= 2LL * kNarrowThreads) return launch_round_narrow_j<C4, 2, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
@@ -2364,22 +2578,42 @@ __global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, T*
 }
 
 // The register round's item tickets: eight counters 64 B apart, one per XCD label, reset on the
-// stream before each launch.  The library's only device allocation: 512 B per device, made once.
+// stream before each launch.  One buffer per (device, stream): launches on one stream are
+// ordered, so they never share counters with a launch in flight elsewhere (two streams sharing
+// one buffer could reset or advance each other's counters and skip items).  The library's only
+// device allocations: 512 B per (device, stream) used, made on first use.
 constexpr size_t kRegTicketBytes = 8 * 64;
 
-int32_t reg_tickets(int32_t** out) {
+int32_t reg_tickets(hipStream_t stream, int32_t** out) {
   static std::mutex mu;
-  static std::vector<int32_t*> per_dev;
+  static std::vector<std::tuple<int, hipStream_t, int32_t*>> bufs;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return fail(TAL_ERR_HIP, "register round: no current device");
   std::lock_guard<std::mutex> lk(mu);
-  if (per_dev.size() <= static_cast<size_t>(dev)) per_dev.resize(dev + 1, nullptr);
-  if (!per_dev[dev]) {
-    void* p = nullptr;
-    if (hipMalloc(&p, kRegTicketBytes) != hipSuccess) return fail(TAL_ERR_HIP, "register round: ticket allocation failed");
-    per_dev[dev] = static_cast<int32_t*>(p);
-  }
-  *out = per_dev[dev];
+  for (const auto& b : bufs)
+    if (std::get<0>(b) == dev && std::get<1>(b) == stream) {
+      *out = std::get<2>(b);
+      return TAL_OK;
+    }
+  void* p = nullptr;
+  if (hipMalloc(&p, kRegTicketBytes) != hipSuccess) return fail(TAL_ERR_HIP, "register round: ticket allocation failed");
+  bufs.emplace_back(dev, stream, static_cast<int32_t*>(p));
+  *out = static_cast<int32_t*>(p);
+  return TAL_OK;
+}
+
+// Compute units of the current device, asked once per device (thread-safe).
+int32_t device_cus(int* n_cu) {
+  static std::mutex mu;
+  static std::vector<int> per_dev;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(TAL_ERR_HIP, "no current device");
+  std::lock_guard<std::mutex> lk(mu);
+  if (per_dev.size() <= static_cast<size_t>(dev)) per_dev.resize(dev + 1, 0);
+  if (per_dev[dev] == 0 &&
+      hipDeviceGetAttribute(&per_dev[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return fail(TAL_ERR_HIP, "multiprocessor count query failed");
+  *n_cu = per_dev[dev];
   return TAL_OK;
 }
 
@@ -2387,22 +2621,17 @@ template <int NB, typename T, bool EXACT>
 int32_t launch_round_reg_nb(const T* pin, T* pout, int64_t ld_out, int64_t n, const int32_t* table,
                             const int64_t* src_off, int32_t n_groups, int32_t off_pairs, int32_t n_pieces,
                             hipStream_t s) {
-  static int blocks_per_cu = -1, n_cu = 0;  // per instantiation, once per process
-  if (blocks_per_cu < 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, k_round_reg<NB, T, EXACT>, 256, 0) != hipSuccess)
-      return fail(TAL_ERR_HIP, "register round: occupancy query failed");
-    blocks_per_cu = std::max(1, blocks_per_cu);
-  }
+  int n_cu = 0;
+  if (int32_t rc = device_cus(&n_cu)) return rc;
+  // resident workgroups per CU: cached per kernel under a mutex (resident_per_cu)
+  const int blocks_per_cu = resident_per_cu(reinterpret_cast<const void*>(k_round_reg<NB, T, EXACT>), 256, 0);
   // persistent: every resident wave (TAL_REG_BLOCKS_PER_CU caps it: A/B probes of how many
   // pieces are in flight per XCD), a multiple of 8 blocks (XCD labels)
   int bpc = blocks_per_cu;
   if (const char* e = getenv("TAL_REG_BLOCKS_PER_CU")) bpc = std::max(1, std::min(bpc, atoi(e)));
   const int grid = std::max(8, n_cu * bpc / 8 * 8);
   int32_t* ticket = nullptr;
-  if (int32_t rc = reg_tickets(&ticket)) return rc;
+  if (int32_t rc = reg_tickets(s, &ticket)) return rc;
   if (hipMemsetAsync(ticket, 0, kRegTicketBytes, s) != hipSuccess)
     return fail(TAL_ERR_HIP, "register round: ticket reset failed");
   k_round_reg<NB, T, EXACT><<<grid, 256, 0, s>>>(pin, pout, ld_out, n, table, src_off, n_groups, off_pairs, n_pieces,
@@ -2431,13 +2660,7 @@ int32_t launch_round_stream_nt(const float* pin, int64_t ld_in, float* pout, int
   const size_t lds = stream_lds_bytes(NT / 64 * kStreamPerWave);
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;
-  static int per_cu = 0;  // resident workgroups per CU (registers / LDS), asked once
-  if (per_cu == 0) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(k), NT, lds) != hipSuccess)
-      nb = 1;
-    per_cu = std::max(1, nb);
-  }
+  const int per_cu = resident_per_cu(reinterpret_cast<const void*>(k), NT, lds);
   const int64_t tiles = (n4 + 63) / 64;
   int64_t gx = std::max<int64_t>(1, 256LL * per_cu / in.n_groups);
   gx = std::min<int64_t>(gx, tiles);
@@ -2943,13 +3166,46 @@ int64_t roww_padded_slots(const int32_t* row_ptr_host, int64_t r0, int64_t nr, i
   return slots;
 }
 
+// Broadcast form: a pass of 64 / c4 rows takes ceil(operands of its longest row / 16) records;
+// passes are dealt to wavefronts longest first, each to the least loaded one.  False when a
+// wavefront would hold more than rmax records.
+bool bc_deal(const std::vector<int32_t>& pass_recs, int waves, int rmax, std::vector<std::vector<int32_t>>* per_wave) {
+  std::vector<int32_t> order(pass_recs.size());
+  for (size_t k = 0; k < order.size(); ++k) order[k] = static_cast<int32_t>(k);
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return pass_recs[a] > pass_recs[b]; });
+  per_wave->assign(static_cast<size_t>(waves), {});
+  std::vector<int32_t> load(static_cast<size_t>(waves), 0);
+  for (int32_t k : order) {
+    const int w = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
+    if (load[w] + pass_recs[k] > rmax) return false;
+    load[w] += pass_recs[k];
+    (*per_wave)[w].push_back(k);
+  }
+  for (auto& v : *per_wave) std::sort(v.begin(), v.end());
+  return true;
+}
+
+// Records of the passes of rows r0 .. r0+nr-1 once ordered by operand count (descending).
+std::vector<int32_t> bc_pass_records(const int32_t* row_ptr_host, int64_t r0, int64_t nr, int32_t c4, bool sorted) {
+  std::vector<int32_t> m(static_cast<size_t>(nr));
+  for (int64_t i = 0; i < nr; ++i) m[i] = row_ptr_host[r0 + i + 1] - row_ptr_host[r0 + i];
+  if (!sorted) std::sort(m.begin(), m.end(), std::greater<int32_t>());
+  const int64_t rpw = 64 / c4;
+  std::vector<int32_t> recs;
+  for (int64_t i = 0; i < nr; i += rpw) recs.push_back((m[i] + 15) / 16);
+  return recs;
+}
+
+constexpr int64_t bc_lds_bytes(int64_t ns, int c4) { return (ns + 1) * c4 * 16; }
+
 // Lay the plan blob out (see tal_round_plan_info).  rb = dense row-block size (0 = sparse
 // form only, -1 = dense when it saves LDS reads); stream_cs > 0 pads each block's entries
 // chunk by chunk for the streamed kernel.
 int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host,
                     const double* w_host, const int32_t* out_row_host, int32_t max_col,
                     Groups& grp, int32_t c4, int32_t dense_rb, int32_t stream_cs,
-                    int32_t* plan_host, int64_t plan_capacity_words, tal_round_plan_info* info) {
+                    int32_t* plan_host, int64_t plan_capacity_words, tal_round_plan_info* info,
+                    int32_t bc_waves = 0, int32_t bc_wg = 2) {
   const int64_t nnz = row_ptr_host[rows];
   const int32_t G = static_cast<int32_t>(grp.srcs.size());
   const std::vector<int32_t>& grp_row_ptr = grp.row_ptr;
@@ -3031,10 +3287,73 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
     lds_need = std::max(lds_need, group_lds_bytes(grp_src_ptr[g + 1] - grp_src_ptr[g], nr, no, c4));
   }
   const int64_t scalar_need = lds_need;
-  const bool roww = c4 < 64 && rows_uniform_weights(rows, row_ptr_host, w_host) && roww_slots_fit(max_col, c4);
+  const bool roww = bc_waves == 0 && c4 < 64 && rows_uniform_weights(rows, row_ptr_host, w_host) &&
+                    roww_slots_fit(max_col, c4);
   std::vector<uint16_t> nsl;   // ROWW slots
   std::vector<int32_t> nrw;    // ROWW row weights
-  if (c4 < 64) {
+  std::vector<int32_t> bcp;    // broadcast form: program offsets (relative to the program region)
+  std::vector<int32_t> bcw;    // broadcast form: the programs
+  int64_t bc_records = 0;
+  const int32_t bc_rmax = bc_waves > 0 ? kBcRecPerWg / bc_waves : 0;
+  if (c4 < 64 && bc_waves > 0) {
+    lds_need = 0;
+    const int32_t rpw = 64 / c4;
+    const float one = 1.0f;
+    int32_t one_bits;
+    memcpy(&one_bits, &one, 4);
+    bcp.assign(static_cast<size_t>(G) * bc_waves, 0);
+    for (int g = 0; g < G; ++g) {
+      const int32_t ns = grp_src_ptr[g + 1] - grp_src_ptr[g];
+      const int32_t r0 = grp_row_ptr[g], nr = grp_row_ptr[g + 1] - r0;
+      lds_need = std::max<int64_t>(lds_need, bc_lds_bytes(ns, c4));
+      const std::vector<int32_t> recs = bc_pass_records(row_ptr_host, r0, nr, c4, true);
+      std::vector<std::vector<int32_t>> per_wave;
+      if (!bc_deal(recs, bc_waves, bc_rmax, &per_wave))
+        return fail(TAL_ERR_CAPACITY, "tal_round_plan_build_bcast: a group's records exceed the wavefronts' registers");
+      for (int w = 0; w < bc_waves; ++w) {
+        if (bcw.size() % 2) bcw.push_back(0);
+        const size_t start = bcw.size();
+        bcp[static_cast<size_t>(g) * bc_waves + w] = static_cast<int32_t>(start);
+        const std::vector<int32_t>& ps = per_wave[w];
+        int32_t n_rec = 0;
+        for (int32_t k : ps) n_rec += recs[k];
+        bc_records += n_rec;
+        const size_t np = ps.size();
+        const size_t data_off = (kBcHdr + bc_rmax + 4 * np + 1) / 2 * 2;
+        bcw.resize(start + data_off + 128 * static_cast<size_t>(n_rec), 0);
+        int32_t* pr = bcw.data() + start;
+        pr[0] = n_rec;
+        pr[1] = static_cast<int32_t>(np);
+        pr[2] = static_cast<int32_t>(data_off);
+        int32_t ri = 0;
+        for (size_t i = 0; i < np; ++i) {
+          const int32_t k = ps[i];
+          const int32_t pr0 = r0 + k * rpw, prows = std::min(rpw, r0 + nr - pr0);
+          const int32_t m_lead = row_ptr_host[pr0 + 1] - row_ptr_host[pr0];
+          for (int sb = 0; sb < 4; ++sb) pr[kBcHdr + bc_rmax + 4 * i + sb] = sb < prows ? out_row_host[pr0 + sb] : -1;
+          for (int32_t c = 0; c < recs[k]; ++c, ++ri) {
+            const int32_t cnt = std::min(16, m_lead - 16 * c);
+            pr[kBcHdr + ri] = cnt | ((c == recs[k] - 1) ? 0x100 : 0) | static_cast<int32_t>(i << 16);
+            int32_t* rec = pr + data_off + 128 * static_cast<size_t>(ri);
+            for (int L = 0; L < 64; ++L) {
+              const int32_t sb = L / c4, j = 16 * c + L % 16;
+              int32_t off = ns * c4 * 16, wb = one_bits;  // identity pad: the -0.0 tile, weight 1.0
+              if (sb < prows) {
+                const int32_t row = pr0 + sb, k0 = row_ptr_host[row];
+                if (j < row_ptr_host[row + 1] - k0) {
+                  off = slot[k0 + j] * c4 * 16;
+                  const float wf = static_cast<float>(w_host[k0 + j]);
+                  memcpy(&wb, &wf, 4);
+                }
+              }
+              rec[2 * L] = off;
+              rec[2 * L + 1] = wb;
+            }
+          }
+        }
+      }
+    }
+  } else if (c4 < 64) {
     lds_need = 0;  // the narrow kernel's carve replaces the staged one
     nrp.assign(static_cast<size_t>(rows) + 1, 0);
     const float one = 1.0f;
@@ -3119,6 +3438,14 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
   in.narrow_roww = roww ? 1 : 0;
   in.off_nrow_w = static_cast<int32_t>(off); off += static_cast<int64_t>(nrw.size());
   in.scalar_lds_bytes = static_cast<int32_t>(scalar_need);
+  in.narrow_bcast = bc_waves > 0 && c4 < 64 ? bc_waves : 0;
+  in.bc_rec_max = in.narrow_bcast ? bc_rmax : 0;
+  in.bc_wg_per_cu = in.narrow_bcast ? bc_wg : 0;
+  in.bc_records = static_cast<int32_t>(bc_records);
+  in.off_bc_prog = static_cast<int32_t>(off); off += static_cast<int64_t>(bcp.size());
+  off = (off + 1) / 2 * 2;  // programs start on an even word (8-B records)
+  const int64_t bc_region = off;
+  off += static_cast<int64_t>(bcw.size());
   if (off > 0x7fffffff) return fail(TAL_ERR_INVALID, "tal_round_plan_build: plan larger than 2^31 words");
   in.words = static_cast<int32_t>(off);
   in.lds_bytes = static_cast<int32_t>(stream_cs > 0 ? stream_lds_bytes(stream_cs) : lds_need);
@@ -3143,6 +3470,8 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
     memcpy(plan_host + in.off_npairs, npr.data(), 4 * npr.size());
   }
   if (!nrw.empty()) memcpy(plan_host + in.off_nrow_w, nrw.data(), 4 * nrw.size());
+  for (size_t k = 0; k < bcp.size(); ++k) plan_host[in.off_bc_prog + k] = static_cast<int32_t>(bc_region + bcp[k]);
+  if (!bcw.empty()) memcpy(plan_host + bc_region, bcw.data(), 4 * bcw.size());
   if (rb) {
     memcpy(plan_host + in.off_grp_blk_ptr, grp_blk_ptr.data(), 4 * (G + 1));
     int64_t pos = in.off_dense;
@@ -3329,10 +3658,15 @@ int64_t tal_round_plan_words(int32_t rows, int64_t nnz) {
 }
 
 
-int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host,
-                             const double* w_host, const int32_t* out_row_host, int32_t c4,
-                             int32_t lds_bytes, int32_t dense_rb, int32_t* plan_host,
-                             int64_t plan_capacity_words, tal_round_plan_info* info) {
+}  // extern "C"
+
+namespace {
+
+int32_t round_plan_build(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host,
+                         const double* w_host, const int32_t* out_row_host, int32_t c4,
+                         int32_t lds_bytes, int32_t dense_rb, int32_t* plan_host,
+                         int64_t plan_capacity_words, tal_round_plan_info* info, int32_t bc_waves,
+                         int32_t bc_wg) {
   if (!info) return fail(TAL_ERR_INVALID, "tal_round_plan_build: bad arguments");
   int32_t max_col = 0;
   int32_t rc = check_csr("tal_round_plan_build", rows, row_ptr_host, col_host, w_host, out_row_host, &max_col);
@@ -3351,6 +3685,12 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
     if (c4 >= 64) return sliced <= lds_bytes;
     // narrow kernel: its own carve (exact ROWW padding; pairs: <= 3 per row) and read-ahead
     // within the budget; the staged scalar tail kernel within the hardware's 160 KiB
+    if (bc_waves > 0) {
+      std::vector<std::vector<int32_t>> per_wave;
+      // staging: at most 4096 float4 loads per tile (J <= 4 at 1024 threads, 8 at 512)
+      return bc_lds_bytes(ns, c4) <= lds_bytes && ns * c4 <= 4096 && sliced <= 160 * 1024 &&
+             bc_deal(bc_pass_records(row_ptr_host, r0, nr, c4, false), bc_waves, kBcRecPerWg / bc_waves, &per_wave);
+    }
     const int64_t narrow = static_cast<int64_t>(
         roww ? narrow_roww_lds_bytes(ns, nr, roww_padded_slots(row_ptr_host, r0, nr, c4, &batches), c4)
              : narrow_lds_bytes(ns, nr, no + 3 * nr, c4));
@@ -3385,7 +3725,34 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
     orow[r] = out_row_host[src];
   }
   return finish_plan(rows, rp.data(), cl.data(), wv.data(), orow.data(), max_col, grp, c4, 0, 0,
-                     plan_host, plan_capacity_words, info);
+                     plan_host, plan_capacity_words, info, bc_waves, bc_wg);
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host,
+                             const double* w_host, const int32_t* out_row_host, int32_t c4,
+                             int32_t lds_bytes, int32_t dense_rb, int32_t* plan_host,
+                             int64_t plan_capacity_words, tal_round_plan_info* info) {
+  return round_plan_build(rows, row_ptr_host, col_host, w_host, out_row_host, c4, lds_bytes, dense_rb,
+                          plan_host, plan_capacity_words, info, 0, 2);
+}
+
+int32_t tal_round_plan_build_bcast(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host,
+                                   const double* w_host, const int32_t* out_row_host, int32_t c4,
+                                   int32_t lds_bytes, int32_t waves, int32_t wg_per_cu, int32_t* plan_host,
+                                   int64_t plan_capacity_words, tal_round_plan_info* info) {
+  if (c4 != 16 && c4 != 32)
+    return fail(TAL_ERR_INVALID, "tal_round_plan_build_bcast: c4 must be 16 or 32");
+  if (waves != 8 && waves != 16)
+    return fail(TAL_ERR_INVALID, "tal_round_plan_build_bcast: waves must be 8 or 16");
+  if (wg_per_cu != 1 && wg_per_cu != 2)
+    return fail(TAL_ERR_INVALID, "tal_round_plan_build_bcast: wg_per_cu must be 1 or 2");
+  if (wg_per_cu == 2 && lds_bytes > 80 * 1024) lds_bytes = 80 * 1024;  // two groups' tiles per CU
+  return round_plan_build(rows, row_ptr_host, col_host, w_host, out_row_host, c4, lds_bytes, 0, plan_host,
+                          plan_capacity_words, info, waves, wg_per_cu);
 }
 
 int32_t tal_round_plan_build_stream(int32_t rows, const int32_t* row_ptr_host,
@@ -3962,6 +4329,152 @@ int32_t tal_halo_exchange(void* comm, int32_t world, const void* const* send_buf
   r = rccl().GroupEnd();
   if (first != ncclSuccess) return comm_fail("ncclSend / ncclRecv", first);
   if (r != ncclSuccess) return comm_fail("ncclGroupEnd", r);
+  g_err.clear();
+  return TAL_OK;
+}
+
+}  // extern "C"
+
+// ==========================================================================================
+// Host reduction: processes that see no GPU (BASELINE config 1 runs the reference's driver on
+// CPU models, decentralized_client.py:399-413 on CPU tensors).  The same arithmetic as the
+// kernels, element by element in operand order, on host pointers; a process that sees a GPU
+// never calls it (aggregate.py dispatches on torch.cuda.is_available()).  Built with
+// -ffp-contract=off like the rest of this file: one rounded multiply and one rounded add per
+// operand in EXACT mode, as torch's `w * clone(v)` and `+=` on CPU.
+// ==========================================================================================
+namespace {
+
+constexpr int64_t kHostBlock = 4096;  // elements per block: every operand of a block is read
+                                      // before the block is written (out may alias an operand)
+
+inline float host_bf16(uint16_t b) {
+  const uint32_t u = static_cast<uint32_t>(b) << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+// fp32 -> bf16 round to nearest even, kept as the fp32 value it represents (NaN stays NaN)
+inline float host_round_bf16(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return f;
+  u = (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+// the stored bf16: NaN as 0xFFFF, as torch's vectorized conversion writes it
+inline uint16_t host_store_bf16(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0xffffu;
+  return static_cast<uint16_t>((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+inline int64_t host_trunc_i64(float v) {
+  if (!(v >= -9.2233720368547758e18f && v < 9.2233720368547758e18f)) return INT64_MIN;
+  return static_cast<int64_t>(v);
+}
+
+// Runs body(e0, e1) over [0, n) in blocks, on up to 16 threads for large n.
+template <class Body>
+void host_blocks(int64_t n, Body body) {
+  const int64_t blocks = (n + kHostBlock - 1) / kHostBlock;
+  unsigned hw = std::thread::hardware_concurrency();
+  const int64_t nt = std::max<int64_t>(1, std::min<int64_t>({blocks / 64, 16, static_cast<int64_t>(hw ? hw : 1)}));
+  auto run = [&](int64_t b0, int64_t b1) {
+    for (int64_t b = b0; b < b1; ++b) body(b * kHostBlock, std::min(n, (b + 1) * kHostBlock));
+  };
+  if (nt == 1) {
+    run(0, blocks);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int64_t t = 0; t < nt; ++t) th.emplace_back(run, blocks * t / nt, blocks * (t + 1) / nt);
+  for (auto& t : th) t.join();
+}
+
+int32_t host_args(const char* fn, const void* const* x, const double* w, int32_t m, const void* out, int64_t n) {
+  if (m <= 0) return fail(TAL_ERR_INVALID, std::string(fn) + ": m must be >= 1");
+  if (n < 0) return fail(TAL_ERR_INVALID, std::string(fn) + ": n < 0");
+  if (!x || !w || (n > 0 && !out)) return fail(TAL_ERR_INVALID, std::string(fn) + ": null pointer");
+  for (int i = 0; i < m; ++i)
+    if (!x[i]) return fail(TAL_ERR_INVALID, std::string(fn) + ": null operand pointer");
+  return TAL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t tal_host_agg_f32(const float* const* x_host, const double* w_host, int32_t m, float* out, int64_t n,
+                         int32_t mode) {
+  if (int32_t rc = host_args("tal_host_agg_f32", reinterpret_cast<const void* const*>(x_host), w_host, m, out, n))
+    return rc;
+  std::vector<float> w(static_cast<size_t>(m));
+  for (int i = 0; i < m; ++i) w[i] = static_cast<float>(w_host[i]);
+  const bool exact = mode == TAL_MODE_EXACT;
+  host_blocks(n, [&](int64_t e0, int64_t e1) {
+    float acc[kHostBlock];
+    const int64_t k = e1 - e0;
+    for (int64_t e = 0; e < k; ++e) acc[e] = w[0] * x_host[0][e0 + e];
+    for (int i = 1; i < m; ++i) {
+      const float wi = w[i];
+      const float* xi = x_host[i] + e0;
+      if (exact)
+        for (int64_t e = 0; e < k; ++e) acc[e] = acc[e] + wi * xi[e];
+      else
+        for (int64_t e = 0; e < k; ++e) acc[e] = std::fma(wi, xi[e], acc[e]);
+    }
+    memcpy(out + e0, acc, 4 * static_cast<size_t>(k));
+  });
+  g_err.clear();
+  return TAL_OK;
+}
+
+int32_t tal_host_agg_i64(const int64_t* const* x_host, const double* w_host, int32_t m, int64_t* out, int64_t n) {
+  if (int32_t rc = host_args("tal_host_agg_i64", reinterpret_cast<const void* const*>(x_host), w_host, m, out, n))
+    return rc;
+  std::vector<float> w(static_cast<size_t>(m));
+  for (int i = 0; i < m; ++i) w[i] = static_cast<float>(w_host[i]);
+  host_blocks(n, [&](int64_t e0, int64_t e1) {
+    float acc[kHostBlock];
+    const int64_t k = e1 - e0;
+    for (int64_t e = 0; e < k; ++e) acc[e] = w[0] * static_cast<float>(x_host[0][e0 + e]);
+    for (int i = 1; i < m; ++i)
+      for (int64_t e = 0; e < k; ++e) acc[e] = acc[e] + w[i] * static_cast<float>(x_host[i][e0 + e]);
+    for (int64_t e = 0; e < k; ++e) out[e0 + e] = host_trunc_i64(acc[e]);
+  });
+  g_err.clear();
+  return TAL_OK;
+}
+
+int32_t tal_host_agg_bf16(const uint16_t* const* x_host, const double* w_host, int32_t m, uint16_t* out, int64_t n,
+                          int32_t mode) {
+  if (int32_t rc = host_args("tal_host_agg_bf16", reinterpret_cast<const void* const*>(x_host), w_host, m, out, n))
+    return rc;
+  std::vector<float> w(static_cast<size_t>(m));
+  for (int i = 0; i < m; ++i) w[i] = static_cast<float>(w_host[i]);
+  const bool exact = mode == TAL_MODE_EXACT;
+  host_blocks(n, [&](int64_t e0, int64_t e1) {
+    float acc[kHostBlock];
+    const int64_t k = e1 - e0;
+    for (int64_t e = 0; e < k; ++e) {
+      const float p = w[0] * host_bf16(x_host[0][e0 + e]);
+      acc[e] = exact ? host_round_bf16(p) : p;
+    }
+    for (int i = 1; i < m; ++i) {
+      const float wi = w[i];
+      const uint16_t* xi = x_host[i] + e0;
+      if (exact)
+        for (int64_t e = 0; e < k; ++e) acc[e] = host_round_bf16(acc[e] + host_round_bf16(wi * host_bf16(xi[e])));
+      else
+        for (int64_t e = 0; e < k; ++e) acc[e] = std::fma(wi, host_bf16(xi[e]), acc[e]);
+    }
+    for (int64_t e = 0; e < k; ++e) out[e0 + e] = host_store_bf16(acc[e]);
+  });
   g_err.clear();
   return TAL_OK;
 }

@@ -103,11 +103,43 @@ def agg_bf16(xs: Sequence[torch.Tensor], weights: Sequence[float], out: torch.Te
 
 
 # ------------------------------------------------------------------------------------------
+# Host reduction (a process that sees no GPU: BASELINE config 1)
+# ------------------------------------------------------------------------------------------
+_HOST_FN = {torch.float32: "tal_host_agg_f32", torch.int64: "tal_host_agg_i64",
+            torch.bfloat16: "tal_host_agg_bf16"}
+
+
+def host_agg(xs: Sequence[torch.Tensor], weights: Sequence[float], out: torch.Tensor,
+             mode: int = MODE_EXACT) -> torch.Tensor:
+    """The library's host reduction (tal_host_agg_*) on contiguous CPU tensors of one dtype:
+    out = sum_i fp32(w_i) * xs[i] with the kernels' arithmetic (fp32 / int64 / bf16, modes as
+    agg_f32 / agg_i64 / agg_bf16).  For processes without a GPU only (aggregate.py dispatches
+    on torch.cuda.is_available()); GPU tensors are refused."""
+    if out.device.type != "cpu" or not out.is_contiguous() or out.dtype not in _HOST_FN:
+        raise ValueError("host_agg: out must be a contiguous CPU float32 / int64 / bfloat16 tensor")
+    if len(xs) == 0 or len(weights) != len(xs):
+        raise ValueError("host_agg: one weight per operand, at least one operand")
+    n = out.numel()
+    for i, x in enumerate(xs):
+        if x.device.type != "cpu" or x.dtype != out.dtype or not x.is_contiguous() or x.numel() != n:
+            raise ValueError(f"host_agg: operand {i} must be a contiguous CPU {out.dtype} tensor of {n} elements")
+    L = _lib.load()
+    P, W = _lib.ptr_array([x.data_ptr() for x in xs]), _lib.double_array(weights)
+    args = [P, W, len(xs), ctypes.c_void_p(out.data_ptr()), n]
+    if out.dtype != torch.int64:
+        args.append(int(mode))
+    check(getattr(L, _HOST_FN[out.dtype])(*args))
+    return out
+
+
+# ------------------------------------------------------------------------------------------
 # K3 round plans
 # ------------------------------------------------------------------------------------------
 LDS_BUDGET = 80 * 1024  # two workgroups per CU overlap one's HBM staging with the other's math
 LDS_BUDGETS = (80 * 1024, 160 * 1024)  # candidates: 2 workgroups / CU, or 1 with bigger groups
 TILE_WIDTHS = (64, 128, 32, 16)  # float4 per staged source per tile (ties keep the earlier)
+BCAST_WIDTHS = (16, 32)          # the narrow kernel's broadcast form (build_plan(bcast=...))
+BCAST_FORMS = ((8, 2), (16, 2), (16, 1))  # (wavefronts per workgroup, workgroups per CU)
 
 
 @dataclass
@@ -134,7 +166,8 @@ class RoundPlan:
         return int(self.info.total_src)
 
 
-def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0, dense: int = 0) -> RoundPlan:
+def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0, dense: int = 0,
+               bcast: int = 0, bcast_wg: int = 2) -> RoundPlan:
     """Tile plan for a round given as CSR (row r: operands col[row_ptr[r]:row_ptr[r+1]] with
     float64 weights w, written to pool row out_row[r]).
 
@@ -148,7 +181,12 @@ def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0, dense:
     dense: 0 (default) = the sparse form; 8 requests dense row blocks; -1 lets the library
     pick dense when one LDS read serves >= 4 operands on average.  The dense form lost every
     measured A/B outside cliques (config 3: 6.2 vs 2.45 ms, config 5: 171 vs 83 ms; round-1
-    tuner candidates), and clique rounds take the K3c plan (default_plan)."""
+    tuner candidates), and clique rounds take the K3c plan (default_plan).
+    bcast = 8 / 16: the narrow kernel's broadcast form (tal_round_plan_build_bcast) with that
+    many wavefronts per workgroup: per-lane operand records in VGPRs, handed to a row's lanes
+    by DPP row broadcasts, so per-operand weights cost no LDS reads (c4 16 / 32 only);
+    bcast_wg = resident workgroups per CU it is compiled for (1: 128 VGPRs at 1024 threads and
+    8 LDS reads in flight per wavefront; 2: 64 VGPRs, two groups' tiles per CU)."""
     row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int32)
     col = np.ascontiguousarray(col, dtype=np.int32)
     w = np.ascontiguousarray(w, dtype=np.float64)
@@ -160,17 +198,21 @@ def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0, dense:
     cap = L.tal_round_plan_words(rows, len(col))
     best = None
     last_err = None
-    cands = [(c, b) for b in ([lds_bytes] if lds_bytes else LDS_BUDGETS) for c in ([c4] if c4 else TILE_WIDTHS)]
+    widths = [c4] if c4 else ((16, 32) if bcast else TILE_WIDTHS)
+    cands = [(c, b) for b in ([lds_bytes] if lds_bytes else LDS_BUDGETS) for c in widths]
     for cand, budget in cands:
         info = RoundPlanInfo()
         P32 = ctypes.POINTER(ctypes.c_int32)
         size = cap
         for _ in range(2):  # the dense tables' size is known only after grouping: retry once
             blob = np.zeros(size, dtype=np.int32)
-            rc = L.tal_round_plan_build(rows, row_ptr.ctypes.data_as(P32), col.ctypes.data_as(P32),
-                                        w.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
-                                        out_row.ctypes.data_as(P32), cand, int(budget), int(dense),
-                                        blob.ctypes.data_as(P32), size, ctypes.byref(info))
+            args = (rows, row_ptr.ctypes.data_as(P32), col.ctypes.data_as(P32),
+                    w.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), out_row.ctypes.data_as(P32), cand, int(budget))
+            if bcast:
+                rc = L.tal_round_plan_build_bcast(*args, int(bcast), int(bcast_wg), blob.ctypes.data_as(P32), size,
+                                                  ctypes.byref(info))
+            else:
+                rc = L.tal_round_plan_build(*args, int(dense), blob.ctypes.data_as(P32), size, ctypes.byref(info))
             if rc == _lib.TAL_ERR_CAPACITY and info.words > size:
                 size = int(info.words)
                 continue
@@ -178,8 +220,11 @@ def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0, dense:
         if rc != _lib.TAL_OK:
             last_err = _lib.TalError(rc, L.tal_last_error().decode())
             continue
-        plan = RoundPlan(info=info, host=blob[: info.words].copy(), rows=rows, nnz=len(col),
-                         spec=dict(c4=int(cand), lds=int(budget), dense=int(dense)))
+        spec = dict(c4=int(cand), lds=int(budget), dense=int(dense))
+        if bcast:
+            spec["bcast"] = int(bcast)
+            spec["bcwg"] = int(bcast_wg)
+        plan = RoundPlan(info=info, host=blob[: info.words].copy(), rows=rows, nnz=len(col), spec=spec)
         key = (_plan_cost(plan.info), -_blocks_per_cu(plan.info))
         if best is None or key < best[0]:
             best = (key, plan)
@@ -595,6 +640,15 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
                 if all(key != k for k, _ in cands):
                     p.spec = dict(c4=c4, lds=budget, dense=dense)
                     cands.append((key, p))
+    for c4 in BCAST_WIDTHS:  # the broadcast form of the narrow kernel
+        for waves, wg in BCAST_FORMS:
+            try:
+                p = build_plan(row_ptr, col, w, out_row, c4=c4, lds_bytes=LDS_BUDGETS[-1], bcast=waves, bcast_wg=wg)
+            except _lib.TalError:
+                continue
+            key = (("bcast", waves, wg), p.info.n_groups, p.info.total_src, 0, p.info.max_src, 0)
+            if all(key != k for k, _ in cands):
+                cands.append((key, p))
     for max_rows, max_src in (() if bf16 else STREAM_GROUPINGS):
         try:
             p = build_stream_plan(row_ptr, col, w, out_row, max_rows, max_src)
@@ -668,7 +722,7 @@ def plan_from_spec(row_ptr, col, w, out_row, spec: dict) -> RoundPlan:
         p = build_stream_plan(row_ptr, col, w, out_row, int(spec["stream_rows"]), int(spec["stream_src"]))
     else:
         p = build_plan(row_ptr, col, w, out_row, c4=int(spec["c4"]), lds_bytes=int(spec["lds"]),
-                       dense=int(spec["dense"]))
+                       dense=int(spec["dense"]), bcast=int(spec.get("bcast", 0)), bcast_wg=int(spec.get("bcwg", 2)))
     p.spec = dict(spec)
     return p
 
