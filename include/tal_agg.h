@@ -171,7 +171,7 @@ typedef struct tal_round_plan_info {
    * w] (even): {n_rec, n_pass, data offset (words from the program, even), 5 x 0},
    * bc_rec_max descriptors {operands in the record (1..16) | last of its pass << 8 | pass << 16},
    * 4 output rows per pass (-1: none), then the n_rec records (128 words each). */
-  int32_t narrow_bcast;     /* wavefronts per workgroup (8 or 16); 0 = not this form */
+  int32_t narrow_bcast;     /* wavefronts per workgroup (8, 12 or 16); 0 = not this form */
   int32_t bc_rec_max;       /* records per wavefront (128 / narrow_bcast) */
   int32_t off_bc_prog;      /* [n_groups * narrow_bcast] program offsets */
   int32_t bc_records;       /* records over all programs */
@@ -200,7 +200,7 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
                              int64_t plan_capacity_words, tal_round_plan_info* info);
 
 /* Broadcast-form narrow plan (see narrow_bcast above): as tal_round_plan_build at c4 16 / 32,
- * with waves (8 or 16) wavefronts per workgroup and wg_per_cu (1 or 2) resident workgroups per CU
+ * with waves (8, 12 or 16) wavefronts per workgroup and wg_per_cu (1 or 2) resident workgroups per CU
  * (2 caps lds_bytes at 80 KiB); a group also needs every wavefront's program
  * to fit 128 / waves records (TAL_ERR_CAPACITY for a row no group can take).  Per-operand
  * weights cost no LDS reads in this form (the centrality strategies on graphs whose degrees

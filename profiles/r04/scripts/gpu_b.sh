@@ -12,7 +12,7 @@ d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; r=d['roof
 print(sys.argv[2], d['dtype'], round(d['ms_per_step'],3), round(r['kernel_ms'],3), round(r['frac'],3), d['parity'], d['parity_k3_vs_k1']['rows_differing'])
 " $1 $2; }
 for dt in f32 bf16; do
-  for spec in '{"c4":16,"lds":163840,"dense":0,"bcast":8,"bcwg":2}' '{"c4":16,"lds":163840,"dense":0,"bcast":16,"bcwg":2}' '{"c4":16,"lds":163840,"dense":0,"bcast":16,"bcwg":1}'; do
+  for spec in '{"c4":16,"lds":163840,"dense":0,"bcast":12,"bcwg":2}' '{"c4":16,"lds":163840,"dense":0,"bcast":16,"bcwg":2}' '{"c4":16,"lds":163840,"dense":0}'; do
     tag=$(echo "$dt$spec" | tr -dc 'a-z0-9')
     timeout -k 10 300 python bench.py $C5 --dtype $dt --plan "$spec" > $OUT/$tag.log 2>&1 || { echo "BENCH FAILED $tag"; tail -20 $OUT/$tag.log; exit 1; }
     summ $OUT/$tag.log $tag

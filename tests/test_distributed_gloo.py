@@ -208,3 +208,59 @@ def test_gloo_transposed_exchange_matches_global_round(tmp_path, world):
         own = np.load(tmp_path / f"town{r}.npy")
         assert np.array_equal(np.load(tmp_path / f"tr{r}.npy").view(np.uint32), ref[own].view(np.uint32))
         assert np.array_equal(np.load(tmp_path / f"ti{r}.npy"), iref[own])
+
+
+def _worker_transposed_class(rank, world, port, out_dir, chunks):
+    """transposed.TransposedRound itself on CPU tensors over gloo (its own rank's column block
+    packed and unpacked locally, the others by all-to-all with a zero split for itself); the
+    K3 launch is replaced by the oracle round on the same work buffers - test infrastructure
+    for a host without a GPU (tests/test_gpu_distributed.py runs the kernels)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from topology_aware_learning_amd import transposed as tr
+    from topology_aware_learning_amd.arena import StateLayout
+
+    orders, ws, pool, ipool = problem()
+    n_dev = len(orders)
+    owner = np.array([(i * 7) % world for i in range(n_dev)], np.int32)  # not contiguous
+    layout = StateLayout.from_layout([("w", (pool.shape[1],), "float32"), ("c", (ipool.shape[1],), "int64")])
+    sr = tr.TransposedRound(layout, orders, ws, rank, world, "cpu", owner=owner, chunks=chunks)
+    rp, col, w = ra.round_csr(sr.orders_pos, sr.weights_pos)
+
+    def oracle_segments(layout_, seg_in, seg_out, plan, mode, n_of=None):
+        for g, fn in (("f32", oracle.round_f32), ("i64", oracle.round_i64)):
+            n = n_of.get(g, 0)
+            if n:
+                x = np.ascontiguousarray(seg_in[g][:, :n].numpy())
+                seg_out[g][:, :n] = torch.from_numpy(np.ascontiguousarray(fn(x, rp, col, w, np.arange(n_dev))))
+
+    tr.run_round_segments = oracle_segments
+    sr.pool_a.f32[:, : pool.shape[1]] = torch.from_numpy(pool[sr.own])
+    sr.pool_a.i64[:, : ipool.shape[1]] = torch.from_numpy(ipool[sr.own])
+    for _ in range(2):
+        sr.step()
+    np.save(os.path.join(out_dir, f"cr{rank}.npy"), sr.pool_a.f32[:, : pool.shape[1]].numpy())
+    np.save(os.path.join(out_dir, f"ci{rank}.npy"), sr.pool_a.i64[:, : ipool.shape[1]].numpy())
+    np.save(os.path.join(out_dir, f"cown{rank}.npy"), np.asarray(sr.own))
+    np.save(os.path.join(out_dir, f"clink{rank}.npy"), np.asarray([sr.link_bytes]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,chunks", [(1, 1), (2, 1), (3, 2), (4, 3)])
+def test_gloo_transposed_round_class_two_rounds(tmp_path, world, chunks):
+    """TransposedRound.step on `world` CPU ranks: two rounds bitwise the oracle's two snapshot
+    rounds; each rank's link bytes count only the other ranks' blocks."""
+    mp.spawn(_worker_transposed_class, args=(world, _free_port(), str(tmp_path), chunks), nprocs=world, join=True)
+    orders, ws, pool, ipool = problem()
+    rp, col, w = ra.round_csr(orders, ws)
+    ref, iref = pool, ipool
+    for _ in range(2):
+        ref = oracle.round_f32(ref, rp, col, w, np.arange(len(orders)))
+        iref = oracle.round_i64(iref, rp, col, w, np.arange(len(orders)))
+    for r in range(world):
+        own = np.load(tmp_path / f"cown{r}.npy")
+        assert np.array_equal(np.load(tmp_path / f"cr{r}.npy").view(np.uint32), ref[own].view(np.uint32))
+        assert np.array_equal(np.load(tmp_path / f"ci{r}.npy"), iref[own])
+        if world == 1:
+            assert int(np.load(tmp_path / f"clink{r}.npy")[0]) == 0

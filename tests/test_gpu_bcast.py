@@ -52,7 +52,7 @@ def _bits_equal(a, b):
     return np.array_equal(na, nb) and np.array_equal(a[~na].view(np.uint32), b[~nb].view(np.uint32))
 
 
-FORMS = [(8, 2), (16, 2), (16, 1)]  # (wavefronts per workgroup, workgroups per CU)
+FORMS = [(8, 2), (12, 2), (16, 2), (16, 1)]  # (wavefronts per workgroup, workgroups per CU)
 
 
 @pytest.mark.parametrize("waves,wg", FORMS)

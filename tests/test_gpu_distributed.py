@@ -126,25 +126,24 @@ def test_virtual_ranks_transposed_two_rounds(cuda, graph, world, dtype, mode, ch
     for sr in srs:
         for k, gid in enumerate(sr.own):
             _put_row(sr.pool_a, k, dtype, pool[gid], ipool[gid], cuda)
-    base = srs[0].base
     rp, col, w = ra.round_csr(orders, ws)
     ref, iref = pool, ipool
     for _ in range(2):
         for k in range(srs[0].chunks):
             for sr in srs:
-                sr.pack(k)
-            for r, sr in enumerate(srs):  # forward all-to-all: chunk k of block r of every model
+                sr.pack(k)  # the own block straight into the head rows of work_in
+            for r, sr in enumerate(srs):  # forward all-to-all: chunk k of block r of every other model
                 for key, s in sr._segs_at(k):
-                    for p, src in enumerate(srs):
-                        s.work_in[k][base[p]: base[p + 1]].copy_(src.segs[key].send[k][r])
+                    for p in sr.peers():
+                        s.work_in[k][sr.rows_of(p)].copy_(srs[p].segs[key].send[k][srs[p].peer_slot(r)])
             for sr in srs:
                 sr.compute(k)
-            for r, sr in enumerate(srs):  # backward all-to-all: my rows of every rank's chunk
+            for r, sr in enumerate(srs):  # backward all-to-all: my rows of every other rank's chunk
                 for key, s in sr._segs_at(k):
-                    for p, src in enumerate(srs):
-                        s.back[k][p].copy_(src.segs[key].work_out[k][base[r]: base[r + 1]])
+                    for p in sr.peers():
+                        s.back[k][sr.peer_slot(p)].copy_(srs[p].segs[key].work_out[k][srs[p].rows_of(r)])
             for sr in srs:
-                sr.unpack(k)
+                sr.unpack(k)  # the own block straight from the head rows of work_out
         if dtype == "f32":
             ref = oracle.round_f32(ref, rp, col, w, np.arange(n))
         else:

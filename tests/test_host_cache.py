@@ -52,15 +52,18 @@ def test_lru_eviction_by_bytes():
     assert len(c.entries) == 2
 
 
-def test_pinned_binding_is_opt_in(monkeypatch):
-    """Without TAL_HOST_PIN a CPU model is never re-pointed to pinned rows (the default host
-    path packs into staging buffers and leaves the model's tensors alone)."""
+def test_pinned_binding_default_and_opt_out(monkeypatch):
+    """Pinned binding of CPU models is the default (TAL_HOST_PIN unset); with TAL_HOST_PIN=0 a
+    CPU model is never re-pointed to pinned rows (the call packs into staging buffers and
+    leaves the model's tensors alone)."""
     from topology_aware_learning_amd.arena import StateLayout
 
+    monkeypatch.delenv("TAL_HOST_PIN", raising=False)
+    assert aggregate._pin_enabled()
     m = torch.nn.Linear(3, 2)
     lay = StateLayout.from_state_dict(m.state_dict())
     ptr = m.weight.data_ptr()
-    monkeypatch.delenv("TAL_HOST_PIN", raising=False)
-    assert aggregate._host_binding(m, lay) is None and m.weight.data_ptr() == ptr
     monkeypatch.setenv("TAL_HOST_PIN", "0")
-    assert aggregate._host_binding(m, lay) is None and aggregate.bound_row(m) is None
+    assert not aggregate._pin_enabled()
+    assert aggregate._host_binding(m, lay) is None and m.weight.data_ptr() == ptr
+    assert aggregate.bound_row(m) is None

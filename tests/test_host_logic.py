@@ -732,3 +732,39 @@ def test_select_pool_pair_keeps_first_unless_clearly_faster():
     # all alike within 1 % (noise): the first two stay
     pair, _ = run([4.20, 4.21, 4.17, 4.18, 4.19, 4.22], noise=0.004)
     assert pair == (0, 1)
+
+
+def test_binding_check_sees_last_entry_and_hooks_uninstall():
+    """the O(1) binding check also compares the last entry (a Tensor.set_ of it,
+    which no hook sees, unbinds the model); uninstall_hooks() restores torch, after which every
+    check is the full per-entry one; bind() installs the hooks again."""
+    import torch.nn as nn
+
+    from topology_aware_learning_amd import arena
+    from topology_aware_learning_amd.arena import ModelPool, StateLayout, bound_row
+
+    def make():
+        return nn.Sequential(nn.Linear(3, 4), nn.BatchNorm1d(4), nn.Linear(4, 2))
+
+    m = make()
+    lay = StateLayout.from_state_dict(m.state_dict())
+    pool = ModelPool(lay, 2, "cpu")
+    pool.bind(m, 1)
+    assert bound_row(m) == (pool, 1)
+    last = list(m.state_dict().values())[-1]  # the last entry (the final Linear's bias)
+    with torch.no_grad():
+        m[2].bias.set_(torch.zeros(2))  # re-pointed without any hook firing
+    assert bound_row(m) is None
+    m2 = make()
+    pool.bind(m2, 0)
+    assert bound_row(m2) == (pool, 0)
+    orig_apply = arena._RESTORE[0][2]
+    arena.uninstall_hooks()
+    assert nn.Module._apply is orig_apply and "data" not in nn.Parameter.__dict__
+    assert bound_row(m2) == (pool, 0)  # full check, still bound
+    m2[0].weight.data = torch.zeros(4, 3)  # no hook now: the full check sees it
+    assert bound_row(m2) is None
+    m3 = make()
+    pool.bind(m3, 0)
+    assert arena._HOOKS and bound_row(m3) == (pool, 0)
+    del last

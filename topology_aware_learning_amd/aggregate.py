@@ -161,19 +161,22 @@ _CACHE: Optional[_OperandCache] = None
 
 
 def _pin_enabled() -> bool:
-    return os.environ.get("TAL_HOST_PIN", "0") not in ("", "0")
+    """Pinned binding of CPU models is the default since round 4 (TAL_HOST_PIN=0 opts out)."""
+    return os.environ.get("TAL_HOST_PIN", "1") not in ("", "0")
 
 
 def _host_binding(model: nn.Module, layout: StateLayout) -> Optional[Tuple[ModelPool, int]]:
     """(pool, row) of a model whose state lives in a pinned host row, or None.
 
-    With TAL_HOST_PIN set, a model whose state is on the CPU and not bound anywhere is bound
-    first: its state is copied once into a pinned one-row host pool and its parameters / buffers
-    become views of that row (ModelPool.bind, as for device pools).  The call then moves its
-    operands host -> device and its result device -> host as one DMA per segment straight
-    from / into the row - no packing of 320 tensors into a staging buffer and no unpacking
-    copy afterwards.  A model whose tensors are replaced later (module.to(), load_state_dict
-    into new tensors) fails the binding check and is bound again on its next call."""
+    By default (TAL_HOST_PIN unset or 1; 0 opts out) a model whose state is on the CPU and not
+    bound anywhere is bound first: its state is copied once into a pinned one-row host pool and
+    its parameters / buffers become views of that row (ModelPool.bind, as for device pools).
+    The call then moves its operands host -> device and its result device -> host as one DMA
+    per segment straight from / into the row - no packing of 320 tensors into a staging buffer
+    and no unpacking copy afterwards (round 3: 25.5 ms per config-3 call packing, the PCIe
+    floor ~17 ms).  A model whose tensors are replaced later (module.to(), load_state_dict
+    into new tensors) fails the binding check and is bound again on its next call; if pinned
+    memory cannot be allocated the call packs as before."""
     b = bound_row(model)
     if b is not None:
         return b if b[0].device.type == "cpu" and b[0].layout == layout else None
@@ -201,8 +204,11 @@ def _bind_pinned(model: nn.Module, layout: StateLayout) -> Optional[Tuple[ModelP
     def pinned(rows_ld, dtype):
         return torch.empty((1, rows_ld), dtype=dtype, pin_memory=rows_ld > 0)
 
-    pool = ModelPool(layout, 1, "cpu", f32=pinned(layout.ld_f32, torch.float32),
-                     i64=pinned(layout.ld_i64, torch.int64), b16=pinned(layout.ld_b16, torch.bfloat16))
+    try:
+        pool = ModelPool(layout, 1, "cpu", f32=pinned(layout.ld_f32, torch.float32),
+                         i64=pinned(layout.ld_i64, torch.int64), b16=pinned(layout.ld_b16, torch.bfloat16))
+    except RuntimeError:  # no pinned memory to be had (locked-memory limit): pack instead
+        return None
     pool.bind(model, 0)
     return pool, 0
 

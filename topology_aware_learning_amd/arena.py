@@ -163,7 +163,8 @@ def by_name_offset(entries: Sequence[Entry], name: str) -> int:
 # ~70 us per model, ten models per call).  Not hooked: `buf.data = x` on a plain-tensor buffer
 # (torch.Tensor itself is left alone); it is seen at the next full check, after any hook event.
 _GEN = [0]
-_HOOKS: list = []
+_HOOKS: list = []      # registration-hook handles
+_RESTORE: list = []    # (owner, attribute, original) of every patched attribute
 
 
 def _invalidate(*_args, **_kw) -> None:
@@ -184,24 +185,40 @@ def _install_hooks() -> None:
         _invalidate()
         return orig(self, *args, **kwargs)
 
-    _apply._tal_orig = orig  # type: ignore[attr-defined]
+    _RESTORE.append((nn.Module, "_apply", orig))
     nn.Module._apply = _apply  # type: ignore[method-assign]
-    _HOOKS.append(_apply)
     for name in ("register_parameter", "register_buffer", "__delattr__"):  # (set to None, del)
         def wrapped(self, *args, _orig=getattr(nn.Module, name), **kwargs):
             _invalidate()
             return _orig(self, *args, **kwargs)
 
+        _RESTORE.append((nn.Module, name, getattr(nn.Module, name)))
         setattr(nn.Module, name, wrapped)
-        _HOOKS.append(wrapped)
     base = torch._C.TensorBase.data
 
     def _set_data(self, value):
         _invalidate()
         base.__set__(self, value)
 
+    _RESTORE.append((nn.Parameter, "data", nn.Parameter.__dict__.get("data")))
     nn.Parameter.data = property(base.__get__, _set_data, doc=base.__doc__)  # type: ignore[assignment]
-    _HOOKS.append(_set_data)
+
+
+def uninstall_hooks() -> None:
+    """Undo what the first bind() installed on torch (registration hooks, the Module._apply /
+    register_* / __delattr__ wrappers, the Parameter.data property).  Bindings stay usable:
+    without the hooks every binding check is the full per-entry one.  bind() installs them
+    again."""
+    for h in _HOOKS:
+        h.remove()
+    _HOOKS.clear()
+    for owner, attr, orig in reversed(_RESTORE):
+        if orig is None:
+            delattr(owner, attr)
+        else:
+            setattr(owner, attr, orig)
+    _RESTORE.clear()
+    _invalidate()
 
 
 def _resolve(module: nn.Module, name: str) -> Tuple[nn.Module, str]:
@@ -251,7 +268,13 @@ class ModelPool:
         """Copy `module`'s state into row r and make its parameters / buffers views of that row.
 
         Parameter objects keep their identity (``param.data`` is re-pointed) so optimizers built
-        before or after binding keep working; buffers are re-registered as views."""
+        before or after binding keep working; buffers are re-registered as views.  The first
+        bind installs torch hooks that make the binding check O(1) (_GEN; uninstall_hooks()
+        removes them).  Re-pointing a bound tensor by a path no hook sees - ``Tensor.set_``,
+        ``torch.utils.swap_tensors``, ``.data =`` on a plain-tensor buffer - is caught by the
+        O(1) check only for the first and the last state entry; for the others it is seen at
+        the next full check (after any hooked event), so do not use those paths on bound
+        models (module.to(), load_state_dict, optimizer steps and in-place updates are safe)."""
         sd = module.state_dict()
         self.layout.check_compatible(sd, "module")
         with torch.no_grad():
@@ -288,13 +311,16 @@ class ModelPool:
             return None
         r = module._tal_row  # type: ignore[attr-defined]
         slots = module._tal_slots  # type: ignore[attr-defined]
-        if module._tal_gen == _GEN[0]:  # type: ignore[attr-defined]
-            # no re-pointing hook fired since the last full check (see _GEN)
-            table, attr = slots[0]
-            t = table.get(attr)
-            if t is not None and t.data_ptr() == module._tal_ptrs[0]:  # type: ignore[attr-defined]
-                return r
-            return None
+        if _HOOKS and module._tal_gen == _GEN[0]:  # type: ignore[attr-defined]
+            # no re-pointing hook fired since the last full check (see _GEN); the first and
+            # the last entry are compared as well (unhooked re-pointing of either is seen)
+            ptrs = module._tal_ptrs  # type: ignore[attr-defined]
+            for k in (0, len(slots) - 1):
+                table, attr = slots[k]
+                t = table.get(attr)
+                if t is None or t.data_ptr() != ptrs[k]:
+                    return None
+            return r
         # after a hook event: every state entry, resolved by name again (a replaced submodule
         # keeps its old tables), must still be the row view bound to it
         gen = _GEN[0]

@@ -1082,11 +1082,32 @@ __device__ __forceinline__ float4 bc_math4(float4 acc, const float4 (&x)[4], int
   }
 }
 
-template <typename T, bool EXACT, bool PIPE>
+// Two operands of batch B (half H): the lean depth for the 64-VGPR fp32 EXACT form, whose records,
+// staging registers and separate products leave room for two data reads in flight, not four.
+template <typename T, bool EXACT, int B, int H>
+__device__ __forceinline__ float4 bc_half(float4 acc, int2 e, uint32_t base) {
+  const float4 x0 = bc_x<4 * B + 2 * H>(e, base), x1 = bc_x<4 * B + 2 * H + 1>(e, base);
+  acc = next4t<T, EXACT>(acc, bc_w<4 * B + 2 * H>(e), x0);
+  return next4t<T, EXACT>(acc, bc_w<4 * B + 2 * H + 1>(e), x1);
+}
+
+// DEPTH = data reads in flight per wavefront: 2, 4 or 8 (see bc_read4 / bc_half).
+template <typename T, bool EXACT, int DEPTH>
 __device__ __forceinline__ float4 bc_record(float4 acc, int2 e, uint32_t base, int cnt) {
   const int nb = (cnt + 3) >> 2;  // wave-uniform
   float4 xa[4], xb[4];
-  if constexpr (PIPE) {
+  if constexpr (DEPTH == 2) {
+#define TAL_BC_LEAN(B)                                      \
+    if (nb > B) {                                           \
+      __builtin_amdgcn_sched_barrier(0);                    \
+      acc = bc_half<T, EXACT, B, 0>(acc, e, base);          \
+      __builtin_amdgcn_sched_barrier(0);                    \
+      acc = bc_half<T, EXACT, B, 1>(acc, e, base);          \
+    }
+    TAL_BC_LEAN(0) TAL_BC_LEAN(1) TAL_BC_LEAN(2) TAL_BC_LEAN(3)
+#undef TAL_BC_LEAN
+    return acc;
+  } else if constexpr (DEPTH == 8) {
     bc_read4<0>(xa, e, base);
     if (nb > 1) bc_read4<1>(xb, e, base);
     __builtin_amdgcn_sched_barrier(0);
@@ -1275,8 +1296,10 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   constexpr int kR = BC ? bc_rec_max<NT>() : 1;
   // BC read depth: 8 data reads in flight where the registers allow it (one workgroup per CU:
   // NP = 1, 128 VGPRs at 1024 threads; 512 threads except fp32 EXACT, whose separate products
-  // and the 8-VGPR staging of 8 loads per lane fill 128), else 4
-  constexpr bool kBcPipe = NP == 1 || (NT <= 512 && !(EXACT && !kIsBf16<T>));
+  // and the 8-VGPR staging of 8 loads per lane fill 128), 2 for fp32 EXACT at two 768- or
+  // 1024-thread workgroups per CU (80 / 64 VGPRs), else 4
+  constexpr bool kF32x = EXACT && !kIsBf16<T>;
+  constexpr int kBcDepth = (NP == 1 || (NT <= 512 && !kF32x)) ? 8 : (kF32x && NT >= 768) ? 2 : 4;
   const int bc_off = BC ? ((ConstI32)p.bc_prog)[g * kW + wave] : 0;
   const ConstI32 prog = (ConstI32)(p.base + bc_off);
   const int bc_n = BC ? prog[0] : 0;
@@ -1345,7 +1368,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
 #ifdef TAL_PROBE_NOCOMP
         (void)d;
 #else
-        acc = bc_record<T, EXACT, kBcPipe>(acc, bc_rec[r], col_base, static_cast<int>(d & 0xffu));
+        acc = bc_record<T, EXACT, kBcDepth>(acc, bc_rec[r], col_base, static_cast<int>(d & 0xffu));
 #endif
         if (d & 0x100u) {  // the pass's last record: store its rows
           const ConstI32 orow = prog + kBcHdr + kR + 4 * static_cast<int>(d >> 16);
@@ -1802,7 +1825,7 @@ int32_t validate_info(const tal_round_plan_info* info) {
   if (info->c4 < 64 && info->dense_rb != 0)
     return fail(TAL_ERR_INVALID, "narrow plans (c4 16 / 32) are sparse");
   if (info->narrow_bcast != 0 &&
-      (info->c4 >= 64 || (info->narrow_bcast != 8 && info->narrow_bcast != 16) ||
+      (info->c4 >= 64 || (info->narrow_bcast != 8 && info->narrow_bcast != 12 && info->narrow_bcast != 16) ||
        info->bc_rec_max != kBcRecPerWg / info->narrow_bcast || info->bc_wg_per_cu < 1 || info->bc_wg_per_cu > 2))
     return fail(TAL_ERR_INVALID, "broadcast-form plan: c4 16 / 32, 8 or 16 wavefronts, 128 / waves records, "
                                  "1 or 2 workgroups per CU");
@@ -1953,6 +1976,8 @@ int32_t launch_round_bcast_nt(const T* pin, int64_t ld_in, T* pout, int64_t ld_o
   const int64_t loads = static_cast<int64_t>(in.max_src) * C4;  // float4 staging loads per tile
   if (loads <= 2LL * NT) return launch_round_bcast_j<C4, NT, 2, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
   if (loads <= 4LL * NT) return launch_round_bcast_j<C4, NT, 4, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  if constexpr (NT == 768)
+    if (loads <= 6LL * NT) return launch_round_bcast_j<C4, NT, 6, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
   if constexpr (NT <= 512)
     if (loads <= 8LL * NT) return launch_round_bcast_j<C4, NT, 8, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
   return fail(TAL_ERR_CAPACITY, "broadcast-form round plan: group tile too large for the workgroup");
@@ -1961,8 +1986,9 @@ int32_t launch_round_bcast_nt(const T* pin, int64_t ld_in, T* pout, int64_t ld_o
 template <int C4, bool EXACT, typename T>
 int32_t launch_round_bcast(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
                            const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
-  return in.narrow_bcast == 8 ? launch_round_bcast_nt<C4, 512, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s)
-                              : launch_round_bcast_nt<C4, 1024, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  if (in.narrow_bcast == 8) return launch_round_bcast_nt<C4, 512, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  if (in.narrow_bcast == 12) return launch_round_bcast_nt<C4, 768, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  return launch_round_bcast_nt<C4, 1024, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
 }
 
 template <int C4, bool EXACT, typename T = float>
@@ -3746,8 +3772,8 @@ int32_t tal_round_plan_build_bcast(int32_t rows, const int32_t* row_ptr_host, co
                                    int64_t plan_capacity_words, tal_round_plan_info* info) {
   if (c4 != 16 && c4 != 32)
     return fail(TAL_ERR_INVALID, "tal_round_plan_build_bcast: c4 must be 16 or 32");
-  if (waves != 8 && waves != 16)
-    return fail(TAL_ERR_INVALID, "tal_round_plan_build_bcast: waves must be 8 or 16");
+  if (waves != 8 && waves != 12 && waves != 16)
+    return fail(TAL_ERR_INVALID, "tal_round_plan_build_bcast: waves must be 8, 12 or 16");
   if (wg_per_cu != 1 && wg_per_cu != 2)
     return fail(TAL_ERR_INVALID, "tal_round_plan_build_bcast: wg_per_cu must be 1 or 2");
   if (wg_per_cu == 2 && lds_bytes > 80 * 1024) lds_bytes = 80 * 1024;  // two groups' tiles per CU

@@ -139,7 +139,7 @@ LDS_BUDGET = 80 * 1024  # two workgroups per CU overlap one's HBM staging with t
 LDS_BUDGETS = (80 * 1024, 160 * 1024)  # candidates: 2 workgroups / CU, or 1 with bigger groups
 TILE_WIDTHS = (64, 128, 32, 16)  # float4 per staged source per tile (ties keep the earlier)
 BCAST_WIDTHS = (16, 32)          # the narrow kernel's broadcast form (build_plan(bcast=...))
-BCAST_FORMS = ((8, 2), (16, 2), (16, 1))  # (wavefronts per workgroup, workgroups per CU)
+BCAST_FORMS = ((8, 2), (12, 2), (16, 2), (16, 1))  # (wavefronts per workgroup, workgroups per CU)
 
 
 @dataclass

@@ -78,6 +78,26 @@ def positions(owner, world: int):
     return own_by_rank, base, pos
 
 
+def positions_own_first(owner, world: int, rank: int):
+    """TransposedRound's row order on rank `rank`: its own models first, then every other
+    rank's in ascending rank order (each rank's models contiguous, in id order).  Own rows
+    first means the forward all-to-all receives into one contiguous tail of the work buffer and
+    the rank's own column block never passes through RCCL: it is packed straight into the
+    head rows and unpacked straight from them.  Returns (own lists per rank, first row of each
+    rank's models, pos[global id])."""
+    owner = np.asarray(owner)
+    own_by_rank = [np.flatnonzero(owner == p).tolist() for p in range(world)]
+    order = [rank] + [p for p in range(world) if p != rank]
+    row_base = np.zeros(world, dtype=np.int64)
+    pos = np.empty(len(owner), dtype=np.int64)
+    r = 0
+    for p in order:
+        row_base[p] = r
+        pos[own_by_rank[p]] = r + np.arange(len(own_by_rank[p]))
+        r += len(own_by_rank[p])
+    return own_by_rank, row_base, pos
+
+
 def exchange_bytes(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: int = 0) -> dict:
     """Link volumes of one round for each exchange.  'halo' / 'transpose': the largest per-rank
     volume (bytes in or out, whichever is larger): distinct remote neighbor models, resp.
@@ -113,8 +133,9 @@ def link_model(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: int = 0
     n_dev = len(orders)
     local = {
         "halo": max(len({j for i in s.orders_local for j in i}) + len(s.own) for s in specs) * row,
-        # K3 over [n_dev, n / world] (sources + outputs) + pack (read own, write send buffer)
-        # + unpack (read received blocks, write own rows)
+        # K3 over [n_dev, n / world] (sources + outputs) + pack (read own, write the send buffer
+        # and the own block's work rows) + unpack (read the received blocks and the own block's
+        # output rows, write own rows); the own block is one of these copies, never RCCL's
         "transpose": -(-2 * n_dev * row // world) + 4 * max(len(s.own) for s in specs) * row,
     }
     out = {}
@@ -143,16 +164,17 @@ def choose_exchange(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: in
 class _ColSeg:
     """One segment's buffers.  Rank p's column block (width <= b) is cut into `chunks` column
     chunks of width bc; chunk k of every block travels and is reduced on its own, so the
-    all-to-alls of one chunk overlap the packing, the round and the unpacking of another."""
+    all-to-alls of one chunk overlap the packing, the round and the unpacking of another.  The
+    peer dimension of send / back skips this rank (peer slot of rank p: p, or p - 1 past it)."""
     n: int                  # elements per model
     b: int                  # block width
     blocks: list            # (first column, width) of each rank's block
     chunks: int
     bc: int                 # chunk width (row stride of the work buffers)
-    send: torch.Tensor      # [chunks, world, own, bc]  my models' chunks, by destination rank
-    work_in: torch.Tensor   # [chunks, R, bc]           chunk k of block `rank` of every model (rank-major)
-    work_out: torch.Tensor  # [chunks, R, bc]           the round's output for it
-    back: torch.Tensor      # [chunks, world, own, bc]  my models' output chunks, by source rank
+    send: torch.Tensor      # [chunks, world-1, own, bc]  my models' chunks, by destination peer
+    work_in: torch.Tensor   # [chunks, R, bc]  chunk k of block `rank` of every model (own rows first)
+    work_out: torch.Tensor  # [chunks, R, bc]  the round's output for it
+    back: torch.Tensor      # [chunks, world-1, own, bc]  my models' output chunks, by source peer
 
     def chunk_blocks(self, k: int):
         """(first column, width) of chunk k of each rank's block."""
@@ -180,7 +202,7 @@ class TransposedRound:
         self.rank, self.world = rank, world
         n_dev = len(orders)
         owner = partition_contiguous(n_dev, world) if owner is None else np.asarray(owner, np.int32)
-        self.own_by_rank, self.base, self.pos = positions(owner, world)
+        self.own_by_rank, self.row_base, self.pos = positions_own_first(owner, world, rank)
         self.own = self.own_by_rank[rank]
         self.local_rows = len(self.own)
         self.rows_all = n_dev
@@ -202,8 +224,9 @@ class TransposedRound:
             def z(*shape, dt=dt):
                 return torch.zeros(*shape, dtype=dt, device=self.device)
 
-            self.segs[g] = _ColSeg(n, b, blocks, c, bc, z(c, world, self.local_rows, bc), z(c, n_dev, bc),
-                                   z(c, n_dev, bc), z(c, world, self.local_rows, bc))
+            peers = max(1, world - 1)
+            self.segs[g] = _ColSeg(n, b, blocks, c, bc, z(c, peers, self.local_rows, bc), z(c, n_dev, bc),
+                                   z(c, n_dev, bc), z(c, peers, self.local_rows, bc))
         self.w_me = {g: s.blocks[rank][1] for g, s in self.segs.items()}
         rp, col, w = csr_from_lists(self.orders_pos, self.weights_pos)
         out_rows = np.arange(n_dev, dtype=np.int32)
@@ -224,11 +247,32 @@ class TransposedRound:
     def _segs_at(self, k: int):
         return [(g, s) for g, s in self.segs.items() if k < s.chunks]
 
+    def peer_slot(self, p: int) -> int:
+        """Index of rank p (!= this rank) in the peer dimension of send / back."""
+        return p if p < self.rank else p - 1
+
+    def peers(self):
+        return [p for p in range(self.world) if p != self.rank]
+
+    def rows_of(self, p: int) -> slice:
+        """The work-buffer rows holding rank p's models."""
+        return slice(int(self.row_base[p]), int(self.row_base[p]) + len(self.own_by_rank[p]))
+
     # phases of chunk k: step() pipelines them; the virtual-rank GPU test interleaves ranks
     def pack(self, k: int = 0) -> None:
+        """Chunk k of my models: block p into send (peer p), my own block straight into the
+        head rows of work_in (it never leaves this GPU)."""
         pools = _pool_segs(self.pool_a)
+        own = self.rows_of(self.rank)
         for g, s in self._segs_at(k):
-            pack_columns(pools[g], self.local_rows, s.chunk_blocks(k), s.bc, s.send[k])
+            cb = s.chunk_blocks(k)
+            for p in self.peers():
+                c0, w = cb[p]
+                if w:
+                    s.send[k][self.peer_slot(p)][:, :w].copy_(pools[g][: self.local_rows, c0: c0 + w])
+            c0, w = cb[self.rank]
+            if w:
+                s.work_in[k][own, :w].copy_(pools[g][: self.local_rows, c0: c0 + w])
 
     def _all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits):
         if self.transport == "host":
@@ -239,10 +283,18 @@ class TransposedRound:
         return dist.all_to_all_single(out.view(-1), inp.view(-1), out_splits, in_splits, group=self.group,
                                       async_op=True)
 
+    def _splits(self, per_rank):
+        """Split sizes in rank order with 0 for this rank (its block stays local)."""
+        return [0 if p == self.rank else int(v) for p, v in enumerate(per_rank)]
+
     def forward_exchange(self, k: int = 0) -> list:
-        """Chunk k of block `rank` of every model into work_in[k]; returns the pending works."""
-        works = [self._all_to_all(s.work_in[k], s.send[k], [len(o) * s.bc for o in self.own_by_rank],
-                                  [self.local_rows * s.bc] * self.world) for _, s in self._segs_at(k)]
+        """Chunk k of block `rank` of every other rank's models into work_in[k] after my own
+        rows; returns the pending works (none at world 1: nothing leaves the GPU)."""
+        if self.world == 1:
+            return []
+        works = [self._all_to_all(s.work_in[k][self.local_rows:], s.send[k],
+                                  self._splits([len(o) * s.bc for o in self.own_by_rank]),
+                                  self._splits([self.local_rows * s.bc] * self.world)) for _, s in self._segs_at(k)]
         return [w for w in works if w is not None]
 
     def compute(self, k: int = 0) -> None:
@@ -251,14 +303,28 @@ class TransposedRound:
                            self.plan, self.mode, n_of={g: s.chunk_blocks(k)[self.rank][1] for g, s in segs})
 
     def backward_exchange(self, k: int = 0) -> list:
-        works = [self._all_to_all(s.back[k], s.work_out[k], [self.local_rows * s.bc] * self.world,
-                                  [len(o) * s.bc for o in self.own_by_rank]) for _, s in self._segs_at(k)]
+        """Every other rank's models' output rows back to their owners (my own stay here)."""
+        if self.world == 1:
+            return []
+        works = [self._all_to_all(s.back[k], s.work_out[k][self.local_rows:],
+                                  self._splits([self.local_rows * s.bc] * self.world),
+                                  self._splits([len(o) * s.bc for o in self.own_by_rank])) for _, s in self._segs_at(k)]
         return [w for w in works if w is not None]
 
     def unpack(self, k: int = 0) -> None:
+        """My models' output chunk k: block p from back (peer p), my own block straight from the
+        head rows of work_out."""
         pools = _pool_segs(self.pool_a)
+        own = self.rows_of(self.rank)
         for g, s in self._segs_at(k):
-            unpack_columns(s.back[k], self.local_rows, s.chunk_blocks(k), s.bc, pools[g])
+            cb = s.chunk_blocks(k)
+            for p in self.peers():
+                c0, w = cb[p]
+                if w:
+                    pools[g][: self.local_rows, c0: c0 + w].copy_(s.back[k][self.peer_slot(p)][:, :w])
+            c0, w = cb[self.rank]
+            if w:
+                pools[g][: self.local_rows, c0: c0 + w].copy_(s.work_out[k][own, :w])
 
     def step(self, timed: bool = False) -> None:
         """One round, chunk-pipelined: pack k+1 and its forward all-to-all are issued before
@@ -309,7 +375,8 @@ class TransposedRound:
 
     @property
     def link_bytes(self) -> int:
-        """Bytes this rank receives over the links per round (both all-to-alls)."""
+        """Bytes this rank receives over the links per round (both all-to-alls; its own block
+        is copied on the GPU, not sent)."""
         r = 0
         for g, s in self.segs.items():
             r += _ESIZE[g] * s.chunks * s.bc * ((self.rows_all - self.local_rows) + self.local_rows * (self.world - 1))
