@@ -195,3 +195,51 @@ def test_config5_bf16_exact_vs_reference(cuda):
     """Config 5 on bf16 models (model.to(torch.bfloat16)) in EXACT mode: the first entry group
     of every output model bitwise the reference's own bf16 arithmetic."""
     _check_c5(cuda, "bf16", "unweighted_module_avg", None)
+
+
+@pytest.mark.parametrize("fn,spec", [("unweighted_module_avg", None),
+                                     ("centrality_module_avg", None),
+                                     ("centrality_module_avg", {"reg": 1}),
+                                     ("centrality_module_avg", {"c4": 16, "lds": 163840, "dense": 0, "bcast": 16, "bcwg": 2})])
+def test_config5_bf16_fma_full_width_within_bound(cuda, fn, spec):
+    """Config 5's bf16 tolerance run (FMA: fp32 accumulation, one rounding) at full width: all
+    256 output models x all 86.6 M columns within the SURVEY §8(a) bound
+        |got - ref| <= 2^-8 |ref| + M_r 2^-24 sum_i |w_i x_i|
+    against an fp32 EXACT round of the same bf16-valued inputs (the fp32 round kernel that
+    test_config5_full_round_vs_reference pins to the reference's sha256), column chunk by
+    column chunk; the default plan (per-operand weights: the broadcast form) and K3r."""
+    fx = _fixture("full_round_c5_vit_sbm256.json")
+    orders = fx["orders"]
+    run = dict(fn=fn, softmax=True, softmax_coeff=10.0)
+    ws = _c5_weights(fx, run, orders)
+    lay = synth.as_bf16(synth.vit_b16_layout())
+    torch.cuda.empty_cache()
+    layout, pin, pout = _pools(cuda, lay, fx["seeds"], "bfloat16")
+    n = layout.n_b16
+    plan = _plan(orders, ws, spec, bf16=True) if spec is not None else None
+    if plan is None:
+        rp, col, w = ra.round_csr(orders, ws)
+        plan = ops.default_plan(rp, col, w, np.arange(len(orders), dtype=np.int32), bf16=True, mode=ops.MODE_FMA)
+    plan = plan.to(cuda)
+    ops.round_bf16(pin.b16, pout.b16, plan, n=n, mode=ops.MODE_FMA)
+    rp, col, w = ra.round_csr(orders, ws)
+    plan32 = ops.default_plan(rp, col, w, np.arange(len(orders), dtype=np.int32)).to(cuda)
+    m_r = torch.tensor([len(o) for o in orders], dtype=torch.float32, device=cuda)[:, None]
+    chunk = 1 << 23
+    worst = 0.0
+    for c0 in range(0, n, chunk):
+        c1 = min(n, c0 + chunk)
+        x32 = pin.b16[:, c0:c1].float().contiguous()
+        ref = torch.empty_like(x32)
+        ops.round_f32(x32, ref, plan32, n=c1 - c0)
+        mag = torch.empty_like(x32)
+        ops.round_f32(x32.abs_(), mag, plan32, n=c1 - c0)  # weights are positive: sum |w x|
+        bound = 2.0 ** -8 * ref.abs() + m_r * 2.0 ** -24 * mag
+        err = (pout.b16[:, c0:c1].float() - ref).abs()
+        ratio = float((err / bound.clamp_min(1e-38)).max())
+        worst = max(worst, ratio)
+        assert ratio <= 1.0, (c0, ratio)
+        del x32, ref, mag, bound, err
+    del pin, pout
+    torch.cuda.empty_cache()
+    assert worst > 0.0  # the comparison saw real rounding

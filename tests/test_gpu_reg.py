@@ -181,9 +181,10 @@ def test_reg_plan_spec_roundtrip_and_i64(cuda):
 
 def test_round_executor_bf16_fma_per_operand_weights(cuda):
     """The product's untimed default for a bf16 FMA round with per-operand (degree-centrality)
-    weights is K3r (ops.default_plan): RoundExecutor on bf16 model rows of the SBM-256 topology,
-    every row bitwise the bf16 FMA oracle (fp32 fused chain, one rounding), the int64 segment
-    through the plan's full form, bitwise the oracle's truncation."""
+    weights is the narrow kernel's broadcast form since round 4 (ops.default_plan; K3r before):
+    RoundExecutor on bf16 model rows of the SBM-256 topology runs it in place (one group, no
+    scratch pool), every row bitwise the bf16 FMA oracle (fp32 fused chain, one rounding), the
+    int64 segment through the plan's scalar form, bitwise the oracle's truncation."""
     from topology_aware_learning_amd.arena import ModelPool, StateLayout
     from topology_aware_learning_amd.round import RoundExecutor
 
@@ -197,7 +198,8 @@ def test_round_executor_bf16_fma_per_operand_weights(cuda):
     pool.b16[:, :lay.n_b16].copy_(x.to(cuda))
     pool.i64[:, :lay.n_i64].copy_(xi.to(cuda))
     ex = RoundExecutor(pool, mode=ops.MODE_FMA)
-    assert isinstance(ex.plan(orders, ws, list(range(rows))), ops.RegPlan)
+    plan = ex.plan(orders, ws, list(range(rows)))
+    assert isinstance(plan, ops.RoundPlan) and plan.info.narrow_bcast and plan.single_group
     bits = x.view(torch.int16).numpy().view(np.uint16)
     ref = oracle.round_bf16(bits, row_ptr, col, w, np.arange(rows, dtype=np.int32), exact=False)
     iref = oracle.round_i64(xi.numpy(), row_ptr, col, w, np.arange(rows, dtype=np.int32))

@@ -580,9 +580,10 @@ def test_default_plan_forms(kind, n, deg, form):
 
 
 def test_default_plan_bf16_per_operand_weights():
-    """Config 5 with degree-centrality softmax weights: bf16 FMA rounds default to register-
-    resident groups (K3r won the round-3 closing table, 29.8 vs 33.1 ms); fp32 and bf16 EXACT
-    keep the narrow pairs form, and unweighted bf16 FMA the narrow ROWW form."""
+    """Config 5 with degree-centrality softmax weights: bf16 FMA rounds default to the narrow
+    kernel's broadcast form (16 wavefronts, 2 workgroups per CU: 23.6-24.0 ms in round 4 against
+    K3r's 29.8), one group so RoundExecutor runs it in place; fp32 and bf16 EXACT keep the
+    narrow pairs form, and unweighted bf16 FMA the narrow ROWW form."""
     import bench
     from topology_aware_learning_amd.round import csr_from_lists
 
@@ -590,7 +591,8 @@ def test_default_plan_bf16_per_operand_weights():
     rp, col, w = csr_from_lists(orders, ws)
     rows = np.arange(len(orders), dtype=np.int32)
     p = ops.default_plan(rp, col, w, rows, bf16=True, mode=ops.MODE_FMA)
-    assert isinstance(p, ops.RegPlan) and p.spec == {"reg": 1}
+    assert isinstance(p, ops.RoundPlan) and p.info.narrow_bcast == 16 and p.info.bc_wg_per_cu == 2
+    assert p.single_group and p.spec["bcast"] == 16
     for kw in (dict(bf16=False, mode=ops.MODE_FMA), dict(bf16=True, mode=ops.MODE_EXACT), dict(bf16=True)):
         q = ops.default_plan(rp, col, w, rows, **kw)
         assert isinstance(q, ops.RoundPlan) and q.info.c4 == 16 and not q.info.narrow_roww

@@ -732,10 +732,13 @@ def default_plan(row_ptr, col, w, out_row, bf16: bool = False, mode: int = MODE_
     the round's uniform-weight clique blocks by K3c when it has any (fp32 pools; the other rows
     by their own sparse plan), else build_plan's sparse form at the tile width and LDS budget
     its cost model picks.  On the round-1 A/B tables this is the measured winner's form for
-    configs 2-5 (tests/test_host_logic.py::test_default_plan_forms).  One exception, from the
-    round-3 closing table: a bf16 round in FMA mode whose narrow plan needs per-operand weights
-    (the pairs form: centrality weights on a graph whose degrees differ) runs as register-
-    resident groups (K3r, 29.8 vs 33.1 ms on config 5 with degree-centrality weights)."""
+    configs 2-5 (tests/test_host_logic.py::test_default_plan_forms).  One exception, from
+    round 4's measurements: a bf16 round in FMA mode whose narrow plan needs per-operand weights
+    (the pairs form: centrality weights on a graph whose degrees differ) runs the narrow
+    kernel's broadcast form, 16 wavefronts, two workgroups per CU (config 5 with
+    degree-centrality weights: 23.6-24.0 ms against 32.1 for the pairs form and 29.8 for the
+    register-resident K3r, which round 3 picked; profiles/r04).  It keeps the narrow plan's
+    single group, so RoundExecutor still runs it in place."""
     if not bf16:
         cp = build_clique_plan(row_ptr, col, w, out_row)
         if cp is not None:
@@ -743,10 +746,12 @@ def default_plan(row_ptr, col, w, out_row, bf16: bool = False, mode: int = MODE_
             return cp
     p = build_plan(row_ptr, col, w, out_row, dense=0)
     if bf16 and mode == MODE_FMA and p.info.c4 < 64 and not p.info.narrow_roww:
-        rp = build_reg_plan(row_ptr, col, w, out_row)
-        if rp is not None:
-            rp.spec = {"reg": 1}
-            return rp
+        try:
+            bp = build_plan(row_ptr, col, w, out_row, c4=p.info.c4, lds_bytes=LDS_BUDGETS[-1], bcast=16, bcast_wg=2)
+        except _lib.TalError:  # a row past 16 x 8 operands: no broadcast form
+            return p
+        if bp.info.n_groups <= p.info.n_groups:
+            return bp
     return p
 
 
