@@ -11,8 +11,9 @@ kernels for every plan form the tuner can pick, and every output row is hashed:
   config 3  random 8-regular graph, 64 x ResNet-50, M = 9          (the benchmark's round)
   config 4  barbell(60, 8), 128 x ResNet-50, M = 3..61              (K3c clique blocks)
   config 5  SBM 8 x 32, 256 x ViT-B/16, M ~ 17                      (K3n narrow tiles),
-            per entry group: fp32 unweighted (all groups), fp32 degree-centrality softmax
-            (per-operand weights, last group), bf16 EXACT (the reference's bf16 ops, first group)
+            per entry group, every group of every output model (round 4; rounds 1-3 pinned one
+            group of the latter two): fp32 unweighted, fp32 degree-centrality softmax
+            (per-operand weights), bf16 EXACT (the reference's bf16 ops)
 """
 from __future__ import annotations
 
@@ -184,16 +185,18 @@ def test_config5_full_round_vs_reference(cuda, spec):
     _check_c5(cuda, "f32", "unweighted_module_avg", spec)
 
 
-@pytest.mark.parametrize("spec", [None, {"reg": 1}])
+@pytest.mark.parametrize("spec", [None, {"reg": 1}, {"c4": 16, "lds": 163840, "dense": 0, "bcast": 8, "bcwg": 2},
+                                  {"c4": 16, "lds": 163840, "dense": 0, "bcast": 16, "bcwg": 2}])
 def test_config5_degree_centrality_vs_reference(cuda, spec):
     """The per-operand-weight form (centrality_module_avg, degree, softmax coeff 10) of config 5
-    at full width: the last entry group of every output model bitwise the reference's."""
+    at full width: every entry group of every output model bitwise the reference's, through the
+    default (pairs) form, K3r and the broadcast forms."""
     _check_c5(cuda, "f32", "centrality_module_avg", spec)
 
 
 def test_config5_bf16_exact_vs_reference(cuda):
-    """Config 5 on bf16 models (model.to(torch.bfloat16)) in EXACT mode: the first entry group
-    of every output model bitwise the reference's own bf16 arithmetic."""
+    """Config 5 on bf16 models (model.to(torch.bfloat16)) in EXACT mode: every entry group of
+    every output model bitwise the reference's own bf16 arithmetic."""
     _check_c5(cuda, "bf16", "unweighted_module_avg", None)
 
 

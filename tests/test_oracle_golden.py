@@ -275,3 +275,24 @@ def test_cosine_oracle_near_ties(case):
             continue
         out = oracle.agg_f32([ins[j][n].reshape(-1) for j in range(M)], w)
         assert np.array_equal(out.view(np.uint32), NEARZ[f"c{ci}_out_{n}"].reshape(-1).view(np.uint32)), n
+
+
+def test_config5_fixture_pins_every_entry_group():
+    """BASELINE config 5's reference digests (make_golden.py full_c5, round 4): fp32 unweighted,
+    fp32 degree-centrality softmax and bf16 unweighted each cover EVERY entry group of every one
+    of the 256 output models (rounds 1-3 pinned one group of the latter two), and the groups
+    tile the ViT-B/16 segments without gaps."""
+    import json
+
+    fx = json.loads((GOLDEN / "full_round_c5_vit_sbm256.json").read_text())
+    ng = len(fx["groups"])
+    assert ng >= 8 and fx["groups"][0]["start"] == 0
+    for a, b in zip(fx["groups"], fx["groups"][1:]):
+        assert b["start"] == a["end"]
+    kinds = {(r["dtype"], r["fn"]) for r in fx["runs"]}
+    assert kinds == {("f32", "unweighted_module_avg"), ("f32", "centrality_module_avg"), ("bf16", "unweighted_module_avg")}
+    for r in fx["runs"]:
+        assert r["groups"] == list(range(ng)), (r["dtype"], r["fn"])
+        assert len(r["sha256"]) == 256
+        assert all(sorted(int(k) for k in row) == list(range(ng)) and all(len(v) == 64 for v in row.values())
+                   for row in r["sha256"])

@@ -35,30 +35,37 @@ def main():
     ap.add_argument("--allocs", type=int, default=6)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--ballast-gb", type=float, default=0.0, help="allocate (and keep) this much first")
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
+    ap.add_argument("--mode", default="exact", choices=["exact", "fma"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     ballast = torch.empty(int(a.ballast_gb * (1 << 30)), dtype=torch.uint8, device=dev) if a.ballast_gb else None
-    lay = StateLayout.from_layout(synth.get_layout(a.model))
-    n, ld = lay.n_f32, lay.ld_f32
+    lay = synth.get_layout(a.model)
+    bf16 = a.dtype == "bf16"
+    mode = ops.MODE_EXACT if a.mode == "exact" else ops.MODE_FMA
+    lay = StateLayout.from_layout(synth.as_bf16(lay) if bf16 else lay)
+    n, ld = (lay.n_b16, lay.ld_b16) if bf16 else (lay.n_f32, lay.ld_f32)
+    dt = torch.bfloat16 if bf16 else torch.float32
+    run = ops.round_bf16 if bf16 else ops.round_f32
     orders, ws = bench.round_spec(a.devices, 8, kind=a.graph)
     rows = len(orders)
     rp, col, w = csr_from_lists(orders, ws)
-    plan = ops.default_plan(rp, col, w, np.arange(rows, dtype=np.int32)).to(dev)
-    src = torch.randn(rows, ld, device=dev)
+    plan = ops.default_plan(rp, col, w, np.arange(rows, dtype=np.int32), bf16=bf16, mode=mode).to(dev)
+    src = torch.randn(rows, ld, device=dev, dtype=dt)  # in its dtype: no fp32 temporary of the pool's size
     pool_elems = rows * ld
-    arena = torch.empty(a.windows * pool_elems, dtype=torch.float32, device=dev)
+    arena = torch.empty(a.windows * pool_elems, dtype=dt, device=dev)
     targets = [("arena", k, arena[k * pool_elems:(k + 1) * pool_elems].view(rows, ld)) for k in range(a.windows)]
-    targets += [("alloc", k, torch.empty(rows, ld, device=dev)) for k in range(a.allocs)]
+    targets += [("alloc", k, torch.empty(rows, ld, dtype=dt, device=dev)) for k in range(a.allocs)]
     for _, _, t in targets:
         t.zero_()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ops.round_f32(src, targets[0][2], plan, n=n)
+    run(src, targets[0][2], plan, n=n, mode=mode)
     torch.cuda.synchronize()
     ms = [[] for _ in targets]
     for _ in range(a.reps):
         for i, (_, _, t) in enumerate(targets):
             s.record()
-            ops.round_f32(src, t, plan, n=n)
+            run(src, t, plan, n=n, mode=mode)
             e.record()
             e.synchronize()
             ms[i].append(s.elapsed_time(e))
@@ -72,7 +79,8 @@ def main():
         print(json.dumps(rec), flush=True)
     arena_ms = [r["ms"] for r in out if r["kind"] == "arena"]
     alloc_ms = [r["ms"] for r in out if r["kind"] == "alloc"]
-    print(json.dumps(dict(summary=True, model=a.model, rows=rows, pool_gb=round(pool_elems * 4 / 2 ** 30, 2),
+    print(json.dumps(dict(summary=True, model=a.model, dtype=a.dtype, rows=rows,
+                          pool_gb=round(pool_elems * src.element_size() / 2 ** 30, 2),
                           plan=plan.spec, arena_ms=arena_ms, alloc_ms=alloc_ms, ballast_gb=a.ballast_gb,
                           arena_spread=round(max(arena_ms) / min(arena_ms), 3),
                           alloc_spread=round(max(alloc_ms) / min(alloc_ms), 3) if alloc_ms else None)), flush=True)
