@@ -8,5 +8,7 @@ timeout -k 10 400 python tools/window_probe.py $C5 --dtype bf16 --mode fma --win
 tail -1 $OUT/window_c5_bf16.log
 timeout -k 10 300 python tools/window_probe.py --windows 24 --allocs 8 --reps 3 > $OUT/window_map2.log 2>&1 || { echo WMAP FAILED; tail -5 $OUT/window_map2.log; exit 1; }
 tail -1 $OUT/window_map2.log
+timeout -k 10 200 python tools/window_probe.py --step-mb 128 --span-gb 6 --allocs 0 --reps 3 > $OUT/window_slide.log 2>&1 || { echo WSLIDE FAILED; tail -5 $OUT/window_slide.log; exit 1; }
+tail -1 $OUT/window_slide.log | cut -c1-400
 bash profiles/r04/scripts/gpu_pmc.sh r04pmc || exit 1
 echo EXIT 0

@@ -2,62 +2,45 @@
 src/experiments/decentralized_main.py on the CPU.
 
 There is no GPU here, so every aggregation runs the product's host reduction (the library's
-tal_host_agg_*, aggregate.py's no-GPU dispatch).  The recorder only observes: it calls the
-product's aggregate_models straight through and notes what the driver handed it (operands in
-reference order, self last, weights) and the result.  The results are checked bitwise against
-the reference's CPU loop in tests/test_host_backend.py; the same run goes through the HIP
-library in tests/test_gpu_interface.py."""
+tal_host_agg_*, aggregate.py's no-GPU dispatch); nothing in the driver is patched.  Every call's
+operands and output bits are checked against the reference's CPU loop in
+tests/test_host_backend.py::test_config1_driver_unpatched (which observes the calls) and the
+sequential 4-ring fixture; the same run goes through the HIP library in
+tests/test_gpu_interface.py."""
 import numpy as np
 import networkx as nx
 import pytest
 import torch
 
 
-@pytest.fixture()
-def recorder(monkeypatch):
-    import src.decentralized_client as dc
-    from topology_aware_learning_amd import aggregate
+def _run_main(args):
+    from src.experiments import decentralized_main
 
-    assert dc.aggregate_models is aggregate.aggregate_models
-    real = aggregate.aggregate_models
-    calls = []
-
-    def observe(operands, weights, target, mode=aggregate.ops.MODE_EXACT):
-        out = real(operands, weights, target, mode)
-        calls.append(dict(ids=[id(m) for m in operands], target=id(target), weights=list(weights),
-                          out={k: v.detach().clone() for k, v in target.state_dict().items()}))
-        return out
-
-    monkeypatch.setattr(dc, "aggregate_models", observe)
-    return calls
+    return decentralized_main.main(args)
 
 
-def test_config1_one_round(tmp_path, monkeypatch, recorder):
+def test_config1_one_round(tmp_path, monkeypatch):
+    """The driver as shipped: nothing patched (the environment only selects the synthetic
+    CIFAR-10 stand-in, there is no dataset download); the aggregations are the product's."""
     monkeypatch.setenv("TAL_SYNTHETIC_DATA", "1")
     monkeypatch.setenv("TAL_SYNTHETIC_SAMPLES", "64")
     monkeypatch.setenv("TAL_DEVICE_POOL", "0")
     topo = tmp_path / "ring8.txt"
     np.savetxt(topo, nx.to_numpy_array(nx.cycle_graph(8)), fmt="%d")
-    from src.experiments import decentralized_main
-
-    rc = decentralized_main.main(["--dataset", "cifar10", "--aggregation_strategy", "unweighted", "--rounds", "1",
-                                  "--epochs", "1", "--topology_file", str(topo), "--out_dir", str(tmp_path / "logs"),
-                                  "--batch_size", "32"])
+    rc = _run_main(["--dataset", "cifar10", "--aggregation_strategy", "unweighted", "--rounds", "1",
+                    "--epochs", "1", "--topology_file", str(topo), "--out_dir", str(tmp_path / "logs"),
+                    "--batch_size", "32"])
     assert rc == 0
-    assert len(recorder) == 8
-    for c in recorder:
-        assert len(c["ids"]) == 3 and c["ids"][-1] == c["target"]  # self last, aggregated in place
-        assert c["weights"] == [1 / 3] * 3
     ckpts = list((tmp_path / "logs").rglob("0_ckpt.pth"))
     assert len(ckpts) == 1
-    ck = torch.load(ckpts[0], weights_only=False)
+    ck = torch.load(ckpts[0], weights_only=False)  # written by this test's own run
     assert ck["round_idx"] == 0 and len(ck["client_state_dicts"]) == 8
-    outs = sorted((tuple(c["out"]["network.0.bias"][:3].tolist()) for c in recorder))
-    saved = sorted(tuple(sd["network.0.bias"][:3].tolist()) for sd in ck["client_state_dicts"])
-    assert outs == saved
+    biases = [sd["network.0.bias"] for sd in ck["client_state_dicts"]]
+    assert all(torch.isfinite(b).all() for b in biases)
+    assert len({tuple(b.tolist()) for b in biases}) == 8  # every client aggregated its own ring window
 
 
-def test_strategy_dispatch_and_unweighted_fl_topology(tmp_path, monkeypatch, recorder):
+def test_strategy_dispatch_and_unweighted_fl_topology(tmp_path, monkeypatch):
     monkeypatch.setenv("TAL_SYNTHETIC_DATA", "1")
     monkeypatch.setenv("TAL_SYNTHETIC_SAMPLES", "32")
     monkeypatch.setenv("TAL_DEVICE_POOL", "0")
@@ -71,8 +54,10 @@ def test_strategy_dispatch_and_unweighted_fl_topology(tmp_path, monkeypatch, rec
                             aggregation_strategy="unweighted_fl", log_dir=str(tmp_path / "l"), train=False)
     assert app.aggregation_function is unweighted_module_avg
     assert np.array_equal(app.topology, np.ones((4, 4)) - np.eye(4))
-    app.run()
-    assert len(recorder) == 4 and all(len(c["ids"]) == 4 for c in recorder)
+    before = [{k: v.clone() for k, v in c.model.state_dict().items()} for c in app.clients]
+    assert app.run() == 0
+    after = [c.model.state_dict() for c in app.clients]
+    assert all(not torch.equal(a["network.0.bias"], b["network.0.bias"]) for a, b in zip(after, before))
 
 
 def test_parsl_standin_dependencies():

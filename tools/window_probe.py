@@ -8,7 +8,11 @@ One input pool (config 3: 64 x ResNet-50, its own allocation), then
 Every target is timed `reps` times, interleaved over targets, median kept.  One JSON line per
 target and a summary line.
 
+With --step-mb the arena is one pool plus --span-gb and the windows slide by --step-mb inside
+it (sub-pool offsets: is the fast / slow boundary finer than a pool?).
+
 Usage: python tools/window_probe.py [--model resnet50] [--windows 12] [--allocs 6] [--reps 3]
+       python tools/window_probe.py --step-mb 128 --span-gb 4
 """
 import argparse
 import json
@@ -37,6 +41,8 @@ def main():
     ap.add_argument("--ballast-gb", type=float, default=0.0, help="allocate (and keep) this much first")
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     ap.add_argument("--mode", default="exact", choices=["exact", "fma"])
+    ap.add_argument("--step-mb", type=int, default=0, help="slide windows by this much (0: back to back)")
+    ap.add_argument("--span-gb", type=float, default=4.0, help="with --step-mb: arena = pool + span")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     ballast = torch.empty(int(a.ballast_gb * (1 << 30)), dtype=torch.uint8, device=dev) if a.ballast_gb else None
@@ -53,8 +59,15 @@ def main():
     plan = ops.default_plan(rp, col, w, np.arange(rows, dtype=np.int32), bf16=bf16, mode=mode).to(dev)
     src = torch.randn(rows, ld, device=dev, dtype=dt)  # in its dtype: no fp32 temporary of the pool's size
     pool_elems = rows * ld
-    arena = torch.empty(a.windows * pool_elems, dtype=dt, device=dev)
-    targets = [("arena", k, arena[k * pool_elems:(k + 1) * pool_elems].view(rows, ld)) for k in range(a.windows)]
+    if a.step_mb:
+        step = a.step_mb * (1 << 20) // src.element_size()
+        span = int(a.span_gb * (1 << 30)) // src.element_size() // step * step
+        arena = torch.empty(pool_elems + span, dtype=dt, device=dev)
+        offs = range(0, span + 1, step)
+    else:
+        arena = torch.empty(a.windows * pool_elems, dtype=dt, device=dev)
+        offs = range(0, a.windows * pool_elems, pool_elems)
+    targets = [("arena", k, arena[o:o + pool_elems].view(rows, ld)) for k, o in enumerate(offs)]
     targets += [("alloc", k, torch.empty(rows, ld, dtype=dt, device=dev)) for k in range(a.allocs)]
     for _, _, t in targets:
         t.zero_()
@@ -73,7 +86,7 @@ def main():
     out = []
     for (kind, k, t), m in zip(targets, ms):
         rec = dict(kind=kind, index=k, ms=round(float(np.median(m)), 4), all_ms=[round(x, 4) for x in m],
-                   offset_gb=round((t.data_ptr() - base) / 2 ** 30, 2) if kind == "arena" else None,
+                   offset_gb=round((t.data_ptr() - base) / 2 ** 30, 3) if kind == "arena" else None,
                    ptr=hex(t.data_ptr()))
         out.append(rec)
         print(json.dumps(rec), flush=True)
@@ -81,7 +94,7 @@ def main():
     alloc_ms = [r["ms"] for r in out if r["kind"] == "alloc"]
     print(json.dumps(dict(summary=True, model=a.model, dtype=a.dtype, rows=rows,
                           pool_gb=round(pool_elems * src.element_size() / 2 ** 30, 2),
-                          plan=plan.spec, arena_ms=arena_ms, alloc_ms=alloc_ms, ballast_gb=a.ballast_gb,
+                          plan=plan.spec, step_mb=a.step_mb, arena_ms=arena_ms, alloc_ms=alloc_ms, ballast_gb=a.ballast_gb,
                           arena_spread=round(max(arena_ms) / min(arena_ms), 3),
                           alloc_spread=round(max(alloc_ms) / min(alloc_ms), 3) if alloc_ms else None)), flush=True)
     del ballast
