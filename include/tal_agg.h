@@ -293,12 +293,15 @@ int32_t tal_agg_round_reg(const void* pool_in, int64_t ld_in, void* pool_out, in
  * order of the torch CPU kernels it runs on (vector_norm, the cascade sum, sum / numel; see
  * oracle/cosine_oracle.c, pinned bitwise by the reference's own values, near-ties included):
  * the result is the reference's fp32 value, so sim_centrality_module_avg's least-similar
- * neighbor (:511-516) is the reference's.  Tensors whose A*B exceeds 32768 are reduced in
- * torch's serial order (torch's own order there depends on its thread count).
+ * neighbor (:511-516) is the reference's.  A tensor's mean over A*B >= 32768 outputs is, in
+ * torch, a two-pass parallel sum whose order depends on the process's intra-op thread count T
+ * (at::parallel_for chunks of ceil(n / min(T, ceil(n / 32768))) elements, then a T-entry
+ * buffer summed); the plan carries T (tal_cosine_plan_set_threads, default 1 = serial), so the
+ * result is torch's for that T.
  *
  * seg_host: 4*n_seg int64 {offset (elements into the flat parameter arena), A, I, B}.
  * The plan (int64 words, tal_cosine_plan_words; copied to the device by the caller, and the
- * host copy passed too) = {n_seg, n_outputs}, per tensor {offset, A, I, B, first output,
+ * host copy passed too) = {n_seg, n_outputs, threads}, per tensor {offset, A, I, B, first output,
  * kind}, per workgroup chunk {tensor, first output, count, 0}.
  *
  * a_ptrs_host / b_ptrs_host: n_pairs device pointers; pair j compares model a_j with b_j
@@ -307,6 +310,8 @@ int32_t tal_agg_round_reg(const void* pool_in, int64_t ld_in, void* pool_out, in
 int64_t tal_cosine_plan_words(const int64_t* seg_host, int32_t n_seg);
 int32_t tal_cosine_plan_build(const int64_t* seg_host, int32_t n_seg, int64_t* plan_host,
                               int64_t plan_capacity_words, int32_t* n_chunks);
+/* Set a built plan's thread word (1..1024; the calling process's torch.get_num_threads()). */
+int32_t tal_cosine_plan_set_threads(int64_t* plan_host, int32_t threads);
 int64_t tal_cosine_scratch_bytes(const int64_t* plan_host, int32_t n_pairs);
 int32_t tal_cosine_params(const float* const* a_ptrs_host, const float* const* b_ptrs_host,
                           int32_t n_pairs, const int64_t* plan_dev, const int64_t* plan_host,

@@ -59,6 +59,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_cosine_scratch.restype = ctypes.c_int64
         L.oracle_cosine_model.argtypes = [P, P, P, ctypes.c_int32, P, P]
         L.oracle_cosine_model.restype = ctypes.c_float
+        L.oracle_cosine_model_t.argtypes = [P, P, P, ctypes.c_int32, ctypes.c_int32, P, P]
+        L.oracle_cosine_model_t.restype = ctypes.c_float
         L.oracle_cosine_outputs.argtypes = [P, P, P, ctypes.c_int32, P, P, P]
         _lib = L
     return _lib
@@ -152,18 +154,20 @@ def round_bf16(pool_in, row_ptr, col, w, out_row, pool_out=None, exact: bool = T
     return pool_out
 
 
-def cosine_model(a, b, segments, per_tensor: bool = False):
+def cosine_model(a, b, segments, per_tensor: bool = False, threads: int = 1):
     """The reference's cosine_similarity(model_1, model_2) of two flat fp32 parameter rows,
     bit for bit (torch's CPU reduction order; cosine_oracle.c).  segments: (offset, A, I, B)
-    per parameter in named_parameters order (arena.StateLayout.param_segments)."""
+    per parameter in named_parameters order (arena.StateLayout.param_segments).  threads: the
+    torch intra-op thread count of the reference's process (matters for tensor means over
+    >= 32768 outputs only)."""
     a = np.ascontiguousarray(a, dtype=np.float32)
     b = np.ascontiguousarray(b, dtype=np.float32)
     seg = np.ascontiguousarray(np.asarray(segments, dtype=np.int64).reshape(-1, 4))
     L = lib()
     scratch = np.empty(max(1, L.oracle_cosine_scratch(seg.ctypes.data, len(seg))), np.float32)
     per = np.empty(len(seg), np.float32)
-    v = L.oracle_cosine_model(a.ctypes.data, b.ctypes.data, seg.ctypes.data, len(seg), scratch.ctypes.data,
-                              per.ctypes.data)
+    v = L.oracle_cosine_model_t(a.ctypes.data, b.ctypes.data, seg.ctypes.data, len(seg), int(threads),
+                                scratch.ctypes.data, per.ctypes.data)
     v = np.float32(v)
     return (v, per) if per_tensor else v
 

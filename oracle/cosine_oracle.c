@@ -28,8 +28,14 @@
  *     contiguous reduction of n >= 8 runs it on 8-wide vectors (lane l sums elements
  *     8 i + l), then the scalar tail, then lanes 0..7; a strided one runs it per column
  *     (columns in chunks of 32 share one 4-row cascade, then chunks of 8, then single columns).
- * Reductions over more than 32768 elements run in parallel in torch (thread-count dependent
- * order); the reference's models never reach that (largest: 4608 outputs per tensor).
+ *   a full sum over n >= 32768 elements (at::internal::GRAIN_SIZE) with T > 1 intra-op threads
+ *     is torch's two_pass_reduction (TensorIteratorReduce.cpp) over at::parallel_for: nt =
+ *     min(T, ceil(n / 32768)) chunks of ceil(n / nt) elements, each chunk's serial sum stored
+ *     into a T-entry buffer of zeros, then the buffer's serial sum (par_sum; pinned against the
+ *     reference's cosine_similarity at T = 1..32 by tests/golden/cosine_threads.json).  The
+ *     per-output norms and sums split over outputs and do not depend on T.  The reference's
+ *     CNNs never reach 32768 outputs per tensor (largest 4608); ViT-B/16's patch embedding has
+ *     196,608.
  *
  * Built with gcc -O2 -ffp-contract=off: every float op rounds to fp32; fmaf is the single
  * rounding fused multiply-add.
@@ -112,6 +118,21 @@ static float inner_sum(const float* x, int64_t n) {
   return 0.f + fin;
 }
 
+/* torch's full sum with T intra-op threads (serial below the grain or at T == 1) */
+#define GRAIN 32768
+#define MAX_THREADS 1024
+static float par_sum(const float* x, int64_t n, int T) {
+  if (n < GRAIN || T <= 1) return inner_sum(x, n);
+  float buf[MAX_THREADS];
+  memset(buf, 0, sizeof(buf));
+  int64_t nt = (n + GRAIN - 1) / GRAIN;
+  if (nt > T) nt = T;
+  const int64_t chunk = (n + nt - 1) / nt;
+  for (int64_t t = 0; t < nt && t * chunk < n; ++t)
+    buf[t] = inner_sum(x + t * chunk, n - t * chunk < chunk ? n - t * chunk : chunk);
+  return inner_sum(buf, T);
+}
+
 typedef struct {
   const float* p;  /* p[i * K + c] */
   int64_t K;
@@ -164,7 +185,7 @@ static float norm_lastdim(const float* x, int64_t I) {
 
 /* mean over the O*K outputs of cos(x1, x2) along dim 1 for one parameter tensor viewed
  * [O, I, K]; scratch: 3 * O * K + I * K floats */
-static float cos_tensor(const float* a, const float* b, int64_t O, int64_t I, int64_t K, float* scratch) {
+static float cos_tensor(const float* a, const float* b, int64_t O, int64_t I, int64_t K, int T, float* scratch) {
   const float eps = 1e-6f;
   float* s = scratch;            /* [O * K] */
   float* n1 = s + O * K;         /* [K] */
@@ -199,7 +220,7 @@ static float cos_tensor(const float* a, const float* b, int64_t O, int64_t I, in
       outer_sum(prod, I, K, s + o * K);
     }
   }
-  return inner_sum(s, O * K) / (float)(O * K);
+  return par_sum(s, O * K, T) / (float)(O * K);
 }
 
 /* cosine_similarity(model_1, model_2) of the reference: segs = (offset, A, I, B) per parameter
@@ -215,16 +236,22 @@ int64_t oracle_cosine_scratch(const int64_t* segs, int32_t nseg) {
   return m;
 }
 
-float oracle_cosine_model(const float* a, const float* b, const int64_t* segs, int32_t nseg, float* scratch,
-                          float* per_tensor) {
+/* threads: torch's intra-op thread count of the reference's process (1..1024) */
+float oracle_cosine_model_t(const float* a, const float* b, const int64_t* segs, int32_t nseg, int32_t threads,
+                            float* scratch, float* per_tensor) {
   float avg = 0.f;
   for (int32_t t = 0; t < nseg; ++t) {
     const int64_t off = segs[4 * t], O = segs[4 * t + 1], I = segs[4 * t + 2], K = segs[4 * t + 3];
-    const float m = cos_tensor(a + off, b + off, O, I, K, scratch);
+    const float m = cos_tensor(a + off, b + off, O, I, K, threads, scratch);
     if (per_tensor) per_tensor[t] = m;
     avg = t == 0 ? 0.f + m : avg + m;  /* python 0 + tensor, then in-place += */
   }
   return avg / (float)nseg;
+}
+
+float oracle_cosine_model(const float* a, const float* b, const int64_t* segs, int32_t nseg, float* scratch,
+                          float* per_tensor) {
+  return oracle_cosine_model_t(a, b, segs, nseg, 1, scratch, per_tensor);
 }
 
 /* Debug view: every tensor's per-output values s (concatenated, tensor order) and means. */
@@ -233,7 +260,7 @@ void oracle_cosine_outputs(const float* a, const float* b, const int64_t* segs, 
   int64_t pos = 0;
   for (int32_t t = 0; t < nseg; ++t) {
     const int64_t off = segs[4 * t], O = segs[4 * t + 1], I = segs[4 * t + 2], K = segs[4 * t + 3];
-    means[t] = cos_tensor(a + off, b + off, O, I, K, scratch);
+    means[t] = cos_tensor(a + off, b + off, O, I, K, 1, scratch);
     memcpy(s_out + pos, scratch, sizeof(float) * O * K);
     pos += O * K;
   }

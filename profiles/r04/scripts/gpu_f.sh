@@ -16,6 +16,8 @@ run() {  # tag, extra args (lib env optional via LIBP)
   TAL_LIB_PATH=$LIBP timeout -k 10 300 python bench.py $C5 "$@" > $OUT/$tag.log 2>&1 || { echo "BENCH FAILED $tag"; tail -20 $OUT/$tag.log; exit 1; }
   summ $OUT/$tag.log $tag
 }
+timeout -k 10 300 python -u -m pytest tests/test_cosine_threads.py tests/test_gpu_kernels.py -k cosine -x -q --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { echo TESTS FAILED; tail -30 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
 PAIRS='{"c4":16,"lds":163840,"dense":0}'
 LIBP=
 for dt in f32 bf16; do

@@ -21,3 +21,16 @@ class Vec(nn.Module):
     def __init__(self, m):
         super().__init__()
         self.v = nn.Parameter(torch.zeros(m))
+
+
+def cos_pair_state(layout, sa, sb, entries, mix):
+    """Two seeded synthetic state_dicts (topology_aware_learning_amd.synth); with `mix`, the
+    second is a + mix * b (fp32, a multiply then an add: a neighbor close to the first, as
+    trained neighbors are).  tests/golden/cosine_threads.json's inputs."""
+    from topology_aware_learning_amd import synth
+
+    a = synth.synth_state_dict(layout, sa, entries=entries)
+    b = synth.synth_state_dict(layout, sb, entries=entries)
+    if mix:
+        b = type(b)((k, a[k] + b[k] * mix) for k in b)
+    return a, b

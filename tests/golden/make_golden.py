@@ -24,6 +24,9 @@ Outputs (all data, no reference source):
   full_round_c5_vit_sbm256.json      BASELINE config 5 (SBM-256, ViT-B/16) at full size per entry
                                      group: fp32 unweighted, fp32 degree-centrality softmax and
                                      bf16 unweighted, every group (round 4; one group before)
+  cosine_threads.json                cosine_similarity on ViT-B/16 parameters (the patch
+                                     embedding's 196,608 outputs: torch's two-pass parallel mean)
+                                     at torch intra-op thread counts 1..64
 
 Usage:  python tests/golden/make_golden.py [generator ...]   (default: all)
 """
@@ -79,7 +82,7 @@ from topology_aware_learning_amd import synth  # noqa: E402
 
 
 sys.path.insert(0, str(HERE.parent))
-from _models import TinyNet, Vec  # noqa: E402
+from _models import TinyNet, Vec, cos_pair_state  # noqa: E402
 
 
 DUMMY = TensorDataset(torch.zeros(4, 1), torch.zeros(4, dtype=torch.long))
@@ -482,6 +485,50 @@ def gen_c5_round(dc, out):
                                    runs=results), indent=1))
 
 
+def _param_holder(sd):
+    """An nn.Module whose named_parameters are `sd`'s tensors in order (cosine_similarity reads
+    named_parameters, decentralized_client.py:670-671)."""
+    m = nn.Module()
+    for k, v in enumerate(sd.values()):
+        m.register_parameter(f"p{k}", nn.Parameter(v.clone(), requires_grad=False))
+    return m
+
+
+COS_THREADS = (1, 2, 3, 4, 5, 6, 7, 8, 12, 16, 32, 64)
+
+
+def gen_cosine_threads(dc, out):
+    """The reference's cosine_similarity over ViT-B/16 parameters (synthetic seeded values) at
+    several torch intra-op thread counts: a tensor mean over >= 32768 outputs (conv_proj.weight,
+    768 x 16 x 16 = 196,608 outputs) is torch's two-pass parallel sum, whose order depends on
+    the thread count.  Cases: the patch embedding alone (its mean is the result), independent
+    and close pairs; the first 16 entries (class token, patch embedding, position embedding,
+    encoder layer 0), close pairs; at every count in COS_THREADS; and the whole model, one close
+    pair, at 1, 8 and 16 threads."""
+    layout = synth.vit_b16_layout()
+    saved = torch.get_num_threads()
+    cases = []
+    specs = [([1], (9600, 9601), None, COS_THREADS), ([1], (9602, 9603), None, COS_THREADS),
+             ([1], (9600, 9601), 0.05, COS_THREADS), ([1], (9604, 9605), 0.01, COS_THREADS),
+             (list(range(16)), (9600, 9601), 0.05, COS_THREADS), (list(range(16)), (9606, 9607), 0.3, COS_THREADS),
+             (None, (9608, 9609), 0.05, (1, 8, 16))]
+    for entries, (sa, sb), mix, threads in specs:
+        a, b = cos_pair_state(layout, sa, sb, entries, mix)
+        ma, mb = _param_holder(a), _param_holder(b)
+        vals = {}
+        for t in threads:
+            torch.set_num_threads(t)
+            v = np.float32(dc.cosine_similarity(ma, mb).item())
+            vals[str(t)] = int(v.view(np.uint32))
+        cases.append(dict(entries=entries, seed_a=sa, seed_b=sb, mix=mix, bits=vals))
+        print("cosine threads", entries if entries is None or len(entries) < 3 else len(entries), sa, sb, mix,
+              len(set(vals.values())), "distinct of", len(vals), flush=True)
+    torch.set_num_threads(saved)
+    out.write_text(json.dumps(dict(model="vit_b16 (synthetic torchvision layout)", fn="cosine_similarity",
+                                   torch=torch.__version__, parallel=torch.__config__.parallel_info().splitlines()[:4],
+                                   cases=cases), indent=1))
+
+
 def gen_weights(dc, out_w, out_c):
     graphs = {
         "cycle_graph(8)": nx.cycle_graph(8),
@@ -649,7 +696,7 @@ def gen_bf16(dc, out_json, out_npz):
 
 
 GENERATORS = ("layouts", "tiny", "weights", "schedulers", "round", "big", "gossip", "bf16", "big_round", "near_ties",
-              "full_c3", "full_c4", "full_c5")
+              "full_c3", "full_c4", "full_c5", "cosine_threads")
 
 
 def main(which=GENERATORS):
@@ -680,6 +727,8 @@ def main(which=GENERATORS):
         gen_full_round(dc, resnet, "c4", HERE / "full_round_c4_resnet50_barbell.json")
     if "full_c5" in which:
         gen_c5_round(dc, HERE / "full_round_c5_vit_sbm256.json")
+    if "cosine_threads" in which:
+        gen_cosine_threads(dc, HERE / "cosine_threads.json")
 
 
 if __name__ == "__main__":

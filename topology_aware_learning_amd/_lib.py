@@ -27,7 +27,7 @@ TAL_ERR_COMM = 4
 TAL_COMM_ID_BYTES = 128
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 EXPORTED = (
     "tal_last_error",
@@ -47,6 +47,7 @@ EXPORTED = (
     "tal_agg_round_reg",
     "tal_cosine_plan_words",
     "tal_cosine_plan_build",
+    "tal_cosine_plan_set_threads",
     "tal_cosine_scratch_bytes",
     "tal_cosine_params",
     "tal_prox_plan_words",
@@ -153,6 +154,7 @@ _SIGS = {
     "tal_agg_round_reg": (_I32, [_P, _I64, _P, _I64, _I64, _I32, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P]),
     "tal_cosine_plan_words": (_I64, [_PI64, _I32]),
     "tal_cosine_plan_build": (_I32, [_PI64, _I32, _PI64, _I64, _PI32]),
+    "tal_cosine_plan_set_threads": (_I32, [_PI64, _I32]),
     "tal_cosine_scratch_bytes": (_I64, [_PI64, _I32]),
     "tal_cosine_params": (_I32, [_PP, _PP, _I32, _P, _PI64, _I32, _P, _P, _P]),
     "tal_prox_plan_words": (_I64, [_PI64, _I32]),

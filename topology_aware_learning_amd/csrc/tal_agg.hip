@@ -45,7 +45,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 18;
+constexpr int kAbiVersion = 19;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -1335,6 +1335,9 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   int64_t t = blockIdx.x;
   if (t < n_tiles) load_tile(t);
   for (; t < n_tiles; t += gridDim.x) {
+#ifdef TAL_PROBE_NOPREFETCH  // A/B probe: each tile's loads issued after the previous tile's math
+    if (t != blockIdx.x) load_tile(t);
+#endif
     __syncthreads();  // the previous tile's readers are done with s_data
     // staging units (float4 slots; W16: slot pairs) of real sources (readfirstlane: the broadcast
     // form's control flow otherwise leaves the compiler unsure that ns is uniform here)
@@ -1352,7 +1355,9 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
       }
     }
     __syncthreads();
+#ifndef TAL_PROBE_NOPREFETCH
     if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
+#endif
     const int64_t col = t * C4 + cl;
     if constexpr (BC) {
       // the records are loop-invariant: without this the compiler hoists every broadcast and
@@ -2758,7 +2763,9 @@ int32_t launch_round_vec(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, i
 // kernels.  All arithmetic is single-rounding fp32 (__f*_rn), in torch's order.
 // ------------------------------------------------------------------------------------------
 constexpr int kCosMaxPairs = 32;
-constexpr int kCosHdr = 2;         // plan words: {n_seg, n_out}
+constexpr int kCosHdr = 3;         // plan words: {n_seg, n_out, torch intra-op threads}
+constexpr int kCosMaxThreads = 1024;
+constexpr int64_t kCosGrain = 32768;  // at::internal::GRAIN_SIZE
 constexpr int kCosSegWords = 6;    // {offset, A, I, B, out_offset, kind}
 constexpr int kCosChunkWords = 4;  // {seg, first output, count, 0}
 constexpr int kCosBlock = 256;
@@ -2945,25 +2952,49 @@ __global__ __launch_bounds__(kCosBlock) void k_cosine_outputs(CosPairs pr, const
   if (l == 0 && live) s[q] = __fadd_rn(0.f, fin);
 }
 
-// per (tensor, pair): mean = inner_sum(s) / numel (torch sum then div_); 8 threads = the lanes
+// torch's serial full sum of s[0 .. n) (scalar_inner_sum below 8 elements, else
+// vectorized_inner_sum: lane l sums elements 8 i + l by row_sum, then the scalar tail, then the
+// lanes in order), without the store's 0 +; valid in thread 0, every thread of the wave calls it
+__device__ __forceinline__ float cos_inner_sum(const float* s, int64_t n, int l) {
+  if (n < kCosVw) return l == 0 ? cos_row_sum([&](int64_t i) { return s[i]; }, n) : 0.f;
+  const int64_t nv = n / kCosVw;
+  const float lane_sum = l < kCosVw ? cos_row_sum([&](int64_t i) { return s[i * kCosVw + l]; }, nv) : 0.f;
+  float tail = 0.f;
+  if (l == 0)
+    for (int64_t k = nv * kCosVw; k < n; ++k) tail = __fadd_rn(tail, s[k]);
+  return cos_group_fold(tail, lane_sum, 0);
+}
+
+// per (tensor, pair): mean = sum(s) / numel (torch sum then div_); 8 threads = the lanes.
+// A sum over >= 32768 elements (at::internal::GRAIN_SIZE) in a process with T > 1 intra-op
+// threads is torch's two-pass reduction (TensorIteratorReduce.cpp two_pass_reduction over
+// at::parallel_for): nt = min(T, ceil(n / 32768)) chunks of ceil(n / nt) elements, chunk t's
+// serial sum stored into a T-entry buffer of zeros (0 + sum), then the buffer's serial sum.
+// T is the plan's thread word (tal_cosine_plan_set_threads; the caller's torch thread count).
 __global__ void k_cosine_means(const int64_t* __restrict__ plan, int n_seg, const float* __restrict__ s_all,
                                float* __restrict__ means) {
+  __shared__ float part[kCosMaxThreads];
   const int seg = blockIdx.x, pair = blockIdx.y;
   const int64_t n_out = plan[1];
+  const int64_t T = plan[2];
   const int64_t* sg = plan + kCosHdr + kCosSegWords * static_cast<int64_t>(seg);
   const int64_t n = sg[1] * sg[3];
   const float* s = s_all + static_cast<int64_t>(pair) * n_out + sg[4];
   const int l = threadIdx.x & 63;
   float fin;
-  if (n < kCosVw) {
-    fin = l == 0 ? cos_row_sum([&](int64_t i) { return s[i]; }, n) : 0.f;
+  if (n < kCosGrain || T <= 1) {
+    fin = cos_inner_sum(s, n, l);
   } else {
-    const int64_t nv = n / kCosVw;
-    const float lane_sum = l < kCosVw ? cos_row_sum([&](int64_t i) { return s[i * kCosVw + l]; }, nv) : 0.f;
-    float tail = 0.f;
-    if (l == 0)
-      for (int64_t k = nv * kCosVw; k < n; ++k) tail = __fadd_rn(tail, s[k]);
-    fin = cos_group_fold(tail, lane_sum, 0);
+    for (int64_t k = l; k < T; k += 64) part[k] = 0.f;
+    __syncthreads();
+    const int64_t nt = min(T, (n + kCosGrain - 1) / kCosGrain);
+    const int64_t chunk = (n + nt - 1) / nt;
+    for (int64_t t = 0; t < nt && t * chunk < n; ++t) {
+      const float c = cos_inner_sum(s + t * chunk, min(chunk, n - t * chunk), l);
+      if (l == 0) part[t] = __fadd_rn(0.f, c);
+    }
+    __syncthreads();
+    fin = cos_inner_sum(part, T, l);
   }
   if (l == 0) means[static_cast<int64_t>(pair) * n_seg + seg] = __fdiv_rn(__fadd_rn(0.f, fin), static_cast<float>(n));
 }
@@ -4055,7 +4086,18 @@ int32_t tal_cosine_plan_build(const int64_t* seg_host, int32_t n_seg, int64_t* p
   if (c > 0x7fffffff) return fail(TAL_ERR_INVALID, "tal_cosine_plan_build: too many chunks");
   plan_host[0] = n_seg;
   plan_host[1] = out;
+  plan_host[2] = 1;  // serial sums until tal_cosine_plan_set_threads says otherwise
   *n_chunks = static_cast<int32_t>(c);
+  g_err.clear();
+  return TAL_OK;
+}
+
+int32_t tal_cosine_plan_set_threads(int64_t* plan_host, int32_t threads) {
+  if (!plan_host || plan_host[0] <= 0 || plan_host[1] <= 0)
+    return fail(TAL_ERR_INVALID, "tal_cosine_plan_set_threads: not a built plan");
+  if (threads < 1 || threads > kCosMaxThreads)
+    return fail(TAL_ERR_INVALID, "tal_cosine_plan_set_threads: threads must be 1..1024");
+  plan_host[2] = threads;
   g_err.clear();
   return TAL_OK;
 }

@@ -892,10 +892,13 @@ class CosinePlan:
     n_chunks: int
     host: np.ndarray
     device: Optional[torch.Tensor] = None
+    threads: int = 1
 
 
-def build_cosine_plan(segments: Sequence[Sequence[int]]) -> CosinePlan:
-    """segments: (offset, A, I, B) per parameter tensor (see tal_agg.h K2)."""
+def build_cosine_plan(segments: Sequence[Sequence[int]], threads: int = 1) -> CosinePlan:
+    """segments: (offset, A, I, B) per parameter tensor (see tal_agg.h K2).  threads: the torch
+    intra-op thread count whose reduction order a tensor mean over >= 32768 outputs follows
+    (the reference's process's torch.get_num_threads(); 1 = torch's serial order)."""
     seg = np.ascontiguousarray(np.asarray(segments, dtype=np.int64).reshape(-1, 4))
     L = _lib.load()
     P64 = ctypes.POINTER(ctypes.c_int64)
@@ -906,7 +909,8 @@ def build_cosine_plan(segments: Sequence[Sequence[int]]) -> CosinePlan:
     nch = ctypes.c_int32()
     check(L.tal_cosine_plan_build(seg.ctypes.data_as(P64), len(seg), blob.ctypes.data_as(P64), words,
                                   ctypes.byref(nch)))
-    return CosinePlan(n_seg=len(seg), n_chunks=nch.value, host=blob)
+    check(L.tal_cosine_plan_set_threads(blob.ctypes.data_as(P64), int(threads)))
+    return CosinePlan(n_seg=len(seg), n_chunks=nch.value, host=blob, threads=int(threads))
 
 
 def cosine(a_list: Sequence[torch.Tensor], b_list: Sequence[torch.Tensor], plan: CosinePlan,

@@ -6,7 +6,9 @@ trailing unit dim), mean per tensor, average over tensors.  K2 performs the refe
 operations in the order of the torch CPU kernels it runs on (include/tal_agg.h), so the
 values are the reference's bit for bit and sim_centrality_module_avg's arg-min (:511) —
 near-ties and exact fp32 ties included — picks the reference's neighbor
-(tests/golden/near_ties.*).
+(tests/golden/near_ties.*).  A tensor mean over >= 32768 outputs (ViT-B/16's patch embedding,
+196,608) is a two-pass parallel sum in torch whose order depends on the intra-op thread count;
+K2 follows torch.get_num_threads() of the calling process (tests/golden/cosine_threads.json).
 """
 from __future__ import annotations
 
@@ -48,10 +50,13 @@ def cosine_pairs(model: nn.Module, others: Sequence[nn.Module]) -> List[float]:
         return []
     layout = layout_of_module(model)
     names = _param_names(model)
-    key = (layout.key, tuple(names))
+    # a tensor mean over >= 32768 outputs follows torch's parallel order for this process's
+    # intra-op thread count, as the reference's own call would (tal_agg.h K2)
+    threads = torch.get_num_threads()
+    key = (layout.key, tuple(names), threads)
     plan = _plans.get(key)
     if plan is None:
-        plan = ops.build_cosine_plan(layout.param_segments(names))
+        plan = ops.build_cosine_plan(layout.param_segments(names), threads=threads)
         _plans[key] = plan
     device = _device_for([model, *others])
     flats = _flat([model, *others], layout, device)
