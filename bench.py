@@ -335,8 +335,13 @@ def main():
         elif trials > 2:
             it = iter(cand)
             pin, pout, placement = select_pool_pair(lambda: next(it), placement_score, trials)
-        else:
-            (pin, pout), placement = cand, None
+        else:  # no room for more candidates (config 5 fp32: 88.6 GB pools): the pair as allocated
+            (pin, pout) = cand
+            ab, ba = min(placement_score(pin, pout), placement_score(pin, pout)), min(placement_score(pout, pin), placement_score(pout, pin))
+            placement = dict(pools=2, dest_ms=[round(ba, 3), round(ab, 3)], chosen=[0, 1],
+                             pair_ms={"0->1": round(ab, 3), "1->0": round(ba, 3)},
+                             first_pair_ms=round((ab + ba) / 2, 3), chosen_pair_ms=round((ab + ba) / 2, 3),
+                             note="two pools fit in 70 % of the free HBM: no other candidate to time")
         del cand
         torch.cuda.empty_cache()  # the candidates not kept
         fill_pool(pin, 1234)

@@ -1024,6 +1024,32 @@ __device__ __forceinline__ float4 narrow_row_roww(uint4 rc, uint32_t base) {
   return narrow_row_tail<T, EXACT>(acc, w, e, base, rem);
 }
 
+// one 16-B-per-lane global->LDS DMA: 64 lanes x 16 B, lane-linear from LDS byte address M0
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_byte_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_byte_addr)
+      : "memory");
+}
+
+// s_waitcnt vmcnt(n) lgkmcnt(0) + s_barrier, n wave-uniform (clamped: waiting longer is safe)
+__device__ __forceinline__ void wait_vm_barrier(int n) {
+#define TAL_WB(k) case k: asm volatile("s_waitcnt vmcnt(" #k ") lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+  switch (n < 0 ? 0 : (n > 31 ? 31 : n)) {
+    TAL_WB(0) TAL_WB(1) TAL_WB(2) TAL_WB(3) TAL_WB(4) TAL_WB(5) TAL_WB(6) TAL_WB(7)
+    TAL_WB(8) TAL_WB(9) TAL_WB(10) TAL_WB(11) TAL_WB(12) TAL_WB(13) TAL_WB(14) TAL_WB(15)
+    TAL_WB(16) TAL_WB(17) TAL_WB(18) TAL_WB(19) TAL_WB(20) TAL_WB(21) TAL_WB(22) TAL_WB(23)
+    TAL_WB(24) TAL_WB(25) TAL_WB(26) TAL_WB(27) TAL_WB(28) TAL_WB(29) TAL_WB(30) TAL_WB(31)
+  }
+#undef TAL_WB
+}
+
 // ---- broadcast form (narrow_bcast, tal_round_plan_build_bcast) ---------------------------
 // A wavefront's plan is a program of records held in VGPRs for the whole launch: record lane L
 // = {LDS byte offset, fp32 weight bits} of operand 16c + L % 16 of row L / C4 of a pass.  Operand
@@ -1238,14 +1264,19 @@ __device__ __forceinline__ int narrow_set(int p, int wave, int nwaves) {
 // adjacent fp32 float4.  Needs an even chunk count, a row stride of an even number of chunks and
 // a 16-B aligned base (the launcher checks), so every pair lies inside its row.
 // BC: the broadcast form (narrow_bcast plans; NT = 64 x the plan's waves per workgroup).
+// DMA (fp32 broadcast form): staging by global->LDS DMA into the tile (no staging registers, so
+// the 1024-thread fp32 EXACT form fits 64 VGPRs without spills); the tile is single-buffered, so
+// a tile's loads are issued after the previous tile's readers are done (the other resident
+// workgroup of the CU computes meanwhile).
 template <int C4, int NT, int J, int NP, bool EXACT, typename T = float, bool ROWW = false, bool W16 = false,
-          bool BC = false>
+          bool BC = false, bool DMA = false>
 __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round_f32_narrow(
     const T* __restrict__ pin, int64_t ld_in4, T* __restrict__ pout, int64_t ld_out4, int64_t n4,
     PlanView p, int64_t n_tiles) {
   static_assert(C4 == 16 || C4 == 32, "narrow tiles are 16 or 32 float4 wide");
   static_assert(NT % C4 == 0, "a block stages whole source tiles");
   static_assert(!W16 || (kIsBf16<T> && J % 2 == 0), "16-B staging lanes: bf16 pools, even J");
+  static_assert(!DMA || (BC && !kIsBf16<T> && !W16), "DMA staging: fp32 broadcast form");
   constexpr int kLd = W16 ? J / 2 : J;       // staging loads per lane
   constexpr int kLps = W16 ? C4 / 2 : C4;    // staging lanes per source and tile
   constexpr int kRpw = 64 / C4;
@@ -1299,7 +1330,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   // and the 8-VGPR staging of 8 loads per lane fill 128), 2 for fp32 EXACT at two 768- or
   // 1024-thread workgroups per CU (80 / 64 VGPRs), else 4
   constexpr bool kF32x = EXACT && !kIsBf16<T>;
-  constexpr int kBcDepth = (NP == 1 || (NT <= 512 && !kF32x)) ? 8 : (kF32x && NT >= 768) ? 2 : 4;
+  constexpr int kBcDepth = (NP == 1 || (NT <= 512 && !kF32x)) ? 8 : (kF32x && NT >= 768 && !DMA) ? 2 : 4;
   const int bc_off = BC ? ((ConstI32)p.bc_prog)[g * kW + wave] : 0;
   const ConstI32 prog = (ConstI32)(p.base + bc_off);
   const int bc_n = BC ? prog[0] : 0;
@@ -1311,12 +1342,14 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   }
   // converted to fp32 when written to LDS, not when loaded
   typedef typename std::conditional<W16, u32x4, typename Io<T>::raw_t>::type raw_t;
-  raw_t v[kLd];
+  raw_t v[DMA ? 1 : kLd];
   auto load_tile = [&](int64_t tt) {
 #ifdef TAL_PROBE_NOLOAD  // A/B probe: no HBM reads (the tile keeps the first tile's values)
     if (tt != blockIdx.x) return;
 #endif
-    if constexpr (W16) {  // 16-B units: chunk pair tt * C4 / 2 + c of each row
+    if constexpr (DMA) {
+      (void)tt;
+    } else if constexpr (W16) {  // 16-B units: chunk pair tt * C4 / 2 + c of each row
       const int64_t col = min(tt * kLps + c, (n4 - 1) / 2);  // past the end: a duplicate
       const u32x4* b = reinterpret_cast<const u32x4*>(pin);
 #pragma unroll
@@ -1333,7 +1366,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
     }
   };
   int64_t t = blockIdx.x;
-  if (t < n_tiles) load_tile(t);
+  if (!DMA && t < n_tiles) load_tile(t);
   for (; t < n_tiles; t += gridDim.x) {
 #ifdef TAL_PROBE_NOPREFETCH  // A/B probe: each tile's loads issued after the previous tile's math
     if (t != blockIdx.x) load_tile(t);
@@ -1343,8 +1376,25 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
     // form's control flow otherwise leaves the compiler unsure that ns is uniform here)
     int staged = __builtin_amdgcn_readfirstlane(ns * kLps);
     asm volatile("" : "+s"(staged));
+    if constexpr (DMA) {
+      // unit k = j NT + threadIdx.x lands at float4 k of the tile: wave-linear 1 KiB per load,
+      // from LDS byte address tile + 16 (j NT + 64 wave); units past the group's sources skip
+      const int64_t dcol = min(t * C4 + c, n4 - 1);  // past the end: a duplicate (cache hit)
+      const uint32_t wbase = lds_addr(s_data) + 1024u * static_cast<uint32_t>(wave);
+#ifdef TAL_PROBE_NOLOAD
+      if (t == blockIdx.x)
+#endif
 #pragma unroll
-    for (int j = 0; j < kLd; ++j) {
+      for (int j = 0; j < kLd; ++j) {
+        const int k = j * NT + static_cast<int>(threadIdx.x);
+        if (k < staged)
+          dma16(reinterpret_cast<const float4*>(pin) + static_cast<int64_t>(srow[j]) * ld_in4 + dcol,
+                wbase + 16u * static_cast<uint32_t>(j * NT));
+      }
+      wait_vm_barrier(0);  // this wave's DMAs (and its last stores) are done; every wave's are
+    }
+#pragma unroll
+    for (int j = 0; j < (DMA ? 0 : kLd); ++j) {
       const int k = j * NT + static_cast<int>(threadIdx.x);
       if constexpr (W16) {
         const int q = 2 * (k < staged ? k : c);
@@ -1354,9 +1404,9 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
         s_data[k < staged ? k : c] = Io<T>::f4(v[j]);
       }
     }
-    __syncthreads();
+    if constexpr (!DMA) __syncthreads();
 #ifndef TAL_PROBE_NOPREFETCH
-    if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
+    if (!DMA && t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
 #endif
     const int64_t col = t * C4 + cl;
     if constexpr (BC) {
@@ -1512,30 +1562,6 @@ __global__ __launch_bounds__(kBlock) void k_round_tiled_scalar(const T* __restri
 // output stores) retires in issue order, and chunk q is resident once at most
 // (DMAs issued after it) + (stores issued after it) ops are outstanding.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_byte_addr) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_byte_addr)
-      : "memory");
-}
-
-// s_waitcnt vmcnt(n) lgkmcnt(0) + s_barrier, n wave-uniform (clamped: waiting longer is safe)
-__device__ __forceinline__ void wait_vm_barrier(int n) {
-#define TAL_WB(k) case k: asm volatile("s_waitcnt vmcnt(" #k ") lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
-  switch (n < 0 ? 0 : (n > 31 ? 31 : n)) {
-    TAL_WB(0) TAL_WB(1) TAL_WB(2) TAL_WB(3) TAL_WB(4) TAL_WB(5) TAL_WB(6) TAL_WB(7)
-    TAL_WB(8) TAL_WB(9) TAL_WB(10) TAL_WB(11) TAL_WB(12) TAL_WB(13) TAL_WB(14) TAL_WB(15)
-    TAL_WB(16) TAL_WB(17) TAL_WB(18) TAL_WB(19) TAL_WB(20) TAL_WB(21) TAL_WB(22) TAL_WB(23)
-    TAL_WB(24) TAL_WB(25) TAL_WB(26) TAL_WB(27) TAL_WB(28) TAL_WB(29) TAL_WB(30) TAL_WB(31)
-  }
-#undef TAL_WB
-}
 
 template <int NT, bool EXACT>
 __global__ __launch_bounds__(NT, 2048 / NT) void k_round_stream(const float* __restrict__ pin, int64_t ld_in4,
@@ -1949,6 +1975,12 @@ int32_t launch_round_narrow_j(const T* pin, int64_t ld_in, T* pout, int64_t ld_o
                         : launch_round_narrow_jr<C4, J, EXACT, T, false>(pin, ld_in, pout, ld_out, n4, v, in, s);
 }
 
+// fp32 broadcast form with DMA staging (TAL_BC_DMA=1; A/B switch while it is measured)
+bool bc_dma_enabled() {
+  const char* e = getenv("TAL_BC_DMA");  // read per launch (tests switch it in-process)
+  return e && e[0] == '1';
+}
+
 // Broadcast form: NT = 64 x the plan's waves; J staging loads per lane cover the largest group.
 template <int C4, int NT, int J, bool EXACT, typename T>
 int32_t launch_round_bcast_j(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
@@ -1963,6 +1995,11 @@ int32_t launch_round_bcast_j(const T* pin, int64_t ld_in, T* pout, int64_t ld_ou
     if (w16)
       k = one ? k_round_f32_narrow<C4, NT, J, 1, EXACT, T, false, true, true>
               : k_round_f32_narrow<C4, NT, J, 0, EXACT, T, false, true, true>;
+  }
+  if constexpr (!kIsBf16<T>) {
+    if (bc_dma_enabled())
+      k = one ? k_round_f32_narrow<C4, NT, J, 1, EXACT, T, false, false, true, true>
+              : k_round_f32_narrow<C4, NT, J, 0, EXACT, T, false, false, true, true>;
   }
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;

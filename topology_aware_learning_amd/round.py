@@ -39,12 +39,15 @@ def csr_from_lists(orders: Sequence[Sequence[int]], weights: Sequence[Sequence[f
 
 class RoundExecutor:
     """Rounds over one pool.  Multi-group plans write a scratch pool (snapshot semantics);
-    placement_trials > 1 allocates that many scratch candidates the first time one is needed,
-    times the round into each and keeps the fastest (HBM placement of the written pool changes
-    the round time bimodally, see arena.select_pool_pair); `placement` records the times."""
+    placement_trials > 1 allocates that many scratch candidates the first time one is needed
+    (at most as many as fit in 60 % of the free HBM), times the round into each and keeps the
+    fastest (where in HBM the written pool sits changes the round time by up to 25 %, see
+    arena.select_pool_pair and DESIGN §5 "Pool placement"); `placement` records the times.
+    The default is 4 candidates.  Single-group plans run in place on `pool` itself, whose
+    placement is the caller's: `calibrated_pool` places it before models are bound."""
 
     def __init__(self, pool: ModelPool, scratch: Optional[ModelPool] = None, mode: int = ops.MODE_EXACT,
-                 placement_trials: int = 1):
+                 placement_trials: int = 4):
         self.pool = pool
         self.scratch = scratch
         self.mode = mode
@@ -55,14 +58,17 @@ class RoundExecutor:
     def _new_scratch(self, plan) -> ModelPool:
         lay = self.pool.layout
         make = lambda: ModelPool(lay, self.pool.rows, self.pool.device)  # noqa: E731
-        if self.placement_trials <= 1:
+        pool_bytes = sum(t.numel() * t.element_size() for _, t, _ in self.pool.segments())
+        fit = int(0.6 * torch.cuda.mem_get_info(self.pool.device)[0] // max(1, pool_bytes))
+        trials = min(self.placement_trials, fit)
+        if trials <= 1:
             return make()
         seg = "b16" if lay.n_b16 else "f32"
         n = lay.n_b16 if lay.n_b16 else lay.n_f32
         run = ops.round_bf16 if lay.n_b16 else ops.round_f32
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         cands, ms = [], []
-        for _ in range(self.placement_trials):
+        for _ in range(trials):
             c = make()
             run(getattr(self.pool, seg), getattr(c, seg), plan, n=n, mode=self.mode)
             s.record()
