@@ -55,18 +55,11 @@ def _bits_equal(a, b):
 FORMS = [(8, 2), (12, 2), (16, 2), (16, 1)]  # (wavefronts per workgroup, workgroups per CU)
 
 
-@pytest.fixture(params=[False, True], ids=["regstage", "dma"])
-def staging(request, monkeypatch):
-    """fp32 staging through registers (prefetched) or by global->LDS DMA (TAL_BC_DMA=1)."""
-    monkeypatch.setenv("TAL_BC_DMA", "1" if request.param else "0")
-    return request.param
-
-
 @pytest.mark.parametrize("waves,wg", FORMS)
 @pytest.mark.parametrize("c4", [16, 32])
 @pytest.mark.parametrize("n", [4099, 70001])
 @pytest.mark.parametrize("graph", list(_GRAPHS))
-def test_round_bcast_f32_vs_oracle(cuda, graph, n, c4, waves, wg, staging):
+def test_round_bcast_f32_vs_oracle(cuda, graph, n, c4, waves, wg):
     g = _GRAPHS[graph]()
     orders, ws = _csr(g, "degcent" if graph in ("regular", "gnp", "sbm", "star") else "unweighted")
     rows = len(orders)
@@ -115,7 +108,7 @@ def test_round_bcast_bf16_vs_oracle(cuda, graph, c4, waves, wg):
             assert np.array_equal(ob.cpu().view(torch.int16).numpy().view(np.uint16), ref), (nn, exact)
 
 
-def test_round_bcast_padded_ld_and_tail(cuda, staging):
+def test_round_bcast_padded_ld_and_tail(cuda):
     """Rows padded past n (ld > n) and n % 4 != 0: the float4 body by the broadcast kernel, the
     tail and the int64 segment by the plan's scalar kernels."""
     orders, ws = bench.round_spec(64, 8, weights="degcent")
@@ -139,7 +132,7 @@ def test_round_bcast_padded_ld_and_tail(cuda, staging):
 
 
 @pytest.mark.parametrize("waves,wg", FORMS)
-def test_round_bcast_config5_topology(cuda, waves, wg, staging):
+def test_round_bcast_config5_topology(cuda, waves, wg):
     """BASELINE config 5's topology with degree-centrality weights (the per-operand-weight case
     this form is for): one group of 256 sources at c4 = 16, every source read once per tile."""
     orders, ws = bench.round_spec(256, 8, kind="sbm", weights="degcent")

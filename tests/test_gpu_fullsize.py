@@ -185,12 +185,13 @@ def test_config5_full_round_vs_reference(cuda, spec):
     _check_c5(cuda, "f32", "unweighted_module_avg", spec)
 
 
-@pytest.mark.parametrize("spec", [None, {"reg": 1}, {"c4": 16, "lds": 163840, "dense": 0, "bcast": 8, "bcwg": 2},
+@pytest.mark.parametrize("spec", [None, {"reg": 1}, {"c4": 16, "lds": 163840, "dense": 0},
                                   {"c4": 16, "lds": 163840, "dense": 0, "bcast": 16, "bcwg": 2}])
 def test_config5_degree_centrality_vs_reference(cuda, spec):
     """The per-operand-weight form (centrality_module_avg, degree, softmax coeff 10) of config 5
     at full width: every entry group of every output model bitwise the reference's, through the
-    default (pairs) form, K3r and the broadcast forms."""
+    default plan (the broadcast form, 8 wavefronts x 2), K3r, the pairs form and the 16 x 2
+    broadcast form."""
     _check_c5(cuda, "f32", "centrality_module_avg", spec)
 
 

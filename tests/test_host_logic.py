@@ -581,9 +581,10 @@ def test_default_plan_forms(kind, n, deg, form):
 
 def test_default_plan_bf16_per_operand_weights():
     """Config 5 with degree-centrality softmax weights: bf16 FMA rounds default to the narrow
-    kernel's broadcast form (16 wavefronts, 2 workgroups per CU: 23.6-24.0 ms in round 4 against
-    K3r's 29.8), one group so RoundExecutor runs it in place; fp32 and bf16 EXACT keep the
-    narrow pairs form, and unweighted bf16 FMA the narrow ROWW form."""
+    kernel's broadcast form (16 wavefronts, 2 workgroups per CU: 23.6-24.3 ms in round 4 against
+    K3r's 29.8), fp32 rounds (either mode) to its 8-wavefront form (42.2 ms against 46.0 for the
+    cost model's two-group pairs plan), each one group so RoundExecutor runs it in place; bf16
+    EXACT keeps the narrow pairs form, and unweighted rounds the narrow ROWW form."""
     import bench
     from topology_aware_learning_amd.round import csr_from_lists
 
@@ -593,13 +594,17 @@ def test_default_plan_bf16_per_operand_weights():
     p = ops.default_plan(rp, col, w, rows, bf16=True, mode=ops.MODE_FMA)
     assert isinstance(p, ops.RoundPlan) and p.info.narrow_bcast == 16 and p.info.bc_wg_per_cu == 2
     assert p.single_group and p.spec["bcast"] == 16
-    for kw in (dict(bf16=False, mode=ops.MODE_FMA), dict(bf16=True, mode=ops.MODE_EXACT), dict(bf16=True)):
+    for kw in (dict(bf16=False, mode=ops.MODE_FMA), dict(bf16=False)):
         q = ops.default_plan(rp, col, w, rows, **kw)
-        assert isinstance(q, ops.RoundPlan) and q.info.c4 == 16 and not q.info.narrow_roww
+        assert isinstance(q, ops.RoundPlan) and q.info.narrow_bcast == 8 and q.info.bc_wg_per_cu == 2
+        assert q.single_group and q.staged_rows() == 256
+    q = ops.default_plan(rp, col, w, rows, bf16=True, mode=ops.MODE_EXACT)
+    assert isinstance(q, ops.RoundPlan) and q.info.c4 == 16 and not q.info.narrow_roww and not q.info.narrow_bcast
     orders, ws = bench.round_spec(256, 8, kind="sbm")
     rp, col, w = csr_from_lists(orders, ws)
-    q = ops.default_plan(rp, col, w, rows, bf16=True, mode=ops.MODE_FMA)
-    assert isinstance(q, ops.RoundPlan) and q.info.narrow_roww
+    for kw in (dict(bf16=True, mode=ops.MODE_FMA), dict(bf16=False)):
+        q = ops.default_plan(rp, col, w, rows, **kw)
+        assert isinstance(q, ops.RoundPlan) and q.info.narrow_roww
 
 
 def test_auto_dense_only_for_cliques():

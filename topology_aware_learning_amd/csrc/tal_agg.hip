@@ -1024,7 +1024,7 @@ __device__ __forceinline__ float4 narrow_row_roww(uint4 rc, uint32_t base) {
   return narrow_row_tail<T, EXACT>(acc, w, e, base, rem);
 }
 
-// one 16-B-per-lane global->LDS DMA: 64 lanes x 16 B, lane-linear from LDS byte address M0
+// one 16-B-per-lane global->LDS DMA (K3s): 64 lanes x 16 B, lane-linear from LDS byte address M0
 __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_byte_addr) {
   uint32_t keep;
   asm volatile(
@@ -1264,19 +1264,14 @@ __device__ __forceinline__ int narrow_set(int p, int wave, int nwaves) {
 // adjacent fp32 float4.  Needs an even chunk count, a row stride of an even number of chunks and
 // a 16-B aligned base (the launcher checks), so every pair lies inside its row.
 // BC: the broadcast form (narrow_bcast plans; NT = 64 x the plan's waves per workgroup).
-// DMA (fp32 broadcast form): staging by global->LDS DMA into the tile (no staging registers, so
-// the 1024-thread fp32 EXACT form fits 64 VGPRs without spills); the tile is single-buffered, so
-// a tile's loads are issued after the previous tile's readers are done (the other resident
-// workgroup of the CU computes meanwhile).
 template <int C4, int NT, int J, int NP, bool EXACT, typename T = float, bool ROWW = false, bool W16 = false,
-          bool BC = false, bool DMA = false>
+          bool BC = false>
 __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round_f32_narrow(
     const T* __restrict__ pin, int64_t ld_in4, T* __restrict__ pout, int64_t ld_out4, int64_t n4,
     PlanView p, int64_t n_tiles) {
   static_assert(C4 == 16 || C4 == 32, "narrow tiles are 16 or 32 float4 wide");
   static_assert(NT % C4 == 0, "a block stages whole source tiles");
   static_assert(!W16 || (kIsBf16<T> && J % 2 == 0), "16-B staging lanes: bf16 pools, even J");
-  static_assert(!DMA || (BC && !kIsBf16<T> && !W16), "DMA staging: fp32 broadcast form");
   constexpr int kLd = W16 ? J / 2 : J;       // staging loads per lane
   constexpr int kLps = W16 ? C4 / 2 : C4;    // staging lanes per source and tile
   constexpr int kRpw = 64 / C4;
@@ -1330,7 +1325,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   // and the 8-VGPR staging of 8 loads per lane fill 128), 2 for fp32 EXACT at two 768- or
   // 1024-thread workgroups per CU (80 / 64 VGPRs), else 4
   constexpr bool kF32x = EXACT && !kIsBf16<T>;
-  constexpr int kBcDepth = (NP == 1 || (NT <= 512 && !kF32x)) ? 8 : (kF32x && NT >= 768 && !DMA) ? 2 : 4;
+  constexpr int kBcDepth = (NP == 1 || (NT <= 512 && !kF32x)) ? 8 : (kF32x && NT >= 768) ? 2 : 4;
   const int bc_off = BC ? ((ConstI32)p.bc_prog)[g * kW + wave] : 0;
   const ConstI32 prog = (ConstI32)(p.base + bc_off);
   const int bc_n = BC ? prog[0] : 0;
@@ -1342,14 +1337,12 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   }
   // converted to fp32 when written to LDS, not when loaded
   typedef typename std::conditional<W16, u32x4, typename Io<T>::raw_t>::type raw_t;
-  raw_t v[DMA ? 1 : kLd];
+  raw_t v[kLd];
   auto load_tile = [&](int64_t tt) {
 #ifdef TAL_PROBE_NOLOAD  // A/B probe: no HBM reads (the tile keeps the first tile's values)
     if (tt != blockIdx.x) return;
 #endif
-    if constexpr (DMA) {
-      (void)tt;
-    } else if constexpr (W16) {  // 16-B units: chunk pair tt * C4 / 2 + c of each row
+    if constexpr (W16) {  // 16-B units: chunk pair tt * C4 / 2 + c of each row
       const int64_t col = min(tt * kLps + c, (n4 - 1) / 2);  // past the end: a duplicate
       const u32x4* b = reinterpret_cast<const u32x4*>(pin);
 #pragma unroll
@@ -1366,7 +1359,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
     }
   };
   int64_t t = blockIdx.x;
-  if (!DMA && t < n_tiles) load_tile(t);
+  if (t < n_tiles) load_tile(t);
   for (; t < n_tiles; t += gridDim.x) {
 #ifdef TAL_PROBE_NOPREFETCH  // A/B probe: each tile's loads issued after the previous tile's math
     if (t != blockIdx.x) load_tile(t);
@@ -1376,25 +1369,8 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
     // form's control flow otherwise leaves the compiler unsure that ns is uniform here)
     int staged = __builtin_amdgcn_readfirstlane(ns * kLps);
     asm volatile("" : "+s"(staged));
-    if constexpr (DMA) {
-      // unit k = j NT + threadIdx.x lands at float4 k of the tile: wave-linear 1 KiB per load,
-      // from LDS byte address tile + 16 (j NT + 64 wave); units past the group's sources skip
-      const int64_t dcol = min(t * C4 + c, n4 - 1);  // past the end: a duplicate (cache hit)
-      const uint32_t wbase = lds_addr(s_data) + 1024u * static_cast<uint32_t>(wave);
-#ifdef TAL_PROBE_NOLOAD
-      if (t == blockIdx.x)
-#endif
 #pragma unroll
-      for (int j = 0; j < kLd; ++j) {
-        const int k = j * NT + static_cast<int>(threadIdx.x);
-        if (k < staged)
-          dma16(reinterpret_cast<const float4*>(pin) + static_cast<int64_t>(srow[j]) * ld_in4 + dcol,
-                wbase + 16u * static_cast<uint32_t>(j * NT));
-      }
-      wait_vm_barrier(0);  // this wave's DMAs (and its last stores) are done; every wave's are
-    }
-#pragma unroll
-    for (int j = 0; j < (DMA ? 0 : kLd); ++j) {
+    for (int j = 0; j < kLd; ++j) {
       const int k = j * NT + static_cast<int>(threadIdx.x);
       if constexpr (W16) {
         const int q = 2 * (k < staged ? k : c);
@@ -1404,9 +1380,9 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
         s_data[k < staged ? k : c] = Io<T>::f4(v[j]);
       }
     }
-    if constexpr (!DMA) __syncthreads();
+    __syncthreads();
 #ifndef TAL_PROBE_NOPREFETCH
-    if (!DMA && t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
+    if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
 #endif
     const int64_t col = t * C4 + cl;
     if constexpr (BC) {
@@ -1975,12 +1951,6 @@ int32_t launch_round_narrow_j(const T* pin, int64_t ld_in, T* pout, int64_t ld_o
                         : launch_round_narrow_jr<C4, J, EXACT, T, false>(pin, ld_in, pout, ld_out, n4, v, in, s);
 }
 
-// fp32 broadcast form with DMA staging (TAL_BC_DMA=1; A/B switch while it is measured)
-bool bc_dma_enabled() {
-  const char* e = getenv("TAL_BC_DMA");  // read per launch (tests switch it in-process)
-  return e && e[0] == '1';
-}
-
 // Broadcast form: NT = 64 x the plan's waves; J staging loads per lane cover the largest group.
 template <int C4, int NT, int J, bool EXACT, typename T>
 int32_t launch_round_bcast_j(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
@@ -1995,11 +1965,6 @@ int32_t launch_round_bcast_j(const T* pin, int64_t ld_in, T* pout, int64_t ld_ou
     if (w16)
       k = one ? k_round_f32_narrow<C4, NT, J, 1, EXACT, T, false, true, true>
               : k_round_f32_narrow<C4, NT, J, 0, EXACT, T, false, true, true>;
-  }
-  if constexpr (!kIsBf16<T>) {
-    if (bc_dma_enabled())
-      k = one ? k_round_f32_narrow<C4, NT, J, 1, EXACT, T, false, false, true, true>
-              : k_round_f32_narrow<C4, NT, J, 0, EXACT, T, false, false, true, true>;
   }
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;

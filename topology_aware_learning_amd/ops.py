@@ -733,22 +733,26 @@ def default_plan(row_ptr, col, w, out_row, bf16: bool = False, mode: int = MODE_
     by their own sparse plan), else build_plan's sparse form at the tile width and LDS budget
     its cost model picks.  On the round-1 A/B tables this is the measured winner's form for
     configs 2-5 (tests/test_host_logic.py::test_default_plan_forms).  One exception, from
-    round 4's measurements: a bf16 round in FMA mode whose narrow plan needs per-operand weights
-    (the pairs form: centrality weights on a graph whose degrees differ) runs the narrow
-    kernel's broadcast form, 16 wavefronts, two workgroups per CU (config 5 with
-    degree-centrality weights: 23.6-24.0 ms against 32.1 for the pairs form and 29.8 for the
-    register-resident K3r, which round 3 picked; profiles/r04).  It keeps the narrow plan's
-    single group, so RoundExecutor still runs it in place."""
+    round 4's measurements: a round whose narrow plan needs per-operand weights (the pairs
+    form: centrality weights on a graph whose degrees differ) runs the narrow kernel's
+    broadcast form with the whole source set in one 160 KiB tile, two workgroups per CU — 16
+    wavefronts for bf16 in FMA mode (config 5 with degree-centrality weights: 23.6-24.3 ms
+    against 32.1-32.6 for the pairs form and 29.8-30.1 for the register-resident K3r, which
+    round 3 picked), 8 for fp32 (42.2 ms against 46.0 for the cost model's two-group pairs
+    plan; profiles/r04/r04f).  It keeps the single group, so RoundExecutor runs it in place."""
     if not bf16:
         cp = build_clique_plan(row_ptr, col, w, out_row)
         if cp is not None:
             cp.spec = dict(clique=1, rest=cp.rest.spec if cp.rest is not None else None)
             return cp
     p = build_plan(row_ptr, col, w, out_row, dense=0)
-    if bf16 and mode == MODE_FMA and p.info.c4 < 64 and not p.info.narrow_roww:
+    if p.info.c4 < 64 and not p.info.narrow_roww and (not bf16 or mode == MODE_FMA):
+        # per-operand weights on a narrow plan: the broadcast form, 16 wavefronts for bf16 FMA,
+        # 8 for fp32 (its 1024-thread form spills), one workgroup's LDS tile holding every source
+        waves = 16 if bf16 else 8
         try:
-            bp = build_plan(row_ptr, col, w, out_row, c4=p.info.c4, lds_bytes=LDS_BUDGETS[-1], bcast=16, bcast_wg=2)
-        except _lib.TalError:  # a row past 16 x 8 operands: no broadcast form
+            bp = build_plan(row_ptr, col, w, out_row, c4=p.info.c4, lds_bytes=LDS_BUDGETS[-1], bcast=waves, bcast_wg=2)
+        except _lib.TalError:  # a row past 128 / waves records: no broadcast form
             return p
         if bp.info.n_groups <= p.info.n_groups:
             return bp
