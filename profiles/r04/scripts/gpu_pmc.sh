@@ -14,6 +14,7 @@ pmc() {  # name pass counters spec dtype
   echo "{\"spec\": $spec, \"dtype\": \"$dt\"}" > $OUT/$name.spec
   timeout -s KILL 240 rocprofv3 --pmc $ctr --output-format csv -d $OUT/${name}_$pass -o pmc -- \
     python3 $R/bench.py $B --dtype $dt --plan "$spec" > $OUT/${name}_$pass.log 2>&1 || { echo "FAIL $name $pass"; tail -5 $OUT/${name}_$pass.log; return 1; }
+  python3 $R/tools/pmc_shrink.py $OUT/${name}_$pass || return 1  # the last round dispatch only (copy-back limit)
   echo "ok $name $pass"
 }
 PAIRS='{"c4":16,"lds":163840,"dense":0}'

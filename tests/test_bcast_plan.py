@@ -37,17 +37,16 @@ def _decode(plan, c4):
                 cnt, last, ps = d & 0xFF, (d >> 8) & 1, d >> 16
                 assert 1 <= cnt <= 16 and ps < n_pass
                 rec = h[o + data + 128 * r: o + data + 128 * (r + 1)].reshape(64, 2)
-                for lane in range(64):
-                    sub, u = lane // c4, lane % 16
-                    assert np.array_equal(rec[lane], rec[sub * c4 + u])  # both DPP rows of a row group
-                    if u >= cnt or lane % c4 >= 16:  # c4 = 32: the second DPP row repeats the first
+                for lane in range(64):  # 4 rows of 16 lanes at both widths (c4 = 32: two chunks a lane)
+                    sub, u = lane // 16, lane % 16
+                    if u >= cnt:
                         continue
                     off, wb = int(rec[lane, 0]), int(rec[lane, 1])
                     assert off % (c4 * 16) == 0
                     acc.setdefault((ps, sub), []).append((off // (c4 * 16), wb))
                 if last:
                     outs = h[o + HDR + R + 4 * ps: o + HDR + R + 4 * ps + 4]
-                    for sub in range(64 // c4):
+                    for sub in range(4):
                         ops_ = acc.pop((ps, sub), [])
                         if outs[sub] < 0:
                             assert all(s == ns and wb == one for s, wb in ops_)
@@ -87,7 +86,7 @@ def test_bcast_programs_decode_to_csr(graph, c4, waves, wg):
     assert info.narrow_bcast == waves and info.c4 == c4 and info.narrow_roww == 0 and info.bc_wg_per_cu == wg
     assert info.lds_bytes <= (80 if wg == 2 else 160) * 1024
     assert max(plan.host[info.off_grp_src_ptr + g + 1] - plan.host[info.off_grp_src_ptr + g]
-               for g in range(info.n_groups)) * c4 <= 4096  # staging: J <= 4096 / threads
+               for g in range(info.n_groups)) * c4 <= (8192 if c4 == 32 else 4096)  # staging: J <= loads / threads
     assert info.lds_bytes == max(
         (plan.host[info.off_grp_src_ptr + g + 1] - plan.host[info.off_grp_src_ptr + g] + 1) * c4 * 16
         for g in range(info.n_groups))
@@ -96,9 +95,9 @@ def test_bcast_programs_decode_to_csr(graph, c4, waves, wg):
     for r in range(rows):
         want = [(int(col[k]), int(np.float32(w[k]).view(np.int32))) for k in range(row_ptr[r], row_ptr[r + 1])]
         assert dec[int(out_rows[r])] == want
-    if graph == "sbm256" and c4 == 16:
+    if graph == "sbm256" and (c4 == 16 or wg == 1):
         assert info.n_groups == 1 and info.total_src == 256  # every source read once per round
-    assert info.bc_records * 16 * (64 // c4) >= len(col)  # a record carries 16 operands of each row of a pass
+    assert info.bc_records * 16 * 4 >= len(col)  # a record carries 16 operands of each row of a pass
 
 
 def test_bcast_rejects_bad_arguments():

@@ -186,12 +186,13 @@ def test_config5_full_round_vs_reference(cuda, spec):
 
 
 @pytest.mark.parametrize("spec", [None, {"reg": 1}, {"c4": 16, "lds": 163840, "dense": 0},
-                                  {"c4": 16, "lds": 163840, "dense": 0, "bcast": 16, "bcwg": 2}])
+                                  {"c4": 16, "lds": 163840, "dense": 0, "bcast": 16, "bcwg": 2},
+                                  {"c4": 32, "lds": 163840, "dense": 0, "bcast": 16, "bcwg": 1}])
 def test_config5_degree_centrality_vs_reference(cuda, spec):
     """The per-operand-weight form (centrality_module_avg, degree, softmax coeff 10) of config 5
     at full width: every entry group of every output model bitwise the reference's, through the
     default plan (the broadcast form, 8 wavefronts x 2), K3r, the pairs form and the 16 x 2
-    broadcast form."""
+    broadcast form, and the two-chunk broadcast form (c4 = 32, one workgroup per CU)."""
     _check_c5(cuda, "f32", "centrality_module_avg", spec)
 
 
@@ -204,7 +205,8 @@ def test_config5_bf16_exact_vs_reference(cuda):
 @pytest.mark.parametrize("fn,spec", [("unweighted_module_avg", None),
                                      ("centrality_module_avg", None),
                                      ("centrality_module_avg", {"reg": 1}),
-                                     ("centrality_module_avg", {"c4": 16, "lds": 163840, "dense": 0, "bcast": 16, "bcwg": 2})])
+                                     ("centrality_module_avg", {"c4": 16, "lds": 163840, "dense": 0, "bcast": 16, "bcwg": 2}),
+                                     ("centrality_module_avg", {"c4": 32, "lds": 163840, "dense": 0, "bcast": 16, "bcwg": 1})])
 def test_config5_bf16_fma_full_width_within_bound(cuda, fn, spec):
     """Config 5's bf16 tolerance run (FMA: fp32 accumulation, one rounding) at full width: all
     256 output models x all 86.6 M columns within the SURVEY §8(a) bound

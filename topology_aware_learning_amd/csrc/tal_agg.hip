@@ -1171,6 +1171,52 @@ __device__ __forceinline__ float4 bc_record(float4 acc, int2 e, uint32_t base, i
   return acc;
 }
 
+// Two-chunk broadcast form (C4 = 32): a row's 16 lanes each own chunks cl and cl + 16 of the
+// 32-chunk (512 B) source tile, so one broadcast address (the second read at +256 B, the
+// instruction's offset) and one broadcast weight serve two float4 of the operand: per operand
+// and float4 the vector ALU does (1 address + 1 weight + 2 x arithmetic) / 2, and the lane
+// carries two independent accumulator chains.  Batches of four operands: 8 data reads in flight.
+template <int B>
+__device__ __forceinline__ void bc2_read4(float4 (&x)[8], int2 e, uint32_t base) {
+#define TAL_BC2_RD(u)                                                                   \
+  {                                                                                     \
+    const uint32_t a = bc_lane<4 * B + u>(static_cast<uint32_t>(e.x)) + base;           \
+    x[2 * u] = lds_f4(a);                                                               \
+    x[2 * u + 1] = lds_f4(a + 256u);                                                    \
+  }
+  TAL_BC2_RD(0) TAL_BC2_RD(1) TAL_BC2_RD(2) TAL_BC2_RD(3)
+#undef TAL_BC2_RD
+}
+
+template <typename T, bool EXACT, int U>
+__device__ __forceinline__ void bc2_op(float4& a0, float4& a1, const float4& x0, const float4& x1, int2 e) {
+  const float w = bc_w<U>(e);
+  if constexpr (EXACT && !kIsBf16<T>) {  // one product live at a time (the 128-VGPR budget)
+    a0 = add4(a0, mul4(w, x0));
+    a1 = add4(a1, mul4(w, x1));
+  } else {
+    a0 = next4t<T, EXACT>(a0, w, x0);
+    a1 = next4t<T, EXACT>(a1, w, x1);
+  }
+}
+
+template <typename T, bool EXACT>
+__device__ __forceinline__ void bc2_record(float4& a0, float4& a1, int2 e, uint32_t base, int cnt) {
+  const int nb = (cnt + 3) >> 2;  // wave-uniform
+  float4 x[8];
+#define TAL_BC2_BATCH(B)                                        \
+  if (nb > B) {                                                 \
+    __builtin_amdgcn_sched_barrier(0);                          \
+    bc2_read4<B>(x, e, base);                                   \
+    bc2_op<T, EXACT, 4 * B + 0>(a0, a1, x[0], x[1], e);         \
+    bc2_op<T, EXACT, 4 * B + 1>(a0, a1, x[2], x[3], e);         \
+    bc2_op<T, EXACT, 4 * B + 2>(a0, a1, x[4], x[5], e);         \
+    bc2_op<T, EXACT, 4 * B + 3>(a0, a1, x[6], x[7], e);         \
+  }
+  TAL_BC2_BATCH(0) TAL_BC2_BATCH(1) TAL_BC2_BATCH(2) TAL_BC2_BATCH(3)
+#undef TAL_BC2_BATCH
+}
+
 template <int C4>
 __device__ __forceinline__ NarrowLds stage_narrow_bc(const PlanView& p, int g, float4* s_data, int nthreads) {
   NarrowLds L;
@@ -1274,7 +1320,9 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   static_assert(!W16 || (kIsBf16<T> && J % 2 == 0), "16-B staging lanes: bf16 pools, even J");
   constexpr int kLd = W16 ? J / 2 : J;       // staging loads per lane
   constexpr int kLps = W16 ? C4 / 2 : C4;    // staging lanes per source and tile
-  constexpr int kRpw = 64 / C4;
+  // BC at C4 = 32: the two-chunk form (4 rows of 16 lanes per pass, like C4 = 16)
+  constexpr bool kX2 = BC && C4 == 32;
+  constexpr int kRpw = kX2 ? 4 : 64 / C4;
   constexpr int kW = NT / 64;
   extern __shared__ float4 s_data[];
   const int g = blockIdx.y;
@@ -1285,8 +1333,8 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   const int c = threadIdx.x % kLps;  // staging: the lane's chunk (W16: chunk pair) of its source
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-  const int sub = lane / C4;
-  const int cl = lane % C4;
+  const int sub = kX2 ? lane / 16 : lane / C4;
+  const int cl = kX2 ? lane % 16 : lane % C4;
   // Staging is branch-free, so that the compiler's wait analysis sees every load land in its
   // register unconditionally (a conditional load made it wait for each load before issuing the
   // next: four serial HBM round trips per tile).  A lane past the group's sources reloads
@@ -1391,6 +1439,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
 #pragma unroll
       for (int r = 0; r < kR; ++r) asm volatile("" : "+v"(bc_rec[r].x), "+v"(bc_rec[r].y));
       float4 acc = make_float4(-0.f, -0.f, -0.f, -0.f);
+      float4 acc1 = acc;  // kX2: chunk cl + 16
 #pragma unroll
       for (int r = 0; r < kR; ++r) {
         if (r >= bc_n) continue;  // wave-uniform (a constant trip count keeps the loop unrolled,
@@ -1399,13 +1448,20 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
 #ifdef TAL_PROBE_NOCOMP
         (void)d;
 #else
-        acc = bc_record<T, EXACT, kBcDepth>(acc, bc_rec[r], col_base, static_cast<int>(d & 0xffu));
+        if constexpr (kX2)
+          bc2_record<T, EXACT>(acc, acc1, bc_rec[r], col_base, static_cast<int>(d & 0xffu));
+        else
+          acc = bc_record<T, EXACT, kBcDepth>(acc, bc_rec[r], col_base, static_cast<int>(d & 0xffu));
 #endif
         if (d & 0x100u) {  // the pass's last record: store its rows
           const ConstI32 orow = prog + kBcHdr + kR + 4 * static_cast<int>(d >> 16);
           const int o0 = orow[0], o1 = orow[1], o2 = orow[2], o3 = orow[3];
           const int o = sub == 0 ? o0 : sub == 1 ? o1 : sub == 2 ? o2 : o3;
           if (o >= 0 && col < n4) Io<T>::st(pout, static_cast<int64_t>(o) * ld_out4 + col, acc);
+          if constexpr (kX2) {
+            if (o >= 0 && col + 16 < n4) Io<T>::st(pout, static_cast<int64_t>(o) * ld_out4 + col + 16, acc1);
+            acc1 = make_float4(-0.f, -0.f, -0.f, -0.f);
+          }
           acc = make_float4(-0.f, -0.f, -0.f, -0.f);
         }
       }
@@ -1807,6 +1863,12 @@ constexpr int64_t group_lds_bytes(int64_t ns, int64_t nr, int64_t no, int c4) {
   return ns * 16 * c4 + (nr + 1 + 2 * no + ns + nr) * 4;
 }
 
+// Tile width (in float4 units) of the scalar kernel (the n mod 4 tail, the int64 segment and
+// unaligned pools): the plan's c4, except for narrow plans, whose scalar tiles stay at 16 so a
+// 32-wide narrow tile of 256 sources (128 KiB) leaves the scalar kernel's tile + plan slice
+// under 160 KiB.
+constexpr int scalar_c4(int c4) { return c4 < 64 ? 16 : c4; }
+
 std::mutex g_lds_mu;
 std::vector<const void*> g_lds_raised;
 
@@ -1851,7 +1913,7 @@ int32_t launch_round_scalar(const T* pin, int64_t ld_in, T* pout, int64_t ld_out
                             int64_t e0, int64_t n, const PlanView& v,
                             const tal_round_plan_info& in, bool exact, hipStream_t s) {
   if (n <= e0) return TAL_OK;
-  const int tile = 4 * in.c4;
+  const int tile = 4 * scalar_c4(in.c4);
   const size_t lds = static_cast<size_t>(in.scalar_lds_bytes);  // the largest group's tile + plan slice
   const int64_t tiles = (n - e0 + tile - 1) / tile;
   if (tiles > 0x7fffffff) return fail(TAL_ERR_INVALID, "too many tiles");
@@ -1959,12 +2021,15 @@ int32_t launch_round_bcast_j(const T* pin, int64_t ld_in, T* pout, int64_t ld_ou
   const bool one = in.bc_wg_per_cu == 1;  // one workgroup per CU: 128 VGPRs at 1024 threads
   const bool w16 = kIsBf16<T> && J % 2 == 0 && narrow_w16_enabled() && n4 % 2 == 0 && (ld_in / 4) % 2 == 0 &&
                    (reinterpret_cast<uintptr_t>(pin) & 15) == 0;
-  auto k = one ? k_round_f32_narrow<C4, NT, J, 1, EXACT, T, false, false, true>
-               : k_round_f32_narrow<C4, NT, J, 0, EXACT, T, false, false, true>;
+  // J = 8 at 1024 threads (the two-chunk form's 128 KiB tile) only with one workgroup per CU
+  constexpr bool kOneOnly = NT == 1024 && J == 8;
+  if (kOneOnly && !one) return fail(TAL_ERR_CAPACITY, "broadcast-form round plan: this tile needs one workgroup per CU");
+  auto k = (one || kOneOnly) ? k_round_f32_narrow<C4, NT, J, 1, EXACT, T, false, false, true>
+                             : k_round_f32_narrow<C4, NT, J, kOneOnly ? 1 : 0, EXACT, T, false, false, true>;
   if constexpr (kIsBf16<T> && J % 2 == 0) {
     if (w16)
-      k = one ? k_round_f32_narrow<C4, NT, J, 1, EXACT, T, false, true, true>
-              : k_round_f32_narrow<C4, NT, J, 0, EXACT, T, false, true, true>;
+      k = (one || kOneOnly) ? k_round_f32_narrow<C4, NT, J, 1, EXACT, T, false, true, true>
+                            : k_round_f32_narrow<C4, NT, J, kOneOnly ? 1 : 0, EXACT, T, false, true, true>;
   }
   int32_t rc = ensure_lds(reinterpret_cast<const void*>(k), lds);
   if (rc) return rc;
@@ -1985,7 +2050,7 @@ int32_t launch_round_bcast_nt(const T* pin, int64_t ld_in, T* pout, int64_t ld_o
   if (loads <= 4LL * NT) return launch_round_bcast_j<C4, NT, 4, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
   if constexpr (NT == 768)
     if (loads <= 6LL * NT) return launch_round_bcast_j<C4, NT, 6, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
-  if constexpr (NT <= 512)
+  if constexpr (NT <= 512 || (NT == 1024 && C4 == 32))
     if (loads <= 8LL * NT) return launch_round_bcast_j<C4, NT, 8, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
   return fail(TAL_ERR_CAPACITY, "broadcast-form round plan: group tile too large for the workgroup");
 }
@@ -3225,9 +3290,10 @@ int64_t roww_padded_slots(const int32_t* row_ptr_host, int64_t r0, int64_t nr, i
   return slots;
 }
 
-// Broadcast form: a pass of 64 / c4 rows takes ceil(operands of its longest row / 16) records;
-// passes are dealt to wavefronts longest first, each to the least loaded one.  False when a
-// wavefront would hold more than rmax records.
+// Broadcast form: a pass is 4 rows (16 lanes each: one float4 chunk per lane at c4 = 16, two
+// at c4 = 32) and takes ceil(operands of its longest row / 16) records; passes are dealt to
+// wavefronts longest first, each to the least loaded one.  False when a wavefront would hold
+// more than rmax records.
 bool bc_deal(const std::vector<int32_t>& pass_recs, int waves, int rmax, std::vector<std::vector<int32_t>>* per_wave) {
   std::vector<int32_t> order(pass_recs.size());
   for (size_t k = 0; k < order.size(); ++k) order[k] = static_cast<int32_t>(k);
@@ -3245,11 +3311,13 @@ bool bc_deal(const std::vector<int32_t>& pass_recs, int waves, int rmax, std::ve
 }
 
 // Records of the passes of rows r0 .. r0+nr-1 once ordered by operand count (descending).
-std::vector<int32_t> bc_pass_records(const int32_t* row_ptr_host, int64_t r0, int64_t nr, int32_t c4, bool sorted) {
+constexpr int32_t kBcRowsPerPass = 4;
+
+std::vector<int32_t> bc_pass_records(const int32_t* row_ptr_host, int64_t r0, int64_t nr, bool sorted) {
   std::vector<int32_t> m(static_cast<size_t>(nr));
   for (int64_t i = 0; i < nr; ++i) m[i] = row_ptr_host[r0 + i + 1] - row_ptr_host[r0 + i];
   if (!sorted) std::sort(m.begin(), m.end(), std::greater<int32_t>());
-  const int64_t rpw = 64 / c4;
+  const int64_t rpw = kBcRowsPerPass;
   std::vector<int32_t> recs;
   for (int64_t i = 0; i < nr; i += rpw) recs.push_back((m[i] + 15) / 16);
   return recs;
@@ -3343,7 +3411,7 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
   for (int g = 0; g < G; ++g) {
     const int64_t nr = grp_row_ptr[g + 1] - grp_row_ptr[g];
     const int64_t no = row_ptr_host[grp_row_ptr[g + 1]] - row_ptr_host[grp_row_ptr[g]];
-    lds_need = std::max(lds_need, group_lds_bytes(grp_src_ptr[g + 1] - grp_src_ptr[g], nr, no, c4));
+    lds_need = std::max(lds_need, group_lds_bytes(grp_src_ptr[g + 1] - grp_src_ptr[g], nr, no, scalar_c4(c4)));
   }
   const int64_t scalar_need = lds_need;
   const bool roww = bc_waves == 0 && c4 < 64 && rows_uniform_weights(rows, row_ptr_host, w_host) &&
@@ -3356,7 +3424,7 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
   const int32_t bc_rmax = bc_waves > 0 ? kBcRecPerWg / bc_waves : 0;
   if (c4 < 64 && bc_waves > 0) {
     lds_need = 0;
-    const int32_t rpw = 64 / c4;
+    const int32_t rpw = kBcRowsPerPass;
     const float one = 1.0f;
     int32_t one_bits;
     memcpy(&one_bits, &one, 4);
@@ -3365,7 +3433,7 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
       const int32_t ns = grp_src_ptr[g + 1] - grp_src_ptr[g];
       const int32_t r0 = grp_row_ptr[g], nr = grp_row_ptr[g + 1] - r0;
       lds_need = std::max<int64_t>(lds_need, bc_lds_bytes(ns, c4));
-      const std::vector<int32_t> recs = bc_pass_records(row_ptr_host, r0, nr, c4, true);
+      const std::vector<int32_t> recs = bc_pass_records(row_ptr_host, r0, nr, true);
       std::vector<std::vector<int32_t>> per_wave;
       if (!bc_deal(recs, bc_waves, bc_rmax, &per_wave))
         return fail(TAL_ERR_CAPACITY, "tal_round_plan_build_bcast: a group's records exceed the wavefronts' registers");
@@ -3395,7 +3463,7 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
             pr[kBcHdr + ri] = cnt | ((c == recs[k] - 1) ? 0x100 : 0) | static_cast<int32_t>(i << 16);
             int32_t* rec = pr + data_off + 128 * static_cast<size_t>(ri);
             for (int L = 0; L < 64; ++L) {
-              const int32_t sb = L / c4, j = 16 * c + L % 16;
+              const int32_t sb = L / 16, j = 16 * c + L % 16;
               int32_t off = ns * c4 * 16, wb = one_bits;  // identity pad: the -0.0 tile, weight 1.0
               if (sb < prows) {
                 const int32_t row = pr0 + sb, k0 = row_ptr_host[row];
@@ -3740,15 +3808,16 @@ int32_t round_plan_build(int32_t rows, const int32_t* row_ptr_host, const int32_
   const bool roww = c4 < 64 && rows_uniform_weights(rows, row_ptr_host, w_host) && roww_slots_fit(max_col, c4);
   std::vector<int32_t> batches;
   auto fits = [&](int64_t ns, int64_t nr, int64_t no, int64_t r0) {
-    const int64_t sliced = group_lds_bytes(ns, nr, no, c4);
+    const int64_t sliced = group_lds_bytes(ns, nr, no, scalar_c4(c4));  // c4 >= 64: the round kernel's own
     if (c4 >= 64) return sliced <= lds_bytes;
     // narrow kernel: its own carve (exact ROWW padding; pairs: <= 3 per row) and read-ahead
     // within the budget; the staged scalar tail kernel within the hardware's 160 KiB
     if (bc_waves > 0) {
       std::vector<std::vector<int32_t>> per_wave;
-      // staging: at most 4096 float4 loads per tile (J <= 4 at 1024 threads, 8 at 512)
-      return bc_lds_bytes(ns, c4) <= lds_bytes && ns * c4 <= 4096 && sliced <= 160 * 1024 &&
-             bc_deal(bc_pass_records(row_ptr_host, r0, nr, c4, false), bc_waves, kBcRecPerWg / bc_waves, &per_wave);
+      // staging: at most 4096 float4 loads per tile at c4 = 16 (J <= 4 at 1024 threads, 8 at
+      // 512), 8192 at c4 = 32 (J = 8 at 1024 threads: one workgroup per CU)
+      return bc_lds_bytes(ns, c4) <= lds_bytes && ns * c4 <= (c4 == 32 ? 8192 : 4096) && sliced <= 160 * 1024 &&
+             bc_deal(bc_pass_records(row_ptr_host, r0, nr, false), bc_waves, kBcRecPerWg / bc_waves, &per_wave);
     }
     const int64_t narrow = static_cast<int64_t>(
         roww ? narrow_roww_lds_bytes(ns, nr, roww_padded_slots(row_ptr_host, r0, nr, c4, &batches), c4)
