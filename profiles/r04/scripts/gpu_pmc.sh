@@ -21,7 +21,8 @@ PAIRS='{"c4":16,"lds":163840,"dense":0}'
 BC16='{"c4":16,"lds":163840,"dense":0,"bcast":16,"bcwg":2}'
 BC8='{"c4":16,"lds":163840,"dense":0,"bcast":8,"bcwg":2}'
 REG='{"reg":1}'
-for run in "bf16_pairs|$PAIRS|bf16" "bf16_bcast16|$BC16|bf16" "bf16_reg|$REG|bf16" "f32_pairs|$PAIRS|f32" "f32_bcast8|$BC8|f32"; do
+X2='{"c4":32,"lds":163840,"dense":0,"bcast":16,"bcwg":1}'
+for run in "bf16_pairs|$PAIRS|bf16" "bf16_bcast16|$BC16|bf16" "bf16_reg|$REG|bf16" "bf16_x2|$X2|bf16" "f32_pairs|$PAIRS|f32" "f32_bcast8|$BC8|f32" "f32_x2|$X2|f32"; do
   IFS='|' read -r name spec dt <<< "$run"
   pmc $name ws "$WS" "$spec" $dt && pmc $name lv "$LV" "$spec" $dt || exit 1
   case $name in *reg) continue;; esac

@@ -581,8 +581,8 @@ def test_default_plan_forms(kind, n, deg, form):
 
 def test_default_plan_bf16_per_operand_weights():
     """Config 5 with degree-centrality softmax weights: bf16 FMA rounds default to the narrow
-    kernel's broadcast form (16 wavefronts, 2 workgroups per CU: 23.6-24.3 ms in round 4 against
-    K3r's 29.8), fp32 rounds (either mode) to its 8-wavefront form (42.2 ms against 46.0 for the
+    kernel's two-chunk broadcast form (c4 = 32, 16 wavefronts, one workgroup per CU: 23.0-23.3
+    ms in round 4 against K3r's 29.8), fp32 rounds (either mode) to its 8-wavefront form (42.2 ms against 46.0 for the
     cost model's two-group pairs plan), each one group so RoundExecutor runs it in place; bf16
     EXACT keeps the narrow pairs form, and unweighted rounds the narrow ROWW form."""
     import bench
@@ -592,8 +592,8 @@ def test_default_plan_bf16_per_operand_weights():
     rp, col, w = csr_from_lists(orders, ws)
     rows = np.arange(len(orders), dtype=np.int32)
     p = ops.default_plan(rp, col, w, rows, bf16=True, mode=ops.MODE_FMA)
-    assert isinstance(p, ops.RoundPlan) and p.info.narrow_bcast == 16 and p.info.bc_wg_per_cu == 2
-    assert p.single_group and p.spec["bcast"] == 16
+    assert isinstance(p, ops.RoundPlan) and p.info.narrow_bcast == 16 and p.info.bc_wg_per_cu == 1
+    assert p.info.c4 == 32 and p.single_group and p.spec["bcast"] == 16 and p.staged_rows() == 256
     for kw in (dict(bf16=False, mode=ops.MODE_FMA), dict(bf16=False)):
         q = ops.default_plan(rp, col, w, rows, **kw)
         assert isinstance(q, ops.RoundPlan) and q.info.narrow_bcast == 8 and q.info.bc_wg_per_cu == 2

@@ -735,11 +735,13 @@ def default_plan(row_ptr, col, w, out_row, bf16: bool = False, mode: int = MODE_
     configs 2-5 (tests/test_host_logic.py::test_default_plan_forms).  One exception, from
     round 4's measurements: a round whose narrow plan needs per-operand weights (the pairs
     form: centrality weights on a graph whose degrees differ) runs the narrow kernel's
-    broadcast form with the whole source set in one 160 KiB tile, two workgroups per CU — 16
-    wavefronts for bf16 in FMA mode (config 5 with degree-centrality weights: 23.6-24.3 ms
-    against 32.1-32.6 for the pairs form and 29.8-30.1 for the register-resident K3r, which
-    round 3 picked), 8 for fp32 (42.2 ms against 46.0 for the cost model's two-group pairs
-    plan; profiles/r04/r04f).  It keeps the single group, so RoundExecutor runs it in place."""
+    broadcast form with the whole source set in one LDS tile — for bf16 in FMA mode the
+    two-chunk form (c4 = 32, 16 wavefronts, one workgroup per CU; config 5 with
+    degree-centrality weights: 23.0-23.3 ms against 23.7-24.4 for the 16 x 2 form, 32.1-32.6 for
+    the pairs form and 29.8-30.1 for the register-resident K3r, which round 3 picked;
+    profiles/r04/r04j, profiles/r04/pmc), for fp32 8 wavefronts x 2 (38.2-42.2 ms against 46.0
+    for the cost model's two-group pairs plan; profiles/r04/r04f).  It keeps the single group,
+    so RoundExecutor runs it in place."""
     if not bf16:
         cp = build_clique_plan(row_ptr, col, w, out_row)
         if cp is not None:
@@ -747,15 +749,18 @@ def default_plan(row_ptr, col, w, out_row, bf16: bool = False, mode: int = MODE_
             return cp
     p = build_plan(row_ptr, col, w, out_row, dense=0)
     if p.info.c4 < 64 and not p.info.narrow_roww and (not bf16 or mode == MODE_FMA):
-        # per-operand weights on a narrow plan: the broadcast form, 16 wavefronts for bf16 FMA,
-        # 8 for fp32 (its 1024-thread form spills), one workgroup's LDS tile holding every source
-        waves = 16 if bf16 else 8
-        try:
-            bp = build_plan(row_ptr, col, w, out_row, c4=p.info.c4, lds_bytes=LDS_BUDGETS[-1], bcast=waves, bcast_wg=2)
-        except _lib.TalError:  # a row past 128 / waves records: no broadcast form
-            return p
-        if bp.info.n_groups <= p.info.n_groups:
-            return bp
+        # per-operand weights on a narrow plan: the broadcast form with every source in one LDS
+        # tile - bf16 FMA: the two-chunk form (c4 = 32, one workgroup per CU) when its 512-B
+        # tiles hold the group, else 16 wavefronts x 2; fp32: 8 wavefronts x 2 (its 1024-thread
+        # two-workgroup form spills; the two-chunk form ran alike)
+        forms = [(32, 16, 1), (16, 16, 2)] if bf16 else [(16, 8, 2)]
+        for c4, waves, wg in forms:
+            try:
+                bp = build_plan(row_ptr, col, w, out_row, c4=c4, lds_bytes=LDS_BUDGETS[-1], bcast=waves, bcast_wg=wg)
+            except _lib.TalError:  # a row past 128 / waves records: no broadcast form
+                continue
+            if bp.info.n_groups <= p.info.n_groups:
+                return bp
     return p
 
 
