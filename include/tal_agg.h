@@ -158,13 +158,15 @@ typedef struct tal_round_plan_info {
    * off_nrow_w.  off_nrow_ptr then counts slots; npairs counts slots. */
   int32_t narrow_roww;
   int32_t off_nrow_w;       /* [rows] fp32 weight bits (narrow_roww) */
-  int32_t scalar_lds_bytes; /* LDS of the staged scalar tail kernel (the largest group) */
+  int32_t scalar_lds_bytes; /* LDS of the staged scalar tail kernel (the largest group; its
+                             * tiles are c4 float4 wide, 16 for narrow plans) */
   /* broadcast form (narrow_bcast > 0, built by tal_round_plan_build_bcast; c4 16 / 32): the
    * LDS holds only the group's data tile and one -0.0 tile (slot max_src).  Each wavefront of
-   * a workgroup runs a fixed program over the group's passes (64 / c4 rows computed together,
-   * rows ordered by operand count, descending), kept in VGPRs for the whole launch: a record
+   * a workgroup runs a fixed program over the group's passes (4 rows computed together, 16
+   * lanes each - one float4 chunk per lane at c4 = 16, chunks cl and cl + 16 at c4 = 32 - rows
+   * ordered by operand count, descending), kept in VGPRs for the whole launch: a record
    * is 64 lanes x {LDS byte offset of the operand's tile column 0, fp32 weight bits} holding
-   * operands 16c .. 16c+15 of every row of the pass (lane L: row L / c4, operand 16c + L % 16;
+   * operands 16c .. 16c+15 of every row of the pass (lane L: row L / 16, operand 16c + L % 16;
    * past a row's count: the -0.0 tile with weight 1.0, an exact identity); the kernel hands
    * operand u to the row's lanes by a DPP row broadcast from lane u, so no per-operand plan
    * read touches LDS.  Program of wavefront w of group g at word off_bc_prog[g * narrow_bcast +
@@ -201,7 +203,8 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
 
 /* Broadcast-form narrow plan (see narrow_bcast above): as tal_round_plan_build at c4 16 / 32,
  * with waves (8, 12 or 16) wavefronts per workgroup and wg_per_cu (1 or 2) resident workgroups per CU
- * (2 caps lds_bytes at 80 KiB); a group also needs every wavefront's program
+ * (2 caps lds_bytes at 80 KiB; a c4 = 32 group of more than 128 sources at 1024 threads
+ * launches only with wg_per_cu 1); a group also needs every wavefront's program
  * to fit 128 / waves records (TAL_ERR_CAPACITY for a row no group can take).  Per-operand
  * weights cost no LDS reads in this form (the centrality strategies on graphs whose degrees
  * differ: decentralized_client.py:572-611). */

@@ -45,7 +45,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 19;
+constexpr int kAbiVersion = 20;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
