@@ -11,6 +11,7 @@ from oracle import reference_alg as ra
 from topology_aware_learning_amd import ops
 
 import bench
+from _pools import dev_rows, host
 
 pytestmark = pytest.mark.gpu
 
@@ -55,11 +56,14 @@ def _bits_equal(a, b):
 FORMS = [(8, 2), (12, 2), (16, 2), (16, 1)]  # (wavefronts per workgroup, workgroups per CU)
 
 
+@pytest.mark.parametrize("pad", [True, False], ids=["vec", "scalar"])
 @pytest.mark.parametrize("waves,wg", FORMS)
 @pytest.mark.parametrize("c4", [16, 32])
 @pytest.mark.parametrize("n", [4099, 70001])
 @pytest.mark.parametrize("graph", list(_GRAPHS))
-def test_round_bcast_f32_vs_oracle(cuda, graph, n, c4, waves, wg):
+def test_round_bcast_f32_vs_oracle(cuda, graph, n, c4, waves, wg, pad):
+    """pad: rows strided by a multiple of 64 elements (the broadcast kernel computes the float4
+    body, the scalar kernel the n % 4 tail) or contiguous odd rows (all by the scalar kernel)."""
     g = _GRAPHS[graph]()
     orders, ws = _csr(g, "degcent" if graph in ("regular", "gnp", "sbm", "star") else "unweighted")
     rows = len(orders)
@@ -70,19 +74,19 @@ def test_round_bcast_f32_vs_oracle(cuda, graph, n, c4, waves, wg):
     ref = oracle.round_f32(pool, row_ptr, col, w, out_rows)
     plan = ops.build_plan(row_ptr, col, w, out_rows, c4=c4, lds_bytes=80 * 1024, bcast=waves, bcast_wg=wg)
     assert plan.info.narrow_bcast == waves and plan.info.bc_wg_per_cu == wg
-    pin = torch.from_numpy(pool).to(cuda)
+    pin = dev_rows(pool, cuda, pad)
     pout = torch.zeros_like(pin)
-    ops.round_f32(pin, pout, plan)
-    assert _bits_equal(pout.cpu().numpy(), ref)
+    ops.round_f32(pin, pout, plan, n=n)
+    assert _bits_equal(host(pout, n), ref)
     # FMA: -0.0 start then one fused chain: bitwise K1-FMA on the same operands
-    ops.round_f32(pin, pout, plan, mode=ops.MODE_FMA)
+    ops.round_f32(pin, pout, plan, n=n, mode=ops.MODE_FMA)
     chk = torch.empty(n, dtype=torch.float32, device=cuda)
     for r in range(0, rows, max(1, rows // 9)):
-        ops.agg_f32([pin[j] for j in orders[r]], ws[r], chk, mode=ops.MODE_FMA)
-        assert torch.equal(chk.view(torch.int32), pout[out_rows[r]].view(torch.int32)), r
+        ops.agg_f32([pin[j, :n] for j in orders[r]], ws[r], chk, mode=ops.MODE_FMA)
+        assert torch.equal(chk.view(torch.int32), pout[out_rows[r], :n].view(torch.int32)), r
     if plan.single_group:  # in place: every source staged before any row of a tile is written
-        ops.round_f32(pin, pin, plan)
-        assert _bits_equal(pin.cpu().numpy(), ref)
+        ops.round_f32(pin, pin, plan, n=n)
+        assert _bits_equal(host(pin, n), ref)
 
 
 @pytest.mark.parametrize("waves,wg", FORMS)
@@ -94,18 +98,18 @@ def test_round_bcast_bf16_vs_oracle(cuda, graph, c4, waves, wg):
     rows = len(orders)
     row_ptr, col, w = ra.round_csr(orders, ws)
     out_rows = np.arange(rows, dtype=np.int32)[::-1].copy()
-    n = 8200  # even chunk count: the 16-B staging lanes; 8198 below takes the 8-B ones
+    n = 8200  # 2050 chunks: the 16-B staging lanes; 8196 (2049 chunks) the 8-B ones; 8198 + tail
     rng = np.random.default_rng(rows + c4)
     bits = oracle.f32_to_bf16(_pool(rng, rows, n, special=True))
     plan = ops.build_plan(row_ptr, col, w, out_rows, c4=c4, lds_bytes=80 * 1024, bcast=waves, bcast_wg=wg)
-    for nn in (n, n - 2):
+    for nn, pad in ((n, False), (n - 4, False), (n - 2, True), (n - 2, False)):
         b = np.ascontiguousarray(bits[:, :nn])
-        pb = torch.from_numpy(b.view(np.int16)).view(torch.bfloat16).to(cuda)
+        pb = dev_rows(b, cuda, pad)
         ob = torch.zeros_like(pb)
         for exact in (True, False):
-            ops.round_bf16(pb, ob, plan, mode=ops.MODE_EXACT if exact else ops.MODE_FMA)
+            ops.round_bf16(pb, ob, plan, n=nn, mode=ops.MODE_EXACT if exact else ops.MODE_FMA)
             ref = oracle.round_bf16(b, row_ptr, col, w, out_rows, exact=exact)
-            assert np.array_equal(ob.cpu().view(torch.int16).numpy().view(np.uint16), ref), (nn, exact)
+            assert np.array_equal(host(ob, nn), ref), (nn, pad, exact)
 
 
 def test_round_bcast_padded_ld_and_tail(cuda):
@@ -143,7 +147,7 @@ def test_round_bcast_config5_topology(cuda, waves, wg):
     n = 16387
     rng = np.random.default_rng(5)
     pool = rng.standard_normal((256, n)).astype(np.float32)
-    pin = torch.from_numpy(pool).to(cuda)
+    pin = dev_rows(pool, cuda)
     pout = torch.zeros_like(pin)
-    ops.round_f32(pin, pout, plan)
-    assert _bits_equal(pout.cpu().numpy(), oracle.round_f32(pool, row_ptr, col, w, out_rows))
+    ops.round_f32(pin, pout, plan, n=n)
+    assert _bits_equal(host(pout, n), oracle.round_f32(pool, row_ptr, col, w, out_rows))

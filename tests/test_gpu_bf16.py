@@ -17,6 +17,7 @@ import torch
 from torch.utils.data import Subset, TensorDataset
 
 import oracle
+from _pools import dev_rows, host
 from oracle import reference_alg as ra
 from topology_aware_learning_amd import ops
 from topology_aware_learning_amd.arena import ModelPool, StateLayout
@@ -118,13 +119,14 @@ def test_round_bf16_vs_oracle(cuda, graph, c4, lds, mode):
     except ops._lib.TalError:  # a row alone does not fit this budget
         assert lds < 64 * 1024
         return
-    pin = _as_torch(pool, cuda)
-    pout = torch.zeros_like(pin)
-    ops.round_bf16(pin, pout, plan, mode=mode)
-    assert np.array_equal(_bits(pout), ref)
-    if plan.single_group:  # in place: snapshot-safe with one group (the tail by the staged kernel)
-        ops.round_bf16(pin, pin, plan, mode=mode)
-        assert np.array_equal(_bits(pin), ref)
+    for pad in (True, False):  # ModelPool's row stride (vector kernel + tail) / odd rows (scalar)
+        pin = dev_rows(pool, cuda, pad)
+        pout = torch.zeros_like(pin)
+        ops.round_bf16(pin, pout, plan, n=n, mode=mode)
+        assert np.array_equal(host(pout, n), ref), pad
+        if plan.single_group:  # in place: snapshot-safe with one group (the tail by the staged kernel)
+            ops.round_bf16(pin, pin, plan, n=n, mode=mode)
+            assert np.array_equal(host(pin, n), ref), pad
 
 
 def test_round_bf16_padded_rows(cuda):

@@ -11,6 +11,7 @@ import pytest
 import torch
 
 import oracle
+from _pools import dev_rows, host
 from oracle import reference_alg as ra
 from topology_aware_learning_amd import ops, synth
 from topology_aware_learning_amd.arena import ModelPool, StateLayout
@@ -207,13 +208,13 @@ def test_round_f32_vs_oracle(cuda, graph, n, c4, lds, dense):
     ref = oracle.round_f32(pool, row_ptr, col, w, out_rows)
     plan = ops.build_plan(row_ptr, col, w, out_rows, c4=c4, lds_bytes=lds, dense=dense)
     assert plan.info.dense_rb == dense
-    pin = torch.from_numpy(pool).to(cuda)
+    pin = dev_rows(pool, cuda)  # rows strided like ModelPool's: the vector kernel + scalar tail
     pout = torch.zeros_like(pin)
-    ops.round_f32(pin, pout, plan)
-    assert _bits_equal(pout.cpu().numpy(), ref)
+    ops.round_f32(pin, pout, plan, n=n)
+    assert _bits_equal(host(pout, n), ref)
     if plan.single_group:  # in place is snapshot-safe with one group
-        ops.round_f32(pin, pin, plan)
-        assert _bits_equal(pin.cpu().numpy(), ref)
+        ops.round_f32(pin, pin, plan, n=n)
+        assert _bits_equal(host(pin, n), ref)
 
 
 _NARROW_GRAPHS = {
@@ -226,11 +227,14 @@ _NARROW_GRAPHS = {
 }
 
 
+@pytest.mark.parametrize("pad", [True, False], ids=["vec", "scalar"])
 @pytest.mark.parametrize("c4,lds", [(16, 160 * 1024), (32, 160 * 1024), (16, 80 * 1024), (32, 24 * 1024)])
 @pytest.mark.parametrize("n", [4099, 70001])
 @pytest.mark.parametrize("graph", list(_NARROW_GRAPHS))
-def test_round_narrow_vs_oracle(cuda, graph, n, c4, lds):
-    """Narrow-tile kernel (c4 16 / 32: 64/c4 rows per wavefront, per-lane plan from LDS)."""
+def test_round_narrow_vs_oracle(cuda, graph, n, c4, lds, pad):
+    """Narrow-tile kernel (c4 16 / 32: 64/c4 rows per wavefront, per-lane plan from LDS).  pad:
+    rows strided by a multiple of 64 elements (the narrow kernel computes the float4 body, the
+    scalar kernel the n % 4 tail) or contiguous odd rows (all by the scalar kernel)."""
     g = _NARROW_GRAPHS[graph]()
     orders, ws = _graph_csr(g, "softmax" if graph in ("regular", "gnp", "sbm") else "unweighted")
     rows = len(orders)
@@ -246,19 +250,19 @@ def test_round_narrow_vs_oracle(cuda, graph, n, c4, lds):
         return
     assert plan.info.c4 == c4 and plan.info.dense_rb == 0
     assert ops.round_kernel_name(plan.info) == "k_round_f32_narrow"
-    pin = torch.from_numpy(pool).to(cuda)
+    pin = dev_rows(pool, cuda, pad)
     pout = torch.zeros_like(pin)
-    ops.round_f32(pin, pout, plan)
-    assert _bits_equal(pout.cpu().numpy(), ref)
-    ops.round_f32(pin, pout, plan, mode=ops.MODE_FMA)
+    ops.round_f32(pin, pout, plan, n=n)
+    assert _bits_equal(host(pout, n), ref)
+    ops.round_f32(pin, pout, plan, n=n, mode=ops.MODE_FMA)
     m = max(len(o) for o in orders)
     fin = np.isfinite(ref)
     tol = m * 2.0 ** -24 * np.abs(np.where(np.isfinite(pool), pool, 0)).max() + 1e-30
-    got = pout.cpu().numpy()
+    got = host(pout, n)
     assert np.max(np.abs(got[fin] - ref[fin])) <= tol
     if plan.single_group:
-        ops.round_f32(pin, pin, plan)
-        assert _bits_equal(pin.cpu().numpy(), ref)
+        ops.round_f32(pin, pin, plan, n=n)
+        assert _bits_equal(host(pin, n), ref)
 
 
 @pytest.mark.parametrize("sign", [1.0, -1.0])
@@ -282,26 +286,26 @@ def test_round_narrow_row_uniform_weights_signed_zero(cuda, sign):
     for c4 in (16, 32):
         plan = ops.build_plan(row_ptr, col, w, out_rows, c4=c4, lds_bytes=80 * 1024)
         assert plan.info.narrow_roww == 1
-        pin = torch.from_numpy(pool).to(cuda)
+        pin = dev_rows(pool, cuda)  # the narrow (ROWW) kernel takes the body, the scalar one the tail
         pout = torch.zeros_like(pin)
-        ops.round_f32(pin, pout, plan)
-        assert _bits_equal(pout.cpu().numpy(), ref), c4
+        ops.round_f32(pin, pout, plan, n=n)
+        assert _bits_equal(host(pout, n), ref), c4
         bits = oracle.f32_to_bf16(pool)
         refb = oracle.round_bf16(bits, row_ptr, col, w, out_rows, exact=True)
-        pb = torch.from_numpy(bits.view(np.int16)).view(torch.bfloat16).to(cuda)
+        pb = dev_rows(bits, cuda)
         ob = torch.zeros_like(pb)
-        ops.round_bf16(pb, ob, plan)
-        assert np.array_equal(ob.cpu().view(torch.int16).numpy().view(np.uint16), refb), c4
+        ops.round_bf16(pb, ob, plan, n=n)
+        assert np.array_equal(host(ob, n), refb), c4
         # FMA mode: the accumulator starts at -0.0 and padding is fma(w, +-0, acc); bitwise
         # against the bf16 oracle's fused chain and, for fp32, against K1-FMA row by row
         refbf = oracle.round_bf16(bits, row_ptr, col, w, out_rows, exact=False)
-        ops.round_bf16(pb, ob, plan, mode=ops.MODE_FMA)
-        assert np.array_equal(ob.cpu().view(torch.int16).numpy().view(np.uint16), refbf), c4
-        ops.round_f32(pin, pout, plan, mode=ops.MODE_FMA)
+        ops.round_bf16(pb, ob, plan, n=n, mode=ops.MODE_FMA)
+        assert np.array_equal(host(ob, n), refbf), c4
+        ops.round_f32(pin, pout, plan, n=n, mode=ops.MODE_FMA)
         chk = torch.empty(n, dtype=torch.float32, device=cuda)
         for r in range(rows):
-            ops.agg_f32([pin[j] for j in orders[r]], ws[r], chk, mode=ops.MODE_FMA)
-            assert torch.equal(chk.view(torch.int32), pout[r].view(torch.int32)), (c4, r)
+            ops.agg_f32([pin[j, :n] for j in orders[r]], ws[r], chk, mode=ops.MODE_FMA)
+            assert torch.equal(chk.view(torch.int32), pout[r, :n].view(torch.int32)), (c4, r)
 
 
 @pytest.mark.parametrize("c4", [16, 32])
@@ -324,10 +328,10 @@ def test_round_narrow_sbm256_one_group(cuda, c4):
     n = 8195
     rng = np.random.default_rng(5)
     pool = rng.standard_normal((rows, n)).astype(np.float32)
-    pin = torch.from_numpy(pool).to(cuda)
+    pin = dev_rows(pool, cuda)
     pout = torch.zeros_like(pin)
-    ops.round_f32(pin, pout, plan)
-    assert _bits_equal(pout.cpu().numpy(), oracle.round_f32(pool, row_ptr, col, w, out_rows))
+    ops.round_f32(pin, pout, plan, n=n)
+    assert _bits_equal(host(pout, n), oracle.round_f32(pool, row_ptr, col, w, out_rows))
 
 
 _STREAM_GRAPHS = {
@@ -354,13 +358,13 @@ def test_round_stream_vs_oracle(cuda, graph, n, grouping):
     ref = oracle.round_f32(pool, row_ptr, col, w, out_rows)
     plan = ops.build_stream_plan(row_ptr, col, w, out_rows, *grouping)
     assert plan.info.stream_cs in (16, 32) and ops.round_kernel_name(plan.info) == "k_round_stream"
-    pin = torch.from_numpy(pool).to(cuda)
+    pin = dev_rows(pool, cuda)
     pout = torch.zeros_like(pin)
-    ops.round_f32(pin, pout, plan)
-    assert _bits_equal(pout.cpu().numpy(), ref)
+    ops.round_f32(pin, pout, plan, n=n)
+    assert _bits_equal(host(pout, n), ref)
     if plan.single_group:
-        ops.round_f32(pin, pin, plan)
-        assert _bits_equal(pin.cpu().numpy(), ref)
+        ops.round_f32(pin, pin, plan, n=n)
+        assert _bits_equal(host(pin, n), ref)
 
 
 def test_round_stream_large_and_fma(cuda):
@@ -428,11 +432,11 @@ def test_round_gossip_matrix(cuda):
     rng = np.random.default_rng(21)
     X = rng.standard_normal((len(W), 10007)).astype(np.float32)
     ref = oracle.round_f32(X, row_ptr, col, w, out_rows)
-    pin = torch.from_numpy(X).to(cuda)
+    pin = dev_rows(X, cuda)
     for plan in (ops.build_plan(row_ptr, col, w, out_rows), ops.build_stream_plan(row_ptr, col, w, out_rows)):
         pout = torch.zeros_like(pin)
-        ops.round_f32(pin, pout, plan)
-        assert _bits_equal(pout.cpu().numpy(), ref)
+        ops.round_f32(pin, pout, plan, n=10007)
+        assert _bits_equal(host(pout, 10007), ref)
     bound = np.abs(W) @ np.abs(X.astype(np.float64)) * 64 * 2.0 ** -24
     assert np.all(np.abs(ref - W @ X.astype(np.float64)) <= bound)
 
@@ -607,13 +611,13 @@ def test_round_clique_through_tuner_and_i64(cuda):
     out_rows = np.arange(rows, dtype=np.int32)
     rng = np.random.default_rng(3)
     pool = rng.standard_normal((rows, 20001)).astype(np.float32)
-    pin = torch.from_numpy(pool).to(cuda)
+    pin = dev_rows(pool, cuda)
     pout = torch.zeros_like(pin)
-    plan = ops.tune_plan(row_ptr, col, w, out_rows, pin, pout)
+    plan = ops.tune_plan(row_ptr, col, w, out_rows, pin, pout, n=20001)
     assert any((c["spec"] or {}).get("clique") for c in plan.candidates)
     cp = ops.plan_from_spec(row_ptr, col, w, out_rows, {"clique": 1}).to(cuda)
-    ops.round_f32(pin, pout, cp)
-    assert _bits_equal(pout.cpu().numpy(), oracle.round_f32(pool, row_ptr, col, w, out_rows))
+    ops.round_f32(pin, pout, cp, n=20001)
+    assert _bits_equal(host(pout, 20001), oracle.round_f32(pool, row_ptr, col, w, out_rows))
     ip = rng.integers(0, 10 ** 6, size=(rows, 5)).astype(np.int64)
     ipo = torch.zeros(rows, 5, dtype=torch.int64, device=cuda)
     ops.round_i64(torch.from_numpy(ip).to(cuda), ipo, cp)
@@ -643,16 +647,16 @@ def test_round_clique_attached_rows_general(cuda, n):
     assert len(cliques) == 1 and len(cliques[0][3]) == 2 and rest == []
     plan = ops.build_clique_plan(row_ptr, col, w, out_rows)
     pool = np.random.default_rng(n).standard_normal((48, n)).astype(np.float32)
-    pin = torch.from_numpy(pool).to(cuda)
-    pout = torch.zeros(rows, n, device=cuda)
-    ops.round_f32(pin, pout, plan)
+    pin = dev_rows(pool, cuda)
+    pout = torch.zeros(rows, pin.shape[1], device=cuda)
+    ops.round_f32(pin, pout, plan, n=n)
     ref = oracle.round_f32(pool, row_ptr, col, w, out_rows, pool_out=np.zeros((rows, n), np.float32))
-    assert _bits_equal(pout.cpu().numpy(), ref)
-    ops.round_f32(pin, pout, plan, mode=ops.MODE_FMA)
+    assert _bits_equal(host(pout, n), ref)
+    ops.round_f32(pin, pout, plan, n=n, mode=ops.MODE_FMA)
     chk = torch.empty(n, device=cuda)
     for r in (rows - 2, rows - 1, 3):
-        ops.agg_f32([pin[j] for j in orders[r]], ws[r], chk, mode=ops.MODE_FMA)
-        assert torch.equal(chk.view(torch.int32), pout[r].view(torch.int32))
+        ops.agg_f32([pin[j, :n] for j in orders[r]], ws[r], chk, mode=ops.MODE_FMA)
+        assert torch.equal(chk.view(torch.int32), pout[r, :n].view(torch.int32))
 
 
 @pytest.mark.parametrize("spec", [None, {"c4": 128, "lds": 81920, "dense": 0}, {"c4": 64, "lds": 81920, "dense": 0},
@@ -669,13 +673,14 @@ def test_full_size_ring32_round_vs_reference(cuda, spec):
     rp, col, w = ra.round_csr(orders, [ra.unweighted_weights(len(o)) for o in orders])
     out_rows = np.arange(32, dtype=np.int32)
     plan = ops.default_plan(rp, col, w, out_rows) if spec is None else ops.plan_from_spec(rp, col, w, out_rows, spec)
-    pin = torch.from_numpy(f).to(cuda)
+    n = f.shape[1]  # 11,183,562: odd rows would run the scalar kernel; ModelPool's stride instead
+    pin = dev_rows(f, cuda)
     pout = torch.empty_like(pin)
     iin = torch.from_numpy(i).to(cuda)
     iout = torch.empty_like(iin)
-    ops.round_f32(pin, pout, plan)
+    ops.round_f32(pin, pout, plan, n=n)
     ops.round_i64(iin, iout, plan)
-    got, igot = pout.cpu().numpy(), iout.cpu().numpy()
+    got, igot = host(pout, n), iout.cpu().numpy()
     for r, row in enumerate(RING32["rows"]):
         assert hashlib.sha256(got[r].tobytes()).hexdigest() == row["sha256_f32"], r
         assert hashlib.sha256(igot[r].tobytes()).hexdigest() == row["sha256_i64"], r

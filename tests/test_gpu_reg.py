@@ -15,6 +15,7 @@ import pytest
 import torch
 
 import oracle
+from _pools import dev_rows, host
 from oracle import reference_alg as ra
 from topology_aware_learning_amd import ops
 
@@ -72,10 +73,12 @@ def test_reg_round_exact_vs_oracle(cuda, graph, n, weights):
     assert plan is not None and plan.max_src <= 64
     rng = np.random.default_rng(n + rows)
     pool = _pool(rng, rows, n, special=True)
-    pin = torch.from_numpy(pool).to(cuda)
-    pout = torch.full_like(pin, float("nan"))
-    ops.round_f32(pin, pout, plan)
-    assert _bits_equal(pout.cpu().numpy(), oracle.round_f32(pool, row_ptr, col, w, out_rows))
+    ref = oracle.round_f32(pool, row_ptr, col, w, out_rows)
+    for pad in (True, False):  # even row stride (K3r) / odd n contiguous (K3r or the full plan)
+        pin = dev_rows(pool, cuda, pad)
+        pout = torch.full_like(pin, float("nan"))
+        ops.round_f32(pin, pout, plan, n=n)
+        assert _bits_equal(host(pout, n), ref), pad
 
 
 def test_reg_round_groups_use_every_register_block():
@@ -102,10 +105,10 @@ def test_reg_round_each_block_count(cuda, cap):
     plan = ops.build_reg_plan(row_ptr, col, w, out_rows, max_src=cap)
     assert plan is not None and (plan.max_src + 15) // 16 == cap // 16
     pool = _pool(np.random.default_rng(cap), rows, 3001)
-    pin = torch.from_numpy(pool).to(cuda)
+    pin = dev_rows(pool, cuda)  # an even row stride: K3r itself (odd rows take the full plan)
     pout = torch.zeros_like(pin)
-    ops.round_f32(pin, pout, plan)
-    assert _bits_equal(pout.cpu().numpy(), oracle.round_f32(pool, row_ptr, col, w, out_rows))
+    ops.round_f32(pin, pout, plan, n=3001)
+    assert _bits_equal(host(pout, 3001), oracle.round_f32(pool, row_ptr, col, w, out_rows))
 
 
 @pytest.mark.parametrize("graph", ["sbm256", "regular40"])

@@ -3325,6 +3325,15 @@ std::vector<int32_t> bc_pass_records(const int32_t* row_ptr_host, int64_t r0, in
 
 constexpr int64_t bc_lds_bytes(int64_t ns, int c4) { return (ns + 1) * c4 * 16; }
 
+// Largest staging (float4 loads per tile) a broadcast-form launch takes: J loads per lane of its
+// 64 x waves threads (launch_round_bcast_nt: J <= 8 at 512 threads, 6 at 768, 4 at 1024 with
+// two workgroups per CU, 8 at 1024 with one and c4 = 32), at most 4096 at c4 = 16 / 8192 at 32.
+constexpr int64_t bc_max_loads(int c4, int waves, int wg_per_cu) {
+  const int64_t j = waves == 16 ? (wg_per_cu == 1 && c4 == 32 ? 8 : 4) : waves == 12 ? 6 : 8;
+  const int64_t cap = c4 == 32 ? 8192 : 4096;
+  return j * 64 * waves < cap ? j * 64 * waves : cap;
+}
+
 // Lay the plan blob out (see tal_round_plan_info).  rb = dense row-block size (0 = sparse
 // form only, -1 = dense when it saves LDS reads); stream_cs > 0 pads each block's entries
 // chunk by chunk for the streamed kernel.
@@ -3814,9 +3823,8 @@ int32_t round_plan_build(int32_t rows, const int32_t* row_ptr_host, const int32_
     // within the budget; the staged scalar tail kernel within the hardware's 160 KiB
     if (bc_waves > 0) {
       std::vector<std::vector<int32_t>> per_wave;
-      // staging: at most 4096 float4 loads per tile at c4 = 16 (J <= 4 at 1024 threads, 8 at
-      // 512), 8192 at c4 = 32 (J = 8 at 1024 threads: one workgroup per CU)
-      return bc_lds_bytes(ns, c4) <= lds_bytes && ns * c4 <= (c4 == 32 ? 8192 : 4096) && sliced <= 160 * 1024 &&
+      // staging: what the form's launch takes (bc_max_loads)
+      return bc_lds_bytes(ns, c4) <= lds_bytes && ns * c4 <= bc_max_loads(c4, bc_waves, bc_wg) && sliced <= 160 * 1024 &&
              bc_deal(bc_pass_records(row_ptr_host, r0, nr, false), bc_waves, kBcRecPerWg / bc_waves, &per_wave);
     }
     const int64_t narrow = static_cast<int64_t>(
