@@ -14,5 +14,5 @@ grep '^{' $OUT/bench.log | python -c "import json,sys; d=json.loads(sys.stdin.re
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c3_trace -o trace -- \
   python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > $OUT/c3_trace.log 2>&1 || { echo FAIL c3_trace; tail -20 $OUT/c3_trace.log; exit 1; }
-tail -1 $OUT/c3_trace.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print({k: d[k] for k in ('value','ms_per_step','parity')}, d['roofline']['frac'], d['roofline']['kernel_ms'])"
+grep "^{" $OUT/c3_trace.log | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print({k: d[k] for k in ('value','ms_per_step','parity')}, d['roofline']['frac'], d['roofline']['kernel_ms'])"
 echo EXIT 0
