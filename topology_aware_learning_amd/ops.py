@@ -646,7 +646,7 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
                 p = build_plan(row_ptr, col, w, out_row, c4=c4, lds_bytes=LDS_BUDGETS[-1], bcast=waves, bcast_wg=wg)
             except _lib.TalError:
                 continue
-            key = (("bcast", waves, wg), p.info.n_groups, p.info.total_src, 0, p.info.max_src, 0)
+            key = (("bcast", c4, waves, wg), p.info.n_groups, p.info.total_src, 0, p.info.max_src, 0)
             if all(key != k for k, _ in cands):
                 cands.append((key, p))
     for max_rows, max_src in (() if bf16 else STREAM_GROUPINGS):
