@@ -1052,9 +1052,9 @@ __device__ __forceinline__ void wait_vm_barrier(int n) {
 
 // ---- broadcast form (narrow_bcast, tal_round_plan_build_bcast) ---------------------------
 // A wavefront's plan is a program of records held in VGPRs for the whole launch: record lane L
-// = {LDS byte offset, fp32 weight bits} of operand 16c + L % 16 of row L / C4 of a pass.  Operand
-// u reaches the 16 lanes of its DPP row (a C4 = 16 row group; half of one at C4 = 32, whose two
-// halves hold the same record) by `row_newbcast:u`, a VALU move, so the row loop reads only
+// = {LDS byte offset, fp32 weight bits} of operand 16c + L % 16 of row L / 16 of a pass (4 rows;
+// at C4 = 32 each lane computes two chunks, bc2_record).  Operand u reaches the 16 lanes of its
+// DPP row (one row of the pass) by `row_newbcast:u`, a VALU move, so the row loop reads only
 // data from LDS: no slot or weight read and no LDS round trip between a batch's slot word and
 // its data reads (the addresses of a whole record are known when the record is).
 constexpr int kBcRecPerWg = 128;  // records per workgroup; a wavefront holds 128 / waves of them
