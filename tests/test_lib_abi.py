@@ -50,6 +50,30 @@ def test_error_status_and_message():
     assert L.tal_cosine_scratch_bytes(None, 1) == -1
 
 
+def test_cosine_plan_threads_word():
+    """The cosine plan carries torch's intra-op thread count (header word 2): 1 after build,
+    set by tal_cosine_plan_set_threads within 1..1024; an unbuilt plan or a count out of range
+    is refused."""
+    import numpy as np
+
+    from topology_aware_learning_amd import ops
+
+    plan = ops.build_cosine_plan([(0, 768, 3, 256), (196608 * 3, 768, 1, 1)])
+    assert plan.host[2] == 1 and plan.threads == 1
+    plan8 = ops.build_cosine_plan([(0, 768, 3, 256)], threads=8)
+    assert plan8.host[2] == 8
+    L = _lib.load()
+    P64 = ctypes.POINTER(ctypes.c_int64)
+    for bad in (0, -3, 1025):
+        assert L.tal_cosine_plan_set_threads(plan.host.ctypes.data_as(P64), bad) == _lib.TAL_ERR_INVALID
+        assert b"threads" in L.tal_last_error()
+    blank = np.zeros(8, dtype=np.int64)
+    assert L.tal_cosine_plan_set_threads(blank.ctypes.data_as(P64), 4) == _lib.TAL_ERR_INVALID
+    assert L.tal_cosine_plan_set_threads(None, 4) == _lib.TAL_ERR_INVALID
+    assert L.tal_cosine_plan_set_threads(plan.host.ctypes.data_as(P64), 1024) == _lib.TAL_OK
+    assert plan.host[2] == 1024
+
+
 def test_halo_exchange_argument_errors():
     """The halo section's entry points validate before touching a GPU or RCCL."""
     L = _lib.load()
