@@ -11,7 +11,7 @@ Python plus the aggregation.  Also
 times RoundExecutor(pool).run directly on the round (its default plan, in place) against the
 bench's K1 floor (64 x one K1 call).  One JSON line per measurement.
 
-usage: python tools/dropin_rate.py [rounds] [--profile[=per_call]]   (--profile: cProfile of the
+usage: python tools/dropin_rate.py [rounds] [--profile[=per_call]] [--switch-us=N]   (--profile: cProfile of the
 batched rounds only, or of the per-call rounds with =per_call; top functions by cumulative and by
 own time)"""
 import json
@@ -33,6 +33,10 @@ import torch  # noqa: E402
 
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    sw = [a for a in sys.argv[1:] if a.startswith("--switch-us=")]
+    if sw:  # A/B probe: the interpreter's thread switch interval (default 5000 us)
+        sys.setswitchinterval(int(sw[0].split("=", 1)[1]) * 1e-6)
+        print(json.dumps(dict(switch_interval_us=int(sw[0].split("=", 1)[1]))), flush=True)
     rounds = int(args[0]) if args else 5
     prof_arg = [a for a in sys.argv[1:] if a.startswith("--profile")]
     profile = bool(prof_arg)
