@@ -272,7 +272,8 @@ def test_prox_term_matches_torch_loop(cuda, k):
             ref = ref + (w - wt).norm(2)
     ref.backward()
     g_ref = [p.grad.clone() for c in cl for p in c.model.parameters()]
-    assert abs(float(fused) - float(ref)) <= 1e-5 * abs(float(ref)) + 1e-6
+    fused_v, ref_v = float(fused.detach()), float(ref.detach())
+    assert abs(fused_v - ref_v) <= 1e-5 * abs(ref_v) + 1e-6
     for a, b in zip(g_fused, g_ref):
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-6)
 
