@@ -894,15 +894,8 @@ __host__ __device__ constexpr size_t narrow_lds_bytes(int64_t max_src, int64_t m
 // runs on the scalar unit; one 16-B record per row (rows padded to whole passes; a padding row
 // reads its pass's first row and stores nothing): {LDS byte address of the row's first slot
 // word, batches of four slots, fp32 weight bits, pool_out row or -1}.
-// Rows per ROWW pass.  A/B probe TAL_PROBE_ROWW_X2 (not the product): at c4 = 16 a pass is 8
-// rows of 8 lanes, each lane two float4 chunks (cl, cl + 8), two workgroups per CU kept.
-#ifdef TAL_PROBE_ROWW_X2
-__host__ __device__ constexpr int roww_rpw(int c4) { return c4 == 16 ? 8 : 64 / c4; }
-#else
-__host__ __device__ constexpr int roww_rpw(int c4) { return 64 / c4; }
-#endif
 __host__ __device__ constexpr int64_t narrow_roww_records(int64_t nr, int c4) {
-  return (nr + roww_rpw(c4) - 1) / roww_rpw(c4) * roww_rpw(c4);
+  return (nr + 64 / c4 - 1) / (64 / c4) * (64 / c4);
 }
 __host__ __device__ constexpr size_t narrow_roww_lds_bytes(int64_t ns, int64_t nr, int64_t nslots, int c4) {
   return static_cast<size_t>((ns + 2) * c4 * 16 + narrow_roww_records(nr, c4) * 16 + (nslots + 8) * 2 + 16);
@@ -920,7 +913,7 @@ __device__ __forceinline__ NarrowLds stage_narrow_roww(const PlanView& p, int g,
   const int e_beg = p.nrow_ptr[r_beg];  // a multiple of 4 (every run is)
   const int ne = p.nrow_ptr[r_beg + L.nr] - e_beg;
   const int ns = p.grp_src_ptr[g + 1] - p.grp_src_ptr[g];
-  constexpr int kRpw = roww_rpw(C4);
+  constexpr int kRpw = 64 / C4;
   const int nrec = static_cast<int>(narrow_roww_records(L.nr, C4));
   // offsets in 32-bit words from s_data (index arithmetic keeps the LDS address space: a
   // pointer rebuilt from an integer would become a generic one and every read a flat load)
@@ -1029,46 +1022,6 @@ __device__ __forceinline__ float4 narrow_row_roww(uint4 rc, uint32_t base) {
     asm volatile("" : "+v"(e.x), "+v"(e.y));
   }
   return narrow_row_tail<T, EXACT>(acc, w, e, base, rem);
-}
-
-// Probe (TAL_PROBE_ROWW_X2): one ROWW row over two chunks (cl and cl + 8 of a 16-chunk tile,
-// the second 128 B further): one address per slot serves both; each half of a batch (two
-// slots, four data reads) is read then computed, so the data in flight stays at four float4.
-template <typename T, bool EXACT>
-__device__ __forceinline__ void narrow_row_roww2(uint4 rc, uint32_t base, float4& acc0, float4& acc1) {
-  const int nb = __builtin_amdgcn_readfirstlane(static_cast<int>(rc.y & 0xffffu));
-  const int rem = __builtin_amdgcn_readfirstlane(static_cast<int>(rc.y >> 16));
-  const float w = __uint_as_float(rc.z);
-  uint32_t q = rc.x;
-  acc0 = make_float4(-0.f, -0.f, -0.f, -0.f);
-  acc1 = acc0;
-  uint2 e = lds_u2(q);
-  for (int b = 0; b < nb; ++b) {
-    const uint32_t a0 = slot_addr_lo(e.x, base), a1 = slot_addr_hi(e.x, base);
-    const uint32_t a2 = slot_addr_lo(e.y, base), a3 = slot_addr_hi(e.y, base);
-    float4 x0 = lds_f4(a0), y0 = lds_f4(a0 + 128u), x1 = lds_f4(a1), y1 = lds_f4(a1 + 128u);
-    asm("v_add_u32 %0, 8, %0" : "+v"(q));
-    e = lds_u2(q);  // next batch (or the read-ahead pad), in flight with this batch's data reads
-    acc0 = next4t<T, EXACT>(acc0, w, x0);
-    acc1 = next4t<T, EXACT>(acc1, w, y0);
-    acc0 = next4t<T, EXACT>(acc0, w, x1);
-    acc1 = next4t<T, EXACT>(acc1, w, y1);
-    __builtin_amdgcn_sched_barrier(0);
-    x0 = lds_f4(a2), y0 = lds_f4(a2 + 128u), x1 = lds_f4(a3), y1 = lds_f4(a3 + 128u);
-    acc0 = next4t<T, EXACT>(acc0, w, x0);
-    acc1 = next4t<T, EXACT>(acc1, w, y0);
-    acc0 = next4t<T, EXACT>(acc0, w, x1);
-    acc1 = next4t<T, EXACT>(acc1, w, y1);
-    asm volatile("" : "+v"(e.x), "+v"(e.y));
-  }
-#pragma unroll
-  for (int u = 0; u < 3; ++u) {  // the 1-3 operand tail from the word read last
-    if (rem <= u) break;  // wave-uniform
-    const uint32_t word = u < 2 ? e.x : e.y;
-    const uint32_t a = u == 1 ? slot_addr_hi(word, base) : slot_addr_lo(word, base);
-    acc0 = next4t<T, EXACT>(acc0, w, lds_f4(a));
-    acc1 = next4t<T, EXACT>(acc1, w, lds_f4(a + 128u));
-  }
 }
 
 // one 16-B-per-lane global->LDS DMA (K3s): 64 lanes x 16 B, lane-linear from LDS byte address M0
@@ -1369,8 +1322,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   constexpr int kLps = W16 ? C4 / 2 : C4;    // staging lanes per source and tile
   // BC at C4 = 32: the two-chunk form (4 rows of 16 lanes per pass, like C4 = 16)
   constexpr bool kX2 = BC && C4 == 32;
-  constexpr bool kRX2 = ROWW && roww_rpw(C4) != 64 / C4;  // probe: 8-lane ROWW rows, two chunks
-  constexpr int kRpw = kX2 ? 4 : ROWW ? roww_rpw(C4) : 64 / C4;
+  constexpr int kRpw = kX2 ? 4 : 64 / C4;
   constexpr int kW = NT / 64;
   extern __shared__ float4 s_data[];
   const int g = blockIdx.y;
@@ -1381,9 +1333,8 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   const int c = threadIdx.x % kLps;  // staging: the lane's chunk (W16: chunk pair) of its source
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-  constexpr int kLpr = 64 / kRpw;  // lanes per row
-  const int sub = lane / kLpr;
-  const int cl = lane % kLpr;
+  const int sub = kX2 ? lane / 16 : lane / C4;
+  const int cl = kX2 ? lane % 16 : lane % C4;
   // Staging is branch-free, so that the compiler's wait analysis sees every load land in its
   // register unconditionally (a conditional load made it wait for each load before issuing the
   // next: four serial HBM round trips per tile).  A lane past the group's sources reloads
@@ -1521,16 +1472,6 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
         const int set = narrow_set(k, wave, kW);
         if (set >= n_sets) continue;  // wave-uniform
         const uint4 rc = lds_u4(rec_lane + 16u * static_cast<uint32_t>(set * kRpw));
-        if constexpr (kRX2) {
-          float4 acc0, acc1;
-          narrow_row_roww2<T, EXACT>(rc, col_base, acc0, acc1);
-          if (static_cast<int32_t>(rc.w) >= 0) {
-            const int64_t o = static_cast<int64_t>(static_cast<int32_t>(rc.w)) * ld_out4;
-            if (col < n4) Io<T>::st(pout, o + col, acc0);
-            if (col + kLpr < n4) Io<T>::st(pout, o + col + kLpr, acc1);
-          }
-          continue;
-        }
 #ifdef TAL_PROBE_NOCOMP  // A/B probe (tools/gpu_k3n_probe.sh): stores without the row arithmetic
         const float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #else
@@ -3343,7 +3284,7 @@ int64_t roww_padded_slots(const int32_t* row_ptr_host, int64_t r0, int64_t nr, i
   for (int64_t i = 0; i < nr; ++i)
     (*batches)[i] = (row_ptr_host[r0 + i + 1] - row_ptr_host[r0 + i] + 3) / 4;
   std::sort(batches->begin(), batches->end(), std::greater<int32_t>());
-  const int64_t rpw = roww_rpw(c4);
+  const int64_t rpw = 64 / c4;
   int64_t slots = 0;
   for (int64_t i = 0; i < nr; i += rpw) slots += 4LL * (*batches)[i] * std::min(rpw, nr - i);
   return slots;
@@ -3566,7 +3507,7 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
           int32_t wb;
           memcpy(&wb, &wf, 4);
           nrw.push_back(wb);
-          const int32_t lead = grp_row_ptr[g] + (r - grp_row_ptr[g]) / roww_rpw(c4) * roww_rpw(c4);
+          const int32_t lead = grp_row_ptr[g] + (r - grp_row_ptr[g]) / (64 / c4) * (64 / c4);
           const int64_t nb = (row_ptr_host[lead + 1] - row_ptr_host[lead] + 3) / 4;
           const size_t start = nsl.size();
           for (int32_t k = k0; k < k1; ++k) nsl.push_back(static_cast<uint16_t>(slot[k] * c4));
