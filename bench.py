@@ -78,10 +78,12 @@ def parse():
     p.add_argument("--weights", default="unweighted", choices=["unweighted", "degcent"],
                    help="unweighted_module_avg (1/M, the metric's config) or centrality_module_avg "
                         "with softmax(10 x degree centrality): per-operand weights")
-    p.add_argument("--halo-transport", default="device", choices=["device", "cabi"],
-                   help="N > 1, halo exchange over nccl: torch.distributed's RCCL (device) or the "
-                        "library's own communicator and gather kernel (cabi, include/tal_agg.h; "
-                        "experimental: not yet run across GPUs)")
+    p.add_argument("--transport", "--halo-transport", dest="halo_transport", default="device",
+                   choices=["device", "cabi"],
+                   help="N > 1 over nccl, either exchange: torch.distributed's RCCL (device) or the "
+                        "library's own communicator (cabi, include/tal_agg.h: tal_comm_* / "
+                        "tal_halo_pack / tal_halo_exchange; the all-to-alls as groups of per-peer "
+                        "sends / receives)")
     p.add_argument("--exchange", default="auto", choices=["auto", "halo", "transpose"],
                    help="N > 1: neighbor models by RCCL P2P (halo) or column blocks by all-to-all "
                         "(transpose); auto = fewer link bytes (transposed.choose_exchange)")
@@ -118,6 +120,51 @@ def round_spec(n_devices: int, degree: int, seed: int = 0, kind: str = "random",
         cent = nx.degree_centrality(g)
         return orders, [tw.centrality(o, cent, True, 10.0) for o in orders]
     return orders, [tw.unweighted(len(o)) for o in orders]
+
+
+SEED_BASE = 9300  # device i's model = synth.synth_state_dict(layout, SEED_BASE + i) (config 3's fixture seeds)
+
+
+def reference_fixture(args, orders, weights):
+    """(seed base, reference) for rowcheck.check_round: the reference's own per-model sha256
+    when this workload is one tests/golden's full-round fixtures cover (BASELINE configs 3, 4
+    and 5, made by the reference's apps on exactly these seeded inputs; config 5 per entry
+    group), else (SEED_BASE, None) - K1 on regenerated operands.  The fixture's operand order
+    must be this run's (a mismatch is a bug, not a skipped check)."""
+    from topology_aware_learning_amd import synth
+
+    if args.max_params or args.mode != "exact":
+        return SEED_BASE, None
+    key = (args.graph, len(orders), args.model, args.dtype, args.weights)
+    name = {("random", 64, "resnet50", "f32", "unweighted"): "full_round_c3_resnet50_rr64.json",
+            ("barbell", 128, "resnet50", "f32", "unweighted"): "full_round_c4_resnet50_barbell.json"}.get(key)
+    if key[:3] == ("sbm", 256, "vit_b16"):
+        name = "full_round_c5_vit_sbm256.json"
+    if name is None or (args.graph == "random" and args.degree != 8):
+        return SEED_BASE, None
+    path = ROOT / "tests" / "golden" / name
+    fx = json.loads(path.read_text())
+    base = int(fx["seeds"][0])
+    if fx["seeds"] != list(range(base, base + len(orders))):
+        raise AssertionError(f"{name}: seeds are not seed_base + device id")
+    if "rows" in fx:  # configs 3 / 4: one digest per segment per model
+        if [r["order"] for r in fx["rows"]] != [list(o) for o in orders]:
+            raise AssertionError(f"{name}: operand order differs from this run's graph")
+        expected = {"f32": {i: [r["sha256_f32"]] for i, r in enumerate(fx["rows"])},
+                    "i64": {i: [r["sha256_i64"]] for i, r in enumerate(fx["rows"])}}
+        nf, ni = synth.layout_counts(synth.get_layout(args.model))
+        return base, dict(name=name, expected=expected, ranges={"f32": [(0, nf)], "i64": [(0, ni)]})
+    fn = "unweighted_module_avg" if args.weights == "unweighted" else "centrality_module_avg"
+    run = next((r for r in fx["runs"] if r["dtype"] == args.dtype and r["fn"] == fn), None)
+    if run is None:
+        return SEED_BASE, None
+    if fx["orders"] != [list(o) for o in orders]:
+        raise AssertionError(f"{name}: operand order differs from this run's graph")
+    seg = "f32" if args.dtype == "f32" else "b16"
+    groups = run["groups"]
+    expected = {seg: {i: [run["sha256"][i][str(g)] for g in groups] for i in range(len(orders))}}
+    ranges = {seg: [(fx["groups"][g]["start"], fx["groups"][g]["end"]) for g in groups]}
+    return base, dict(name=name + f" {args.dtype} {fn}", expected=expected, ranges=ranges)
 
 
 def fill_pool(pool, seed: int):
@@ -252,7 +299,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from topology_aware_learning_amd import ops, synth
+    from topology_aware_learning_amd import ops, rowcheck, synth
     from topology_aware_learning_amd.arena import ModelPool, StateLayout, select_pool_pair
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -288,6 +335,9 @@ def main():
     orders, weights = round_spec(n_dev_total, args.degree, kind=args.graph, weights=args.weights)
     n_dev_total = len(orders)
     M = max(len(o) for o in orders)
+    # every device's model is synth's seeded model of its global id, so any rank can check any
+    # output row without trusting what the exchange delivered (rowcheck)
+    seed_base, reference = reference_fixture(args, orders, weights)
 
     if not sharded:
         from topology_aware_learning_amd import ops as _ops
@@ -344,7 +394,7 @@ def main():
                              note="two pools fit in 70 % of the free HBM: no other candidate to time")
         del cand
         torch.cuda.empty_cache()  # the candidates not kept
-        fill_pool(pin, 1234)
+        rowcheck.fill_owned(pin, lay, range(rows), seed_base)
         log(f"placement {placement}")
         if tune:  # time every plan candidate on the pools the steps use (once per topology)
             plan = _ops.tune_plan(row_ptr, col, w, out_rows, seg(pin), seg(pout), n=n_float, mode=mode)
@@ -373,6 +423,11 @@ def main():
                 bad_rows.append(r)
         parity_ok = not bad_rows
         del chk, chk_i
+        ref_check = None
+        if reference is not None:  # the round's outputs against the reference's own digests
+            ref_check = rowcheck.check_round(pout, range(rows), lay, orders, weights, seed_base, mode,
+                                             reference=reference)
+            parity_ok = parity_ok and ref_check["rows_differing"] == 0
         tol = bf16_tolerance(pin, pout, orders[0], weights[0], n_float, dev) if bf16 else None
 
         log(f"parity {parity_ok} ({len(bad_rows)} rows differ); timing {args.steps} steps")
@@ -403,6 +458,7 @@ def main():
                                                   spec=plan.spec),
             per_call_equivalent_GBps=per_call_bytes / (k_ms * 1e-3) / 1e9,
             parity_k3_vs_k1=dict(rows_checked=rows, rows_differing=len(bad_rows), first_bad=bad_rows[:8]),
+            parity_vs_reference=ref_check,
             valu=valu_floor(len(col), rows, n_float, k_ms, mode))
         if tol is not None:
             result_extra["bf16_vs_fp32_reference_row0"] = tol
@@ -420,14 +476,22 @@ def main():
         sr = make_round(layout, orders, weights, rank, world, dev, exchange=args.exchange, mode=mode,
                         tune=not args.no_tune,
                         transport="host" if args.dist_backend == "gloo" else args.halo_transport)
-        fill_pool(sr.pool_a, 1234 + rank)
+        rowcheck.fill_owned(sr.pool_a, lay, sr.own_ids, seed_base)
         sr.step()
-        # spot check: one output row (halo) / row block (transpose) of this rank == K1 on its
-        # operands as received, bitwise
+        # every output row this rank owns, against the reference's digests or K1 on operands
+        # regenerated from their seeds - never on what the exchange delivered (rowcheck)
+        chk = rowcheck.check_round(sr.own_rows(), sr.own_ids, lay, orders, weights, seed_base, mode,
+                                   reference=reference)
         cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # collectives' scalars
-        ok = torch.tensor([int(sr.spot_check())], device=cdev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        parity_dist = bool(ok.item())
+        cnt = torch.tensor([chk["rows_checked"], chk["rows_differing"]], dtype=torch.int64, device=cdev)
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+        bad_all = [None] * world
+        dist.all_gather_object(bad_all, chk["first_bad"])
+        rows_checked, rows_differing = int(cnt[0].item()), int(cnt[1].item())
+        parity_dist = rows_differing == 0 and rows_checked == n_dev_total
+        parity_rows = dict(rows_checked=rows_checked, rows_differing=rows_differing,
+                           first_bad=sorted(j for b in bad_all for j in b)[:8], reference=chk["reference"],
+                           devices=n_dev_total)
         for _ in range(args.warmup):
             sr.step()
         torch.cuda.synchronize(dev)
@@ -454,7 +518,7 @@ def main():
         ms_step = 1e3 * el / args.steps
         chosen = model[sr.exchange_kind]
         result_extra = dict(kernel=",".join(sorted({ops.round_kernel_name(p) for p in sr.plans.values()})),
-                            exchange=sr.exchange_kind, link_bytes_in_per_round=sr.link_bytes,
+                            parity_rows=parity_rows, exchange=sr.exchange_kind, transport=sr.transport, link_bytes_in_per_round=sr.link_bytes,
                             link_GBps_in=sr.link_bytes / (el / args.steps) / 1e9,
                             bound_model=dict(per_exchange={k: {kk: (round(vv, 3) if isinstance(vv, float) else vv)
                                                                 for kk, vv in v.items()} for k, v in model.items()},

@@ -160,6 +160,8 @@ def cosine_model(a, b, segments, per_tensor: bool = False, threads: int = 1):
     per parameter in named_parameters order (arena.StateLayout.param_segments).  threads: the
     torch intra-op thread count of the reference's process (matters for tensor means over
     >= 32768 outputs only)."""
+    if not 1 <= int(threads) <= 1024:  # cosine_oracle.c MAX_THREADS (the library's limit too)
+        raise ValueError(f"threads must be in 1..1024, got {threads}")
     a = np.ascontiguousarray(a, dtype=np.float32)
     b = np.ascontiguousarray(b, dtype=np.float32)
     seg = np.ascontiguousarray(np.asarray(segments, dtype=np.int64).reshape(-1, 4))

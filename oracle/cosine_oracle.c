@@ -123,6 +123,7 @@ static float inner_sum(const float* x, int64_t n) {
 #define MAX_THREADS 1024
 static float par_sum(const float* x, int64_t n, int T) {
   if (n < GRAIN || T <= 1) return inner_sum(x, n);
+  if (T > MAX_THREADS) return NAN;  /* callers validate 1 <= T <= MAX_THREADS */
   float buf[MAX_THREADS];
   memset(buf, 0, sizeof(buf));
   int64_t nt = (n + GRAIN - 1) / GRAIN;
@@ -239,6 +240,7 @@ int64_t oracle_cosine_scratch(const int64_t* segs, int32_t nseg) {
 /* threads: torch's intra-op thread count of the reference's process (1..1024) */
 float oracle_cosine_model_t(const float* a, const float* b, const int64_t* segs, int32_t nseg, int32_t threads,
                             float* scratch, float* per_tensor) {
+  if (threads < 1 || threads > MAX_THREADS) return NAN;
   float avg = 0.f;
   for (int32_t t = 0; t < nseg; ++t) {
     const int64_t off = segs[4 * t], O = segs[4 * t + 1], I = segs[4 * t + 2], K = segs[4 * t + 3];

@@ -264,3 +264,131 @@ def test_gloo_transposed_round_class_two_rounds(tmp_path, world, chunks):
         assert np.array_equal(np.load(tmp_path / f"ci{r}.npy"), iref[own])
         if world == 1:
             assert int(np.load(tmp_path / f"clink{r}.npy")[0]) == 0
+
+
+# ------------------------------------------------------------------------------------------
+# the sharded bench's parity check (rowcheck): every owned output row against K1 on operands
+# regenerated from their seeds, so a corrupted exchange fails it where spot_check passes
+
+_RC_LAYOUT = [("w", (203,), "float32"), ("bn.running_var", (9,), "float32"),
+              ("bn.num_batches_tracked", (), "int64"), ("b", (5,), "float32")]
+
+
+def _patch_oracle_kernels(set_=setattr):
+    """Test infrastructure for a host without a GPU: the oracle in place of the kernels (K1 for
+    rowcheck / spot_check, the K3 round for the round classes); plans remember their CSR.
+    set_: setattr in a spawned worker, monkeypatch.setattr in the test process."""
+    from topology_aware_learning_amd import distributed as dd
+    from topology_aware_learning_amd import ops
+    from topology_aware_learning_amd import transposed as tr
+
+    def agg_f32(xs, w, out, mode=0, **kw):
+        out.copy_(torch.from_numpy(oracle.agg_f32([x.contiguous().numpy() for x in xs], w)))
+
+    def agg_i64(xs, w, out, **kw):
+        out.copy_(torch.from_numpy(oracle.agg_i64([x.contiguous().numpy() for x in xs], w)))
+
+    orig = ops.default_plan
+
+    def default_plan(rp, col, w, out, **kw):
+        p = orig(rp, col, w, out, **kw)
+        p._csr = (rp, col, w, out)
+        return p
+
+    def oracle_segments(layout_, seg_in, seg_out, plan, mode, n_of=None):
+        rp, col, w, out = plan._csr
+        for g, fn in (("f32", oracle.round_f32), ("i64", oracle.round_i64)):
+            n = getattr(layout_, "n_" + g) if n_of is None else n_of.get(g, 0)
+            if n:
+                x = np.ascontiguousarray(seg_in[g][:, :n].numpy())
+                res = fn(x, rp, col, w, out)
+                seg_out[g][np.asarray(out), :n] = torch.from_numpy(np.ascontiguousarray(res[np.asarray(out)]))
+
+    for mod, name, fn in ((ops, "agg_f32", agg_f32), (ops, "agg_i64", agg_i64), (ops, "default_plan", default_plan),
+                          (dd, "run_round_segments", oracle_segments), (tr, "run_round_segments", oracle_segments)):
+        set_(mod, name, fn)
+
+
+def _worker_rowcheck(rank, world, port, out_dir, exchange, corrupt):
+    import json
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _patch_oracle_kernels()
+    from topology_aware_learning_amd import distributed as dd
+    from topology_aware_learning_amd import ops, rowcheck
+    from topology_aware_learning_amd import transposed as tr
+    from topology_aware_learning_amd.arena import StateLayout
+
+    orders, ws, _, _ = problem()
+    layout = StateLayout.from_layout(_RC_LAYOUT)
+    if exchange == "halo":
+        def exch(sr):
+            for r in dd.post_exchange(sr.spec, [t for _, t, _ in sr.pool_a.segments()], None, sr.packers):
+                r.wait()
+            if corrupt and rank == 0:  # one value of the first received halo row
+                sr.pool_a.f32[len(sr.spec.own), 0] += 1.0
+            return []
+
+        sr = dd.ShardedRound(layout, orders, ws, rank, world, "cpu", exchange=exch)
+        assert sr.spec.halo
+    else:
+        sr = tr.TransposedRound(layout, orders, ws, rank, world, "cpu", chunks=1)
+        fwd = sr.forward_exchange
+
+        def forward(k=0):
+            for w in fwd(k):
+                w.wait()
+            if corrupt and rank == 0:  # one value of the first received column chunk
+                sr.segs["f32"].work_in[k][sr.local_rows, 0] += 1.0
+            return []
+
+        sr.forward_exchange = forward
+    rowcheck.fill_owned(sr.pool_a, _RC_LAYOUT, sr.own_ids, 500)
+    sr.step()
+    chk = rowcheck.check_round(sr.own_rows(), sr.own_ids, _RC_LAYOUT, orders, ws, 500, ops.MODE_EXACT)
+    with open(os.path.join(out_dir, f"rc{rank}.json"), "w") as f:
+        json.dump(dict(chk, spot=bool(sr.spot_check())), f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("exchange", ["halo", "transpose"])
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_gloo_rowcheck_catches_a_corrupted_exchange(tmp_path, exchange, corrupt):
+    """Two gloo ranks, one round of ShardedRound / TransposedRound, rowcheck on every owned
+    row: clean exchange -> every row checked, none differs; one received halo value (or one
+    all-to-all chunk value) changed -> rows differ, while spot_check - K1 on the operands as
+    received, the bench's round-4 check - still passes on every rank."""
+    import json
+
+    mp.spawn(_worker_rowcheck, args=(2, _free_port(), str(tmp_path), exchange, corrupt), nprocs=2, join=True)
+    res = [json.loads((tmp_path / f"rc{r}.json").read_text()) for r in range(2)]
+    assert sum(r["rows_checked"] for r in res) == len(problem()[0])
+    assert all(r["spot"] for r in res)
+    assert all(r["reference"].startswith("K1") for r in res)
+    differing = sum(r["rows_differing"] for r in res)
+    assert (differing > 0) == corrupt, res
+
+
+def test_rowcheck_batches_regenerated_operands(monkeypatch):
+    """check_against_k1 in batches smaller than the round (a tight budget): same verdict."""
+    _patch_oracle_kernels(monkeypatch.setattr)
+    from topology_aware_learning_amd import ops, rowcheck
+    from topology_aware_learning_amd.arena import ModelPool, StateLayout
+
+    orders, ws, _, _ = problem()
+    layout = StateLayout.from_layout(_RC_LAYOUT)
+    n = len(orders)
+    pin, pout = ModelPool(layout, n, "cpu"), ModelPool(layout, n, "cpu")
+    rowcheck.fill_owned(pin, _RC_LAYOUT, range(n), 7)
+    rp, col, w = ra.round_csr(orders, ws)
+    pout.f32[:, :layout.n_f32] = torch.from_numpy(oracle.round_f32(pin.f32[:, :layout.n_f32].numpy().copy(), rp, col, w,
+                                                                   np.arange(n)))
+    pout.i64[:, :1] = torch.from_numpy(oracle.round_i64(pin.i64[:, :1].numpy().copy(), rp, col, w, np.arange(n)))
+    for budget in (1, 6 * 4 * layout.ld_f32, 1 << 30):
+        assert rowcheck.check_against_k1(pout, range(n), _RC_LAYOUT, orders, ws, 7, ops.MODE_EXACT,
+                                         budget_bytes=budget) == []
+    pout.f32[3, 100] += 1.0
+    pout.i64[9, 0] += 1
+    assert rowcheck.check_against_k1(pout, range(n), _RC_LAYOUT, orders, ws, 7, ops.MODE_EXACT, budget_bytes=1) == [3, 9]

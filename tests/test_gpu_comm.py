@@ -154,3 +154,100 @@ def test_virtual_ranks_messages_from_cabi_pack(cuda, graph, world, dtype):
         got = _get_rows(sr.own_rows(), len(sr.spec.own), dtype)
         assert np.array_equal(got, ref[sr.spec.own].view(got.dtype))
         assert np.array_equal(sr.own_rows().i64[: len(sr.spec.own), :1].cpu().numpy(), iref[sr.spec.own])
+
+
+@pytest.mark.parametrize("graph,world,dtype,chunks", [("regular", 4, "f32", 1), ("sbm256", 8, "f32", 2),
+                                                      ("barbell60", 8, "bf16", 3), ("ring", 3, "bf16", 1)])
+def test_virtual_ranks_transposed_through_cabi_exchange(cuda, comm1, graph, world, dtype, chunks):
+    """The transposed exchange's C-ABI transport without a second GPU: `world` TransposedRounds
+    in one process; every per-peer message of both all-to-alls (forward_messages /
+    backward_messages, exactly the tensors _exchange_cabi hands to tal_halo_exchange) moves
+    through the library's RCCL communicator - a world-1 communicator sending rank p's message
+    to itself into rank r's receive buffer - two rounds, bitwise the oracle."""
+    from test_gpu_distributed import _get_rows, _graph, _put_row, _seg_setup
+
+    from oracle import reference_alg as ra
+    from topology_aware_learning_amd import ops
+    from topology_aware_learning_amd.distributed import partition_contiguous
+    from topology_aware_learning_amd.transposed import TransposedRound
+
+    import networkx as nx
+
+    g = nx.cycle_graph(13) if graph == "ring" else _graph(graph)
+    n = g.number_of_nodes()
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(n)]
+    ws = [ra.unweighted_weights(len(o)) for o in orders]
+    layout, pool, ipool = _seg_setup(dtype, n, 3)
+    owner = partition_contiguous(n, world)
+    srs = [TransposedRound(layout, orders, ws, r, world, cuda, owner=owner, chunks=chunks) for r in range(world)]
+    for sr in srs:
+        for k, gid in enumerate(sr.own):
+            _put_row(sr.pool_a, k, dtype, pool[gid], ipool[gid], cuda)
+    rp, col, w = ra.round_csr(orders, ws)
+    ref, iref = pool, ipool
+    moved = 0
+
+    def through_comm(messages, k):
+        nonlocal moved
+        for r, sr in enumerate(srs):
+            for key, _ in sr._segs_at(k):
+                recvs = messages(sr, k, key)[1]
+                for p in sr.peers():
+                    send = messages(srs[p], k, key)[0][r]
+                    assert send.shape == recvs[p].shape and send.is_contiguous() and recvs[p].is_contiguous()
+                    if send.numel():
+                        comm1.exchange([send], [recvs[p]])
+                        moved += 1
+
+    for _ in range(2):
+        for k in range(srs[0].chunks):
+            for sr in srs:
+                sr.pack(k)
+            through_comm(lambda sr, k, key: sr.forward_messages(k, key), k)
+            for sr in srs:
+                sr.compute(k)
+            through_comm(lambda sr, k, key: sr.backward_messages(k, key), k)
+            for sr in srs:
+                sr.unpack(k)
+        ref = (oracle.round_f32(ref, rp, col, w, np.arange(n)) if dtype == "f32"
+               else oracle.round_bf16(ref, rp, col, w, np.arange(n)))
+        iref = oracle.round_i64(iref, rp, col, w, np.arange(n))
+    torch.cuda.synchronize()
+    assert moved > 0
+    for sr in srs:
+        got = _get_rows(sr.own_rows(), sr.local_rows, dtype)
+        assert np.array_equal(got, ref[sr.own].view(got.dtype))
+        assert np.array_equal(sr.own_rows().i64[: sr.local_rows, :1].cpu().numpy(), iref[sr.own])
+
+
+def test_transposed_round_cabi_transport_world1(cuda, tmp_path):
+    """TransposedRound(transport="cabi") at world 1: the communicator is made through the
+    library (unique id broadcast over the torch.distributed group), the own block never enters
+    RCCL, the round equals the oracle bit for bit."""
+    import networkx as nx
+    import torch.distributed as dist
+
+    from topology_aware_learning_amd.arena import StateLayout
+    from topology_aware_learning_amd.transposed import make_round
+
+    dist.init_process_group("gloo", init_method=f"file://{tmp_path}/pg", rank=0, world_size=1)
+    try:
+        g = nx.random_regular_graph(4, 12, seed=1)
+        orders = [sorted(g.neighbors(i)) + [i] for i in range(12)]
+        weights = [[1 / len(o)] * len(o) for o in orders]
+        lay = StateLayout.from_layout([("w", (70001,), "float32"), ("b", (13,), "float32"), ("nbt", (), "int64")])
+        sr = make_round(lay, orders, weights, 0, 1, cuda, exchange="transpose", transport="cabi")
+        assert sr.transport == "cabi" and sr.exchange_kind == "transpose"
+        gen = torch.Generator(device=cuda).manual_seed(7)
+        sr.pool_a.f32.normal_(generator=gen)
+        before = sr.pool_a.f32[:, : lay.n_f32].cpu().numpy().copy()
+        sr.step()
+        torch.cuda.synchronize()
+        rp = np.cumsum([0] + [len(o) for o in orders]).astype(np.int32)
+        ref = oracle.round_f32(before, rp, np.concatenate(orders).astype(np.int32), np.concatenate(weights),
+                               np.arange(12, dtype=np.int32))
+        got = sr.pool_a.f32[:, : lay.n_f32].cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+        sr.comm.close()
+    finally:
+        dist.destroy_process_group()

@@ -219,13 +219,20 @@ def test_bench_world8_rehearsal(cuda, tmp_path, graph, model, dtype, exchange):
     d = json.loads(line[0])
     assert d["n_gpus"] == 8 and d["parity"] is True
     assert d["config"]["devices"] == {"sbm": 256, "barbell": 128, "random": 512}[graph]
+    pr = d["parity_rows"]  # every owned output row of every rank, vs K1 on regenerated operands
+    assert pr["rows_checked"] == pr["devices"] == d["config"]["devices"] and pr["rows_differing"] == 0
+    assert pr["reference"].startswith("K1")  # --max-params: no reference fixture for the cut layout
     assert d["value"] > 0 and d["link_bytes_in_per_round"] > 0
     if exchange != "auto":
         assert d["exchange"] == exchange
 
 
-@pytest.mark.parametrize("exchange,tune", [("halo", False), ("transpose", False), ("transpose", True)])
-def test_bench_sharded_one_rank_rccl(cuda, tmp_path, exchange, tune):
+@pytest.mark.parametrize("exchange,tune,model,transport", [
+    ("halo", False, "cifar10", "device"), ("transpose", False, "cifar10", "device"),
+    ("transpose", True, "cifar10", "device"), ("halo", False, "resnet50", "device"),
+    ("transpose", False, "resnet50", "device"), ("halo", False, "cifar10", "cabi"),
+    ("transpose", False, "cifar10", "cabi")])
+def test_bench_sharded_one_rank_rccl(cuda, tmp_path, exchange, tune, model, transport):
     """bench.py's sharded branch on a one-rank RCCL (backend "nccl") process group: the
     exchange's collectives (batched P2P group / all_to_all_single on device tensors, the
     spot-check all-reduce, barriers) on the real transport with nothing to move — the RCCL
@@ -238,15 +245,83 @@ def test_bench_sharded_one_rank_rccl(cuda, tmp_path, exchange, tune):
     from conftest import ROOT
 
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
-    port = 28700 + (os.getpid() % 400) + (0 if exchange == "halo" else 3) + (20 if tune else 0)
+    port = 28700 + (os.getpid() % 400) + (0 if exchange == "halo" else 3) + (20 if tune else 0) + (40 if model == "resnet50" else 0) + (60 if transport == "cabi" else 0)
+    # cifar10: a 16-device 4-regular graph (rowcheck: K1 on regenerated operands); resnet50: BASELINE
+    # config 3 itself (rowcheck: the reference's sha256 of all 64 output models)
+    shape = ["--devices-per-gpu", "16", "--degree", "4"] if model == "cifar10" else []
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
            "--master-addr", "127.0.0.1", f"--master-port={port}", str(ROOT / "bench.py"), "--gpus", "1",
-           "--sharded", "--dist-backend", "nccl", "--exchange", exchange, "--model", "cifar10",
-           "--devices-per-gpu", "16", "--degree", "4", "--steps", "2", "--warmup", "1"] + ([] if tune else ["--no-tune"])
+           "--sharded", "--dist-backend", "nccl", "--exchange", exchange, "--model", model, *shape,
+           "--transport", transport, "--steps", "2", "--warmup", "1"] + ([] if tune else ["--no-tune"])
     out = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-3000:]
     line = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(line) == 1, out.stdout[-2000:]
     d = json.loads(line[0])
     assert d["n_gpus"] == 1 and d["parity"] is True and d["exchange"] == exchange
-    assert d["config"]["parallelism"] == f"{exchange}-sharded x1"
+    assert d["config"]["parallelism"] == f"{exchange}-sharded x1" and d["transport"] == transport
+    pr = d["parity_rows"]
+    assert pr["rows_checked"] == d["config"]["devices"] and pr["rows_differing"] == 0
+    assert pr["reference"].startswith("K1" if model == "cifar10" else "reference sha256")
+
+
+def _rc_round(cuda, exchange, corrupt):
+    """One round of 4 virtual ranks on a 48-device 8-regular graph with seeded models
+    (rowcheck.fill_owned), the exchange done by in-process copies; with corrupt=True one value of
+    rank 0's first received halo row (halo) or first received column-chunk row (transpose) is
+    changed after it arrives.  Returns (rows checked, rows differing, every spot_check passed)."""
+    from topology_aware_learning_amd import rowcheck
+    from topology_aware_learning_amd.transposed import TransposedRound
+
+    lay = [("w", (1001,), "float32"), ("bn.running_var", (7,), "float32"), ("bn.num_batches_tracked", (), "int64"),
+           ("b", (13,), "float32")]
+    layout = StateLayout.from_layout(lay)
+    world = 4
+    g = nx.random_regular_graph(8, 48, seed=0)
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(48)]
+    ws = [ra.unweighted_weights(len(o)) for o in orders]
+    if exchange == "halo":
+        srs = [ShardedRound(layout, orders, ws, r, world, cuda, exchange=lambda sr: []) for r in range(world)]
+    else:
+        srs = [TransposedRound(layout, orders, ws, r, world, cuda, chunks=1) for r in range(world)]
+    for sr in srs:
+        rowcheck.fill_owned(sr.pool_a, lay, sr.own_ids, 300)
+    if exchange == "halo":
+        _virtual_halo_exchange(srs)
+        if corrupt:
+            srs[0].pool_a.f32[len(srs[0].spec.own), 0] += 1.0
+        for sr in srs:
+            sr.step()
+    else:
+        for sr in srs:
+            sr.pack(0)
+        for r, sr in enumerate(srs):
+            for key, s in sr._segs_at(0):
+                for p in sr.peers():
+                    s.work_in[0][sr.rows_of(p)].copy_(srs[p].segs[key].send[0][srs[p].peer_slot(r)])
+        if corrupt:
+            srs[0].segs["f32"].work_in[0][srs[0].local_rows, 0] += 1.0
+        for sr in srs:
+            sr.compute(0)
+        for r, sr in enumerate(srs):
+            for key, s in sr._segs_at(0):
+                for p in sr.peers():
+                    s.back[0][sr.peer_slot(p)].copy_(srs[p].segs[key].work_out[0][srs[p].rows_of(r)])
+        for sr in srs:
+            sr.unpack(0)
+    torch.cuda.synchronize()
+    res = [rowcheck.check_round(sr.own_rows(), sr.own_ids, lay, orders, ws, 300, ops.MODE_EXACT) for sr in srs]
+    return (sum(r["rows_checked"] for r in res), sum(r["rows_differing"] for r in res),
+            all(sr.spot_check() for sr in srs))
+
+
+@pytest.mark.parametrize("exchange", ["halo", "transpose"])
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_rowcheck_catches_a_corrupted_exchange(cuda, exchange, corrupt):
+    """The sharded bench's parity check on the GPU (K3 rounds, K1 on operands regenerated from
+    their seeds): a clean exchange passes with all 48 rows checked; one corrupted received halo
+    value or all-to-all chunk value fails it, while spot_check (K1 on the operands as received)
+    passes on every rank either way."""
+    checked, differing, spots = _rc_round(cuda, exchange, corrupt)
+    assert checked == 48 and spots
+    assert (differing > 0) == corrupt

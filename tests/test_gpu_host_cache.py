@@ -75,3 +75,26 @@ def test_pinned_rows_round_equals_default(cuda, monkeypatch, cache_gb):
     assert all(t.is_pinned() for t in got[7].state_dict().values())  # re-bound after the swap
     b = aggregate.bound_row(got[0])
     assert b is not None and b[0].device.type == "cpu" and b[0].f32.is_pinned()
+
+
+def test_pinned_budget_falls_back_to_packing(cuda, monkeypatch):
+    """TAL_HOST_PIN_GB caps the page-locked bytes the bindings hold: with room for 5 models the
+    first 5 models a round touches are bound, the rest are packed per call, and the round's bits
+    are the default path's."""
+    g = nx.random_regular_graph(4, 12, seed=3)
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(12)]
+    monkeypatch.setenv("TAL_HOST_CACHE_GB", "0")
+    monkeypatch.setenv("TAL_HOST_PIN", "0")
+    ref = _models(12, 9)
+    _round(ref, orders)
+    monkeypatch.setenv("TAL_HOST_PIN", "1")
+    got = _models(12, 9)
+    lay = aggregate.layout_of_module(got[0])
+    row = 4 * lay.ld_f32 + 8 * lay.ld_i64 + 2 * lay.ld_b16
+    monkeypatch.setenv("TAL_HOST_PIN_GB", str((aggregate._PIN["used"] + 5.5 * row) / (1 << 30)))
+    _round(got, orders)
+    bound = [aggregate.bound_row(m) is not None for m in got]
+    assert sum(bound) == 5
+    for ma, mb in zip(ref, got):
+        for (k, ta), tb in zip(ma.state_dict().items(), mb.state_dict().values()):
+            assert torch.equal(ta, tb), k

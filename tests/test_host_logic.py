@@ -775,3 +775,35 @@ def test_binding_check_sees_last_entry_and_hooks_uninstall():
     pool.bind(m3, 0)
     assert arena._HOOKS and bound_row(m3) == (pool, 0)
     del last
+
+
+@pytest.mark.parametrize("graph,devices,model,dtype,weights,mode,fixture", [
+    ("random", 64, "resnet50", "f32", "unweighted", "exact", "full_round_c3_resnet50_rr64.json"),
+    ("barbell", 128, "resnet50", "f32", "unweighted", "exact", "full_round_c4_resnet50_barbell.json"),
+    ("sbm", 256, "vit_b16", "f32", "unweighted", "exact", "full_round_c5_vit_sbm256.json f32 unweighted_module_avg"),
+    ("sbm", 256, "vit_b16", "f32", "degcent", "exact", "full_round_c5_vit_sbm256.json f32 centrality_module_avg"),
+    ("sbm", 256, "vit_b16", "bf16", "unweighted", "exact", "full_round_c5_vit_sbm256.json bf16 unweighted_module_avg"),
+    ("sbm", 256, "vit_b16", "bf16", "unweighted", "fma", None),
+    ("random", 512, "resnet50", "f32", "unweighted", "exact", None)])
+def test_bench_reference_fixture_choice(graph, devices, model, dtype, weights, mode, fixture):
+    """bench.reference_fixture: the BASELINE configs the reference's full-round fixtures cover
+    get their per-model digests (operand order checked against this run's graph, seeds =
+    base + device id); other workloads (bf16 FMA, weak scaling) fall back to K1 on regenerated
+    operands."""
+    import argparse
+
+    import bench
+
+    a = argparse.Namespace(graph=graph, model=model, dtype=dtype, weights=weights, mode=mode, max_params=0, degree=8)
+    orders, ws = bench.round_spec(devices, 8, kind=graph, weights=weights)
+    base, ref = bench.reference_fixture(a, orders, ws)
+    if fixture is None:
+        assert ref is None and base == bench.SEED_BASE
+        return
+    assert ref["name"] == fixture
+    assert base == {"c3": 9300, "c4": 9400, "c5": 9500}[fixture.split("_")[2]]
+    for seg, exp in ref["expected"].items():
+        assert sorted(exp) == list(range(devices))
+        assert all(len(v) == len(ref["ranges"][seg]) for v in exp.values())
+    a.max_params = 4096  # a cut layout is never the fixture's
+    assert bench.reference_fixture(a, orders, ws)[1] is None

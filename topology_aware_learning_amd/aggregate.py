@@ -190,6 +190,33 @@ def _host_binding(model: nn.Module, layout: StateLayout) -> Optional[Tuple[Model
 
 
 _bind_lock = threading.Lock()
+_PIN = {"used": 0, "budget": None}
+
+
+def _pin_budget() -> int:
+    """Bytes of page-locked host memory the pinned bindings may hold at once: TAL_HOST_PIN_GB,
+    else a quarter of the host memory available when the first model is bound (page-locked
+    memory cannot be swapped or reclaimed, so tens of ViT-sized models must not take it all).
+    Past the budget a model is packed per call as with TAL_HOST_PIN=0."""
+    gb = os.environ.get("TAL_HOST_PIN_GB", "")
+    if gb:
+        return int(float(gb) * (1 << 30))
+    if _PIN["budget"] is None:
+        avail = 0
+        try:
+            with open("/proc/meminfo") as f:
+                for line in f:
+                    if line.startswith("MemAvailable:"):
+                        avail = int(line.split()[1]) * 1024
+                        break
+        except OSError:
+            pass
+        _PIN["budget"] = avail // 4 if avail else 16 << 30
+    return int(_PIN["budget"])
+
+
+def _pin_release(nbytes: int) -> None:
+    _PIN["used"] -= nbytes
 
 
 def _bind_pinned(model: nn.Module, layout: StateLayout) -> Optional[Tuple[ModelPool, int]]:
@@ -200,6 +227,9 @@ def _bind_pinned(model: nn.Module, layout: StateLayout) -> Optional[Tuple[ModelP
         layout.check_compatible(sd, "model")
     except ValueError:
         return None
+    nbytes = 4 * layout.ld_f32 + 8 * layout.ld_i64 + 2 * layout.ld_b16
+    if _PIN["used"] + nbytes > _pin_budget():
+        return None
 
     def pinned(rows_ld, dtype):
         return torch.empty((1, rows_ld), dtype=dtype, pin_memory=rows_ld > 0)
@@ -209,6 +239,8 @@ def _bind_pinned(model: nn.Module, layout: StateLayout) -> Optional[Tuple[ModelP
                          i64=pinned(layout.ld_i64, torch.int64), b16=pinned(layout.ld_b16, torch.bfloat16))
     except RuntimeError:  # no pinned memory to be had (locked-memory limit): pack instead
         return None
+    _PIN["used"] += nbytes
+    weakref.finalize(pool, _pin_release, nbytes)  # the row lives as long as the model bound to it
     pool.bind(model, 0)
     return pool, 0
 

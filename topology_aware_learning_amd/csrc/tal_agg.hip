@@ -1349,10 +1349,11 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
     srow[j] = p.src_row[s_beg + (src < ns ? src : 0)];
   }
   __syncthreads();  // plan slice staged
-  // pairs form: the first NP row sets' extents in registers (ROWW reads its records instead)
-  constexpr int kNP = (NP > 0 && !ROWW) ? NP : 1;
+  // pairs form: the first NP row sets' extents in registers (ROWW reads its records instead; the
+  // broadcast form has no row extents at all - stage_narrow_bc leaves L.rowptr / L.out null)
+  constexpr int kNP = (NP > 0 && !ROWW && !BC) ? NP : 1;
   int rq0[kNP], rq1[kNP], rout[kNP];
-  if constexpr (!ROWW) {
+  if constexpr (!ROWW && !BC) {
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       const int r = narrow_set(k, wave, kW) * kRpw + sub;
@@ -1483,18 +1484,20 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
       }
       continue;
     }
+    if constexpr (!ROWW && !BC) {  // the pairs form (the other two forms continued above)
 #pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      if (rq1[k] > rq0[k]) {
-        const float4 acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, rq0[k], rq1[k], cl);
-        if (col < n4) Io<T>::st(pout, static_cast<int64_t>(rout[k]) * ld_out4 + col, acc);
+      for (int k = 0; k < NP; ++k) {
+        if (rq1[k] > rq0[k]) {
+          const float4 acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, rq0[k], rq1[k], cl);
+          if (col < n4) Io<T>::st(pout, static_cast<int64_t>(rout[k]) * ld_out4 + col, acc);
+        }
       }
-    }
-    for (int k = NP; k * kW < n_sets; ++k) {  // row sets beyond the register-held ones
-      const int r = narrow_set(k, wave, kW) * kRpw + sub;
-      if (r < L.nr) {
-        const float4 acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, L.rowptr[r], L.rowptr[r + 1], cl);
-        if (col < n4) Io<T>::st(pout, static_cast<int64_t>(L.out[r]) * ld_out4 + col, acc);
+      for (int k = NP; k * kW < n_sets; ++k) {  // row sets beyond the register-held ones
+        const int r = narrow_set(k, wave, kW) * kRpw + sub;
+        if (r < L.nr) {
+          const float4 acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, L.rowptr[r], L.rowptr[r + 1], cl);
+          if (col < n4) Io<T>::st(pout, static_cast<int64_t>(L.out[r]) * ld_out4 + col, acc);
+        }
       }
     }
   }

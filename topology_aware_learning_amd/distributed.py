@@ -278,10 +278,10 @@ class ShardedRound:
         self.group = group
         # exchange(self) -> requests; default: RCCL/gloo P2P.  Tests may pass an in-process copy.
         # transport "host": the exchange is staged through host memory (gloo rehearsal runs);
-        # "cabi" (experimental: its RCCL exchange has run with one rank only - RCCL refuses two
-        # ranks on one GPU - while its messages are tested across virtual ranks,
-        # tests/test_gpu_comm.py): the library's own RCCL communicator and gather kernel
-        # (comm.HaloComm) on a side stream, the unique id broadcast through the torch.distributed group
+        # "cabi": the library's own RCCL communicator and gather kernel (comm.HaloComm) on a
+        # side stream, the unique id broadcast through the torch.distributed group (its messages
+        # are checked across virtual ranks and through a world-1 communicator on one GPU,
+        # tests/test_gpu_comm.py; RCCL refuses two ranks on one GPU)
         if transport not in ("device", "host", "cabi"):
             raise ValueError(f"unknown transport {transport!r}")
         self.transport = transport
@@ -358,6 +358,11 @@ class ShardedRound:
     def own_rows(self) -> ModelPool:
         """Pool whose rows [0, local_rows) hold this rank's current models."""
         return self.pool_a
+
+    @property
+    def own_ids(self) -> List[int]:
+        """Global device ids of own_rows()'s rows 0, 1, ..."""
+        return self.spec.own
 
     @property
     def kernel_bytes(self) -> int:

@@ -81,7 +81,7 @@ class RoundExecutor:
         best = int(np.argmin(ms))
         self.placement = dict(scratch_ms=ms, chosen=best)
         keep = cands[best]
-        del cands
+        del cands, c  # (the loop variable still held the last candidate)
         torch.cuda.empty_cache()
         return keep
 
@@ -180,6 +180,6 @@ def calibrated_pool(layout, rows: int, device, trials: int = 8, degree: int = 8)
     best = int(np.argmin(ms))
     keep = cands[best]  # still all zeros: the rounds mixed zero rows
     keep.placement_ms = dict(in_place_ms=ms, chosen=best)
-    del cands
+    del cands, c, t  # (the loop variables still held the last candidate)
     torch.cuda.empty_cache()
     return keep

@@ -51,8 +51,11 @@ def cosine_pairs(model: nn.Module, others: Sequence[nn.Module]) -> List[float]:
     layout = layout_of_module(model)
     names = _param_names(model)
     # a tensor mean over >= 32768 outputs follows torch's parallel order for this process's
-    # intra-op thread count, as the reference's own call would (tal_agg.h K2)
-    threads = torch.get_num_threads()
+    # intra-op thread count, as the reference's own call would (tal_agg.h K2).  The plan holds
+    # at most 1024 (tal_cosine_plan_set_threads); a process with more intra-op threads gets
+    # 1024's order, which differs from torch's only for a tensor mean over > 1024 x 32768
+    # outputs (none in the reference's models: ViT-B/16's largest is 196,608)
+    threads = max(1, min(torch.get_num_threads(), 1024))
     key = (layout.key, tuple(names), threads)
     plan = _plans.get(key)
     if plan is None:

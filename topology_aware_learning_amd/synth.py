@@ -137,32 +137,70 @@ def counter_f32_torch(seed: int, start: int, n: int, device, out: "torch.Tensor"
     return out
 
 
+_ROWGEN: dict = {}
+
+
+def _row_plan(layout: Layout, dtype: str, device):
+    """How a `dtype` segment row maps onto the generator's positions (cached per layout, dtype
+    and device): the total position count, the segment's contiguous position runs as
+    (first position, first segment column, length), a device index of every segment column's
+    position when there is more than one run, and the segment columns of float32 running_var
+    entries (|v| + 0.5, as synth_state_dict makes them)."""
+    key = (tuple(layout), dtype, str(device))
+    hit = _ROWGEN.get(key)
+    if hit is not None:
+        return hit
+    runs, rv, pos, off = [], [], 0, 0
+    for name, shape, dt in layout:
+        n = numel(shape)
+        if dt == dtype and n:
+            if runs and runs[-1][0] + runs[-1][2] == pos:
+                runs[-1][2] += n
+            else:
+                runs.append([pos, off, n])
+            if dtype == "float32" and name.endswith("running_var"):
+                rv.append((off, n))
+            off += n
+        pos += n
+    fidx = None
+    if len(runs) > 1:
+        lo = runs[0][0]  # positions relative to the first run's
+        fidx = torch.cat([torch.arange(p0 - lo, p0 - lo + n, dtype=torch.int64) for p0, _, n in runs]).to(device)
+    rvidx = torch.cat([torch.arange(a, a + n, dtype=torch.int64) for a, n in rv]).to(device) if rv else None
+    hit = (pos, [tuple(r) for r in runs], fidx, rvidx, off)
+    _ROWGEN[key] = hit
+    return hit
+
+
 def fill_rows_torch(seg: "torch.Tensor", layout: Layout, seeds: Sequence[int], dtype: str = "float32",
                     chunk: int = 1 << 25) -> None:
     """seg[r, :n] = the `dtype` entries of synth_state_dict(layout, seeds[r]) concatenated in
     state_dict order (a pool segment row), generated on seg's device.  float32, bfloat16 (the
-    bf16 of the fp32 counter value, as synth_state_dict makes it) and int64 segments."""
-    ents = []
-    pos = 0
-    for name, shape, dt in layout:
-        n = numel(shape)
-        if dt == dtype:
-            ents.append((name, pos, n))
-        pos += n
+    bf16 of the fp32 counter value, as synth_state_dict makes it) and int64 segments.
+
+    A float row is generated over the layout's whole position range in `chunk`-sized launches
+    (the int64 positions in between are a few dozen wasted elements) and its columns gathered
+    once, so a row costs a fixed ~20 element-wise launches per chunk, not per entry (ResNet-50:
+    320 entries; the sharded bench regenerates hundreds of operand rows to check a round)."""
+    total, runs, fidx, rvidx, n = _row_plan(layout, dtype, seg.device)
+    if dtype == "int64":  # a few counters per model: host values
+        for r, seed in enumerate(seeds):
+            for p0, c0, k in runs:
+                seg[r, c0:c0 + k].copy_(torch.from_numpy(counter_i64(seed, p0, k)))
+        return
+    if not n:
+        return
+    lo = runs[0][0]
+    hi = runs[-1][0] + runs[-1][2]
+    full = torch.empty(hi - lo, dtype=torch.float32, device=seg.device)
     for r, seed in enumerate(seeds):
-        off = 0
-        for name, p0, n in ents:
-            if dtype == "int64":  # a few counters per model: host values
-                seg[r, off:off + n].copy_(torch.from_numpy(counter_i64(seed, p0, n)))
-                off += n
-                continue
-            for c0 in range(0, n, chunk):
-                c1 = min(n, c0 + chunk)
-                v = counter_f32_torch(seed, p0 + c0, c1 - c0, seg.device)
-                if dtype == "float32" and name.endswith("running_var"):  # (bf16 entries: as made)
-                    v = v.abs() + 0.5
-                seg[r, off + c0:off + c1].copy_(v)  # bfloat16: round to nearest even, as .to()
-            off += n
+        for c0 in range(lo, hi, chunk):
+            c1 = min(hi, c0 + chunk)
+            counter_f32_torch(seed, c0, c1 - c0, seg.device, out=full[c0 - lo:c1 - lo])
+        v = full if fidx is None else full.index_select(0, fidx)
+        if rvidx is not None:  # (v may be `full` itself: regenerated for the next row anyway)
+            v[rvidx] = v[rvidx].abs() + 0.5
+        seg[r, :n].copy_(v)  # bfloat16: round to nearest even, as .to()
 
 
 # ------------------------------------------------------------------------------------------

@@ -195,7 +195,12 @@ class TransposedRound:
                  mode: int = ops.MODE_EXACT, owner: Optional[np.ndarray] = None, group=None,
                  tune: bool = False, transport: str = "device", chunks: Optional[int] = None):
         self.layout = layout
-        self.transport = transport  # "host": all-to-alls staged through host memory (gloo rehearsal)
+        # "device": torch.distributed all_to_all_single (RCCL); "host": staged through host
+        # memory (gloo rehearsal); "cabi": the library's own RCCL communicator (include/tal_agg.h
+        # tal_halo_exchange), each all-to-all as one group of per-peer sends / receives
+        if transport not in ("device", "host", "cabi"):
+            raise ValueError(f"unknown transport {transport!r}")
+        self.transport = transport
         self.device = torch.device(device)
         self.mode = mode
         self.group = group
@@ -241,6 +246,11 @@ class TransposedRound:
         self.staged_sources = self.plan.staged_rows()
         self.exchange_kind = "transpose"
         self._events: list = []
+        if transport == "cabi":
+            from .comm import shared_halo_comm
+
+            self.comm = shared_halo_comm(world, rank, device, group)
+            self.comm_stream = torch.cuda.Stream(self.device)
         if dist.is_available() and dist.is_initialized():
             dist.barrier(group=group)
 
@@ -287,11 +297,50 @@ class TransposedRound:
         """Split sizes in rank order with 0 for this rank (its block stays local)."""
         return [0 if p == self.rank else int(v) for p, v in enumerate(per_rank)]
 
+    def forward_messages(self, k: int, g: str):
+        """The forward all-to-all of chunk k, segment g, as per-peer messages: (sends, recvs),
+        entry p = the contiguous tensor going to / coming from rank p (None for this rank):
+        my models' chunk of block p, and block `rank`'s chunk of p's models (their work rows)."""
+        s = self.segs[g]
+        sends, recvs = [None] * self.world, [None] * self.world
+        for p in self.peers():
+            sends[p] = s.send[k][self.peer_slot(p)]
+            recvs[p] = s.work_in[k][self.rows_of(p)]
+        return sends, recvs
+
+    def backward_messages(self, k: int, g: str):
+        """The backward all-to-all of chunk k, segment g, as per-peer messages: p's models' output
+        rows of my block go to p; my models' output chunk of block p comes from p."""
+        s = self.segs[g]
+        sends, recvs = [None] * self.world, [None] * self.world
+        for p in self.peers():
+            sends[p] = s.work_out[k][self.rows_of(p)]
+            recvs[p] = s.back[k][self.peer_slot(p)]
+        return sends, recvs
+
+    def _exchange_cabi(self, k: int, messages) -> list:
+        """One RCCL group per segment through the C-ABI (tal_halo_exchange) on the comm stream,
+        after everything queued so far on the current stream (the packing, the round that wrote
+        the outputs, the unpacking that last read the receive buffers); the compute stream waits
+        on the returned request's event."""
+        from .distributed import _StreamRequest
+
+        cur = torch.cuda.current_stream(self.device)
+        self.comm_stream.wait_stream(cur)
+        for g, _ in self._segs_at(k):
+            sends, recvs = messages(k, g)
+            self.comm.exchange(sends, recvs, self.comm_stream)
+        ev = torch.cuda.Event()
+        ev.record(self.comm_stream)
+        return [_StreamRequest(ev, self.device)]
+
     def forward_exchange(self, k: int = 0) -> list:
         """Chunk k of block `rank` of every other rank's models into work_in[k] after my own
         rows; returns the pending works (none at world 1: nothing leaves the GPU)."""
         if self.world == 1:
             return []
+        if self.transport == "cabi":
+            return self._exchange_cabi(k, self.forward_messages)
         works = [self._all_to_all(s.work_in[k][self.local_rows:], s.send[k],
                                   self._splits([len(o) * s.bc for o in self.own_by_rank]),
                                   self._splits([self.local_rows * s.bc] * self.world)) for _, s in self._segs_at(k)]
@@ -306,6 +355,8 @@ class TransposedRound:
         """Every other rank's models' output rows back to their owners (my own stay here)."""
         if self.world == 1:
             return []
+        if self.transport == "cabi":
+            return self._exchange_cabi(k, self.backward_messages)
         works = [self._all_to_all(s.back[k], s.work_out[k][self.local_rows:],
                                   self._splits([self.local_rows * s.bc] * self.world),
                                   self._splits([len(o) * s.bc for o in self.own_by_rank])) for _, s in self._segs_at(k)]
@@ -368,6 +419,11 @@ class TransposedRound:
         return self.pool_a
 
     @property
+    def own_ids(self) -> List[int]:
+        """Global device ids of own_rows()'s rows 0, 1, ..."""
+        return self.own
+
+    @property
     def kernel_bytes(self) -> int:
         """Algorithmic HBM bytes of one round's K3 launches (staged sources + written rows)."""
         return sum(_ESIZE[g] * self.w_me[g] for g, _ in float_segments(self.layout)) * (
@@ -395,15 +451,14 @@ def make_round(layout: StateLayout, orders, weights, rank: int, world: int, devi
                mode: int = ops.MODE_EXACT, owner: Optional[np.ndarray] = None, group=None, tune: bool = False,
                transport: str = "device"):
     """This rank's sharded round with the given exchange ('halo' | 'transpose' | 'auto');
-    transport 'host' stages the exchange through host memory (gloo rehearsal runs only),
-    'cabi' moves a halo exchange through the library's own RCCL communicator (the transposed
-    exchange's all-to-alls stay on torch.distributed)."""
+    transport 'device' = torch.distributed's RCCL, 'host' stages the exchange through host
+    memory (gloo rehearsal runs only), 'cabi' moves either exchange through the library's own
+    RCCL communicator (tal_comm_* / tal_halo_pack / tal_halo_exchange: per-peer messages in one
+    RCCL group; an all-to-all is such a group)."""
     owner = partition_contiguous(len(orders), world) if owner is None else np.asarray(owner, np.int32)
     if exchange == "auto":
         exchange = choose_exchange(orders, owner, world, layout.n_f32, layout.n_i64, layout.n_b16)
     cls = {"halo": ShardedRound, "transpose": TransposedRound}[exchange]
-    if exchange == "transpose" and transport == "cabi":
-        transport = "device"
     r = cls(layout, orders, weights, rank, world, device, mode=mode, owner=owner, group=group, tune=tune,
             transport=transport)
     r.exchange_kind = exchange
