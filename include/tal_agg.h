@@ -360,6 +360,15 @@ int32_t tal_host_agg_i64(const int64_t* const* x_host, const double* w_host, int
 int32_t tal_host_agg_bf16(const uint16_t* const* x_host, const double* w_host, int32_t m, uint16_t* out,
                           int64_t n, int32_t mode);
 
+/* K2's cosine similarity on HOST pointers (replaces the reference's cosine_similarity,
+ * src/decentralized_client.py:661-681, where it runs: on CPU tensors inside
+ * sim_centrality_module_avg, :482-490, in a process without a GPU).  out[j] = cosine of the
+ * flat fp32 parameter rows a_host[j] / b_host[j] under a plan from tal_cosine_plan_build (its
+ * thread word set by tal_cosine_plan_set_threads): the same fp32 operations in the same order
+ * as tal_cosine_params, i.e. torch's CPU order, bit for bit.  Up to 16 host threads. */
+int32_t tal_host_cosine(const float* const* a_host, const float* const* b_host, int32_t n_pairs,
+                        const int64_t* plan_host, float* out);
+
 /* ---- Multi-GPU halo exchange (SURVEY §8(b) tal_halo_exchange, §8(e)) ---------------------
  * Reference: the models that cross workers are shipped by Parsl as Python objects
  * (decentralized_app.py:627-629, parsl_setup.py:191-203).  Sharded one process per GPU, each

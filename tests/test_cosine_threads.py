@@ -58,6 +58,49 @@ def test_oracle_cosine_threads_below_grain_is_serial():
         assert oracle.cosine_model(a, b, segs, threads=t).view(np.uint32) == base.view(np.uint32)
 
 
+@pytest.mark.parametrize("case", FIX["cases"], ids=_ids)
+def test_host_k2_cosine_threads_bitwise_reference(case):
+    """The library's host K2 (tal_host_cosine, what a process without a GPU runs) at every
+    thread count the fixture holds: the reference's value bit for bit."""
+    from topology_aware_learning_amd import ops
+
+    flat, segs = _case_inputs(case)
+    a, b = (torch.from_numpy(x) for x in flat)
+    for t, bits in case["bits"].items():
+        plan = ops.build_cosine_plan(segs, threads=int(t))
+        got = ops.host_cosine([a, a], [b, a], plan).numpy()
+        assert int(got[0].view(np.uint32)) == bits, (t, got[0], np.uint32(bits).view(np.float32))
+        assert got[1] == np.float32(1.0) or abs(float(got[1]) - 1.0) < 1e-6
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="the host K2 runs only without a GPU")
+def test_interface_cosine_follows_process_threads_on_host():
+    """src.decentralized_client.cosine_similarity with no GPU visible (the host K2) follows the
+    calling process's torch thread count, as the reference's call does."""
+    import torch.nn as nn
+
+    import src.decentralized_client as dc
+
+    case = next(c for c in FIX["cases"] if c["entries"] == [1] and len(set(c["bits"].values())) > 2)
+    a, b = cos_pair_state(VIT, case["seed_a"], case["seed_b"], case["entries"], case["mix"])
+
+    def holder(sd):
+        m = nn.Module()
+        for k, v in enumerate(sd.values()):
+            m.register_parameter(f"p{k}", nn.Parameter(v.clone(), requires_grad=False))
+        return m
+
+    ma, mb = holder(a), holder(b)
+    saved = torch.get_num_threads()
+    try:
+        for t in ("1", "3", "5", "8"):
+            torch.set_num_threads(int(t))
+            got = np.float32(dc.cosine_similarity(ma, mb))
+            assert int(got.view(np.uint32)) == case["bits"][t], t
+    finally:
+        torch.set_num_threads(saved)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", FIX["cases"], ids=_ids)
 def test_k2_cosine_threads_bitwise_reference(case):

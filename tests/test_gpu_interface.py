@@ -310,10 +310,14 @@ def test_host_reduction_unused_with_a_gpu(cuda, monkeypatch):
         raise AssertionError("host reduction called with a GPU visible")
 
     monkeypatch.setattr(ops, "host_agg", refuse)
-    case = next(c for c in TINY["cases"] if c["fn"] == "unweighted_module_avg")
-    clients, _ = build_clients(case, "cpu", cuda)
-    res = dc.unweighted_module_avg(clients[-1], 0, *clients).result()
-    sd = res[1].model.state_dict()
-    for name, _, _ in LAYOUT:
-        assert sd[name].device.type == "cpu"
-        assert bits_equal(sd[name].detach().numpy(), TINYZ[f"c{case['case']}_out_{name}"]), name
+    monkeypatch.setattr(ops, "host_cosine", refuse)
+    for fn in ("unweighted_module_avg", "sim_centrality_module_avg"):
+        case = next(c for c in TINY["cases"] if c["fn"] == fn)
+        clients, _ = build_clients(case, "cpu", cuda)
+        res = getattr(dc, fn)(clients[-1], 0, *clients, centrality_metric=case["centrality_metric"],
+                              centrality_dict=CENT, softmax=case["softmax"],
+                              softmax_coeff=case["softmax_coeff"]).result()
+        sd = res[1].model.state_dict()
+        for name, _, _ in LAYOUT:
+            assert sd[name].device.type == "cpu"
+            assert bits_equal(sd[name].detach().numpy(), TINYZ[f"c{case['case']}_out_{name}"]), (fn, name)

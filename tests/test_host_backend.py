@@ -48,15 +48,13 @@ def _bits_equal(a, b):
 
 
 def test_every_app_bit_exact_on_host():
-    """Every app of the reference interface except sim_centrality_module_avg (its cosine
-    similarity is the GPU kernel K2) on CPU models: bitwise the reference's outputs, special
-    values and int64 truncation included."""
+    """Every app of the reference interface on CPU models, sim_centrality_module_avg included
+    (its cosine similarities through the library's host K2, tal_host_cosine): bitwise the
+    reference's outputs, special values and int64 truncation included."""
     import src.decentralized_client as dc
 
     done = 0
     for case in TINY["cases"]:
-        if case["fn"] == "sim_centrality_module_avg":
-            continue
         ci = case["case"]
         clients = []
         for oi, idx in enumerate(case["order"]):
@@ -70,7 +68,61 @@ def test_every_app_bit_exact_on_host():
         for name, _, _ in LAYOUT:
             assert _bits_equal(sd[name].detach().numpy(), TINYZ[f"c{ci}_out_{name}"]), (ci, case["fn"], name)
         done += 1
-    assert done == len(TINY["cases"]) - 24
+    assert done == len(TINY["cases"])
+    assert sum(c["fn"] == "sim_centrality_module_avg" for c in TINY["cases"]) == 24
+
+
+def test_cosine_similarity_tiny_cases_on_host():
+    """The reference's cosine_similarity values of the tiny cases (self vs every operand), from
+    the host K2, bit for bit."""
+    import src.decentralized_client as dc
+
+    checked = 0
+    for case in TINY["cases"]:
+        if "cosine" not in case:
+            continue
+        ci = case["case"]
+        ms = []
+        for oi in range(len(case["order"])):
+            m = TinyNet()
+            m.load_state_dict({n: torch.from_numpy(TINYZ[f"c{ci}_in{oi}_{n}"].copy()) for n, _, _ in LAYOUT})
+            ms.append(m)
+        for j, ref in enumerate(case["cosine"]):
+            got = dc.cosine_similarity(ms[-1], ms[j])
+            assert _bits_equal(np.float32(got.item()), np.float32(ref)), (ci, j, float(got), ref)
+            checked += 1
+    assert checked > 0
+
+
+NEAR = json.loads((GOLDEN / "near_ties.json").read_text())
+NEARZ = np.load(GOLDEN / "near_ties.npz")
+
+
+def test_sim_centrality_near_ties_on_host():
+    """sim_centrality_module_avg on the near-tie fixtures (fp32 ties, 1-4 ulp gaps, fp32-vs-exact
+    order flips) with no GPU: the reference's similarities, least-similar pick and output bits."""
+    import src.decentralized_client as dc
+
+    cent = {k: {int(i): v for i, v in d.items()} for k, d in NEAR["centrality"].items()}
+    kinds = set()
+    for case in NEAR["cases"]:
+        ci = case["case"]
+        clients = []
+        for oi, idx in enumerate(case["order"]):
+            m = TinyNet()
+            m.load_state_dict({n: torch.from_numpy(NEARZ[f"c{ci}_in{oi}_{n}"].copy()) for n, _, _ in NEAR["layout"]})
+            clients.append((["r"], _client(idx, m, 10)))
+        for j, ref in enumerate(case["cosine"]):
+            got = dc.cosine_similarity(clients[-1][1].model, clients[j][1].model)
+            assert _bits_equal(np.float32(got.item()), np.float32(ref)), (ci, j)
+        res = dc.sim_centrality_module_avg(clients[-1], 0, *clients, centrality_metric=NEAR["centrality_metric"],
+                                           centrality_dict=cent, softmax=NEAR["softmax"],
+                                           softmax_coeff=NEAR["softmax_coeff"]).result()
+        sd = res[1].model.state_dict()
+        for name, _, _ in NEAR["layout"]:
+            assert _bits_equal(sd[name].detach().numpy(), NEARZ[f"c{ci}_out_{name}"]), (ci, case["kind"], name)
+        kinds.add(case["kind"])
+    assert kinds == {"tie", "flip", "close"}
 
 
 def test_every_app_bit_exact_bf16_models_on_host():
@@ -203,3 +255,71 @@ def test_config1_driver_unpatched(tmp_path, monkeypatch):
     assert ckpts
     ck = torch.load(ckpts[-1], weights_only=False)
     assert len(ck["client_state_dicts"]) == 8
+
+
+def test_config1_driver_degcent_sim_unpatched(tmp_path, monkeypatch):
+    """decentralized_main.py --aggregation_strategy degCent_sim --softmax with no GPU (config 1's
+    setting) on an 8-node barbell(3, 2) (unequal degrees, so the least-similar neighbor decides
+    the softmax sign): every call's similarities equal the C oracle's cosine on the operands it
+    read, its weights the reference rule's (oracle/reference_alg.py) on those similarities,
+    and its output the reference's CPU loop with those weights, bit for bit."""
+    import src.decentralized_client as dc
+    import oracle
+    from oracle import reference_alg as ra
+    from oracle import torch_path
+    from topology_aware_learning_amd import aggregate
+    from topology_aware_learning_amd.arena import StateLayout
+
+    monkeypatch.setenv("TAL_SYNTHETIC_DATA", "1")
+    monkeypatch.setenv("TAL_SYNTHETIC_SAMPLES", "64")
+    monkeypatch.setenv("TAL_DEVICE_POOL", "0")
+    real_agg, real_rule = aggregate.aggregate_models, dc._w.sim_centrality
+    calls, rules = [], []
+
+    def observe(operands, weights, target, mode=ops.MODE_EXACT):
+        before = [{k: v.detach().clone() for k, v in m.state_dict().items()} for m in operands]
+        out = real_agg(operands, weights, target, mode)
+        calls.append((before, list(weights), {k: v.detach().clone() for k, v in target.state_dict().items()}))
+        return out
+
+    def rule(order, me, cent, sims, softmax, coeff):
+        rules.append((list(order), me, dict(cent), dict(sims), softmax, coeff))
+        return real_rule(order, me, cent, sims, softmax, coeff)
+
+    monkeypatch.setattr(dc, "aggregate_models", observe)
+    monkeypatch.setattr(dc._w, "sim_centrality", rule)
+    from concurrent.futures import ThreadPoolExecutor
+
+    from src import _parsl_compat as pc
+
+    if not pc.HAVE_PARSL:
+        serial = ThreadPoolExecutor(max_workers=1)
+        for label in ("threadpool_executor", "decentral_train", "experiment"):
+            monkeypatch.setitem(pc._executors, label, serial)
+    topo = tmp_path / "barbell.txt"
+    np.savetxt(topo, nx.to_numpy_array(nx.barbell_graph(3, 2)), fmt="%d")
+    from src.experiments import decentralized_main
+
+    rc = decentralized_main.main(["--dataset", "cifar10", "--aggregation_strategy", "degCent_sim", "--softmax",
+                                  "--rounds", "2", "--epochs", "1", "--topology_file", str(topo),
+                                  "--out_dir", str(tmp_path / "logs"), "--batch_size", "32"])
+    assert rc == 0
+    assert len(calls) == len(rules) == 16
+    threads = torch.get_num_threads()
+    signs = set()
+    for (before, w, out), (order, me, cent, sims, softmax, coeff) in zip(calls, rules):
+        assert order[-1] == me and len(before) == len(order)
+        lay = StateLayout.from_state_dict(before[-1])
+        segs = lay.param_segments(list(before[-1]))  # the CIFAR CNN: every entry a parameter
+        flat = [np.concatenate([t.reshape(-1).numpy() for t in sd.values()]) for sd in before]
+        for j, idx in enumerate(order[:-1]):
+            ref = oracle.cosine_model(flat[-1], flat[j], segs, threads=min(threads, 1024))
+            assert np.float32(sims[idx]).view(np.uint32) == ref.view(np.uint32), (me, idx)
+        w_ref, c = ra.sim_centrality_weights(order, me, cent, sims, softmax, coeff)
+        assert w == [float(x) for x in w_ref]
+        signs.add(np.sign(c))
+        ref_out = {k: v.clone() for k, v in before[-1].items()}
+        torch_path.aggregate_call(before, w, ref_out)
+        for k in ref_out:
+            assert np.array_equal(ref_out[k].reshape(-1).numpy().view(np.uint8), out[k].reshape(-1).numpy().view(np.uint8)), k
+    assert signs == {-1.0, 1.0}  # both softmax signs were taken

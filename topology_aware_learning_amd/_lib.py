@@ -27,7 +27,7 @@ TAL_ERR_COMM = 4
 TAL_COMM_ID_BYTES = 128
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 EXPORTED = (
     "tal_last_error",
@@ -63,6 +63,7 @@ EXPORTED = (
     "tal_host_agg_f32",
     "tal_host_agg_i64",
     "tal_host_agg_bf16",
+    "tal_host_cosine",
 )
 
 
@@ -170,6 +171,7 @@ _SIGS = {
     "tal_host_agg_f32": (_I32, [_PP, _PD, _I32, _P, _I64, _I32]),
     "tal_host_agg_i64": (_I32, [_PP, _PD, _I32, _P, _I64]),
     "tal_host_agg_bf16": (_I32, [_PP, _PD, _I32, _P, _I64, _I32]),
+    "tal_host_cosine": (_I32, [_PP, _PP, _I32, _PI64, _P]),
 }
 
 _lock = threading.Lock()

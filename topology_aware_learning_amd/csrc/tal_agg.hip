@@ -45,7 +45,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 20;
+constexpr int kAbiVersion = 21;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -4555,6 +4555,134 @@ int32_t host_args(const char* fn, const void* const* x, const double* w, int32_t
   return TAL_OK;
 }
 
+// Host cosine similarity (K2's arithmetic on host pointers, for the `*_sim` strategies in a
+// process that sees no GPU).  It walks the same plan as K2 (tal_cosine_plan_build: per-tensor
+// kind, output offset, 256-output chunks; the thread word) and performs the same fp32 operations
+// in the same order - torch's CPU kernels' order, bit for bit: plain fp32 + and * here (this
+// file is built with -ffp-contract=off), std::fma where torch fuses, sqrtss for sqrt.
+struct HostCos {
+  // torch multi_row_sum for one stream: the 4-level cascade whose level boundaries depend only
+  // on the element index (a column of a 32-column group is this case too)
+  template <class Load>
+  static float cascade(Load x, int64_t size) {
+    int64_t lg = 0;
+    while ((int64_t{1} << lg) < size) ++lg;
+    const int64_t lp = lg / 4 > 4 ? lg / 4 : 4;
+    const int64_t step = int64_t{1} << lp;
+    float lv[4] = {0.f, 0.f, 0.f, 0.f};
+    int64_t i = 0;
+    for (; i + step <= size;) {
+      for (const int64_t e = i + step; i < e; ++i) lv[0] = lv[0] + x(i);
+      for (int j = 1; j < 4; ++j) {
+        lv[j] = lv[j] + lv[j - 1];
+        lv[j - 1] = 0.f;
+        if (i & ((step - 1) << (j * lp))) break;
+      }
+    }
+    for (; i < size; ++i) lv[0] = lv[0] + x(i);
+    return ((lv[0] + lv[1]) + lv[2]) + lv[3];
+  }
+  // torch row_sum: four interleaved cascades (elements 4 i + k), the rest into the first, then
+  // the other three added to it in order
+  template <class Load>
+  static float row(Load x, int64_t size) {
+    const int64_t q = size / 4;
+    float p[4];
+    for (int k = 0; k < 4; ++k) p[k] = cascade([&](int64_t i) { return x(4 * i + k); }, q);
+    for (int64_t i = 4 * q; i < size; ++i) p[0] = p[0] + x(i);
+    return ((p[0] + p[1]) + p[2]) + p[3];
+  }
+  // torch's serial full sum of n contiguous values (without the store's 0 +): below 8 one
+  // row_sum; else 8 lanes (lane l: elements 8 i + l), the tail from 0, then the lanes in order
+  template <class Load>
+  static float inner(Load x, int64_t n) {
+    if (n < kCosVw) return row(x, n);
+    const int64_t nv = n / kCosVw;
+    float t = 0.f;
+    for (int64_t k = nv * kCosVw; k < n; ++k) t = t + x(k);
+    for (int l = 0; l < kCosVw; ++l) t = t + row([&](int64_t i) { return x(i * kCosVw + l); }, nv);
+    return t;
+  }
+  static float clampn(float v) { return v < 1e-6f ? 1e-6f : v; }  // NaN stays NaN
+  // every output of chunk ch (plan words) of one pair
+  static void outputs(const int64_t* plan, int64_t ch, const float* a0, const float* b0, float* s_all) {
+    const int64_t n_seg = plan[0];
+    const int64_t* c = plan + kCosHdr + kCosSegWords * n_seg + kCosChunkWords * ch;
+    const int64_t* sg = plan + kCosHdr + kCosSegWords * c[0];
+    const int64_t I = sg[2], B = sg[3];
+    const float* a = a0 + sg[0];
+    const float* b = b0 + sg[0];
+    float* s = s_all + sg[4];
+    for (int64_t q = c[1]; q < c[1] + c[2]; ++q) {
+      if (sg[5] == kCosElem) {
+        const float n1 = clampn(std::sqrt(std::fma(a[q], a[q], 0.f)));
+        const float n2 = clampn(std::sqrt(std::fma(b[q], b[q], 0.f)));
+        s[q] = 0.f + (a[q] / n1) * (b[q] / n2);
+      } else if (sg[5] == kCosCol) {  // reduced dim strided by B
+        const int64_t k = q % B;
+        const float* x = a + (q / B) * I * B + k;
+        const float* y = b + (q / B) * I * B + k;
+        float m1 = 0.f, m2 = 0.f;
+        for (int64_t i = 0; i < I; ++i) {
+          m1 = std::fma(x[i * B], x[i * B], m1);
+          m2 = std::fma(y[i * B], y[i * B], m2);
+        }
+        const float n1 = clampn(std::sqrt(m1)), n2 = clampn(std::sqrt(m2));
+        auto pr = [&](int64_t i) { return (x[i * B] / n1) * (y[i * B] / n2); };
+        // columns in groups of 32 share one cascade; groups of 8 and single columns: row_sum
+        s[q] = 0.f + ((B >= kCosVw && k < B / 32 * 32) ? cascade(pr, I) : row(pr, I));
+      } else {  // kCosRow: reduced dim contiguous, torch's 8-lane norm then its inner sum
+        const float* x = a + q * I;
+        const float* y = b + q * I;
+        const int64_t ve = I - I % kCosVw;
+        float l1[kCosVw] = {}, l2[kCosVw] = {};
+        for (int64_t d = 0; d < ve; d += kCosVw)
+          for (int l = 0; l < kCosVw; ++l) {
+            l1[l] = std::fma(x[d + l], x[d + l], l1[l]);
+            l2[l] = std::fma(y[d + l], y[d + l], l2[l]);
+          }
+        float t1 = l1[0], t2 = l2[0];
+        for (int l = 1; l < kCosVw; ++l) {
+          t1 = t1 + l1[l];
+          t2 = t2 + l2[l];
+        }
+        int64_t d = ve;
+        for (const int64_t e = ve + (I - ve) / 4 * 4; d < e; ++d) {  // groups of 4: square, add
+          t1 = t1 + x[d] * x[d];
+          t2 = t2 + y[d] * y[d];
+        }
+        for (; d < I; ++d) {  // the last < 4: fused
+          t1 = std::fma(x[d], x[d], t1);
+          t2 = std::fma(y[d], y[d], t2);
+        }
+        const float n1 = clampn(std::sqrt(t1)), n2 = clampn(std::sqrt(t2));
+        s[q] = 0.f + inner([&](int64_t i) { return (x[i] / n1) * (y[i] / n2); }, I);
+      }
+    }
+  }
+  // mean of one tensor's outputs: torch's sum (two-pass over T threads' chunks for >= 32768
+  // outputs when T > 1) / numel
+  static float mean(const int64_t* plan, int64_t seg, const float* s_all) {
+    const int64_t* sg = plan + kCosHdr + kCosSegWords * seg;
+    const int64_t n = sg[1] * sg[3], T = plan[2];
+    const float* s = s_all + sg[4];
+    float fin;
+    if (n < kCosGrain || T <= 1) {
+      fin = inner([&](int64_t i) { return s[i]; }, n);
+    } else {
+      std::vector<float> part(static_cast<size_t>(T), 0.f);
+      const int64_t nt = std::min(T, (n + kCosGrain - 1) / kCosGrain);
+      const int64_t chunk = (n + nt - 1) / nt;
+      for (int64_t t = 0; t < nt && t * chunk < n; ++t) {
+        const float* c = s + t * chunk;
+        part[t] = 0.f + inner([&](int64_t i) { return c[i]; }, std::min(chunk, n - t * chunk));
+      }
+      fin = inner([&](int64_t i) { return part[i]; }, T);
+    }
+    return (0.f + fin) / static_cast<float>(n);
+  }
+};
+
 }  // namespace
 
 extern "C" {
@@ -4625,6 +4753,38 @@ int32_t tal_host_agg_bf16(const uint16_t* const* x_host, const double* w_host, i
     }
     for (int64_t e = 0; e < k; ++e) out[e0 + e] = host_store_bf16(acc[e]);
   });
+  g_err.clear();
+  return TAL_OK;
+}
+
+int32_t tal_host_cosine(const float* const* a_host, const float* const* b_host, int32_t n_pairs,
+                        const int64_t* plan_host, float* out) {
+  if (!a_host || !b_host || !plan_host || !out || n_pairs <= 0 || plan_host[0] <= 0 || plan_host[1] <= 0 ||
+      plan_host[2] < 1 || plan_host[2] > kCosMaxThreads)
+    return fail(TAL_ERR_INVALID, "tal_host_cosine: bad arguments");
+  for (int j = 0; j < n_pairs; ++j)
+    if (!a_host[j] || !b_host[j]) return fail(TAL_ERR_INVALID, "tal_host_cosine: null model pointer");
+  const int64_t n_seg = plan_host[0], n_out = plan_host[1];
+  int64_t n_chunks = 0;  // chunk words follow the segment words; count them from the segments
+  for (int64_t t = 0; t < n_seg; ++t) {
+    const int64_t* sg = plan_host + kCosHdr + kCosSegWords * t;
+    const int64_t per = cos_chunk_outputs(static_cast<int>(sg[5]));
+    n_chunks += (sg[1] * sg[3] + per - 1) / per;
+  }
+  std::vector<float> s_all(static_cast<size_t>(n_out));
+  std::vector<float> means(static_cast<size_t>(n_seg));
+  for (int j = 0; j < n_pairs; ++j) {
+    // outputs chunk by chunk, then the means tensor by tensor, each on up to 16 host threads
+    host_blocks(n_chunks * kHostBlock, [&](int64_t e0, int64_t) {
+      HostCos::outputs(plan_host, e0 / kHostBlock, a_host[j], b_host[j], s_all.data());
+    });
+    host_blocks(n_seg * kHostBlock, [&](int64_t e0, int64_t) {
+      means[static_cast<size_t>(e0 / kHostBlock)] = HostCos::mean(plan_host, e0 / kHostBlock, s_all.data());
+    });
+    float avg = 0.f + means[0];  // 0 + mean_0, += mean_t in parameter order, / len(params)
+    for (int64_t t = 1; t < n_seg; ++t) avg = avg + means[static_cast<size_t>(t)];
+    out[j] = avg / static_cast<float>(n_seg);
+  }
   g_err.clear();
   return TAL_OK;
 }

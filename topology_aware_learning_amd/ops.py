@@ -946,3 +946,20 @@ def cosine(a_list: Sequence[torch.Tensor], b_list: Sequence[torch.Tensor], plan:
                               ctypes.c_void_p(scratch.data_ptr()), ctypes.c_void_p(out.data_ptr()),
                               _stream(dev, stream)))
     return out
+
+
+def host_cosine(a_list: Sequence[torch.Tensor], b_list: Sequence[torch.Tensor], plan: CosinePlan) -> torch.Tensor:
+    """K2's arithmetic on the host (tal_host_cosine): cosine_similarity(a_j, b_j) for flat
+    contiguous CPU fp32 parameter arenas, the reference's fp32 value bit for bit, in a process
+    that sees no GPU (similarity.cosine_pairs dispatches on torch.cuda.is_available())."""
+    if len(a_list) != len(b_list) or not a_list:
+        raise ValueError("need matching, non-empty a/b lists")
+    for i, t in enumerate(list(a_list) + list(b_list)):
+        if t.device.type != "cpu" or t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError(f"host_cosine: model {i} must be a contiguous CPU float32 tensor")
+    out = torch.empty(len(a_list), dtype=torch.float32)
+    L = _lib.load()
+    check(L.tal_host_cosine(_lib.ptr_array([t.data_ptr() for t in a_list]), _lib.ptr_array([t.data_ptr() for t in b_list]),
+                            len(a_list), plan.host.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                            ctypes.c_void_p(out.data_ptr())))
+    return out

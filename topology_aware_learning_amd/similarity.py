@@ -1,4 +1,6 @@
-"""Model-to-model cosine similarity on the GPU (K2), for the `*_sim` aggregation strategies.
+"""Model-to-model cosine similarity (K2), for the `*_sim` aggregation strategies: the GPU kernels,
+or - in a process that sees no GPU - the library's host form of the same arithmetic
+(tal_host_cosine).
 
 Reference: cosine_similarity, src/decentralized_client.py:661-681 — over `named_parameters`
 (buffers excluded), nn.CosineSimilarity(dim=1, eps=1e-6) per tensor (1-D tensors get a
@@ -61,7 +63,27 @@ def cosine_pairs(model: nn.Module, others: Sequence[nn.Module]) -> List[float]:
     if plan is None:
         plan = ops.build_cosine_plan(layout.param_segments(names), threads=threads)
         _plans[key] = plan
+    if not torch.cuda.is_available():  # no GPU (config 1's setting): the library's host K2
+        flats = _host_flat([model, *others], layout)
+        return [float(x) for x in ops.host_cosine([flats[0]] * len(others), flats[1:], plan).tolist()]
     device = _device_for([model, *others])
     flats = _flat([model, *others], layout, device)
     res = ops.cosine([flats[0]] * len(others), flats[1:], plan)
     return [float(x) for x in res.cpu().tolist()]
+
+
+def _host_flat(models: Sequence[nn.Module], layout) -> List[torch.Tensor]:
+    """Each model's fp32 segment as a contiguous CPU tensor: a pinned-row view when the model
+    is bound to a host row, else its fp32 entries concatenated in state_dict order."""
+    out = []
+    for j, m in enumerate(models):
+        b = bound_row(m)
+        if b is not None and b[0].device.type == "cpu" and b[0].layout == layout:
+            out.append(b[0].row_f32(b[1]))
+            continue
+        sd = m.state_dict()
+        layout.check_compatible(sd, f"model {j}")
+        if any(t.device.type != "cpu" for t in sd.values()):
+            raise RuntimeError("no GPU is visible, but a model has tensors off the CPU")
+        out.append(torch.cat([t.detach().reshape(-1) for t in layout.flatten_cat(sd, "f32")]))
+    return out
