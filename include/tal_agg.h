@@ -213,6 +213,12 @@ int32_t tal_round_plan_build_bcast(int32_t rows, const int32_t* row_ptr_host, co
                                    int32_t lds_bytes, int32_t waves, int32_t wg_per_cu, int32_t* plan_host,
                                    int64_t plan_capacity_words, tal_round_plan_info* info);
 
+/* The broadcast form's staging limit: the most float4 staging loads per column tile (sources x
+ * c4) one group of a (c4, waves, wg_per_cu) broadcast plan may need - the planner caps groups
+ * at it and the launcher stages up to it (one table in the library for both).  -1 for a form
+ * that does not exist. */
+int64_t tal_round_bcast_max_loads(int32_t c4, int32_t waves, int32_t wg_per_cu);
+
 /* Streamed plan (see stream_cs above).  Rows keep their order; consecutive rows share a group
  * while the group has at most max_group_rows rows (<= 128) and, if max_group_src > 0, at
  * most max_group_src distinct sources.  Every row must list its operands in reference order

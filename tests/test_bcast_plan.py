@@ -85,10 +85,10 @@ def test_bcast_programs_decode_to_csr(graph, c4, waves, wg):
     info = plan.info
     assert info.narrow_bcast == waves and info.c4 == c4 and info.narrow_roww == 0 and info.bc_wg_per_cu == wg
     assert info.lds_bytes <= (80 if wg == 2 else 160) * 1024
-    # staging: what the form's launch takes (J <= 8 at 512 threads, 6 at 768, 4 at 1024 with two
-    # workgroups per CU, 8 at 1024 with one at c4 = 32), at most 4096 / 8192 float4 at c4 16 / 32
-    j = {8: 8, 12: 6, 16: 8 if (wg == 1 and c4 == 32) else 4}[waves]
-    max_loads = min(j * 64 * waves, 8192 if c4 == 32 else 4096)
+    # staging: at most what the form's launch stages - the library's one table, which the
+    # launcher reads too (tests/test_gpu_bcast.py launches plans at and past the limit)
+    max_loads = ops._lib.load().tal_round_bcast_max_loads(c4, waves, wg)
+    assert max_loads >= 2 * 64 * waves
     assert max(plan.host[info.off_grp_src_ptr + g + 1] - plan.host[info.off_grp_src_ptr + g]
                for g in range(info.n_groups)) * c4 <= max_loads
     assert info.lds_bytes == max(
@@ -105,6 +105,8 @@ def test_bcast_programs_decode_to_csr(graph, c4, waves, wg):
 
 
 def test_bcast_rejects_bad_arguments():
+    L = ops._lib.load()
+    assert L.tal_round_bcast_max_loads(64, 16, 2) == -1 and L.tal_round_bcast_max_loads(16, 10, 2) == -1
     orders, ws = bench.round_spec(64, 8)
     row_ptr, col, w = ra.round_csr(orders, ws)
     out = np.arange(64, dtype=np.int32)

@@ -151,3 +151,50 @@ def test_round_bcast_config5_topology(cuda, waves, wg):
     pout = torch.zeros_like(pin)
     ops.round_f32(pin, pout, plan, n=n)
     assert _bits_equal(host(pout, n), oracle.round_f32(pool, row_ptr, col, w, out_rows))
+
+
+def _limit_round(k, shape):
+    """A round needing k distinct sources: "wide" = ceil(k / 4) rows of 4 consecutive sources
+    each (the planner's greedy grouping keeps them in one group while the union fits), "single"
+    = one row of all k sources (plus rows for every source's own output)."""
+    if shape == "wide":
+        orders = [list(range(4 * r, min(k, 4 * r + 4))) for r in range(-(-k // 4))]
+    else:
+        orders = [list(range(k))]
+    ws = [[1.0 / (len(o) + j) + 1e-3 * j for j in range(len(o))] for o in orders]  # per-operand weights
+    return orders, ws
+
+
+@pytest.mark.parametrize("shape", ["wide", "single"])
+@pytest.mark.parametrize("waves,wg", FORMS)
+@pytest.mark.parametrize("c4", [16, 32])
+def test_round_bcast_staging_limit(cuda, c4, waves, wg, shape):
+    """Each broadcast form at its largest admissible group (the library's staging table,
+    tal_round_bcast_max_loads, which the planner and the launcher both read) and one source past
+    it: whatever plan the planner returns launches (TAL_OK) and is bitwise the oracle; a group
+    at the limit stays one group; past it the planner splits the group or - a single row that
+    cannot be split - refuses with TAL_ERR_CAPACITY.  The launcher never refuses a planned
+    round (the failure behind round 4's call_r04j and world-8 rehearsal)."""
+    L = ops._lib.load()
+    limit = L.tal_round_bcast_max_loads(c4, waves, wg) // c4  # sources per group
+    n = 2 * 64 * c4 + 12  # two column tiles of every width, and a scalar tail
+    for k in (limit, limit + 1):
+        orders, ws = _limit_round(k, shape)
+        rows = len(orders)
+        row_ptr, col, w = ra.round_csr(orders, ws)
+        out_rows = np.arange(rows, dtype=np.int32) + k  # outputs after the sources
+        try:
+            plan = ops.build_plan(row_ptr, col, w, out_rows, c4=c4, lds_bytes=160 * 1024, bcast=waves, bcast_wg=wg)
+        except ops._lib.TalError as exc:
+            assert exc.code == ops._lib.TAL_ERR_CAPACITY and shape == "single", (k, str(exc))
+            continue
+        if k == limit and shape == "wide":
+            assert plan.info.n_groups == 1 and plan.info.max_src == limit
+        assert plan.info.max_src <= limit
+        rng = np.random.default_rng(k + c4 + waves)
+        pool = rng.standard_normal((k + rows, n)).astype(np.float32)
+        ref = oracle.round_f32(pool, row_ptr, col, w, out_rows)
+        pin = dev_rows(pool, cuda, True)
+        pout = pin.clone()
+        ops.round_f32(pin, pout, plan, n=n)  # raises on any launch refusal
+        assert _bits_equal(host(pout, n), ref), (k, shape)

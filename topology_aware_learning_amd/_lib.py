@@ -39,6 +39,7 @@ EXPORTED = (
     "tal_round_plan_words",
     "tal_round_plan_build",
     "tal_round_plan_build_bcast",
+    "tal_round_bcast_max_loads",
     "tal_round_plan_build_stream",
     "tal_agg_round_f32",
     "tal_agg_round_i64",
@@ -144,6 +145,7 @@ _SIGS = {
         _I32,
         [_I32, _PI32, _PI32, _PD, _PI32, _I32, _I32, _I32, _I32, _PI32, _I64, ctypes.POINTER(RoundPlanInfo)],
     ),
+    "tal_round_bcast_max_loads": (_I64, [_I32, _I32, _I32]),
     "tal_round_plan_build_stream": (
         _I32,
         [_I32, _PI32, _PI32, _PD, _PI32, _I32, _I32, _PI32, _I64, ctypes.POINTER(RoundPlanInfo)],

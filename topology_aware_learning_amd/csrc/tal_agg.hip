@@ -1953,6 +1953,32 @@ int32_t launch_round_persistent(const T* pin, int64_t ld_in, T* pout, int64_t ld
 
 constexpr int kNarrowThreads = 1024;
 
+// The broadcast form's staging table - the ONE place its limits live: the launcher picks its
+// instantiation from it (launch_round_bcast_nt) and the planner caps groups with it
+// (bc_max_loads, round_plan_build), so a plan the planner returns always launches.
+// J = float4 staging loads per lane, NT = 64 x waves threads.  Instantiated: J = 2 and 4 for
+// every form, 6 at 768 threads, 8 at 512 threads and at 1024 threads with c4 = 32 and one
+// workgroup per CU (the two-chunk form's 128 KiB tile; with two workgroups per CU 1024
+// threads x 8 loads do not fit 64 VGPRs).
+constexpr int bc_j_max(int c4, int nt, int wg_per_cu) {
+  return nt == 512 ? 8 : nt == 768 ? 6 : (nt == 1024 && c4 == 32 && wg_per_cu == 1) ? 8 : 4;
+}
+// the J a launch of `loads` float4 staging loads per tile uses (0: more than the form stages)
+constexpr int bc_j_for(int c4, int nt, int wg_per_cu, int64_t loads) {
+  for (int j : {2, 4, 6, 8})
+    if (j <= bc_j_max(c4, nt, wg_per_cu) && (j != 6 || nt == 768) && loads <= static_cast<int64_t>(j) * nt) return j;
+  return 0;
+}
+// sources per group the records can address: 4096 float4 at c4 = 16, 8192 at c4 = 32 (256)
+constexpr int64_t bc_max_loads(int c4, int waves, int wg_per_cu) {
+  const int64_t j = bc_j_max(c4, 64 * waves, wg_per_cu);
+  const int64_t cap = c4 == 32 ? 8192 : 4096;
+  return j * 64 * waves < cap ? j * 64 * waves : cap;
+}
+static_assert(bc_j_for(16, 1024, 2, 4096) == 4 && bc_j_for(16, 1024, 2, 4097) == 0, "16 x 2");
+static_assert(bc_j_for(32, 1024, 1, 8192) == 8 && bc_j_for(32, 1024, 2, 4097) == 0, "two-chunk form");
+static_assert(bc_j_for(16, 768, 2, 4096) == 6 && bc_j_for(16, 512, 2, 4096) == 8, "12 x 2, 8 x 2");
+
 // Workgroups of `kernel` resident per CU with `lds` bytes of dynamic LDS (registers and LDS both
 // count), asked from the runtime once per (kernel, lds) - a persistent grid larger than what is
 // resident would run a second, straggling wave of workgroups.
@@ -2049,12 +2075,24 @@ template <int C4, int NT, bool EXACT, typename T>
 int32_t launch_round_bcast_nt(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4,
                               const PlanView& v, const tal_round_plan_info& in, hipStream_t s) {
   const int64_t loads = static_cast<int64_t>(in.max_src) * C4;  // float4 staging loads per tile
-  if (loads <= 2LL * NT) return launch_round_bcast_j<C4, NT, 2, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
-  if (loads <= 4LL * NT) return launch_round_bcast_j<C4, NT, 4, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
-  if constexpr (NT == 768)
-    if (loads <= 6LL * NT) return launch_round_bcast_j<C4, NT, 6, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
-  if constexpr (NT <= 512 || (NT == 1024 && C4 == 32))
-    if (loads <= 8LL * NT) return launch_round_bcast_j<C4, NT, 8, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
+  switch (bc_j_for(C4, NT, in.bc_wg_per_cu, loads)) {  // the staging table (bc_j_max)
+    case 2:
+      return launch_round_bcast_j<C4, NT, 2, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
+    case 4:
+      return launch_round_bcast_j<C4, NT, 4, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
+    case 6:
+      if constexpr (NT == 768)
+        return launch_round_bcast_j<C4, NT, 6, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
+      break;
+    case 8:
+      if constexpr (bc_j_max(C4, NT, 1) >= 8)
+        return launch_round_bcast_j<C4, NT, 8, EXACT, T>(pin, ld_in, pout, ld_out, n4, v, in, s);
+      break;
+    default:
+      break;
+  }
+  // a plan from tal_round_plan_build_bcast never gets here (its groups are capped by the same
+  // table); a hand-made or mismatched plan does
   return fail(TAL_ERR_CAPACITY, "broadcast-form round plan: group tile too large for the workgroup");
 }
 
@@ -3328,15 +3366,6 @@ std::vector<int32_t> bc_pass_records(const int32_t* row_ptr_host, int64_t r0, in
 
 constexpr int64_t bc_lds_bytes(int64_t ns, int c4) { return (ns + 1) * c4 * 16; }
 
-// Largest staging (float4 loads per tile) a broadcast-form launch takes: J loads per lane of its
-// 64 x waves threads (launch_round_bcast_nt: J <= 8 at 512 threads, 6 at 768, 4 at 1024 with
-// two workgroups per CU, 8 at 1024 with one and c4 = 32), at most 4096 at c4 = 16 / 8192 at 32.
-constexpr int64_t bc_max_loads(int c4, int waves, int wg_per_cu) {
-  const int64_t j = waves == 16 ? (wg_per_cu == 1 && c4 == 32 ? 8 : 4) : waves == 12 ? 6 : 8;
-  const int64_t cap = c4 == 32 ? 8192 : 4096;
-  return j * 64 * waves < cap ? j * 64 * waves : cap;
-}
-
 // Lay the plan blob out (see tal_round_plan_info).  rb = dense row-block size (0 = sparse
 // form only, -1 = dense when it saves LDS reads); stream_cs > 0 pads each block's entries
 // chunk by chunk for the streamed kernel.
@@ -3877,6 +3906,12 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
                              int64_t plan_capacity_words, tal_round_plan_info* info) {
   return round_plan_build(rows, row_ptr_host, col_host, w_host, out_row_host, c4, lds_bytes, dense_rb,
                           plan_host, plan_capacity_words, info, 0, 2);
+}
+
+int64_t tal_round_bcast_max_loads(int32_t c4, int32_t waves, int32_t wg_per_cu) {
+  if ((c4 != 16 && c4 != 32) || (waves != 8 && waves != 12 && waves != 16) || (wg_per_cu != 1 && wg_per_cu != 2))
+    return -1;
+  return bc_max_loads(c4, waves, wg_per_cu);
 }
 
 int32_t tal_round_plan_build_bcast(int32_t rows, const int32_t* row_ptr_host, const int32_t* col_host,

@@ -577,7 +577,6 @@ def _sub_csr(row_ptr, col, w, out_row, rows):
     return rp, col[sel], w[sel], np.asarray(out_row)[rows]
 
 
-STREAM_GROUPINGS = ((64, 0), (128, 0), (64, 96))  # (max rows, max sources) per streamed group
 
 
 def _csr(row_ptr, col, w, out_row):
@@ -617,67 +616,64 @@ def build_stream_plan(row_ptr, col, w, out_row, max_group_rows: int = 64, max_gr
 
 
 def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.Tensor,
-              n: Optional[int] = None, reps: int = 3, mode: int = MODE_EXACT) -> RoundPlan:
-    """Pick the plan by measurement: every (tile width, LDS budget, sparse/dense) candidate that
-    builds runs `reps` times on the real pools (pool_out must not alias pool_in) and the fastest
-    median wins.  Costs a few rounds once per topology; the model-based choice of build_plan is
-    the fallback when only one candidate builds."""
+              n: Optional[int] = None, reps: int = 5, mode: int = MODE_EXACT,
+              margin: float = 0.01) -> RoundPlan:
+    """Pick the plan by measurement, anchored on the untimed default (default_plan).
+
+    Candidates are the forms that have won a measured round on some BASELINE config (DESIGN §4
+    "Plan forms and their selection"): the sparse form at every tile width and LDS budget whose
+    staging stays within 1.25 x the fewest staged sources of any candidate (multi-group plans
+    that re-read sources - config 3's 80 KiB c4 = 128 plan stages 3.7x - never won), the
+    broadcast forms, and the clique plan.  Dense row blocks, the streamed form and the
+    register-resident groups lost every measured A/B outside their probes (BENCH_r04: 5.9, 7.0
+    and 8.5-16 ms against 2.0 ms on config 3) and are built only on request (plan_from_spec).
+
+    Each candidate runs `reps` times, interleaved rep by rep with the others, and is judged by
+    its median.  A candidate replaces the default only when its median beats the default's by
+    more than `margin` (round 4: the tuner's single short timings once kept a plan slower than
+    the default - 23.74 vs 22.89 ms).  pool_out must not alias pool_in."""
     if pool_in.data_ptr() == pool_out.data_ptr():
         raise ValueError("tune_plan needs distinct input / output pools")
     bf16 = pool_in.dtype == torch.bfloat16  # bf16 rounds: sparse and narrow plans only
     run = round_bf16 if bf16 else round_f32
-    cands = []
+    base = default_plan(row_ptr, col, w, out_row, bf16=bf16, mode=mode)
+    if base.spec is None:
+        base.spec = {}
+    cands = [(("default",), base)]
+    sparse = []
     for c4 in TILE_WIDTHS:
         for budget in LDS_BUDGETS:
-            for dense in ((0,) if c4 < 64 or bf16 else (0, 8)):
-                try:
-                    p = build_plan(row_ptr, col, w, out_row, c4=c4, lds_bytes=budget, dense=dense)
-                except _lib.TalError:
-                    continue
-                if dense and not p.info.dense_rb:
-                    continue
-                key = (p.info.c4, p.info.n_groups, p.info.total_src, p.info.dense_rb, p.info.max_src, 0)
-                if all(key != k for k, _ in cands):
-                    p.spec = dict(c4=c4, lds=budget, dense=dense)
-                    cands.append((key, p))
+            try:
+                p = build_plan(row_ptr, col, w, out_row, c4=c4, lds_bytes=budget, dense=0)
+            except _lib.TalError:
+                continue
+            sparse.append(p)
+    if sparse:
+        fewest = min(p.staged_rows() for p in sparse)
+        for p in sparse:
+            key = (p.info.c4, p.info.n_groups, p.info.total_src, p.info.max_src)
+            if p.staged_rows() <= 1.25 * fewest and all(key != k for k, _ in cands) and p.spec != base.spec:
+                cands.append((key, p))
     for c4 in BCAST_WIDTHS:  # the broadcast form of the narrow kernel
         for waves, wg in BCAST_FORMS:
             try:
                 p = build_plan(row_ptr, col, w, out_row, c4=c4, lds_bytes=LDS_BUDGETS[-1], bcast=waves, bcast_wg=wg)
             except _lib.TalError:
                 continue
-            key = (("bcast", c4, waves, wg), p.info.n_groups, p.info.total_src, 0, p.info.max_src, 0)
-            if all(key != k for k, _ in cands):
+            key = ("bcast", c4, waves, wg)
+            if all(key != k for k, _ in cands) and p.spec != base.spec:
                 cands.append((key, p))
-    for max_rows, max_src in (() if bf16 else STREAM_GROUPINGS):
-        try:
-            p = build_stream_plan(row_ptr, col, w, out_row, max_rows, max_src)
-        except (_lib.TalError, ValueError):
-            continue
-        key = (p.info.c4, p.info.n_groups, p.info.total_src, p.info.dense_rb, p.info.max_src, p.info.stream_cs)
-        if all(key != k for k, _ in cands):
-            p.spec = dict(stream_rows=max_rows, stream_src=max_src)
-            cands.append((key, p))
-    if not bf16:
+    if not bf16 and not isinstance(base, CliquePlan):
         cp = build_clique_plan(row_ptr, col, w, out_row)
         if cp is not None:
-            cp.spec = dict(clique=1)
-            if cp.rest is not None:  # the rows outside the cliques get their own tuned plan
-                r_rp, r_col, r_w, r_out = _sub_csr(row_ptr, col, w, out_row, cp.rest_rows)
-                cp.rest = tune_plan(r_rp, r_col, r_w, r_out, pool_in, pool_out, n=n, reps=reps, mode=mode)
-                cp.spec["rest"] = cp.rest.spec
-            cands.append((("clique", cp.n_cliques, cp.staged_rows(), 0, cp.mmax, 0), cp))
-    if not bf16 or mode == MODE_FMA:  # register-resident groups (K3r; bf16 in FMA mode only)
-        rp = build_reg_plan(row_ptr, col, w, out_row)
-        if rp is not None:
-            rp.spec = dict(reg=1)
-            cands.append((("reg", rp.n_groups, rp.group_sources, 0, rp.max_src, 0), rp))
-    if not cands:
-        return build_plan(row_ptr, col, w, out_row, dense=0)
+            cp.spec = dict(clique=1, rest=cp.rest.spec if cp.rest is not None else None)
+            cands.append((("clique",), cp))
+    if isinstance(base, CliquePlan) and base.rest is not None:  # the rows outside the cliques: tuned too
+        r_rp, r_col, r_w, r_out = _sub_csr(row_ptr, col, w, out_row, base.rest_rows)
+        base.rest = tune_plan(r_rp, r_col, r_w, r_out, pool_in, pool_out, n=n, reps=reps, mode=mode, margin=margin)
+        base.spec = dict(clique=1, rest=base.rest.spec)
     if len(cands) == 1:
-        return cands[0][1].to(pool_in.device)
-    best, best_t = None, None
-    timings = []
+        return base.to(pool_in.device)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _, p in cands:
         p.to(pool_in.device)
@@ -692,13 +688,14 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
             e.record()
             e.synchronize()
             ts[k].append(s.elapsed_time(e))
-    for (key, p), tk in zip(cands, ts):
-        t = float(np.median(tk))
-        timings.append({"c4": key[0], "groups": key[1], "staged": key[2], "dense_rb": key[3],
-                        "max_src": key[4], "stream_cs": key[5], "ms": round(t, 4), "spec": p.spec})
-        if best_t is None or t < best_t:
-            best, best_t = p, t
-    best.tuned_ms = best_t
+    med = [float(np.median(tk)) for tk in ts]
+    timings = [{"form": "/".join(map(str, key)), "ms": round(t, 4), "all_ms": [round(x, 4) for x in tk], "spec": p.spec}
+               for (key, p), t, tk in zip(cands, med, ts)]
+    k_best = int(np.argmin(med))
+    if med[k_best] >= (1.0 - margin) * med[0]:
+        k_best = 0  # not clearly faster than the default: keep the default
+    best = cands[k_best][1]
+    best.tuned_ms = med[k_best]
     best.candidates = timings
     return best
 
@@ -740,8 +737,10 @@ def default_plan(row_ptr, col, w, out_row, bf16: bool = False, mode: int = MODE_
     degree-centrality weights: 23.0-23.3 ms against 23.7-24.4 for the 16 x 2 form, 32.1-32.6 for
     the pairs form and 29.8-30.1 for the register-resident K3r, which round 3 picked;
     profiles/r04/r04j, profiles/r04/pmc), for fp32 8 wavefronts x 2 (38.2-42.2 ms against 46.0
-    for the cost model's two-group pairs plan; profiles/r04/r04f).  It keeps the single group,
-    so RoundExecutor runs it in place."""
+    for the cost model's two-group pairs plan; profiles/r04/r04f).  The broadcast plan is taken
+    only when it has no more groups than the sparse plan; RoundExecutor runs a single-group
+    plan (config 5's: every source in one tile) in place and a multi-group one through its
+    scratch pool."""
     if not bf16:
         cp = build_clique_plan(row_ptr, col, w, out_row)
         if cp is not None:
