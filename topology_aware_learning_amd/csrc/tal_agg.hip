@@ -21,6 +21,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <mutex>
 #include <string>
@@ -45,7 +46,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 21;
+constexpr int kAbiVersion = 22;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -796,6 +797,19 @@ constexpr int kStreamPerWave = 2;      // sources each wavefront moves per chunk
 constexpr int kStreamMaxRows = 128;    // 16 wavefronts x one 8-row block
 constexpr size_t stream_lds_bytes(int cs) { return static_cast<size_t>(kStreamDepth + 1) * cs * 64 * 16; }
 
+// Tile walk of the persistent kernels: tile of workgroup b's i-th step over a grid of G.
+// walk = 1: t = i*G + b (the workgroups sweep the columns together, G tiles wide); walk = K > 1:
+// runs of K consecutive tiles per workgroup, the grid sweeping G*K tiles together; walk = 0:
+// one contiguous range of ceil(n_tiles / G) tiles per workgroup (every workgroup in its own part
+// of each row).  Strictly increasing in i; n_tiles or more once the workgroup is done.
+// tal_set_tile_walk() (probe switch, default 1) picks it for every launch.
+__device__ __forceinline__ int64_t walk_tile(int64_t i, int64_t b, int64_t G, int walk, int64_t n_tiles) {
+  if (walk == 1) return i * G + b;
+  if (walk > 1) return (i / walk) * G * walk + b * walk + (i % walk);
+  const int64_t per = (n_tiles + G - 1) / G;
+  return i < per ? b * per + i : n_tiles;
+}
+
 // Persistent form (the fast path): each workgroup walks column tiles t, t+gridDim.x, ...;
 // every lane owns J fixed staging slots (source, column) and keeps the next tile's J float4
 // loads in flight in registers while the workgroup computes the current tile from LDS.
@@ -804,7 +818,7 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const T* __restrict
                                                              int64_t ld_in4,
                                                              T* __restrict__ pout,
                                                              int64_t ld_out4, int64_t n4,
-                                                             PlanView p, int64_t n_tiles) {
+                                                             PlanView p, int64_t n_tiles, int walk) {
   extern __shared__ float4 s_data[];
   const int g = blockIdx.y;
   const int s_beg = p.grp_src_ptr[g];
@@ -815,7 +829,6 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const T* __restrict
   // of C4) of staged source k / C4; only the source's pool row is kept per slot (-1 = unused)
   static_assert(NT % C4 == 0, "a block stages whole source tiles");
   constexpr int kLd = J, kLps = C4;  // staging as k_round_f32_narrow without its 16-B bf16 lanes
-  constexpr bool W16 = false;
   // Branch-free staging (see k_round_f32_narrow): a slot past the group's sources reloads source
   // 0's chunk of its column and writes it where source 0's own slot does (the same value).
   // The write index and (dense form, whose registers are tight) the load addresses are recomputed
@@ -837,25 +850,22 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const T* __restrict
       v[j] = Io<T>::ld_raw(pin, static_cast<int64_t>(r) * ld_in4 + col);
     }
   };
-  int64_t t = blockIdx.x;
+  const int64_t G = gridDim.x;
+  int64_t i = 0;
+  int64_t t = walk_tile(0, blockIdx.x, G, walk, n_tiles);
   if (t < n_tiles) load_tile(t);
-  for (; t < n_tiles; t += gridDim.x) {
+  for (; t < n_tiles; t = walk_tile(++i, blockIdx.x, G, walk, n_tiles)) {
+    const int64_t t_next = walk_tile(i + 1, blockIdx.x, G, walk, n_tiles);
     __syncthreads();  // the previous tile's readers are done with s_data
-    int staged = ns * kLps;  // staging units (float4 slots; W16: slot pairs) of real sources
+    int staged = ns * kLps;  // staging units (float4 slots) of real sources
     asm volatile("" : "+s"(staged));
 #pragma unroll
     for (int j = 0; j < kLd; ++j) {
       const int k = j * NT + static_cast<int>(threadIdx.x);
-      if constexpr (W16) {
-        const int q = 2 * (k < staged ? k : c);
-        s_data[q] = Io<T>::f4(u32x2{v[j].x, v[j].y});
-        s_data[q + 1] = Io<T>::f4(u32x2{v[j].z, v[j].w});
-      } else {
-        s_data[k < staged ? k : c] = Io<T>::f4(v[j]);
-      }
+      s_data[k < staged ? k : c] = Io<T>::f4(v[j]);
     }
     __syncthreads();
-    if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
+    if (t_next < n_tiles) load_tile(t_next);  // in flight during this tile's math
     if constexpr (DENSE)
       emit_tile_dense<C4, NT, kDenseRb, EXACT>(s_data, p, g, r_beg, nr, ns, pout, ld_out4, t * C4, n4);
     else
@@ -1307,14 +1317,14 @@ __device__ __forceinline__ int narrow_set(int p, int wave, int nwaves) {
 // 0 for two (64 VGPRs: the extents are then read from LDS each pass).
 // W16 (bf16 pools): staging loads are 16 B per lane (two 4-element chunks, C4/2 lanes per source
 // and tile, J/2 loads per lane) instead of 8 B; each lane writes its two chunks to LDS as two
-// adjacent fp32 float4.  Needs an even chunk count, a row stride of an even number of chunks and
+// fp32 float4, 8 slots apart (cpos below).  Needs an even chunk count, a row stride of an even number of chunks and
 // a 16-B aligned base (the launcher checks), so every pair lies inside its row.
 // BC: the broadcast form (narrow_bcast plans; NT = 64 x the plan's waves per workgroup).
 template <int C4, int NT, int J, int NP, bool EXACT, typename T = float, bool ROWW = false, bool W16 = false,
           bool BC = false>
 __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round_f32_narrow(
     const T* __restrict__ pin, int64_t ld_in4, T* __restrict__ pout, int64_t ld_out4, int64_t n4,
-    PlanView p, int64_t n_tiles) {
+    PlanView p, int64_t n_tiles, int walk) {
   static_assert(C4 == 16 || C4 == 32, "narrow tiles are 16 or 32 float4 wide");
   static_assert(NT % C4 == 0, "a block stages whole source tiles");
   static_assert(!W16 || (kIsBf16<T> && J % 2 == 0), "16-B staging lanes: bf16 pools, even J");
@@ -1335,6 +1345,14 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int sub = kX2 ? lane / 16 : lane / C4;
   const int cl = kX2 ? lane % 16 : lane % C4;
+  // W16: where column cl of a source sits in its LDS tile.  A staging lane holds two adjacent
+  // columns 2c, 2c+1; written side by side, the eight lanes of a ds_write_b128 group span 256 B
+  // and meet twice on every bank (banks are (a/4) mod 32 for writes: 2-way).
+  // So within each 16-column block the even columns sit in slots 0..7 and the odd ones in 8..15
+  // (column 2c'+h at slot 8h+c'): each write instruction's group covers 128 contiguous bytes, and
+  // a ds_read_b128 lane group still meets each 16-B slot of a bank row once (the map is a
+  // bijection on each 16-column block and every read group takes whole-block-aligned lane sets).
+  const int cpos = W16 ? ((cl & ~15) | ((cl & 1) << 3) | ((cl & 15) >> 1)) : cl;
   // Staging is branch-free, so that the compiler's wait analysis sees every load land in its
   // register unconditionally (a conditional load made it wait for each load before issuing the
   // next: four serial HBM round trips per tile).  A lane past the group's sources reloads
@@ -1364,7 +1382,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   }
   const int n_sets = (L.nr + kRpw - 1) / kRpw;
   // ROWW: this lane's column base in the data tile, and its record offset within a pass
-  const uint32_t col_base = lds_addr(s_data + cl);
+  const uint32_t col_base = lds_addr(s_data + cpos);
   const uint32_t rec_lane = L.rec + 16u * static_cast<uint32_t>(sub);
   // BC: this wavefront's program (wave-uniform: scalar loads) and its records, loaded once
   // before the first staging loads (the records never wait behind them)
@@ -1389,7 +1407,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   raw_t v[kLd];
   auto load_tile = [&](int64_t tt) {
 #ifdef TAL_PROBE_NOLOAD  // A/B probe: no HBM reads (the tile keeps the first tile's values)
-    if (tt != blockIdx.x) return;
+    if (tt != walk_tile(0, blockIdx.x, gridDim.x, walk, n_tiles)) return;
 #endif
     if constexpr (W16) {  // 16-B units: chunk pair tt * C4 / 2 + c of each row
       const int64_t col = min(tt * kLps + c, (n4 - 1) / 2);  // past the end: a duplicate
@@ -1407,11 +1425,14 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
       }
     }
   };
-  int64_t t = blockIdx.x;
+  const int64_t G = gridDim.x;
+  int64_t i = 0;
+  int64_t t = walk_tile(0, blockIdx.x, G, walk, n_tiles);
   if (t < n_tiles) load_tile(t);
-  for (; t < n_tiles; t += gridDim.x) {
+  for (; t < n_tiles; t = walk_tile(++i, blockIdx.x, G, walk, n_tiles)) {
+    const int64_t t_next = walk_tile(i + 1, blockIdx.x, G, walk, n_tiles);
 #ifdef TAL_PROBE_NOPREFETCH  // A/B probe: each tile's loads issued after the previous tile's math
-    if (t != blockIdx.x) load_tile(t);
+    if (i != 0) load_tile(t);
 #endif
     __syncthreads();  // the previous tile's readers are done with s_data
     // staging units (float4 slots; W16: slot pairs) of real sources (readfirstlane: the broadcast
@@ -1421,17 +1442,18 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
 #pragma unroll
     for (int j = 0; j < kLd; ++j) {
       const int k = j * NT + static_cast<int>(threadIdx.x);
-      if constexpr (W16) {
-        const int q = 2 * (k < staged ? k : c);
+      if constexpr (W16) {  // unit u = source u / kLps, chunk pair c: slots cpos(2c), cpos(2c) + 8
+        const int u = k < staged ? k : c;
+        const int q = u + (u & ~7);
         s_data[q] = Io<T>::f4(u32x2{v[j].x, v[j].y});
-        s_data[q + 1] = Io<T>::f4(u32x2{v[j].z, v[j].w});
+        s_data[q + 8] = Io<T>::f4(u32x2{v[j].z, v[j].w});
       } else {
         s_data[k < staged ? k : c] = Io<T>::f4(v[j]);
       }
     }
     __syncthreads();
 #ifndef TAL_PROBE_NOPREFETCH
-    if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
+    if (t_next < n_tiles) load_tile(t_next);  // in flight during this tile's math
 #endif
     const int64_t col = t * C4 + cl;
     if constexpr (BC) {
@@ -1488,14 +1510,14 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
 #pragma unroll
       for (int k = 0; k < NP; ++k) {
         if (rq1[k] > rq0[k]) {
-          const float4 acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, rq0[k], rq1[k], cl);
+          const float4 acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, rq0[k], rq1[k], cpos);
           if (col < n4) Io<T>::st(pout, static_cast<int64_t>(rout[k]) * ld_out4 + col, acc);
         }
       }
       for (int k = NP; k * kW < n_sets; ++k) {  // row sets beyond the register-held ones
         const int r = narrow_set(k, wave, kW) * kRpw + sub;
         if (r < L.nr) {
-          const float4 acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, L.rowptr[r], L.rowptr[r + 1], cl);
+          const float4 acc = narrow_row<T, EXACT, (NP > 0)>(s_data, L.pairs, L.rowptr[r], L.rowptr[r + 1], cpos);
           if (col < n4) Io<T>::st(pout, static_cast<int64_t>(L.out[r]) * ld_out4 + col, acc);
         }
       }
@@ -1934,6 +1956,10 @@ int32_t launch_round_scalar(const T* pin, int64_t ld_in, T* pout, int64_t ld_out
 template <int C4>
 constexpr int round_threads() { return C4 >= 128 ? 512 : 1024; }
 
+// The persistent kernels' tile walk (walk_tile); a process-wide probe switch, 1 by default.
+std::atomic<int> g_tile_walk{1};
+int tile_walk() { return g_tile_walk.load(std::memory_order_relaxed); }
+
 template <int C4, int J, bool EXACT, bool DENSE, typename T = float>
 int32_t launch_round_persistent(const T* pin, int64_t ld_in, T* pout, int64_t ld_out,
                                 int64_t n4, const PlanView& v, const tal_round_plan_info& in,
@@ -1947,7 +1973,7 @@ int32_t launch_round_persistent(const T* pin, int64_t ld_in, T* pout, int64_t ld
   int64_t gx = std::max<int64_t>(1, 256 * per_cu / in.n_groups);
   gx = std::min<int64_t>(gx, tiles);
   const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(in.n_groups));
-  k<<<grid, kRoundThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles);
+  k<<<grid, kRoundThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles, tile_walk());
   return check_launch("round kernel (persistent)");
 }
 
@@ -2031,7 +2057,7 @@ int32_t launch_round_narrow_jr(const T* pin, int64_t ld_in, T* pout, int64_t ld_
   int64_t gx = std::max<int64_t>(1, 256 * per_cu / in.n_groups);
   gx = std::min<int64_t>(gx, tiles);
   const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(in.n_groups));
-  k<<<grid, kNarrowThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles);
+  k<<<grid, kNarrowThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles, tile_walk());
   return check_launch("round kernel (narrow tiles)");
 }
 
@@ -2067,7 +2093,7 @@ int32_t launch_round_bcast_j(const T* pin, int64_t ld_in, T* pout, int64_t ld_ou
   int64_t gx = std::max<int64_t>(1, 256 * per_cu / in.n_groups);
   gx = std::min<int64_t>(gx, tiles);
   const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(in.n_groups));
-  k<<<grid, NT, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles);
+  k<<<grid, NT, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles, tile_walk());
   return check_launch("round kernel (narrow tiles, broadcast form)");
 }
 
@@ -3906,6 +3932,12 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
                              int64_t plan_capacity_words, tal_round_plan_info* info) {
   return round_plan_build(rows, row_ptr_host, col_host, w_host, out_row_host, c4, lds_bytes, dense_rb,
                           plan_host, plan_capacity_words, info, 0, 2);
+}
+
+int32_t tal_set_tile_walk(int32_t walk) {
+  if (walk < 0 || walk > 64) return fail(TAL_ERR_INVALID, "tile walk: 0 (one range per workgroup) or 1..64 tiles per run");
+  g_tile_walk.store(walk);
+  return TAL_OK;
 }
 
 int64_t tal_round_bcast_max_loads(int32_t c4, int32_t waves, int32_t wg_per_cu) {
