@@ -219,14 +219,6 @@ int32_t tal_round_plan_build_bcast(int32_t rows, const int32_t* row_ptr_host, co
  * that does not exist. */
 int64_t tal_round_bcast_max_loads(int32_t c4, int32_t waves, int32_t wg_per_cu);
 
-/* Tile walk of the persistent round kernels (K3 persistent and K3n, every form), process-wide:
- * 1 (the default) - workgroup b takes column tiles b, b + G, b + 2G, ... (the grid sweeps each
- * row's columns together); K in 2..64 - runs of K consecutive tiles per workgroup; 0 - one
- * contiguous range of ceil(tiles / G) tiles per workgroup.  Results are identical for every
- * walk (each tile is computed the same way); only the order in which HBM is touched changes.
- * A measurement switch (tools/form_placement_probe.py); TAL_ERR_INVALID outside 0..64. */
-int32_t tal_set_tile_walk(int32_t walk);
-
 /* Streamed plan (see stream_cs above).  Rows keep their order; consecutive rows share a group
  * while the group has at most max_group_rows rows (<= 128) and, if max_group_src > 0, at
  * most max_group_src distinct sources.  Every row must list its operands in reference order

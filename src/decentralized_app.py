@@ -276,39 +276,33 @@ class DecentrallearnApp:
 
         from src.decentralized_client import aggregation_weights
 
-        done_of: dict = {}  # id(future) -> its result: each distinct future resolved once per round
-
-        def res(x):
-            if not isinstance(x, Future):
-                return x
-            r = done_of.get(id(x))
-            if r is None:
-                r = done_of[id(x)] = x.result()
-            return r
-
-        orders, weights, out_rows, done = [], [], [], []
-        row_of: dict = {}  # id(model) -> pool row: each model's binding is checked once per round
+        # each distinct future of the round resolved once (64 training futures behind 640 operand
+        # references at config 3), each distinct model's pool row checked once
+        memo: dict = {}
+        for _, agg_client, agg_neighbors, _ in batch:
+            for x in (agg_client, *agg_neighbors):
+                if id(x) not in memo:
+                    memo[id(x)] = x.result() if isinstance(x, Future) else x
+        row_of: dict = {}  # id(model) -> pool row
 
         def pool_row(m) -> int:
-            r = row_of.get(id(m))
-            if r is None:
-                b = bound_row(m)
-                if b is None or b[0] is not self.pool:
-                    raise RuntimeError("TAL_BATCHED_ROUND needs every model bound to the device pool")
-                r = row_of[id(m)] = b[1]
-            return r
+            b = bound_row(m)
+            if b is None or b[0] is not self.pool:
+                raise RuntimeError("TAL_BATCHED_ROUND needs every model bound to the device pool")
+            row_of[id(m)] = b[1]
+            return b[1]
 
+        orders, weights, out_rows, done = [], [], [], []
         for future, agg_client, agg_neighbors, kwargs in batch:
-            me = res(agg_client)
-            nbrs = [res(f) for f in agg_neighbors]
-            got = aggregation_weights(self.aggregation_function, me, *nbrs, **kwargs)
+            me = memo[id(agg_client)]
+            got = aggregation_weights(self.aggregation_function, me, *[memo[id(f)] for f in agg_neighbors], **kwargs)
             done.append((future, me))
             if got is None:  # test_agg: no-op
                 continue
-            rows = [pool_row(m) for m in list(got[0]) + [me[1].model]]
-            orders.append(rows[:-1])
-            weights.append([float(x) for x in got[1]])
-            out_rows.append(rows[-1])
+            orders.append([row_of[id(m)] if id(m) in row_of else pool_row(m) for m in got[0]])
+            weights.append(list(map(float, got[1])))
+            m = me[1].model
+            out_rows.append(row_of[id(m)] if id(m) in row_of else pool_row(m))
         if self.seed is not None:  # the apps seed torch per call (reference :395); same end state
             torch.manual_seed(self.seed)
         if orders:

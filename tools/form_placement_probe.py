@@ -7,11 +7,11 @@ and `allocs` separate allocations made after it (mostly fast).  Every plan form 
 writing into every destination, `reps` times, interleaved over forms and destinations; median
 kept.  One JSON line per (form, destination) and one summary line per form.
 
-Round 5: --walks times each form under each tile walk (tal_set_tile_walk: 1 = the grid sweeps
-the columns together, the default; K > 1 = runs of K tiles per workgroup; 0 = one contiguous
-range per workgroup), --forms picks forms by index.
+Round 5 also timed every form under three other tile walks (runs of 2 and 8 tiles per workgroup,
+one contiguous range per workgroup; a kernel switch since removed): slow windows stayed slow under
+every walk (profiles/r05/r05c/walk_probe.jsonl).
 
-Usage: python tools/form_placement_probe.py [--windows 8] [--allocs 4] [--reps 3] [--walks 1,0] [--forms 0,2]
+Usage: python tools/form_placement_probe.py [--windows 8] [--allocs 4] [--reps 3]
 """
 import argparse
 import json
@@ -46,11 +46,7 @@ def main():
     ap.add_argument("--allocs", type=int, default=4)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--in-place", action="store_true", help="also time each form in place on every target")
-    ap.add_argument("--walks", default="1", help="comma-separated tile walks (tal_set_tile_walk)")
-    ap.add_argument("--forms", default="", help="comma-separated indices into FORMS (default: all)")
     a = ap.parse_args()
-    walks = [int(x) for x in a.walks.split(",")]
-    forms = [FORMS[int(i)] for i in a.forms.split(",")] if a.forms else FORMS
     dev = torch.device("cuda", 0)
     lay = StateLayout.from_layout(synth.get_layout("resnet50"))
     n, ld = lay.n_f32, lay.ld_f32
@@ -59,10 +55,9 @@ def main():
     rp, col, w = csr_from_lists(orders, ws)
     out_rows = np.arange(rows, dtype=np.int32)
     plans = []
-    for spec in forms:
+    for spec in FORMS:
         try:
-            p = ops.plan_from_spec(rp, col, w, out_rows, spec).to(dev)
-            plans += [(dict(spec, walk=wk), p) for wk in walks]
+            plans.append((spec, ops.plan_from_spec(rp, col, w, out_rows, spec).to(dev)))
         except Exception as exc:  # a form this round cannot build
             print(json.dumps(dict(spec=spec, error=str(exc))), flush=True)
     src = torch.randn(rows, ld, device=dev)
@@ -74,19 +69,14 @@ def main():
     for _, _, t in targets:
         t.copy_(src)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    def set_walk(spec):
-        ops.set_tile_walk(spec["walk"])
-
-    for spec, p in plans:
-        set_walk(spec)
+    for _, p in plans:
         ops.round_f32(src, targets[0][2], p, n=n)
     torch.cuda.synchronize()
     modes = [False, True] if a.in_place else [False]
     ms = {(i, j, ip): [] for i in range(len(plans)) for j in range(len(targets)) for ip in modes}
     for _ in range(a.reps):
         for j, (_, _, t) in enumerate(targets):
-            for i, (spec, p) in enumerate(plans):
-                set_walk(spec)
+            for i, (_, p) in enumerate(plans):
                 for ip in modes:
                     if ip and not p.single_group:
                         continue
@@ -113,7 +103,6 @@ def main():
                                       groups=p.info.n_groups, windows_ms=[round(v, 3) for v in win],
                                       allocs_ms=[round(v, 3) for v in alc], worst=round(max(per), 4),
                                       median=round(float(np.median(per)), 4), best=round(min(per), 4))), flush=True)
-    ops.set_tile_walk(1)
 
 
 if __name__ == "__main__":

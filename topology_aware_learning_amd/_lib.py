@@ -27,7 +27,7 @@ TAL_ERR_COMM = 4
 TAL_COMM_ID_BYTES = 128
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 22
+ABI_VERSION = 21
 
 EXPORTED = (
     "tal_last_error",
@@ -40,7 +40,6 @@ EXPORTED = (
     "tal_round_plan_build",
     "tal_round_plan_build_bcast",
     "tal_round_bcast_max_loads",
-    "tal_set_tile_walk",
     "tal_round_plan_build_stream",
     "tal_agg_round_f32",
     "tal_agg_round_i64",
@@ -147,7 +146,6 @@ _SIGS = {
         [_I32, _PI32, _PI32, _PD, _PI32, _I32, _I32, _I32, _I32, _PI32, _I64, ctypes.POINTER(RoundPlanInfo)],
     ),
     "tal_round_bcast_max_loads": (_I64, [_I32, _I32, _I32]),
-    "tal_set_tile_walk": (_I32, [_I32]),
     "tal_round_plan_build_stream": (
         _I32,
         [_I32, _PI32, _PI32, _PD, _PI32, _I32, _I32, _PI32, _I64, ctypes.POINTER(RoundPlanInfo)],

@@ -21,7 +21,6 @@
 #include <string.h>
 
 #include <algorithm>
-#include <atomic>
 #include <cmath>
 #include <mutex>
 #include <string>
@@ -46,7 +45,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 22;
+constexpr int kAbiVersion = 21;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -797,19 +796,6 @@ constexpr int kStreamPerWave = 2;      // sources each wavefront moves per chunk
 constexpr int kStreamMaxRows = 128;    // 16 wavefronts x one 8-row block
 constexpr size_t stream_lds_bytes(int cs) { return static_cast<size_t>(kStreamDepth + 1) * cs * 64 * 16; }
 
-// Tile walk of the persistent kernels: tile of workgroup b's i-th step over a grid of G.
-// walk = 1: t = i*G + b (the workgroups sweep the columns together, G tiles wide); walk = K > 1:
-// runs of K consecutive tiles per workgroup, the grid sweeping G*K tiles together; walk = 0:
-// one contiguous range of ceil(n_tiles / G) tiles per workgroup (every workgroup in its own part
-// of each row).  Strictly increasing in i; n_tiles or more once the workgroup is done.
-// tal_set_tile_walk() (probe switch, default 1) picks it for every launch.
-__device__ __forceinline__ int64_t walk_tile(int64_t i, int64_t b, int64_t G, int walk, int64_t n_tiles) {
-  if (walk == 1) return i * G + b;
-  if (walk > 1) return (i / walk) * G * walk + b * walk + (i % walk);
-  const int64_t per = (n_tiles + G - 1) / G;
-  return i < per ? b * per + i : n_tiles;
-}
-
 // Persistent form (the fast path): each workgroup walks column tiles t, t+gridDim.x, ...;
 // every lane owns J fixed staging slots (source, column) and keeps the next tile's J float4
 // loads in flight in registers while the workgroup computes the current tile from LDS.
@@ -818,7 +804,7 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const T* __restrict
                                                              int64_t ld_in4,
                                                              T* __restrict__ pout,
                                                              int64_t ld_out4, int64_t n4,
-                                                             PlanView p, int64_t n_tiles, int walk) {
+                                                             PlanView p, int64_t n_tiles) {
   extern __shared__ float4 s_data[];
   const int g = blockIdx.y;
   const int s_beg = p.grp_src_ptr[g];
@@ -850,12 +836,9 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const T* __restrict
       v[j] = Io<T>::ld_raw(pin, static_cast<int64_t>(r) * ld_in4 + col);
     }
   };
-  const int64_t G = gridDim.x;
-  int64_t i = 0;
-  int64_t t = walk_tile(0, blockIdx.x, G, walk, n_tiles);
+  int64_t t = blockIdx.x;
   if (t < n_tiles) load_tile(t);
-  for (; t < n_tiles; t = walk_tile(++i, blockIdx.x, G, walk, n_tiles)) {
-    const int64_t t_next = walk_tile(i + 1, blockIdx.x, G, walk, n_tiles);
+  for (; t < n_tiles; t += gridDim.x) {
     __syncthreads();  // the previous tile's readers are done with s_data
     int staged = ns * kLps;  // staging units (float4 slots) of real sources
     asm volatile("" : "+s"(staged));
@@ -865,7 +848,7 @@ __global__ __launch_bounds__(NT) void k_round_f32_persistent(const T* __restrict
       s_data[k < staged ? k : c] = Io<T>::f4(v[j]);
     }
     __syncthreads();
-    if (t_next < n_tiles) load_tile(t_next);  // in flight during this tile's math
+    if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
     if constexpr (DENSE)
       emit_tile_dense<C4, NT, kDenseRb, EXACT>(s_data, p, g, r_beg, nr, ns, pout, ld_out4, t * C4, n4);
     else
@@ -1324,7 +1307,7 @@ template <int C4, int NT, int J, int NP, bool EXACT, typename T = float, bool RO
           bool BC = false>
 __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round_f32_narrow(
     const T* __restrict__ pin, int64_t ld_in4, T* __restrict__ pout, int64_t ld_out4, int64_t n4,
-    PlanView p, int64_t n_tiles, int walk) {
+    PlanView p, int64_t n_tiles) {
   static_assert(C4 == 16 || C4 == 32, "narrow tiles are 16 or 32 float4 wide");
   static_assert(NT % C4 == 0, "a block stages whole source tiles");
   static_assert(!W16 || (kIsBf16<T> && J % 2 == 0), "16-B staging lanes: bf16 pools, even J");
@@ -1407,7 +1390,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   raw_t v[kLd];
   auto load_tile = [&](int64_t tt) {
 #ifdef TAL_PROBE_NOLOAD  // A/B probe: no HBM reads (the tile keeps the first tile's values)
-    if (tt != walk_tile(0, blockIdx.x, gridDim.x, walk, n_tiles)) return;
+    if (tt != blockIdx.x) return;
 #endif
     if constexpr (W16) {  // 16-B units: chunk pair tt * C4 / 2 + c of each row
       const int64_t col = min(tt * kLps + c, (n4 - 1) / 2);  // past the end: a duplicate
@@ -1425,14 +1408,11 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
       }
     }
   };
-  const int64_t G = gridDim.x;
-  int64_t i = 0;
-  int64_t t = walk_tile(0, blockIdx.x, G, walk, n_tiles);
+  int64_t t = blockIdx.x;
   if (t < n_tiles) load_tile(t);
-  for (; t < n_tiles; t = walk_tile(++i, blockIdx.x, G, walk, n_tiles)) {
-    const int64_t t_next = walk_tile(i + 1, blockIdx.x, G, walk, n_tiles);
+  for (; t < n_tiles; t += gridDim.x) {
 #ifdef TAL_PROBE_NOPREFETCH  // A/B probe: each tile's loads issued after the previous tile's math
-    if (i != 0) load_tile(t);
+    if (t != blockIdx.x) load_tile(t);
 #endif
     __syncthreads();  // the previous tile's readers are done with s_data
     // staging units (float4 slots; W16: slot pairs) of real sources (readfirstlane: the broadcast
@@ -1453,7 +1433,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
     }
     __syncthreads();
 #ifndef TAL_PROBE_NOPREFETCH
-    if (t_next < n_tiles) load_tile(t_next);  // in flight during this tile's math
+    if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
 #endif
     const int64_t col = t * C4 + cl;
     if constexpr (BC) {
@@ -1956,10 +1936,6 @@ int32_t launch_round_scalar(const T* pin, int64_t ld_in, T* pout, int64_t ld_out
 template <int C4>
 constexpr int round_threads() { return C4 >= 128 ? 512 : 1024; }
 
-// The persistent kernels' tile walk (walk_tile); a process-wide probe switch, 1 by default.
-std::atomic<int> g_tile_walk{1};
-int tile_walk() { return g_tile_walk.load(std::memory_order_relaxed); }
-
 template <int C4, int J, bool EXACT, bool DENSE, typename T = float>
 int32_t launch_round_persistent(const T* pin, int64_t ld_in, T* pout, int64_t ld_out,
                                 int64_t n4, const PlanView& v, const tal_round_plan_info& in,
@@ -1973,7 +1949,7 @@ int32_t launch_round_persistent(const T* pin, int64_t ld_in, T* pout, int64_t ld
   int64_t gx = std::max<int64_t>(1, 256 * per_cu / in.n_groups);
   gx = std::min<int64_t>(gx, tiles);
   const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(in.n_groups));
-  k<<<grid, kRoundThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles, tile_walk());
+  k<<<grid, kRoundThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles);
   return check_launch("round kernel (persistent)");
 }
 
@@ -2057,7 +2033,7 @@ int32_t launch_round_narrow_jr(const T* pin, int64_t ld_in, T* pout, int64_t ld_
   int64_t gx = std::max<int64_t>(1, 256 * per_cu / in.n_groups);
   gx = std::min<int64_t>(gx, tiles);
   const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(in.n_groups));
-  k<<<grid, kNarrowThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles, tile_walk());
+  k<<<grid, kNarrowThreads, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles);
   return check_launch("round kernel (narrow tiles)");
 }
 
@@ -2093,7 +2069,7 @@ int32_t launch_round_bcast_j(const T* pin, int64_t ld_in, T* pout, int64_t ld_ou
   int64_t gx = std::max<int64_t>(1, 256 * per_cu / in.n_groups);
   gx = std::min<int64_t>(gx, tiles);
   const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(in.n_groups));
-  k<<<grid, NT, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles, tile_walk());
+  k<<<grid, NT, lds, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v, tiles);
   return check_launch("round kernel (narrow tiles, broadcast form)");
 }
 
@@ -3932,12 +3908,6 @@ int32_t tal_round_plan_build(int32_t rows, const int32_t* row_ptr_host, const in
                              int64_t plan_capacity_words, tal_round_plan_info* info) {
   return round_plan_build(rows, row_ptr_host, col_host, w_host, out_row_host, c4, lds_bytes, dense_rb,
                           plan_host, plan_capacity_words, info, 0, 2);
-}
-
-int32_t tal_set_tile_walk(int32_t walk) {
-  if (walk < 0 || walk > 64) return fail(TAL_ERR_INVALID, "tile walk: 0 (one range per workgroup) or 1..64 tiles per run");
-  g_tile_walk.store(walk);
-  return TAL_OK;
 }
 
 int64_t tal_round_bcast_max_loads(int32_t c4, int32_t waves, int32_t wg_per_cu) {

@@ -763,13 +763,6 @@ def default_plan(row_ptr, col, w, out_row, bf16: bool = False, mode: int = MODE_
     return p
 
 
-def set_tile_walk(walk: int) -> None:
-    """The persistent round kernels' tile walk, process-wide (tal_set_tile_walk): 1 (default) the
-    grid sweeps each row's columns together, K > 1 runs of K tiles per workgroup, 0 one contiguous
-    range per workgroup.  Results are bitwise the same for every walk; a measurement switch."""
-    _lib.check(_lib.load().tal_set_tile_walk(int(walk)))
-
-
 def round_kernel_name(plan) -> str:
     """Which K3 kernel tal_agg_round_f32 launches for this plan or plan info (mirrors
     launch_round_vec); clique plans name the K3c kernel (their rest rows run a second one)."""

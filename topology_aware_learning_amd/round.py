@@ -86,7 +86,7 @@ class RoundExecutor:
         return keep
 
     def plan(self, orders, weights, out_rows) -> ops.RoundPlan:
-        key = (tuple(tuple(o) for o in orders), tuple(tuple(float(x) for x in w) for w in weights), tuple(out_rows))
+        key = (tuple(map(tuple, orders)), tuple(tuple(map(float, w)) for w in weights), tuple(out_rows))
         p = self._plans.get(key)
         if p is None:
             row_ptr, col, w = csr_from_lists(orders, weights)
