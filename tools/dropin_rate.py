@@ -6,6 +6,9 @@ src/decentralized_app.py with its clients' models bound to the device pool:
              the 2-thread app pool, each a K1 launch (the reference's form)
   batched    TAL_BATCHED_ROUND=1: the round's 64 aggregations as one RoundExecutor.run (K3)
 
+each timed per round (synchronised before and after every round: latency) and over rounds run
+back to back with one synchronisation at the end (throughput: *_back_to_back).
+
 Training is replaced by an already resolved future holding the model as it stands (no app is
 submitted) so a round is the driver's own Python plus the aggregation.  Also
 times RoundExecutor(pool).run directly on the round (its default plan, in place) against the
@@ -111,6 +114,26 @@ def main():
         ms = 1e3 * float(np.median(ts))
         print(json.dumps(dict(mode=mode, rounds=len(ts), ms_per_round_median=round(ms, 3),
                               ms_per_round_all=[round(1e3 * x, 3) for x in ts],
+                              params_per_s=64 * 23_574_015 / (ms * 1e-3))), flush=True)
+    # the same rounds back to back with ONE synchronisation at the end (a driver never waits for
+    # the GPU between rounds: round r+1's Python runs while round r's kernels do; a round's
+    # futures resolve at launch and the stream orders the next round's reads after its writes)
+    for mode in ("per_call", "batched"):
+        app.batched_round = mode == "batched"
+        for f in app._federated_round(r):  # warm
+            f.result()
+        app.round_states.pop(r, None)
+        r += 1
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        for _ in range(rounds):
+            for f in app._federated_round(r):
+                f.result()
+            app.round_states.pop(r, None)
+            r += 1
+        torch.cuda.synchronize(dev)
+        ms = 1e3 * (time.perf_counter() - t) / rounds
+        print(json.dumps(dict(mode=mode + "_back_to_back", rounds=rounds, ms_per_round=round(ms, 3),
                               params_per_s=64 * 23_574_015 / (ms * 1e-3))), flush=True)
     # the K1 floor: one aggregation call per client with nothing around it
     pool = app.pool
