@@ -215,14 +215,8 @@ def check(rc: int) -> None:
 
 
 def ptr_array(ptrs) -> ctypes.Array:
-    arr = (ctypes.c_void_p * len(ptrs))()
-    for i, p in enumerate(ptrs):
-        arr[i] = int(p)
-    return arr
+    return (ctypes.c_void_p * len(ptrs))(*map(int, ptrs))
 
 
 def double_array(vals) -> ctypes.Array:
-    arr = (ctypes.c_double * len(vals))()
-    for i, v in enumerate(vals):
-        arr[i] = float(v)
-    return arr
+    return (ctypes.c_double * len(vals))(*map(float, vals))

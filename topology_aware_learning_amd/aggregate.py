@@ -334,6 +334,11 @@ def aggregate_models(operands: Sequence[nn.Module], weights: Sequence[float], ta
     # row); the target's pool then gives the layout without rebuilding its state_dict
     tb = bound_row(target)
     bounds = [bound_row(m) for m in operands]
+    if tb is not None and tb[0].device.type == "cuda" and all(b is not None and b[0] is tb[0] for b in bounds):
+        # every model a row of one device pool (the driver's binding): K1 on the rows in place,
+        # addresses from the pool instead of a view per row and segment
+        ops.agg_pool_rows(tb[0], [b[1] for b in bounds], [float(x) for x in weights], tb[1], mode)
+        return target
     layout = tb[0].layout if tb is not None else layout_of_module(target)
     device = next((b[0].device for b in [tb, *bounds] if b is not None and b[0].device.type == "cuda"), None)
     if device is None:

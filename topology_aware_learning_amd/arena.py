@@ -251,6 +251,13 @@ class ModelPool:
     def row_b16(self, r: int) -> torch.Tensor:
         return self.b16[r, : self.layout.n_b16]
 
+    def row_ptrs(self, seg: str, rows: Sequence[int]) -> List[int]:
+        """Addresses of segment `seg` ("f32", "b16", "i64") of each of `rows`, without building
+        a tensor view per row (the per-call path: ten operands per app call)."""
+        t = getattr(self, seg)
+        base, step = t.data_ptr(), t.stride(0) * t.element_size()
+        return [base + step * r for r in rows]
+
     def segments(self):
         """(name, pool tensor, elements per row) of the layout's non-empty segments."""
         lay = self.layout

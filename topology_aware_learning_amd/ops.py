@@ -88,6 +88,46 @@ def agg_model_f32(xs: Sequence[torch.Tensor], xis: Sequence[torch.Tensor], weigh
                               ctypes.c_void_p(out_i.data_ptr()), n_i, int(mode), _stream(out.device, stream)))
 
 
+def agg_pool_rows(pool, rows: Sequence[int], weights: Sequence[float], out_row: int,
+                  mode: int = MODE_EXACT, stream=None) -> None:
+    """K1 on rows of one device-resident ModelPool: row out_row <- sum_i fp32(w_i) * row rows[i],
+    every segment of the layout (fp32 + int64 in one launch, as agg_model_f32; otherwise one
+    launch per segment), out_row may be one of the operands (the app's own model, in place).
+    The arithmetic of agg_model_f32 / agg_f32 / agg_bf16 / agg_i64 on the rows' views, with the
+    operand addresses computed from the pool (the pool's tensors are checked once per call, not
+    each row view): the per-call app path on pool-bound models (decentralized_client.py:399-413)."""
+    if pool.device.type != "cuda":
+        raise ValueError(f"agg_pool_rows needs a device pool (got {pool.device}); the aggregation has no CPU path")
+    m = len(rows)
+    if m == 0:
+        raise ValueError("at least one operand is required")
+    if len(weights) != m:
+        raise ValueError(f"{m} operands but {len(weights)} weights")
+    for r in (*rows, out_row):
+        if not 0 <= int(r) < pool.rows:
+            raise IndexError(f"row {r} outside the pool's {pool.rows} rows")
+    lay = pool.layout
+    W = _lib.double_array(weights)
+    s = _stream(pool.device, stream)
+    L = _lib.load()
+    rows = [int(r) for r in rows]
+    if lay.n_f32 and lay.n_i64 and not lay.n_b16:
+        check(L.tal_agg_model_f32(_lib.ptr_array(pool.row_ptrs("f32", rows)), _lib.ptr_array(pool.row_ptrs("i64", rows)),
+                                  W, m, ctypes.c_void_p(pool.row_ptrs("f32", [out_row])[0]), lay.n_f32,
+                                  ctypes.c_void_p(pool.row_ptrs("i64", [out_row])[0]), lay.n_i64, int(mode), s))
+        return
+    for seg, n in (("f32", lay.n_f32), ("b16", lay.n_b16), ("i64", lay.n_i64)):
+        if not n:
+            continue
+        P = _lib.ptr_array(pool.row_ptrs(seg, rows))
+        out = ctypes.c_void_p(pool.row_ptrs(seg, [out_row])[0])
+        if seg == "i64":
+            check(L.tal_agg_i64(P, W, m, out, n, s))
+        else:
+            fn = L.tal_agg_f32 if seg == "f32" else L.tal_agg_bf16
+            check(fn(P, W, m, out, n, int(mode), s))
+
+
 def agg_bf16(xs: Sequence[torch.Tensor], weights: Sequence[float], out: torch.Tensor,
              mode: int = MODE_EXACT, stream=None) -> torch.Tensor:
     """K1 on bf16 buffers.  MODE_EXACT: the reference's torch ops on bf16 tensors (every product
