@@ -135,6 +135,50 @@ def main():
         ms = 1e3 * (time.perf_counter() - t) / rounds
         print(json.dumps(dict(mode=mode + "_back_to_back", rounds=rounds, ms_per_round=round(ms, 3),
                               params_per_s=64 * 23_574_015 / (ms * 1e-3))), flush=True)
+    # where a synchronised batched round's host time goes: round start -> batch collected ->
+    # RoundExecutor.run entered -> launches issued -> round returned (wrappers around the
+    # driver's own methods; the GPU is synchronised before each round)
+    import src.decentralized_app as dam
+    import topology_aware_learning_amd.round as rmod
+
+    marks = {}
+    orig_batched, orig_run = app._batched_aggregation, rmod.RoundExecutor.run
+
+    def batched(batch):
+        marks["collected"] = time.perf_counter()
+        return orig_batched(batch)
+
+    def run(self, *a, **k):
+        marks["run_entered"] = time.perf_counter()
+        out = orig_run(self, *a, **k)
+        marks["launched"] = time.perf_counter()
+        return out
+
+    app._batched_aggregation = batched
+    rmod.RoundExecutor.run = run
+    app.batched_round = True
+    phases = []
+    for k in range(rounds + 1):
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        futs = app._federated_round(r)
+        t_ret = time.perf_counter()
+        for f in futs:
+            f.result()
+        torch.cuda.synchronize(dev)
+        t_end = time.perf_counter()
+        if k:
+            phases.append([marks["collected"] - t, marks["run_entered"] - marks["collected"],
+                           marks["launched"] - marks["run_entered"], t_ret - marks["launched"], t_end - t_ret])
+        app.round_states.pop(r, None)
+        r += 1
+    app._batched_aggregation, rmod.RoundExecutor.run = orig_batched, orig_run
+    med = np.median(np.array(phases), axis=0) * 1e3
+    print(json.dumps(dict(batched_phases_ms=dict(
+        driver_loops=round(float(med[0]), 3), weights_and_rows=round(float(med[1]), 3),
+        plan_and_launch=round(float(med[2]), 3), futures_resolved=round(float(med[3]), 3),
+        gpu_tail=round(float(med[4]), 3)))), flush=True)
+    del dam
     # the K1 floor: one aggregation call per client with nothing around it
     pool = app.pool
     orders = [sorted(c.neighbors) + [c.idx] for c in app.clients]
