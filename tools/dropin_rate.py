@@ -97,6 +97,45 @@ def main():
         pstats.Stats(pr, stream=out).sort_stats("tottime").print_stats(30)
         print(out.getvalue(), flush=True)
         return
+    if "--per-call-breakdown" in sys.argv:  # app-thread time inside a per-call round, by part
+        import threading
+
+        import src.decentralized_client as dc
+
+        spent = {"aggregate_models": [], "manual_seed": []}
+        lock = threading.Lock()
+        orig_agg, orig_seed = dc.aggregate_models, torch.manual_seed
+
+        def timed(name, fn):
+            def w(*a, **k):
+                t = time.perf_counter()
+                out = fn(*a, **k)
+                with lock:
+                    spent[name].append(time.perf_counter() - t)
+                return out
+            return w
+
+        dc.aggregate_models = timed("aggregate_models", orig_agg)
+        torch.manual_seed = timed("manual_seed", orig_seed)
+        app.batched_round = False
+        ts = []
+        for k in range(rounds + 1):
+            for v in spent.values():
+                v.clear()
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            for f in app._federated_round(r):
+                f.result()
+            torch.cuda.synchronize(dev)
+            if k:
+                ts.append(dict(round_ms=1e3 * (time.perf_counter() - t), calls=len(spent["aggregate_models"]),
+                               **{f"{n}_ms_total": 1e3 * sum(v) for n, v in spent.items()},
+                               **{f"{n}_us_median": 1e6 * float(np.median(v)) for n, v in spent.items() if v}))
+            app.round_states.pop(r, None)
+            r += 1
+        dc.aggregate_models, torch.manual_seed = orig_agg, orig_seed
+        for row in ts:
+            print(json.dumps({k: round(v, 3) if isinstance(v, float) else v for k, v in row.items()}), flush=True)
     for mode in ("per_call", "batched", "per_call", "batched"):
         app.batched_round = mode == "batched"
         ts = []
