@@ -274,7 +274,7 @@ class DecentrallearnApp:
         from topology_aware_learning_amd.arena import bound_row
         from topology_aware_learning_amd.round import RoundExecutor
 
-        from src.decentralized_client import aggregation_weights
+        from src.decentralized_client import aggregation_weights, manual_seed
 
         # each distinct future of the round resolved once (64 training futures behind 640 operand
         # references at config 3), each distinct model's pool row checked once
@@ -304,7 +304,7 @@ class DecentrallearnApp:
             m = me[1].model
             out_rows.append(row_of[id(m)] if id(m) in row_of else pool_row(m))
         if self.seed is not None:  # the apps seed torch per call (reference :395); same end state
-            torch.manual_seed(self.seed)
+            manual_seed(self.seed)
         if orders:
             if self._executor is None:
                 self._executor = RoundExecutor(self.pool)

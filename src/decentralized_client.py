@@ -207,10 +207,26 @@ def _scale_weights(client_future, neighbor_futures, **kwargs):
     return [client_future[1].model], [1 / len(neighbor_futures)]
 
 
+def manual_seed(seed: int) -> None:
+    """The end state of the reference's per-call ``torch.manual_seed(seed)`` (:395, :423, :460,
+    :566, :624): the CPU generator and every initialised GPU's default generator seeded.  torch's
+    own function also walks its lazy-init, MPS, XPU and custom-device paths in Python (≈ 115-320 µs
+    per call holding the GIL on the GPU box, more than the aggregation's own host work); with the
+    GPU runtime initialised and no other accelerator backend those steps do nothing, so this
+    seeds the same generators directly and otherwise defers to torch."""
+    seed = int(seed)
+    if torch.cuda.is_initialized() and not (torch.backends.mps.is_available() or torch.xpu.is_available()):
+        for g in torch.cuda.default_generators:
+            g.manual_seed(seed)
+        torch.default_generator.manual_seed(seed)
+    else:
+        torch.manual_seed(seed)
+
+
 def _app(name, weights_fn, doc):
     def app(client_future, seed: int, *neighbor_futures, **kwargs):
         if seed is not None:
-            torch.manual_seed(seed)
+            manual_seed(seed)
         operands, w = weights_fn(client_future, neighbor_futures, **kwargs)
         aggregate_models(operands, w, client_future[1].model)
         return client_future

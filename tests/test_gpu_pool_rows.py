@@ -81,3 +81,23 @@ def test_pool_rows_rejects_bad_rows(cuda):
     with pytest.raises(ValueError):
         ops.agg_pool_rows(host, [0], [1.0], 1)
     np.testing.assert_equal(a.rows, 4)
+
+
+def test_app_seed_matches_torch_manual_seed(cuda):
+    """The apps' per-call seeding (src.decentralized_client.manual_seed) leaves the CPU and every
+    GPU generator exactly as the reference's torch.manual_seed(seed) does."""
+    from src.decentralized_client import manual_seed
+
+    for seed in (0, 7, 2 ** 40 + 3):
+        torch.manual_seed(seed)
+        ref_cpu = torch.default_generator.get_state()
+        ref_gpu = [g.get_state() for g in torch.cuda.default_generators]
+        torch.manual_seed(seed + 1)
+        torch.rand(3, device=cuda)
+        manual_seed(seed)
+        assert torch.equal(torch.default_generator.get_state(), ref_cpu)
+        for g, ref in zip(torch.cuda.default_generators, ref_gpu):
+            assert torch.equal(g.get_state(), ref)
+        a = torch.rand(5, device=cuda)
+        torch.manual_seed(seed)
+        assert torch.equal(a, torch.rand(5, device=cuda))

@@ -807,3 +807,16 @@ def test_bench_reference_fixture_choice(graph, devices, model, dtype, weights, m
         assert all(len(v) == len(ref["ranges"][seg]) for v in exp.values())
     a.max_params = 4096  # a cut layout is never the fixture's
     assert bench.reference_fixture(a, orders, ws)[1] is None
+
+
+def test_app_seed_matches_torch_manual_seed_cpu():
+    """Without a GPU runtime the apps' seeding defers to torch.manual_seed (same CPU state)."""
+    import torch
+
+    from src.decentralized_client import manual_seed
+
+    torch.manual_seed(11)
+    ref = torch.default_generator.get_state()
+    torch.manual_seed(12)
+    manual_seed(11)
+    assert torch.equal(torch.default_generator.get_state(), ref)
