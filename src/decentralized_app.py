@@ -274,7 +274,7 @@ class DecentrallearnApp:
         from topology_aware_learning_amd.arena import bound_row
         from topology_aware_learning_amd.round import RoundExecutor
 
-        from src.decentralized_client import aggregation_weights, manual_seed
+        from src.decentralized_client import manual_seed, weight_rule
 
         # each distinct future of the round resolved once (64 training futures behind 640 operand
         # references at config 3), each distinct model's pool row checked once
@@ -293,12 +293,13 @@ class DecentrallearnApp:
             return b[1]
 
         orders, weights, out_rows, done = [], [], [], []
+        rule = weight_rule(self.aggregation_function)  # None for test_agg: a no-op
         for future, agg_client, agg_neighbors, kwargs in batch:
             me = memo[id(agg_client)]
-            got = aggregation_weights(self.aggregation_function, me, *[memo[id(f)] for f in agg_neighbors], **kwargs)
             done.append((future, me))
-            if got is None:  # test_agg: no-op
+            if rule is None:
                 continue
+            got = rule(me, [memo[id(f)] for f in agg_neighbors], **kwargs)
             orders.append([row_of[id(m)] if id(m) in row_of else pool_row(m) for m in got[0]])
             weights.append(list(map(float, got[1])))
             m = me[1].model

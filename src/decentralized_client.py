@@ -256,13 +256,12 @@ def test_agg(client_future, seed: int, *neighbor_futures, **kwargs):
     return client_future
 
 
-def aggregation_weights(app, client_future, *neighbor_futures, **kwargs):
-    """(operand models, float64 weights) the app would aggregate for this call, without
-    aggregating; None for test_agg.  Used by the batched round (TAL_BATCHED_ROUND=1)."""
-    fn = getattr(getattr(app, "__wrapped__", app), "_tal_weights", None)
-    if fn is None:
-        return None
-    return fn(client_future, neighbor_futures, **kwargs)
+def weight_rule(app):
+    """The app's weight rule, rule(client_future, neighbor_futures, **kwargs) -> (operand
+    models, float64 weights), or None for test_agg (a no-op).  Used by the batched round
+    (TAL_BATCHED_ROUND=1), which looks it up once per round."""
+    return getattr(getattr(app, "__wrapped__", app), "_tal_weights", None)
+
 
 
 def cosine_similarity(model_1, model_2):
