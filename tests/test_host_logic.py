@@ -820,3 +820,26 @@ def test_app_seed_matches_torch_manual_seed_cpu():
     torch.manual_seed(12)
     manual_seed(11)
     assert torch.equal(torch.default_generator.get_state(), ref)
+
+
+def test_default_plan_rows_wider_than_a_tile():
+    """A row of more distinct sources than one LDS tile holds (unweighted_fl over 700 clients):
+    fp32 rounds get the streamed form, bf16 rounds and rows out of reference order one K1 call
+    per row - never a capacity error (host-side plan building, no GPU)."""
+    import networkx as nx
+
+    from topology_aware_learning_amd import ops
+    from topology_aware_learning_amd.round import csr_from_lists
+
+    g = nx.complete_graph(700)
+    orders = [sorted(g.neighbors(i)) + [i] for i in range(700)]
+    rp, col, w = csr_from_lists(orders, [[1 / 700] * 700 for _ in orders])
+    rows = np.arange(700, dtype=np.int32)
+    p = ops.default_plan(rp, col, w, rows)
+    assert ops.round_kernel_name(p) == "k_round_stream" and not p.single_group
+    q = ops.default_plan(rp, col, w, rows, bf16=True)
+    assert isinstance(q, ops.RowCallPlan) and q.staged_rows() == 700 * 700 and not q.single_group
+    assert isinstance(ops.plan_from_spec(rp, col, w, rows, q.spec), ops.RowCallPlan)
+    self_first = [[i] + sorted(g.neighbors(i)) for i in range(700)]
+    rp2, col2, w2 = csr_from_lists(self_first, [[1 / 700] * 700 for _ in self_first])
+    assert isinstance(ops.default_plan(rp2, col2, w2, rows), ops.RowCallPlan)

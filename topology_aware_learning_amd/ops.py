@@ -206,6 +206,69 @@ class RoundPlan:
         return int(self.info.total_src)
 
 
+@dataclass
+class RowCallPlan:
+    """A round as one K1 call per row, out of place (snapshot semantics): the fallback for a
+    round with a row of more distinct sources than any LDS-tiled form stages in one tile
+    (> ~620 at c4 = 16) on a bf16 pool, where the streamed form (fp32 only) cannot take it
+    either - e.g. the reference's `unweighted_fl` strategy (every other client a neighbor,
+    decentralized_app.py:386-389) with many clients under the batched round.  K1 chains any
+    operand count in reference order, so every row is bitwise its per-call aggregation."""
+    row_ptr: np.ndarray
+    col: np.ndarray
+    w: np.ndarray
+    out_row: np.ndarray
+    device: Optional[torch.device] = None
+    tuned_ms: Optional[float] = None
+    candidates: Optional[list] = None
+    spec: Optional[dict] = None
+
+    @property
+    def rows(self) -> int:
+        return len(self.out_row)
+
+    @property
+    def single_group(self) -> bool:
+        return False  # rows read other rows' pre-round values: never in place
+
+    def staged_rows(self) -> int:
+        """Source rows read from HBM per column: every operand of every row."""
+        return int(len(self.col))
+
+    def to(self, device) -> "RowCallPlan":
+        self.device = torch.device(device)
+        return self
+
+
+def row_call_plan(row_ptr, col, w, out_row) -> RowCallPlan:
+    rp, cl, ww, orow = _csr(row_ptr, col, w, out_row)
+    return RowCallPlan(rp, cl, ww, orow, spec={"rows_k1": 1})
+
+
+def _round_rows(pool_in, pool_out, plan: RowCallPlan, n, dtype, mode, stream):
+    _require_gpu(pool_in, "pool_in", dtype)
+    _require_gpu(pool_out, "pool_out", dtype)
+    if pool_in.dim() != 2 or pool_out.dim() != 2:
+        raise ValueError("pools must be 2-D [models, ld]")
+    if pool_in.data_ptr() == pool_out.data_ptr():
+        raise ValueError("a per-row round runs out of place (snapshot semantics)")
+    n = pool_in.shape[1] if n is None else int(n)
+    if plan.col.max(initial=-1) >= pool_in.shape[0] or plan.out_row.max(initial=-1) >= pool_out.shape[0]:
+        raise ValueError("plan rows beyond the pools")
+    for r in range(plan.rows):
+        a, b = int(plan.row_ptr[r]), int(plan.row_ptr[r + 1])
+        xs = [pool_in[int(j), :n] for j in plan.col[a:b]]
+        out = pool_out[int(plan.out_row[r]), :n]
+        ws = plan.w[a:b].tolist()
+        if dtype == torch.int64:
+            agg_i64(xs, ws, out, stream=stream)
+        elif dtype == torch.bfloat16:
+            agg_bf16(xs, ws, out, mode=mode, stream=stream)
+        else:
+            agg_f32(xs, ws, out, mode=mode, stream=stream)
+    return pool_out
+
+
 def build_plan(row_ptr, col, w, out_row, c4: int = 0, lds_bytes: int = 0, dense: int = 0,
                bcast: int = 0, bcast_wg: int = 2) -> RoundPlan:
     """Tile plan for a round given as CSR (row r: operands col[row_ptr[r]:row_ptr[r+1]] with
@@ -755,6 +818,8 @@ def plan_from_spec(row_ptr, col, w, out_row, spec: dict) -> RoundPlan:
             raise ValueError("plan spec asks for register groups but a row has too many sources")
         p.spec = dict(spec)
         return p
+    if "rows_k1" in spec:
+        return row_call_plan(row_ptr, col, w, out_row)
     if "stream_rows" in spec:
         p = build_stream_plan(row_ptr, col, w, out_row, int(spec["stream_rows"]), int(spec["stream_src"]))
     else:
@@ -780,13 +845,31 @@ def default_plan(row_ptr, col, w, out_row, bf16: bool = False, mode: int = MODE_
     for the cost model's two-group pairs plan; profiles/r04/r04f).  The broadcast plan is taken
     only when it has no more groups than the sparse plan; RoundExecutor runs a single-group
     plan (config 5's: every source in one tile) in place and a multi-group one through its
-    scratch pool."""
-    if not bf16:
-        cp = build_clique_plan(row_ptr, col, w, out_row)
-        if cp is not None:
-            cp.spec = dict(clique=1, rest=cp.rest.spec if cp.rest is not None else None)
-            return cp
-    p = build_plan(row_ptr, col, w, out_row, dense=0)
+    scratch pool.  A round with a row of more distinct sources than one LDS tile holds (e.g.
+    `unweighted_fl` over > ~620 clients) gets the streamed form (fp32) or one K1 call per row
+    (RowCallPlan, bf16 pools)."""
+    try:
+        if not bf16:
+            cp = build_clique_plan(row_ptr, col, w, out_row)
+            if cp is not None:
+                cp.spec = dict(clique=1, rest=cp.rest.spec if cp.rest is not None else None)
+                return cp
+        p = build_plan(row_ptr, col, w, out_row, dense=0)
+    except _lib.TalError as exc:
+        if exc.code != _lib.TAL_ERR_CAPACITY:
+            raise
+        # a row with more distinct sources than one LDS tile holds: fp32 rounds stream their
+        # sources through an LDS ring (any group size; rows in reference order); bf16 pools,
+        # which the streamed kernel does not take, and other operand orders run one K1 call
+        # per row
+        if not bf16:
+            try:
+                p = build_stream_plan(row_ptr, col, w, out_row)
+                p.spec = {"stream_rows": 64, "stream_src": 0}
+                return p
+            except _lib.TalError:
+                pass
+        return row_call_plan(row_ptr, col, w, out_row)
     if p.info.c4 < 64 and not p.info.narrow_roww and (not bf16 or mode == MODE_FMA):
         # per-operand weights on a narrow plan: the broadcast form with every source in one LDS
         # tile - bf16 FMA: the two-chunk form (c4 = 32, one workgroup per CU) when its 512-B
@@ -810,6 +893,8 @@ def round_kernel_name(plan) -> str:
         return "k_round_clique"
     if isinstance(plan, RegPlan):
         return "k_round_reg"
+    if isinstance(plan, RowCallPlan):
+        return "k_agg (one call per row)"
     info = plan.info if isinstance(plan, RoundPlan) else plan
     if info.stream_cs:
         return "k_round_stream"
@@ -846,6 +931,8 @@ def round_f32(pool_in: torch.Tensor, pool_out: torch.Tensor, plan, n: Optional[i
         return _round_clique(pool_in, pool_out, plan, n, mode, stream)
     if isinstance(plan, RegPlan):
         return _round_reg(pool_in, pool_out, plan, n, torch.float32, mode, stream)
+    if isinstance(plan, RowCallPlan):
+        return _round_rows(pool_in, pool_out, plan, n, torch.float32, mode, stream)
     return _round(pool_in, pool_out, plan, n, torch.float32, mode, stream)
 
 
@@ -885,6 +972,8 @@ def round_i64(pool_in: torch.Tensor, pool_out: torch.Tensor, plan: RoundPlan, n:
               stream=None) -> torch.Tensor:
     if isinstance(plan, (CliquePlan, RegPlan)):
         plan = plan.full
+    if isinstance(plan, RowCallPlan):
+        return _round_rows(pool_in, pool_out, plan, n, torch.int64, MODE_EXACT, stream)
     return _round(pool_in, pool_out, plan, n, torch.int64, MODE_EXACT, stream)
 
 
@@ -895,6 +984,8 @@ def round_bf16(pool_in: torch.Tensor, pool_out: torch.Tensor, plan: RoundPlan, n
         plan = plan.full
     if isinstance(plan, RegPlan):
         return _round_reg(pool_in, pool_out, plan, n, torch.bfloat16, mode, stream)
+    if isinstance(plan, RowCallPlan):
+        return _round_rows(pool_in, pool_out, plan, n, torch.bfloat16, mode, stream)
     return _round(pool_in, pool_out, plan, n, torch.bfloat16, mode, stream)
 
 
