@@ -66,7 +66,8 @@ int32_t tal_agg_f32(const float* const* x_host, const double* w_host, int32_t m,
 /* int64 buffers (num_batches_tracked): torch promotes `python_float * int64_tensor` to
  * fp32, accumulates in fp32 and load_state_dict's copy_ truncates toward zero
  * (decentralized_client.py:407-413).  NaN / out-of-range results give INT64_MIN, as the
- * x86 cvttss2si the reference runs on does. */
+ * x86 cvttss2si the reference runs on does.  Any m >= 1 (past 256 operands: passes through
+ * an fp32 scratch, as tal_agg_bf16); out may alias any x[i]. */
 int32_t tal_agg_i64(const int64_t* const* x_host, const double* w_host, int32_t m,
                     int64_t* out, int64_t n, void* stream);
 
@@ -84,8 +85,10 @@ int32_t tal_agg_model_f32(const float* const* x_host, const int64_t* const* xi_h
  * own ops on bf16 tensors (decentralized_client.py:407-411 - `w * clone(v)` and `+=` each
  * round their fp32 result to bf16, nearest even), bit-identical to it; TAL_MODE_FMA: fp32
  * fused accumulation rounded to bf16 once (|error| <= 2^-8 |result| + M 2^-24 sum|w x|).  NaN
- * results are stored as 0xFFFF (torch's vectorized conversion).  m <= 256; out may alias
- * any x[i]. */
+ * results are stored as 0xFFFF (torch's vectorized conversion).  Any m >= 1: past 256
+ * operands the ordered chain runs in passes of 256 through an fp32 scratch of n elements,
+ * allocated and freed in stream order (hipMallocAsync), carrying the same running value the
+ * one-pass kernel keeps in registers; out may alias any x[i]. */
 int32_t tal_agg_bf16(const uint16_t* const* x_host, const double* w_host, int32_t m,
                      uint16_t* out, int64_t n, int32_t mode, void* stream);
 

@@ -56,3 +56,54 @@ def test_unweighted_fl_round_700_clients(cuda, dtype):
             assert np.array_equal(exp, got[r].view(torch.int16).numpy().view(np.uint16)), r
         exp_i = oracle.agg_i64([xi[j] for j in orders[r]], ws[r])
         assert np.array_equal(exp_i, got_i[r]), r
+
+
+@pytest.mark.parametrize("m", [257, 600])
+@pytest.mark.parametrize("kind", ["bf16_exact", "bf16_fma", "i64", "f32"])
+def test_k1_past_256_operands(cuda, kind, m):
+    """K1 (the per-call path) on more operands than one kernel-argument table holds: bitwise the
+    oracle's single ordered chain, with out aliasing the last operand (the app's own model)."""
+    rng = np.random.default_rng(m)
+    n = 3001
+    w = rng.uniform(0.0, 2.0 / m, m)
+    if kind == "i64":
+        x = rng.integers(-10 ** 6, 10 ** 6, (m, n)).astype(np.int64)
+        exp = oracle.agg_i64(list(x), w)
+        dev = torch.from_numpy(x).to(cuda)
+        ops.agg_i64([dev[j] for j in range(m)], w.tolist(), dev[m - 1])
+        got = dev[m - 1].cpu().numpy()
+        assert np.array_equal(got, exp)
+        return
+    if kind == "f32":
+        x = rng.standard_normal((m, n)).astype(np.float32)
+        exp = oracle.agg_f32(list(x), w)
+        dev = torch.from_numpy(x).to(cuda)
+        ops.agg_f32([dev[j] for j in range(m)], w.tolist(), dev[m - 1])
+        assert np.array_equal(dev[m - 1].cpu().numpy().view(np.uint32), exp.view(np.uint32))
+        return
+    exact = kind == "bf16_exact"
+    bits = oracle.f32_to_bf16(rng.standard_normal((m, n)).astype(np.float32))
+    exp = oracle.agg_bf16(list(bits), w, exact=exact)
+    dev = torch.from_numpy(bits.view(np.int16)).to(cuda).view(torch.bfloat16)
+    ops.agg_bf16([dev[j] for j in range(m)], w.tolist(), dev[m - 1], mode=ops.MODE_EXACT if exact else ops.MODE_FMA)
+    got = dev[m - 1].view(torch.int16).cpu().numpy().view(np.uint16)
+    assert np.array_equal(got, exp)
+
+
+def test_pool_rows_app_past_256_operands(cuda):
+    """The per-call app path on pool rows (agg_pool_rows) with 300 operands of a ResNet-like
+    fp32 + int64 layout: bitwise the oracle (fp32 chain and int64 truncation)."""
+    m = 300
+    lay = StateLayout.from_layout([("w", (2000,), "float32"), ("n", (), "int64")])
+    pool = ModelPool(lay, m, cuda)
+    g = torch.Generator(device=cuda).manual_seed(9)
+    pool.f32.normal_(generator=g)
+    pool.i64.random_(0, 10 ** 6, generator=g)
+    x = pool.f32[:, :lay.n_f32].cpu().numpy()
+    xi = pool.i64[:, :lay.n_i64].cpu().numpy()
+    w = [1.0 / m] * m
+    ops.agg_pool_rows(pool, list(range(m)), w, m - 1)
+    exp = oracle.agg_f32(list(x), w)
+    exp_i = oracle.agg_i64(list(xi), w)
+    assert np.array_equal(pool.f32[m - 1, :lay.n_f32].cpu().numpy().view(np.uint32), exp.view(np.uint32))
+    assert np.array_equal(pool.i64[m - 1, :lay.n_i64].cpu().numpy(), exp_i)

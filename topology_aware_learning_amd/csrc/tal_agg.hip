@@ -45,7 +45,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 21;
+constexpr int kAbiVersion = 22;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -639,6 +639,59 @@ __global__ __launch_bounds__(kBlock) void k_agg_b16_scalar(OpTableB16 t, int m, 
     for (int k = 1; k < m; ++k) acc = next1t<uint16_t, EXACT>(acc, t.w[k], Io<uint16_t>::ld1(t.x[k], e));
     Io<uint16_t>::st1(out, e, acc);
   }
+}
+
+// K1 past kMaxOps operands for bf16 and int64 buffers: the ordered chain over m operands runs
+// in passes of up to kMaxOps (one kernel-argument table each), the running sum kept in an fp32
+// scratch between passes - exactly the register value the one-pass kernels carry (bf16 EXACT:
+// a bf16 value; FMA and int64: the unrounded fp32 sum) - and stored to `out` (rounded /
+// truncated) only by the last pass, so `out` may alias any operand.  One element per thread.
+template <typename T>
+struct OpTableT {
+  const T* x[kMaxOps];
+  float w[kMaxOps];
+};
+
+template <typename T, bool EXACT>
+__global__ __launch_bounds__(kBlock) void k_agg_chain(OpTableT<T> t, int m, bool first, bool last, float* acc,
+                                                      T* out, int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n; e += stride) {
+    float a;
+    int k0 = 0;
+    if constexpr (std::is_same<T, int64_t>::value) {
+      if (first) { a = __fmul_rn(t.w[0], static_cast<float>(t.x[0][e])); k0 = 1; } else { a = acc[e]; }
+      for (int k = k0; k < m; ++k) a = __fadd_rn(a, __fmul_rn(t.w[k], static_cast<float>(t.x[k][e])));
+      if (last) out[e] = trunc_i64(a); else acc[e] = a;
+    } else {
+      if (first) { a = first1t<T, EXACT>(t.w[0], Io<T>::ld1(t.x[0], e)); k0 = 1; } else { a = acc[e]; }
+      for (int k = k0; k < m; ++k) a = next1t<T, EXACT>(a, t.w[k], Io<T>::ld1(t.x[k], e));
+      if (last) Io<T>::st1(out, e, a); else acc[e] = a;
+    }
+  }
+}
+
+// Host side of k_agg_chain: m > kMaxOps operands, an fp32 scratch of n elements allocated and
+// freed in stream order (nothing persistent).
+template <typename T, bool EXACT>
+int32_t agg_chain(const T* const* x_host, const double* w_host, int32_t m, T* out, int64_t n, hipStream_t s,
+                  const char* who) {
+  float* acc = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void**>(&acc), static_cast<size_t>(n) * sizeof(float), s) != hipSuccess)
+    return fail(TAL_ERR_HIP, std::string(who) + ": scratch allocation failed");
+  for (int base = 0; base < m; base += kMaxOps) {
+    OpTableT<T> t;
+    const int cnt = std::min(kMaxOps, m - base);
+    for (int i = 0; i < cnt; ++i) {
+      t.x[i] = x_host[base + i];
+      t.w[i] = static_cast<float>(w_host[base + i]);
+    }
+    for (int i = cnt; i < kMaxOps; ++i) { t.x[i] = nullptr; t.w[i] = 0.f; }
+    k_agg_chain<T, EXACT><<<grid_for(n), kBlock, 0, s>>>(t, cnt, base == 0, base + cnt >= m, acc, out, n);
+  }
+  const int32_t rc = check_launch(who);
+  if (hipFreeAsync(acc, s) != hipSuccess && rc == TAL_OK) return fail(TAL_ERR_HIP, std::string(who) + ": scratch free failed");
+  return rc;
 }
 
 // Compute one column tile from LDS.  A wavefront owns whole rows (row index wave-uniform, so
@@ -3757,8 +3810,11 @@ int32_t tal_agg_i64(const int64_t* const* x_host, const double* w_host, int32_t 
   if (n < 0) return fail(TAL_ERR_INVALID, "tal_agg_i64: n < 0");
   if (!x_host || !w_host || (n > 0 && !out)) return fail(TAL_ERR_INVALID, "tal_agg_i64: null pointer");
   if (n == 0) { g_err.clear(); return TAL_OK; }
-  if (m > kMaxOps)
-    return fail(TAL_ERR_INVALID, "tal_agg_i64: more than 256 operands: use tal_agg_round_i64");
+  if (m > kMaxOps) {  // the chain in passes through an fp32 scratch (k_agg_chain)
+    for (int i = 0; i < m; ++i)
+      if (!x_host[i]) return fail(TAL_ERR_INVALID, "tal_agg_i64: null operand pointer");
+    return agg_chain<int64_t, true>(x_host, w_host, m, out, n, static_cast<hipStream_t>(stream), "tal_agg_i64");
+  }
   OpTableI64 t;
   for (int i = 0; i < m; ++i) {
     if (!x_host[i]) return fail(TAL_ERR_INVALID, "tal_agg_i64: null operand pointer");
@@ -4088,11 +4144,16 @@ int32_t tal_agg_round_reg(const void* pool_in, int64_t ld_in, void* pool_out, in
 int32_t tal_agg_bf16(const uint16_t* const* x_host, const double* w_host, int32_t m, uint16_t* out,
                      int64_t n, int32_t mode, void* stream) {
   if (m <= 0) return fail(TAL_ERR_INVALID, "tal_agg_bf16: m must be >= 1");
-  if (m > kMaxOps)
-    return fail(TAL_ERR_INVALID, "tal_agg_bf16: more than 256 operands: use tal_agg_round_bf16");
   if (n < 0) return fail(TAL_ERR_INVALID, "tal_agg_bf16: n < 0");
   if (!x_host || !w_host || (n > 0 && !out)) return fail(TAL_ERR_INVALID, "tal_agg_bf16: null pointer");
   if (n == 0) { g_err.clear(); return TAL_OK; }
+  if (m > kMaxOps) {  // the chain in passes through an fp32 scratch (k_agg_chain)
+    for (int i = 0; i < m; ++i)
+      if (!x_host[i]) return fail(TAL_ERR_INVALID, "tal_agg_bf16: null operand pointer");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    return mode == TAL_MODE_EXACT ? agg_chain<uint16_t, true>(x_host, w_host, m, out, n, s, "tal_agg_bf16")
+                                  : agg_chain<uint16_t, false>(x_host, w_host, m, out, n, s, "tal_agg_bf16");
+  }
   OpTableB16 t;
   bool vec = aligned8(out);
   for (int i = 0; i < m; ++i) {
