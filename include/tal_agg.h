@@ -59,7 +59,9 @@ int32_t tal_abi_version(void);
  * out[e] = sum_{i<M} fp32(w_host[i]) * x[i][e]   for e < n  (fp32 segment)
  * Replaces decentralized_client.py:399-411 (+ the fp32 part of load_state_dict :413).
  * x_host: host array of M device pointers.  out may alias any x[i] (the reference's
- * aggregating client is itself the last operand, decentralized_app.py:625).  */
+ * aggregating client is itself the last operand, decentralized_app.py:625).  Any M >= 1:
+ * past 256 operands further passes continue the ordered chain from out, or - when an operand
+ * past the first 256 aliases out - from a stream-ordered fp32 scratch (as tal_agg_bf16).  */
 int32_t tal_agg_f32(const float* const* x_host, const double* w_host, int32_t m,
                     float* out, int64_t n, int32_t mode, void* stream);
 

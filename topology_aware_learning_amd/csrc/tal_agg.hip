@@ -3784,7 +3784,14 @@ int32_t tal_agg_f32(const float* const* x_host, const double* w_host, int32_t m,
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool exact = mode == TAL_MODE_EXACT;
   // Operands beyond kMaxOps are folded in by further passes that continue the same ordered
-  // chain from `out` (stored exactly in fp32, so the result is unchanged).
+  // chain from `out` (stored exactly in fp32, so the result is unchanged).  A later pass must
+  // not read an operand that aliases `out` after out was overwritten (the reference's own
+  // model is the last operand, decentralized_app.py:625): then the chain runs through an fp32
+  // scratch instead and `out` is written by the last pass only.
+  for (int i = kMaxOps; i < m; ++i)
+    if (x_host[i] == out)
+      return exact ? agg_chain<float, true>(x_host, w_host, m, out, n, s, "tal_agg_f32")
+                   : agg_chain<float, false>(x_host, w_host, m, out, n, s, "tal_agg_f32");
   for (int base = 0; base < m; base += kMaxOps) {
     OpTableF32 t;
     const int cnt = std::min(kMaxOps, m - base);
@@ -3793,11 +3800,6 @@ int32_t tal_agg_f32(const float* const* x_host, const double* w_host, int32_t m,
       t.w[i] = static_cast<float>(w_host[base + i]);
     }
     for (int i = cnt; i < kMaxOps; ++i) { t.x[i] = nullptr; t.w[i] = 0.f; }
-    // a later pass must not read an operand that aliases `out` after out was overwritten
-    if (base > 0)
-      for (int i = 0; i < cnt; ++i)
-        if (t.x[i] == out)
-          return fail(TAL_ERR_INVALID, "tal_agg_f32: out aliases an operand beyond the first 256");
     if (exact) launch_pass<true>(t, cnt, base > 0, vec, out, n, s);
     else launch_pass<false>(t, cnt, base > 0, vec, out, n, s);
   }
