@@ -157,7 +157,11 @@ struct OpTableI64 {
 // so keeping it out of the caches leaves L2/MALL to the output stream (measured +15-20 % at
 // M = 9 on MI355X, tools/tune/k1_variants.hip).
 __device__ __forceinline__ float4 ld_stream(const float* base, int64_t i) {
+#ifdef TAL_PROBE_LD_PLAIN  // A/B probe: cached operand loads
+  const v4f q = reinterpret_cast<const v4f*>(base)[i];
+#else
   const v4f q = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(base) + i);
+#endif
   return make_float4(q.x, q.y, q.z, q.w);
 }
 
@@ -455,7 +459,11 @@ __device__ __forceinline__ GroupLds stage_group(const PlanView& p, int g, void* 
 
 __device__ __forceinline__ void st_stream(float* base, int64_t i, float4 v) {
   const v4f q = {v.x, v.y, v.z, v.w};
+#ifdef TAL_PROBE_ST_PLAIN  // A/B probe: cached output stores
+  reinterpret_cast<v4f*>(base)[i] = q;
+#else
   __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(base) + i);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
