@@ -46,7 +46,9 @@ def main():
     ap.add_argument("--allocs", type=int, default=4)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--in-place", action="store_true", help="also time each form in place on every target")
+    ap.add_argument("--forms", default="", help="comma-separated indices into FORMS (default: all)")
     a = ap.parse_args()
+    forms = [FORMS[int(i)] for i in a.forms.split(",")] if a.forms else FORMS
     dev = torch.device("cuda", 0)
     lay = StateLayout.from_layout(synth.get_layout("resnet50"))
     n, ld = lay.n_f32, lay.ld_f32
@@ -55,7 +57,7 @@ def main():
     rp, col, w = csr_from_lists(orders, ws)
     out_rows = np.arange(rows, dtype=np.int32)
     plans = []
-    for spec in FORMS:
+    for spec in forms:
         try:
             plans.append((spec, ops.plan_from_spec(rp, col, w, out_rows, spec).to(dev)))
         except Exception as exc:  # a form this round cannot build
