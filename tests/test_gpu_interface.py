@@ -225,6 +225,49 @@ def test_driver_batched_round(cuda, tmp_path, monkeypatch):
     assert rc == 0 and runs == [8, 8]
 
 
+@pytest.mark.parametrize("strategy,participation", [("weighted", 0.5), ("unweighted", 0.75), ("test_agg", 1.0)])
+def test_driver_batched_round_partial(cuda, tmp_path, monkeypatch, strategy, participation):
+    """TAL_BATCHED_ROUND=1 with part of the clients selected (the others keep their trained
+    model, decentralized_app.py:599-604), data-size weights, and test_agg (no aggregation): each
+    round's launch covers exactly the selected clients with surviving neighbors, and the pool
+    after it equals the oracle's snapshot round over those rows, the other rows untouched."""
+    import oracle
+
+    monkeypatch.setenv("TAL_SYNTHETIC_DATA", "1")
+    monkeypatch.setenv("TAL_SYNTHETIC_SAMPLES", "64")
+    monkeypatch.setenv("TAL_BATCHED_ROUND", "1")
+    real_run = RoundExecutor.run
+    runs = []
+
+    def checked_run(self, orders, weights, out_rows=None, sequential=False):
+        lay = self.pool.layout
+        f_in = self.pool.f32[:, : lay.n_f32].cpu().numpy().copy()
+        i_in = self.pool.i64[:, : lay.n_i64].cpu().numpy().copy()
+        real_run(self, orders, weights, out_rows, sequential)
+        rp, col, w = ra.round_csr(orders, weights)
+        ref = f_in.copy()
+        iref = i_in.copy()
+        oracle.round_f32(f_in, rp, col, w, np.asarray(out_rows), pool_out=ref)
+        oracle.round_i64(i_in, rp, col, w, np.asarray(out_rows), pool_out=iref)
+        assert np.array_equal(self.pool.f32[:, : lay.n_f32].cpu().numpy().view(np.uint32), ref.view(np.uint32))
+        assert np.array_equal(self.pool.i64[:, : lay.n_i64].cpu().numpy(), iref)
+        runs.append(sorted(out_rows))
+
+    monkeypatch.setattr(RoundExecutor, "run", checked_run)
+    topo = tmp_path / "rr12.txt"
+    np.savetxt(topo, nx.to_numpy_array(nx.random_regular_graph(3, 12, seed=1)), fmt="%d")
+    from src.experiments import decentralized_main
+
+    rc = decentralized_main.main(["--dataset", "cifar10", "--aggregation_strategy", strategy, "--rounds", "2",
+                                  "--epochs", "1", "--topology_file", str(topo), "--out_dir", str(tmp_path / "logs"),
+                                  "--batch_size", "32", "--participation", str(participation)])
+    assert rc == 0
+    if strategy == "test_agg":
+        assert runs == []  # nothing to aggregate: no launch
+    else:
+        assert len(runs) == 2 and all(len(r) == int(12 * participation) for r in runs)
+
+
 def test_checkpoint_from_device_pool(cuda, tmp_path):
     """SURVEY §8(f) row 2 on the GPU: the checkpoint is written from the pool rows and reads
     back (reference loader and pool loader) bit-identically."""
