@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     ap.add_argument("--mode", default="exact", choices=["exact", "fma"])
     ap.add_argument("--fill", default="pool", choices=["pool", "randn"])
+    ap.add_argument("--in-place", action="store_true", help="round in place on the input pool (single-group plans)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     lay = synth.get_layout(a.model)
@@ -58,7 +59,7 @@ def main():
     print(f"plan c4={i.c4} groups={i.n_groups} staged={i.total_src} max_src={i.max_src} dense_rb={i.dense_rb} "
           f"stream_cs={i.stream_cs} lds={i.lds_bytes} kernel={ops.round_kernel_name(i)}", flush=True)
     pin = ModelPool(layout, rows, dev)
-    pout = ModelPool(layout, rows, dev)
+    pout = pin if a.in_place else ModelPool(layout, rows, dev)
     if a.fill == "randn":
         for _, t, _ in pin.segments():
             if t.dtype.is_floating_point:
