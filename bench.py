@@ -473,11 +473,17 @@ def main():
     else:
         from topology_aware_learning_amd.transposed import make_round
 
+        # per-rank progress on stderr: a first multi-GPU run that stalls names its phase
+        rlog = (lambda msg: log(f"rank {rank}/{world}: {msg}"))
+        rlog(f"{n_dev_total} devices, {layout.n_f32 + layout.n_b16} float params per model; building the round")
         sr = make_round(layout, orders, weights, rank, world, dev, exchange=args.exchange, mode=mode,
                         tune=not args.no_tune,
                         transport="host" if args.dist_backend == "gloo" else args.halo_transport)
+        rlog(f"{sr.exchange_kind} exchange over {sr.transport}, {len(sr.own_ids)} own devices; first round")
         rowcheck.fill_owned(sr.pool_a, lay, sr.own_ids, seed_base)
         sr.step()
+        torch.cuda.synchronize(dev)
+        rlog("first round done; checking every owned row")
         # every output row this rank owns, against the reference's digests or K1 on operands
         # regenerated from their seeds - never on what the exchange delivered (rowcheck)
         chk = rowcheck.check_round(sr.own_rows(), sr.own_ids, lay, orders, weights, seed_base, mode,
@@ -492,6 +498,7 @@ def main():
         parity_rows = dict(rows_checked=rows_checked, rows_differing=rows_differing,
                            first_bad=sorted(j for b in bad_all for j in b)[:8], reference=chk["reference"],
                            devices=n_dev_total)
+        rlog(f"rows checked {rows_checked}, differing {rows_differing}; {args.warmup} warm-up + {args.steps} timed rounds")
         for _ in range(args.warmup):
             sr.step()
         torch.cuda.synchronize(dev)
