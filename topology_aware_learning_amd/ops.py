@@ -107,6 +107,9 @@ def agg_pool_rows(pool, rows: Sequence[int], weights: Sequence[float], out_row: 
         if not 0 <= int(r) < pool.rows:
             raise IndexError(f"row {r} outside the pool's {pool.rows} rows")
     lay = pool.layout
+    for seg, t, n in pool.segments():
+        if t.dim() != 2 or t.stride(1) != 1 or t.shape[1] < n:
+            raise ValueError(f"pool segment {seg} must be [rows, ld] with unit column stride")
     W = _lib.double_array(weights)
     s = _stream(pool.device, stream)
     L = _lib.load()
