@@ -253,24 +253,29 @@ class DecentrallearnApp:
             kwargs = dict(centrality_metric=self.centrality_metric, centrality_dict=self.centrality_dict,
                           softmax=self.softmax, softmax_coeff=self.aggregation_scheduler.get_softmax_coeff())
             if batch is not None:  # collected; the whole round runs below as one K3 launch
-                future = Future()
-                batch.append((future, agg_client, agg_neighbors, kwargs))
-            else:
-                future = self.aggregation_function(agg_client, self.seed, *agg_neighbors, **kwargs)
+                batch.append((len(futures), client.idx, agg_client, agg_neighbors, kwargs))
+                futures.append(None)  # its future is made after the launch (below)
+                continue
+            future = self.aggregation_function(agg_client, self.seed, *agg_neighbors, **kwargs)
             futures.append(future)
             nxt[client.idx]["agg"] = future
         if batch:
-            self._batched_aggregation(batch)
+            # the launch first, then the round's futures (already resolved: the aggregation is
+            # stream-ordered behind the launch), so their setup runs under the kernel
+            for (pos, idx, *_), me in zip(batch, self._batched_aggregation(batch)):
+                future = Future()
+                future.set_result(me)
+                futures[pos] = nxt[idx]["agg"] = future
         self.aggregation_scheduler.step(round_idx)
         return futures
 
-    def _batched_aggregation(self, batch) -> None:
+    def _batched_aggregation(self, batch) -> list:
         """The round's aggregations as ONE K3 launch over the device pool (RoundExecutor):
         every aggregation reads the models as they were after training (snapshot semantics,
         SURVEY §8(a)).  The reference's per-call apps instead read neighbors that an earlier
         call of the same round may already have overwritten, in an order its 2-thread pool
         decides; per call each result is the same arithmetic (same operands in the same order,
-        same fp32 weights)."""
+        same fp32 weights).  Returns each entry's aggregated (results, client) tuple, in order."""
         from topology_aware_learning_amd.arena import bound_row
         from topology_aware_learning_amd.round import RoundExecutor
 
@@ -279,7 +284,7 @@ class DecentrallearnApp:
         # each distinct future of the round resolved once (64 training futures behind 640 operand
         # references at config 3), each distinct model's pool row checked once
         memo: dict = {}
-        for _, agg_client, agg_neighbors, _ in batch:
+        for _, _, agg_client, agg_neighbors, _ in batch:
             for x in (agg_client, *agg_neighbors):
                 if id(x) not in memo:
                     memo[id(x)] = x.result() if isinstance(x, Future) else x
@@ -294,9 +299,9 @@ class DecentrallearnApp:
 
         orders, weights, out_rows, done = [], [], [], []
         rule = weight_rule(self.aggregation_function)  # None for test_agg: a no-op
-        for future, agg_client, agg_neighbors, kwargs in batch:
+        for _, _, agg_client, agg_neighbors, kwargs in batch:
             me = memo[id(agg_client)]
-            done.append((future, me))
+            done.append(me)
             if rule is None:
                 continue
             got = rule(me, [memo[id(f)] for f in agg_neighbors], **kwargs)
@@ -310,5 +315,4 @@ class DecentrallearnApp:
             if self._executor is None:
                 self._executor = RoundExecutor(self.pool)
             self._executor.run(orders, weights, out_rows)
-        for future, me in done:
-            future.set_result(me)
+        return done
