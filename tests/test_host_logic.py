@@ -843,3 +843,21 @@ def test_default_plan_rows_wider_than_a_tile():
     self_first = [[i] + sorted(g.neighbors(i)) for i in range(700)]
     rp2, col2, w2 = csr_from_lists(self_first, [[1 / 700] * 700 for _ in self_first])
     assert isinstance(ops.default_plan(rp2, col2, w2, rows), ops.RowCallPlan)
+
+
+def test_pool_row_addresses_and_cpu_pool_refused():
+    """ModelPool.row_ptrs is the row views' data_ptr (padded rows, every segment), and the
+    per-call pool path refuses a host pool before touching the library (no GPU needed)."""
+    import pytest
+    import torch
+
+    from topology_aware_learning_amd import ops
+    from topology_aware_learning_amd.arena import ModelPool, StateLayout
+
+    lay = StateLayout.from_layout([("w", (1001,), "float32"), ("h", (7,), "bfloat16"), ("n", (), "int64")])
+    pool = ModelPool(lay, 5, "cpu")
+    for seg, view in (("f32", pool.row_f32), ("b16", pool.row_b16), ("i64", pool.row_i64)):
+        assert pool.row_ptrs(seg, [0, 3, 4]) == [view(r).data_ptr() for r in (0, 3, 4)]
+    with pytest.raises(ValueError, match="device pool"):
+        ops.agg_pool_rows(pool, [0, 1], [0.5, 0.5], 1)
+    assert torch.equal(pool.f32, torch.zeros_like(pool.f32))
