@@ -98,3 +98,42 @@ def test_pinned_budget_falls_back_to_packing(cuda, monkeypatch):
     for ma, mb in zip(ref, got):
         for (k, ta), tb in zip(ma.state_dict().items(), mb.state_dict().values()):
             assert torch.equal(ta, tb), k
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_host_pipeline_equals_single_stream(cuda, monkeypatch, dtype):
+    """The chunked H2D / K1 / D2H pipeline of all-pinned host calls (TAL_HOST_PIPE, the default)
+    gives the single-stream path's bits, on models of several column chunks (9.4 M elements:
+    three 4 M-element chunks, the last partial) with an int64 buffer, in a sequential round where
+    each call reads models earlier calls wrote."""
+    import numpy as np
+
+    import oracle
+
+    def models(seed):
+        torch.manual_seed(seed)
+        ms = []
+        for _ in range(6):
+            m = torch.nn.Module()
+            m.w = torch.nn.Parameter(torch.randn(9_400_003).to(dtype))
+            m.register_buffer("count", torch.tensor(1000, dtype=torch.int64))
+            ms.append(m)
+        return ms
+
+    orders = [[1, 2, 0], [0, 2, 1], [1, 3, 4, 2], [2, 4, 3], [0, 3, 5, 4], [4, 5]]
+    out = {}
+    for pipe in ("1", "0"):
+        monkeypatch.setenv("TAL_HOST_PIPE", pipe)
+        ms = models(7)
+        first = [m.w.detach().clone() for m in ms]
+        for i, o in enumerate(orders):
+            aggregate.aggregate_models([ms[j] for j in o], [1 / len(o)] * len(o), ms[i])
+        out[pipe] = (ms, first)
+    for a, b in zip(out["1"][0], out["0"][0]):
+        assert a.w.device.type == "cpu" and torch.equal(a.w.view(torch.int16 if dtype == torch.bfloat16 else torch.int32),
+                                                        b.w.view(torch.int16 if dtype == torch.bfloat16 else torch.int32))
+        assert int(a.count) == int(b.count)
+    if dtype == torch.float32:  # the first call against the oracle directly
+        ms0 = out["1"][1]
+        exp = oracle.agg_f32([ms0[j].numpy() for j in orders[0]], [1 / 3] * 3)
+        assert np.array_equal(out["1"][0][0].w.detach().numpy().view(np.uint32), exp.view(np.uint32))

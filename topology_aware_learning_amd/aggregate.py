@@ -160,6 +160,12 @@ def _host_cache() -> Optional[_OperandCache]:
 _CACHE: Optional[_OperandCache] = None
 
 
+def _pipe_enabled() -> bool:
+    """The chunked H2D / K1 / D2H pipeline for all-pinned host calls (TAL_HOST_PIPE=0: one
+    stream, whole segments)."""
+    return os.environ.get("TAL_HOST_PIPE", "1") not in ("", "0")
+
+
 def _pin_enabled() -> bool:
     """Pinned binding of CPU models is the default since round 4 (TAL_HOST_PIN=0 opts out)."""
     return os.environ.get("TAL_HOST_PIN", "1") not in ("", "0")
@@ -315,6 +321,69 @@ def _stage(models: Sequence[nn.Module], layout: StateLayout, device) -> List[dic
     return out
 
 
+# The host-memory call (every model in a pinned host row) as a pipeline over column chunks:
+# chunk c's operand H2Ds, its K1 and its result's D2H run on three streams, so the D2H of one
+# chunk and the K1 of another overlap the H2D of the next (PCIe is full duplex).  The
+# unpipelined form queues all H2Ds, then K1, then the D2H on one stream.
+_PIPE_CHUNK = 4 << 20  # elements per chunk of a float segment (16 MiB fp32)
+_PIPE_STREAMS: dict = {}
+
+
+def _pipe_streams(device: torch.device):
+    key = (device.index, threading.get_ident())  # per thread: the reference runs two calls at once
+    st = _PIPE_STREAMS.get(key)
+    if st is None:
+        st = _PIPE_STREAMS[key] = tuple(torch.cuda.Stream(device) for _ in range(3))
+    return st
+
+
+def _k1(g: str, xs, w, out, mode, stream) -> None:
+    if g == "i64":
+        ops.agg_i64(xs, w, out, stream=stream)
+    elif g == "b16":
+        ops.agg_bf16(xs, w, out, mode=mode, stream=stream)
+    else:
+        ops.agg_f32(xs, w, out, mode=mode, stream=stream)
+
+
+def _pipelined_host_call(hbs, target_hb, layout: StateLayout, w: List[float], mode: int, device) -> None:
+    """target's row <- sum_i w_i * row of hbs[i], every model a pinned host row (the reference's
+    CPU models after their first call): per segment, column chunks flow H2D -> K1 -> D2H on three
+    streams.  K1 on a chunk is the same per-element arithmetic as on the whole segment."""
+    sizes = {g: n for g, n in _seg_sizes(layout).items() if n}
+    h2d, comp, d2h = _pipe_streams(device)
+    start = torch.cuda.Event()
+    start.record(torch.cuda.current_stream(device))
+    for st in (h2d, comp, d2h):
+        st.wait_event(start)
+    m = len(hbs)
+    src = [_row_segments(hb[0], hb[1], sizes) for hb in hbs]
+    dst = _row_segments(target_hb[0], target_hb[1], sizes)
+    keep = []
+    for g, n in sizes.items():
+        ld = (n + 63) // 64 * 64  # 256-B aligned operand rows: chunks keep K1's vector path
+        dev = torch.empty((m, ld), dtype=_SEG_DTYPE[g], device=device)
+        out = torch.empty(ld, dtype=_SEG_DTYPE[g], device=device)
+        keep += [dev, out]
+        step = n if g == "i64" else _PIPE_CHUNK
+        for a in range(0, n, step):
+            b = min(n, a + step)
+            with torch.cuda.stream(h2d):
+                for j in range(m):
+                    dev[j, a:b].copy_(src[j][g][a:b], non_blocking=True)
+            landed = torch.cuda.Event()
+            landed.record(h2d)
+            comp.wait_event(landed)
+            _k1(g, [dev[j, a:b] for j in range(m)], w, out[a:b], mode, comp)
+            done = torch.cuda.Event()
+            done.record(comp)
+            d2h.wait_event(done)
+            with torch.cuda.stream(d2h):
+                dst[g][a:b].copy_(out[a:b], non_blocking=True)
+    d2h.synchronize()  # the call returns with the model written, as the reference's load_state_dict
+    del keep
+
+
 _AGG = {"f32": lambda xs, w, out, mode: ops.agg_f32(xs, w, out, mode=mode),
         "b16": lambda xs, w, out, mode: ops.agg_bf16(xs, w, out, mode=mode),
         "i64": lambda xs, w, out, mode: ops.agg_i64(xs, w, out)}
@@ -345,6 +414,11 @@ def aggregate_models(operands: Sequence[nn.Module], weights: Sequence[float], ta
         device = _device_for(list(operands) + [target])
     host_target = _host_binding(target, layout) if tb is None or tb[0].device.type == "cpu" else None
     sizes = {g: n for g, n in _seg_sizes(layout).items() if n}
+    if host_target is not None and _host_cache() is None and _pipe_enabled():
+        hbs = [_host_binding(m, layout) for m in operands]
+        if all(h is not None for h in hbs):  # every model in a pinned host row
+            _pipelined_host_call(hbs, host_target, layout, [float(x) for x in weights], mode, device)
+            return target
 
     ptrs: dict = {g: [None] * len(operands) for g in sizes}
     unbound = []
