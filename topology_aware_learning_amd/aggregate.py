@@ -333,13 +333,8 @@ def _pipe_streams(device: torch.device):
     key = (device.index, threading.get_ident())  # per thread: the reference runs two calls at once
     st = _PIPE_STREAMS.get(key)
     if st is None:
-        st = _PIPE_STREAMS[key] = tuple(torch.cuda.Stream(device) for _ in range(2 + _pipe_h2d_streams()))
+        st = _PIPE_STREAMS[key] = tuple(torch.cuda.Stream(device) for _ in range(3))
     return st
-
-
-def _pipe_h2d_streams() -> int:
-    """Streams the operand H2Ds alternate over (TAL_HOST_PIPE_H2D, default 1)."""
-    return max(1, int(os.environ.get("TAL_HOST_PIPE_H2D", "1") or 1))
 
 
 def _k1(g: str, xs, w, out, mode, stream) -> None:
@@ -356,10 +351,10 @@ def _pipelined_host_call(hbs, target_hb, layout: StateLayout, w: List[float], mo
     CPU models after their first call): per segment, column chunks flow H2D -> K1 -> D2H on three
     streams.  K1 on a chunk is the same per-element arithmetic as on the whole segment."""
     sizes = {g: n for g, n in _seg_sizes(layout).items() if n}
-    comp, d2h, *h2ds = _pipe_streams(device)
+    h2d, comp, d2h = _pipe_streams(device)
     start = torch.cuda.Event()
     start.record(torch.cuda.current_stream(device))
-    for st in (comp, d2h, *h2ds):
+    for st in (h2d, comp, d2h):
         st.wait_event(start)
     m = len(hbs)
     src = [_row_segments(hb[0], hb[1], sizes) for hb in hbs]
@@ -373,13 +368,12 @@ def _pipelined_host_call(hbs, target_hb, layout: StateLayout, w: List[float], mo
         step = n if g == "i64" else _PIPE_CHUNK
         for a in range(0, n, step):
             b = min(n, a + step)
-            for k, h2d in enumerate(h2ds):  # operand j on H2D stream j mod len(h2ds)
-                with torch.cuda.stream(h2d):
-                    for j in range(k, m, len(h2ds)):
-                        dev[j, a:b].copy_(src[j][g][a:b], non_blocking=True)
-                landed = torch.cuda.Event()
-                landed.record(h2d)
-                comp.wait_event(landed)
+            with torch.cuda.stream(h2d):
+                for j in range(m):
+                    dev[j, a:b].copy_(src[j][g][a:b], non_blocking=True)
+            landed = torch.cuda.Event()
+            landed.record(h2d)
+            comp.wait_event(landed)
             _k1(g, [dev[j, a:b] for j in range(m)], w, out[a:b], mode, comp)
             done = torch.cuda.Event()
             done.record(comp)
