@@ -1441,10 +1441,17 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   const ConstI32 prog = (ConstI32)(p.base + bc_off);
   const int bc_n = BC ? prog[0] : 0;
   int2 bc_rec[kR];
+  // the program's record words, in SGPRs for the whole kernel: read in the tile loop, each was a
+  // scalar load the compiler hoisted into the previous record's batch, and a scalar load in
+  // flight forces lgkmcnt(0) (SMEM returns out of order) - every batch then waited for all of
+  // its LDS reads before its first multiply
+  int bc_d[kR];
   if constexpr (BC) {
     const int2* recs = reinterpret_cast<const int2*>(p.base + (bc_off + prog[2])) + lane;
 #pragma unroll
     for (int r = 0; r < kR; ++r) bc_rec[r] = r < bc_n ? recs[64 * r] : make_int2(0, 0);
+#pragma unroll
+    for (int r = 0; r < kR; ++r) bc_d[r] = r < bc_n ? prog[kBcHdr + r] : 0;
   }
   // converted to fp32 when written to LDS, not when loaded
   typedef typename std::conditional<W16, u32x4, typename Io<T>::raw_t>::type raw_t;
@@ -1502,13 +1509,15 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
       // address of the tile loop out of it (hundreds of VGPRs, then spills)
 #pragma unroll
       for (int r = 0; r < kR; ++r) asm volatile("" : "+v"(bc_rec[r].x), "+v"(bc_rec[r].y));
+#pragma unroll
+      for (int r = 0; r < kR; ++r) asm volatile("" : "+s"(bc_d[r]));
       float4 acc = make_float4(-0.f, -0.f, -0.f, -0.f);
       float4 acc1 = acc;  // kX2: chunk cl + 16
 #pragma unroll
       for (int r = 0; r < kR; ++r) {
         if (r >= bc_n) continue;  // wave-uniform (a constant trip count keeps the loop unrolled,
                                   // so the records stay in registers)
-        const uint32_t d = static_cast<uint32_t>(prog[kBcHdr + r]);
+        const uint32_t d = static_cast<uint32_t>(bc_d[r]);
 #ifdef TAL_PROBE_NOCOMP
         (void)d;
 #else
