@@ -1517,7 +1517,11 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
       for (int r = 0; r < kR; ++r) {
         if (r >= bc_n) continue;  // wave-uniform (a constant trip count keeps the loop unrolled,
                                   // so the records stay in registers)
+#ifdef TAL_PROBE_BC_SMEM  // A/B probe: the record word read in the loop (round 4's form)
+        const uint32_t d = static_cast<uint32_t>(prog[kBcHdr + r]);
+#else
         const uint32_t d = static_cast<uint32_t>(bc_d[r]);
+#endif
 #ifdef TAL_PROBE_NOCOMP
         (void)d;
 #else
