@@ -2982,10 +2982,22 @@ __device__ __forceinline__ void cos_multi_row(Load load, int64_t size, float* ou
 #pragma unroll
     for (int k = 0; k < NR; ++k) acc[j][k] = 0.f;
   int64_t i = 0;
+  // the level-0 run of `step` (a power of two >= 16) elements in batches of kU: the batch's
+  // loads are issued together, then added in order (each stream k keeps torch's order), so a
+  // serial chain waits on one memory latency per batch, not per element
+  constexpr int kU = NR == 1 ? 8 : 4;
   while (i + step <= size) {
-    for (int64_t j = 0; j < step; ++j, ++i)
+    for (int64_t j = 0; j < step; j += kU, i += kU) {
+      float v[kU][NR];
 #pragma unroll
-      for (int k = 0; k < NR; ++k) acc[0][k] = __fadd_rn(acc[0][k], load(i, k));
+      for (int u = 0; u < kU; ++u)
+#pragma unroll
+        for (int k = 0; k < NR; ++k) v[u][k] = load(i + u, k);
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+#pragma unroll
+        for (int k = 0; k < NR; ++k) acc[0][k] = __fadd_rn(acc[0][k], v[u][k]);
+    }
 #pragma unroll
     for (int j = 1; j < kL; ++j) {
 #pragma unroll
@@ -3064,8 +3076,22 @@ __global__ __launch_bounds__(kCosBlock) void k_cosine_outputs(CosPairs pr, const
     const int64_t o = q / B, k = q % B;
     const float* x1 = a + o * I * B + k;
     const float* x2 = b + o * I * B + k;
-    float m1 = 0.f, m2 = 0.f;  // torch NormTwoOps: fma in index order
-    for (int64_t i = 0; i < I; ++i) {
+    float m1 = 0.f, m2 = 0.f;  // torch NormTwoOps: fma in index order (loads in batches of 8)
+    int64_t i0 = 0;
+    for (; i0 + 8 <= I; i0 += 8) {
+      float u1[8], u2[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        u1[u] = x1[(i0 + u) * B];
+        u2[u] = x2[(i0 + u) * B];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        m1 = __fmaf_rn(u1[u], u1[u], m1);
+        m2 = __fmaf_rn(u2[u], u2[u], m2);
+      }
+    }
+    for (int64_t i = i0; i < I; ++i) {
       m1 = __fmaf_rn(x1[i * B], x1[i * B], m1);
       m2 = __fmaf_rn(x2[i * B], x2[i * B], m2);
     }
@@ -3093,11 +3119,26 @@ __global__ __launch_bounds__(kCosBlock) void k_cosine_outputs(CosPairs pr, const
   const int64_t vec_end = I - I % kCosVw;
   // vector_norm (reduce-lastdim kernel): lane accumulators fma over whole vectors
   float m1 = 0.f, m2 = 0.f;
-  if (live)
-    for (int64_t d = l; d < vec_end; d += kCosVw) {
+  if (live) {  // loads in batches of 8 vectors, fma in index order
+    int64_t d = l;
+    for (; d + 7 * kCosVw < vec_end; d += 8 * kCosVw) {
+      float u1[8], u2[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        u1[u] = x1[d + u * kCosVw];
+        u2[u] = x2[d + u * kCosVw];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        m1 = __fmaf_rn(u1[u], u1[u], m1);
+        m2 = __fmaf_rn(u2[u], u2[u], m2);
+      }
+    }
+    for (; d < vec_end; d += kCosVw) {
       m1 = __fmaf_rn(x1[d], x1[d], m1);
       m2 = __fmaf_rn(x2[d], x2[d], m2);
     }
+  }
   float t1 = __shfl(m1, gbase, 64), t2 = __shfl(m2, gbase, 64);  // lane 0 starts the fold
   for (int j = 1; j < kCosVw; ++j) {
     t1 = __fadd_rn(t1, __shfl(m1, gbase + j, 64));
