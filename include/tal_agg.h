@@ -380,6 +380,22 @@ int32_t tal_host_agg_bf16(const uint16_t* const* x_host, const double* w_host, i
 int32_t tal_host_cosine(const float* const* a_host, const float* const* b_host, int32_t n_pairs,
                         const int64_t* plan_host, float* out);
 
+/* ---- Synthetic pool rows (test / benchmark inputs) --------------------------
+ * Not a reference interface: the reference trains its models; the benchmark and the full-size
+ * parity tests need seeded models whose outputs the reference-generated sha256 fixtures pin
+ * (tests/golden/full_round_c{3,4,5}_*.json).  Fills n_rows rows (pitch ld elements) of one pool
+ * segment with synth.py's counter generator: element at generator position p of the row seeded
+ * s is u = splitmix64(p ^ (s & 0xFFFFFFFF) << 40) turned into fp32 (dtype 0: sign bit 31,
+ * exponent 121 + bits 23..25, mantissa bits 0..22; |v| + 0.5 in the running_var ranges), bf16
+ * (dtype 1: that fp32 value rounded to nearest even) or int64 (dtype 2: u % hi).
+ * table (int64, on the device; the host copy passed too): {n_rows, n, n_runs, n_rv, hi, 0, 0, 0},
+ * seeds[n_rows], runs[n_runs] {generator position, first column, length} tiling columns
+ * [0, n) in order, running_var ranges[n_rv] {first column, length} ascending (dtype 0 only).
+ * One launch for the whole segment (the torch form took ~20 element-wise launches per 32 M
+ * elements per row). */
+int32_t tal_fill_counter(void* seg, int64_t ld, int32_t dtype, const int64_t* table_dev,
+                         const int64_t* table_host, void* stream);
+
 /* ---- Multi-GPU halo exchange (SURVEY §8(b) tal_halo_exchange, §8(e)) ---------------------
  * Reference: the models that cross workers are shipped by Parsl as Python objects
  * (decentralized_app.py:627-629, parsl_setup.py:191-203).  Sharded one process per GPU, each

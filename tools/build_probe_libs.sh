@@ -1,6 +1,7 @@
 # Build A/B probe variants of the library into tools/tune/ (not the product), with the product's
 # own hipcc flags (topology_aware_learning_amd/build.py) plus the variant's.
-# Usage: bash tools/build_probe_libs.sh NAME:FLAGS ...   e.g. nocomp:-DTAL_PROBE_NOCOMP
+# Usage: bash tools/build_probe_libs.sh NAME:FLAGS ...   e.g. o2:-O2  (the product source carries no
+# probe switches since round 6: a variant is a -D / flag the kernels read, or a copy of the source)
 cd "$(dirname "$0")/.."
 base=$(python -c "from topology_aware_learning_amd.build import HIPCC_FLAGS; print(' '.join(HIPCC_FLAGS))")
 pids=()

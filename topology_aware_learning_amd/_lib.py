@@ -27,7 +27,7 @@ TAL_ERR_COMM = 4
 TAL_COMM_ID_BYTES = 128
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 22
+ABI_VERSION = 23
 
 EXPORTED = (
     "tal_last_error",
@@ -61,6 +61,7 @@ EXPORTED = (
     "tal_comm_destroy",
     "tal_halo_pack",
     "tal_halo_exchange",
+    "tal_fill_counter",
     "tal_host_agg_f32",
     "tal_host_agg_i64",
     "tal_host_agg_bf16",
@@ -170,6 +171,7 @@ _SIGS = {
     "tal_comm_destroy": (_I32, [_P]),
     "tal_halo_pack": (_I32, [_P, _I64, _I64, _P, _I32, _I64, _P, _P]),
     "tal_halo_exchange": (_I32, [_P, _I32, _PP, _PI64, _PP, _PI64, _P]),
+    "tal_fill_counter": (_I32, [_P, _I64, _I32, _P, _PI64, _P]),
     "tal_host_agg_f32": (_I32, [_PP, _PD, _I32, _P, _I64, _I32]),
     "tal_host_agg_i64": (_I32, [_PP, _PD, _I32, _P, _I64]),
     "tal_host_agg_bf16": (_I32, [_PP, _PD, _I32, _P, _I64, _I32]),

@@ -45,7 +45,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 22;
+constexpr int kAbiVersion = 23;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -157,11 +157,7 @@ struct OpTableI64 {
 // so keeping it out of the caches leaves L2/MALL to the output stream (measured +15-20 % at
 // M = 9 on MI355X, tools/tune/k1_variants.hip).
 __device__ __forceinline__ float4 ld_stream(const float* base, int64_t i) {
-#ifdef TAL_PROBE_LD_PLAIN  // A/B probe: cached operand loads
-  const v4f q = reinterpret_cast<const v4f*>(base)[i];
-#else
   const v4f q = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(base) + i);
-#endif
   return make_float4(q.x, q.y, q.z, q.w);
 }
 
@@ -459,11 +455,7 @@ __device__ __forceinline__ GroupLds stage_group(const PlanView& p, int g, void* 
 
 __device__ __forceinline__ void st_stream(float* base, int64_t i, float4 v) {
   const v4f q = {v.x, v.y, v.z, v.w};
-#ifdef TAL_PROBE_ST_PLAIN  // A/B probe: cached output stores
-  reinterpret_cast<v4f*>(base)[i] = q;
-#else
   __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(base) + i);
-#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1457,9 +1449,6 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   typedef typename std::conditional<W16, u32x4, typename Io<T>::raw_t>::type raw_t;
   raw_t v[kLd];
   auto load_tile = [&](int64_t tt) {
-#ifdef TAL_PROBE_NOLOAD  // A/B probe: no HBM reads (the tile keeps the first tile's values)
-    if (tt != blockIdx.x) return;
-#endif
     if constexpr (W16) {  // 16-B units: chunk pair tt * C4 / 2 + c of each row
       const int64_t col = min(tt * kLps + c, (n4 - 1) / 2);  // past the end: a duplicate
       const u32x4* b = reinterpret_cast<const u32x4*>(pin);
@@ -1479,9 +1468,6 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
   int64_t t = blockIdx.x;
   if (t < n_tiles) load_tile(t);
   for (; t < n_tiles; t += gridDim.x) {
-#ifdef TAL_PROBE_NOPREFETCH  // A/B probe: each tile's loads issued after the previous tile's math
-    if (t != blockIdx.x) load_tile(t);
-#endif
     __syncthreads();  // the previous tile's readers are done with s_data
     // staging units (float4 slots; W16: slot pairs) of real sources (readfirstlane: the broadcast
     // form's control flow otherwise leaves the compiler unsure that ns is uniform here)
@@ -1500,9 +1486,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
       }
     }
     __syncthreads();
-#ifndef TAL_PROBE_NOPREFETCH
     if (t + gridDim.x < n_tiles) load_tile(t + gridDim.x);  // in flight during this tile's math
-#endif
     const int64_t col = t * C4 + cl;
     if constexpr (BC) {
       // the records are loop-invariant: without this the compiler hoists every broadcast and
@@ -1517,19 +1501,11 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
       for (int r = 0; r < kR; ++r) {
         if (r >= bc_n) continue;  // wave-uniform (a constant trip count keeps the loop unrolled,
                                   // so the records stay in registers)
-#ifdef TAL_PROBE_BC_SMEM  // A/B probe: the record word read in the loop (round 4's form)
-        const uint32_t d = static_cast<uint32_t>(prog[kBcHdr + r]);
-#else
         const uint32_t d = static_cast<uint32_t>(bc_d[r]);
-#endif
-#ifdef TAL_PROBE_NOCOMP
-        (void)d;
-#else
         if constexpr (kX2)
           bc2_record<T, EXACT>(acc, acc1, bc_rec[r], col_base, static_cast<int>(d & 0xffu));
         else
           acc = bc_record<T, EXACT, kBcDepth>(acc, bc_rec[r], col_base, static_cast<int>(d & 0xffu));
-#endif
         if (d & 0x100u) {  // the pass's last record: store its rows
           const ConstI32 orow = prog + kBcHdr + kR + 4 * static_cast<int>(d >> 16);
           const int o0 = orow[0], o1 = orow[1], o2 = orow[2], o3 = orow[3];
@@ -1549,11 +1525,7 @@ __global__ __launch_bounds__(NT, NP == 0 ? 2 * NT / 256 : NT / 256) void k_round
         const int set = narrow_set(k, wave, kW);
         if (set >= n_sets) continue;  // wave-uniform
         const uint4 rc = lds_u4(rec_lane + 16u * static_cast<uint32_t>(set * kRpw));
-#ifdef TAL_PROBE_NOCOMP  // A/B probe (tools/gpu_k3n_probe.sh): stores without the row arithmetic
-        const float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#else
         const float4 acc = narrow_row_roww<T, EXACT>(rc, col_base);
-#endif
         if (static_cast<int32_t>(rc.w) >= 0 && col < n4) {
           Io<T>::st(pout, static_cast<int64_t>(static_cast<int32_t>(rc.w)) * ld_out4 + col, acc);
         }
@@ -2089,10 +2061,8 @@ int32_t launch_round_narrow_jr(const T* pin, int64_t ld_in, T* pout, int64_t ld_
   // row extents in registers
   constexpr int kNP = J >= 12 ? kNarrowPasses / 2 : kNarrowPasses;  // J = 12: VGPRs for the staging
   auto k = k_round_f32_narrow<C4, kNarrowThreads, J, kNP, EXACT, T, ROWW>;
-#ifndef TAL_PROBE_ONEWG  // probe: keep one workgroup per CU (the register-rich variant)
   if constexpr (J <= 4)
     if (2 * lds <= 160 * 1024) k = k_round_f32_narrow<C4, kNarrowThreads, J, 0, EXACT, T, ROWW>;
-#endif
   if constexpr (kIsBf16<T> && J >= 2 && J <= 4) {
     // whole chunk pairs per row (an even chunk count and stride) from a 16-B aligned base: no
     // pair reaches past a row's last chunk
@@ -2744,9 +2714,6 @@ __global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, T*
   const v2f_t zn = {-0.f, -0.f};  // the neutral operand's register pair
   int s_next = take();
   v32f X0, X1, X2, X3;
-#ifdef TAL_PROBE_REG_NOLOAD
-  bool loaded = false;
-#endif
   for (;;) {
     const int s = s_next;
     if (s >= items) break;
@@ -2761,18 +2728,11 @@ __global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, T*
 #define TAL_RBASES(J)                                                                            \
     _Pragma("unroll") for (int k = 0; k < 16; ++k)                                               \
       b[k] = pbase + static_cast<uint64_t>(soff[s0 + (J) * 16 + k]);
-#ifdef TAL_PROBE_REG_NOLOAD  // A/B probe: sources loaded for a wave's first item only
-    if (!loaded) {
-      loaded = true;
-#endif
     TAL_RBASES(0)
     X0 = reg_load_block<0, kB>(b, loff);
     if constexpr (NB > 1) { TAL_RBASES(1) X1 = reg_load_block<1, kB>(b, loff); }
     if constexpr (NB > 2) { TAL_RBASES(2) X2 = reg_load_block<2, kB>(b, loff); }
     if constexpr (NB > 3) { TAL_RBASES(3) X3 = reg_load_block<3, kB>(b, loff); }
-#ifdef TAL_PROBE_REG_NOLOAD
-    }
-#endif
 #undef TAL_RBASES
     reg_wait<NB, kB>(X0, X1, X2, X3);
     s_next = take();
@@ -2781,11 +2741,7 @@ __global__ __launch_bounds__(256) void k_round_reg(const T* __restrict__ pin, T*
       v2f_t ca = {-0.f, -0.f}, cb = {-0.f, -0.f};
       const uint32_t off = pr[3];
       const uint32_t last = off + 64u * pr[2];  // the loop goes on while (next record's offset + 64) <= last
-#ifndef TAL_PROBE_REG_NOCOMP  // A/B probe: the stores without the row arithmetic
       reg_pair<NB, EXACT>(ca, cb, base, off, last, X0, X1, X2, X3, zn);
-#else
-      (void)last;
-#endif
       reg_store<T>(pout, ld_out, static_cast<int32_t>(pr[0]), col, n, ca);
       if (static_cast<int32_t>(pr[1]) >= 0) reg_store<T>(pout, ld_out, static_cast<int32_t>(pr[1]), col, n, cb);
     }
@@ -4464,6 +4420,116 @@ int32_t tal_prox_grad(const float* w, const float* const* wt_host, int32_t k, co
   }
   g_err.clear();
   return TAL_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------
+// Synthetic pool rows: synth.py's counter generator, one launch per pool segment
+// ------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int kFillHeader = 8;  // {n_rows, n, n_runs, n_rv, hi, 0, 0, 0}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// counter_f32 (synth.py): random sign, exponent 121..128, the low 23 bits as mantissa
+__device__ __forceinline__ uint32_t counter_f32_bits(uint64_t u) {
+  return static_cast<uint32_t>(((u >> 31) & 1u) << 31 | (121u + ((u >> 23) & 7u)) << 23 | (u & 0x7FFFFFu));
+}
+
+// Block (x, r) fills columns of segment row r; each lane finds its column's generator position
+// from the run table (run = {position, first column, length}, ascending columns covering
+// [0, n)), starting from the run of the block's first column (found once, block-uniform) and
+// stepping forward, so a lane walks at most the few runs one 256-column stretch crosses.
+template <int DT>  // 0 fp32, 1 bf16 (nearest even of the fp32 value), 2 int64 (u % hi)
+__global__ __launch_bounds__(kBlock) void k_fill_counter(void* __restrict__ seg, int64_t ld,
+                                                         const int64_t* __restrict__ tab) {
+  const int64_t n = tab[1];
+  const int n_runs = static_cast<int>(tab[2]), n_rv = static_cast<int>(tab[3]);
+  const uint64_t hi = static_cast<uint64_t>(tab[4]);
+  const int64_t* seeds = tab + kFillHeader;
+  const int64_t* runs = seeds + tab[0];
+  const int64_t* rv = runs + 3 * n_runs;
+  const int64_t r = blockIdx.y;
+  const uint64_t key = (static_cast<uint64_t>(seeds[r]) & 0xFFFFFFFFull) << 40;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t c0 = static_cast<int64_t>(blockIdx.x) * kBlock; c0 < n; c0 += stride) {
+    int lo = 0, hi_r = n_runs - 1;  // last run starting at or before c0 (uniform)
+    while (lo < hi_r) {
+      const int mid = (lo + hi_r + 1) >> 1;
+      if (runs[3 * mid + 1] <= c0) lo = mid;
+      else hi_r = mid - 1;
+    }
+    int vlo = 0, vhi = n_rv - 1;  // last running_var range starting at or before c0
+    while (vlo < vhi) {
+      const int mid = (vlo + vhi + 1) >> 1;
+      if (rv[2 * mid] <= c0) vlo = mid;
+      else vhi = mid - 1;
+    }
+    const int64_t c = c0 + threadIdx.x;
+    if (c >= n) break;
+    int k = lo;
+    while (k + 1 < n_runs && runs[3 * (k + 1) + 1] <= c) ++k;
+    const uint64_t u = splitmix64(static_cast<uint64_t>(runs[3 * k] + (c - runs[3 * k + 1])) ^ key);
+    if constexpr (DT == 2) {
+      static_cast<int64_t*>(seg)[r * ld + c] = static_cast<int64_t>(u % hi);
+    } else {
+      uint32_t bits = counter_f32_bits(u);
+      if constexpr (DT == 0) {
+        int v = vlo;
+        while (v + 1 < n_rv && rv[2 * (v + 1)] <= c) ++v;
+        if (n_rv > 0 && c >= rv[2 * v] && c < rv[2 * v] + rv[2 * v + 1])  // |v| + 0.5 in fp32
+          bits = __float_as_uint(__fadd_rn(__uint_as_float(bits & 0x7FFFFFFFu), 0.5f));
+        static_cast<float*>(seg)[r * ld + c] = __uint_as_float(bits);
+      } else {  // finite values: nearest even is the add-and-truncate form
+        static_cast<uint16_t*>(seg)[r * ld + c] = static_cast<uint16_t>((bits + 0x7FFFu + ((bits >> 16) & 1u)) >> 16);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t tal_fill_counter(void* seg, int64_t ld, int32_t dtype, const int64_t* table_dev,
+                         const int64_t* table_host, void* stream) {
+  if (!seg || !table_dev || !table_host || dtype < 0 || dtype > 2)
+    return fail(TAL_ERR_INVALID, "tal_fill_counter: bad arguments");
+  const int64_t n_rows = table_host[0], n = table_host[1], n_runs = table_host[2], n_rv = table_host[3];
+  const int64_t hi = table_host[4];
+  if (n_rows < 0 || n_rows > 65535 || n < 0 || n > ld || n_runs < 0 || n_rv < 0 || (dtype == 2 && hi <= 0))
+    return fail(TAL_ERR_INVALID, "tal_fill_counter: bad table header");
+  if (n_rows == 0 || n == 0) {
+    g_err.clear();
+    return TAL_OK;
+  }
+  // the runs must tile [0, n) in ascending columns (every lane's walk then stays in the table)
+  const int64_t* runs = table_host + kFillHeader + n_rows;
+  int64_t col = 0;
+  for (int64_t k = 0; k < n_runs; ++k) {
+    if (runs[3 * k + 1] != col || runs[3 * k + 2] <= 0 || runs[3 * k] < 0)
+      return fail(TAL_ERR_INVALID, "tal_fill_counter: runs must tile the columns in order");
+    col += runs[3 * k + 2];
+  }
+  if (col != n) return fail(TAL_ERR_INVALID, "tal_fill_counter: runs do not cover the row");
+  const int64_t* rv = runs + 3 * n_runs;
+  for (int64_t k = 0; k < n_rv; ++k)
+    if (rv[2 * k] < 0 || rv[2 * k + 1] < 0 || (k && rv[2 * k] < rv[2 * k - 2] + rv[2 * k - 1]))
+      return fail(TAL_ERR_INVALID, "tal_fill_counter: running_var ranges must ascend without overlap");
+  const unsigned gx = static_cast<unsigned>(std::min<int64_t>((n + kBlock - 1) / kBlock, 4096));
+  const dim3 grid(gx, static_cast<unsigned>(n_rows));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (dtype == 0) k_fill_counter<0><<<grid, kBlock, 0, s>>>(seg, ld, table_dev);
+  else if (dtype == 1) k_fill_counter<1><<<grid, kBlock, 0, s>>>(seg, ld, table_dev);
+  else k_fill_counter<2><<<grid, kBlock, 0, s>>>(seg, ld, table_dev);
+  return check_launch("tal_fill_counter");
 }
 
 }  // extern "C"

@@ -1096,3 +1096,26 @@ def host_cosine(a_list: Sequence[torch.Tensor], b_list: Sequence[torch.Tensor], 
                             len(a_list), plan.host.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
                             ctypes.c_void_p(out.data_ptr())))
     return out
+
+
+# ------------------------------------------------------------------------------------------
+# Synthetic pool rows (benchmark / full-size test inputs)
+# ------------------------------------------------------------------------------------------
+_FILL_TORCH = {0: torch.float32, 1: torch.bfloat16, 2: torch.int64}
+
+
+def fill_counter(seg: torch.Tensor, table: np.ndarray, dtype_code: int, stream=None) -> torch.Tensor:
+    """tal_fill_counter: rows 0..n_rows-1 of the [rows, ld] segment `seg` = synth's counter
+    generator per `table` (synth.fill_table), one launch for all rows."""
+    if seg.device.type != "cuda" or seg.dtype != _FILL_TORCH[int(dtype_code)]:
+        raise ValueError(f"fill_counter needs a GPU {_FILL_TORCH[int(dtype_code)]} segment (got {seg.device} {seg.dtype})")
+    tab = np.ascontiguousarray(table, dtype=np.int64)
+    n_rows, n = int(tab[0]), int(tab[1])
+    if seg.dim() != 2 or seg.stride(1) != 1 or seg.shape[0] < n_rows or seg.shape[1] < n:
+        raise ValueError(f"seg must be [>= {n_rows}, >= {n}] with unit column stride (got {tuple(seg.shape)})")
+    dev_tab = torch.from_numpy(tab).to(seg.device)
+    L = _lib.load()
+    check(L.tal_fill_counter(ctypes.c_void_p(seg.data_ptr()), seg.stride(0), int(dtype_code),
+                             ctypes.c_void_p(dev_tab.data_ptr()), tab.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                             _stream(seg.device, stream)))
+    return seg

@@ -172,16 +172,51 @@ def _row_plan(layout: Layout, dtype: str, device):
     return hit
 
 
+_FILL_DT = {"float32": 0, "bfloat16": 1, "int64": 2}
+_FILL_HI = 1_000_000  # counter_i64's default range
+
+
+def fill_table(layout: Layout, seeds: Sequence[int], dtype: str = "float32") -> np.ndarray:
+    """The int64 table of tal_fill_counter (include/tal_agg.h) for the `dtype` segment rows of
+    synth_state_dict(layout, seed) for each seed: header, seeds, the segment's generator-position
+    runs and (float32) its running_var column ranges."""
+    runs, rv, pos, off = [], [], 0, 0
+    for name, shape, dt in layout:
+        k = numel(shape)
+        if dt == dtype and k:
+            if runs and runs[-1][0] + runs[-1][2] == pos:
+                runs[-1][2] += k
+            else:
+                runs.append([pos, off, k])
+            if dtype == "float32" and name.endswith("running_var"):
+                if rv and rv[-1][0] + rv[-1][1] == off:
+                    rv[-1][1] += k
+                else:
+                    rv.append([off, k])
+            off += k
+        pos += k
+    head = [len(seeds), off, len(runs), len(rv), _FILL_HI, 0, 0, 0]
+    seeds = [int(s) & 0xFFFFFFFF for s in seeds]
+    return np.array(head + seeds + [v for r in runs for v in r] + [v for r in rv for v in r], dtype=np.int64)
+
+
 def fill_rows_torch(seg: "torch.Tensor", layout: Layout, seeds: Sequence[int], dtype: str = "float32",
                     chunk: int = 1 << 25) -> None:
     """seg[r, :n] = the `dtype` entries of synth_state_dict(layout, seeds[r]) concatenated in
     state_dict order (a pool segment row), generated on seg's device.  float32, bfloat16 (the
     bf16 of the fp32 counter value, as synth_state_dict makes it) and int64 segments.
 
-    A float row is generated over the layout's whole position range in `chunk`-sized launches
-    (the int64 positions in between are a few dozen wasted elements) and its columns gathered
-    once, so a row costs a fixed ~20 element-wise launches per chunk, not per entry (ResNet-50:
-    320 entries; the sharded bench regenerates hundreds of operand rows to check a round)."""
+    On a GPU: one tal_fill_counter launch for all the rows (the library's generator kernel).
+    Round 5's torch form (kept below for CPU tensors: the gloo tests) took ~20 element-wise
+    launches per `chunk` per row - about 15,000 dispatches for 256 ViT-B/16 rows - and crashed
+    the process under rocprofv3 --pmc, which serializes and samples every dispatch."""
+    if seg.device.type == "cuda":
+        if not len(seeds):
+            return
+        from . import ops  # the library; no CPU fallback on a GPU tensor
+
+        ops.fill_counter(seg, fill_table(layout, seeds, dtype), _FILL_DT[dtype])
+        return
     total, runs, fidx, rvidx, n = _row_plan(layout, dtype, seg.device)
     if dtype == "int64":  # a few counters per model: host values
         for r, seed in enumerate(seeds):
