@@ -1,0 +1,88 @@
+"""K2's staged chunks (round 6): whole output slabs of both models of a pair in LDS, the norms'
+chains, the level-0 cascade runs and each output's cascade / lane fold computed from there
+(k_cosine_staged).  Bitwise the oracle (torch's CPU order, oracle/cosine_oracle.c) at the
+edges of the staging: column tensors with B < 32 at every chunk size (the ResNet 3 x 3 convs'
+one slab per chunk at I = 512 up to 28 slabs for conv1's I = 3; the last chunk partial), slabs
+at the LDS capacity and one element past it (the direct form), streams whose length is not a
+multiple of the run width (a partial last run), row tensors of I < 8 (one sequence), 8 <= I
+with a tail past the last vector and rows at the capacity; segments starting at every 4-byte
+offset inside a 16-byte chunk; more pairs than one launch takes; a whole ResNet-50 model.
+Reference: cosine_similarity, /root/reference/src/decentralized_client.py:661-681.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from topology_aware_learning_amd import ops, synth
+from topology_aware_learning_amd.arena import StateLayout
+
+pytestmark = pytest.mark.gpu
+
+# (A, I, B): column kind B > 1, row kind B == 1
+_SHAPES = [
+    (64, 3, 9), (61, 3, 9),            # conv1: 28 slabs per chunk, the last chunk partial
+    (8, 512, 9), (3, 511, 9),          # one slab per chunk (4,608 floats: the capacity); 511: a partial run
+    (6, 256, 9), (5, 128, 9), (9, 64, 9),
+    (4, 100, 2), (3, 37, 31), (2, 148, 31),  # B 2 / 31; 148 x 31 = 4,588
+    (3, 4609, 1), (2, 513, 9),         # one element past the capacity: the direct form
+    (5, 4608, 1), (7, 2048, 1), (33, 512, 1),
+    (40, 7, 1), (9, 8, 1), (11, 13, 1), (6, 100, 1), (3, 1030, 1),
+]
+
+
+def _models(rng, segs, n):
+    total = max(o + a * i * b for o, a, i, b in segs)
+    return [rng.standard_normal(total).astype(np.float32) for _ in range(n)]
+
+
+def _check(cuda, rows, segs, a_idx, b_idx):
+    dev = [torch.from_numpy(r).to(cuda) for r in rows]
+    plan = ops.build_cosine_plan(segs)
+    got = ops.cosine([dev[j] for j in a_idx], [dev[j] for j in b_idx], plan).cpu().numpy()
+    for k, (ja, jb) in enumerate(zip(a_idx, b_idx)):
+        ref = np.float32(oracle.cosine_model(rows[ja], rows[jb], segs))
+        assert got[k].view(np.uint32) == ref.view(np.uint32), (segs, k, got[k], ref)
+
+
+@pytest.mark.parametrize("shape", _SHAPES, ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("mis", [0, 1, 3])
+def test_staged_shapes_vs_oracle(cuda, shape, mis):
+    """One tensor per plan, its segment starting `mis` floats past a 16-byte boundary."""
+    a, i, b = shape
+    segs = [(mis, a, i, b)]
+    rng = np.random.default_rng(a * 1000 + i * 10 + b + mis)
+    rows = _models(rng, segs, 4)
+    _check(cuda, rows, segs, [0, 0, 0], [1, 2, 3])
+    _check(cuda, rows, segs, [1, 2, 3], [0, 0, 0])  # each pair a different `a`
+
+
+def test_staged_all_shapes_one_plan(cuda):
+    """Every shape above in one model (staged and direct chunks in one launch pair), odd offsets."""
+    segs, off = [], 5
+    for a, i, b in _SHAPES:
+        segs.append((off, a, i, b))
+        off += a * i * b + 3
+    rows = _models(np.random.default_rng(11), segs, 5)
+    _check(cuda, rows, segs, [0, 0, 0, 0], [1, 2, 3, 4])
+
+
+def test_staged_more_pairs_than_one_launch(cuda):
+    segs = [(0, 8, 64, 9), (4608, 16, 72, 1), (4608 + 1152, 30, 1, 1)]
+    rows = _models(np.random.default_rng(3), segs, 36)
+    _check(cuda, rows, segs, [0] * 35, list(range(1, 36)))
+
+
+def test_staged_resnet50_model(cuda):
+    """A whole ResNet-50 parameter set (161 tensors: 3 x 3 convs staged one slab per chunk, 1 x 1
+    convs as staged rows, 1-D parameters direct) for 3 pairs, against the oracle."""
+    lay = synth.get_layout("resnet50")
+    layout = StateLayout.from_layout(lay)
+    segs = layout.param_segments(synth.param_names(lay))
+    flat = []
+    for s in (9300, 9301, 9302, 9303):
+        sd = synth.synth_state_dict(lay, s)
+        flat.append(torch.cat([v.reshape(-1) for (n, _, d), v in zip(lay, sd.values()) if d == "float32"]).numpy())
+    _check(cuda, flat, segs, [0, 0, 0], [1, 2, 3])

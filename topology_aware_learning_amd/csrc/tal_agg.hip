@@ -2903,15 +2903,78 @@ int32_t launch_round_vec(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, i
 // kernels.  All arithmetic is single-rounding fp32 (__f*_rn), in torch's order.
 // ------------------------------------------------------------------------------------------
 constexpr int kCosMaxPairs = 32;
-constexpr int kCosHdr = 3;         // plan words: {n_seg, n_out, torch intra-op threads}
+constexpr int kCosHdr = 4;         // plan words: {n_seg, n_out, torch intra-op threads, staged chunks}
 constexpr int kCosMaxThreads = 1024;
 constexpr int64_t kCosGrain = 32768;  // at::internal::GRAIN_SIZE
-constexpr int kCosSegWords = 6;    // {offset, A, I, B, out_offset, kind}
-constexpr int kCosChunkWords = 4;  // {seg, first output, count, 0}
+constexpr int kCosSegWords = 7;    // {offset, A, I, B, out_offset, kind, outputs per chunk}
+constexpr int kCosChunkWords = 4;  // {seg, first output, count, staged (1) or direct (0)}
 constexpr int kCosBlock = 256;
 constexpr int kCosVw = 8;          // Vectorized<float> width of torch's sum kernel (as run)
 enum { kCosElem = 0, kCosRow = 1, kCosCol = 2 };
 constexpr int64_t cos_chunk_outputs(int kind) { return kind == kCosRow ? kCosBlock / kCosVw : kCosBlock; }
+
+// Staged chunks (round 6): a workgroup stages whole output slabs of both models of one pair -
+// consecutive rows x[o, :] (row kind) or consecutive [I, B] blocks x[o, :, :] (column kind
+// with B < 32), contiguous in memory - into LDS with coalesced 16-B loads, then runs every
+// chain from LDS: the norms' serial FMA chains (torch's order), the products' level-0 cascade
+// runs (independent: each starts from 0), then each output's cascade / lane fold.  The direct
+// form (one thread or 8 lanes per output, loads strided by B or 8 lanes 32 B wide) was bound by
+// the strided gather (37.7 L1 accesses per load instruction, profiles/r05/r05k2pmc).
+constexpr int kCosStageFloats = 4608;  // per model (18 KiB): one ResNet-50 512 x 512 x 3 x 3 slab
+constexpr int kCosStageOut = 256;      // outputs per staged chunk
+constexpr int kCosStageRows = 32;      // row-kind rows per staged chunk (lane accumulators in LDS)
+constexpr int kCosStageItems = 1024;   // level-0 runs per staged chunk
+constexpr int kCosStageBlock = 256;
+
+__host__ __device__ inline int64_t cos_log2_ceil(int64_t x) {
+  int64_t r = 0;
+  while ((int64_t{1} << r) < x) ++r;
+  return r;
+}
+
+// torch multi_row_sum's level width over `size` elements: 2^max(4, ceil(log2 size) / 4)
+__host__ __device__ inline int64_t cos_lp(int64_t size) {
+  const int64_t l = cos_log2_ceil(size) / 4;
+  return l > 4 ? l : 4;
+}
+
+// row_sum over `len` elements: 4 interleaved streams of len / 4, each cut into level-0 runs of
+// 2^lp (the last one partial); runs per stream
+__host__ __device__ inline int64_t cos_runs(int64_t len) {
+  const int64_t si = len / 4;
+  const int64_t step = int64_t{1} << cos_lp(si);
+  return (si + step - 1) / step;
+}
+
+// A staged output's row_sum sequences: nl lanes (8: torch's vector lanes over a contiguous row
+// of >= 8; else 1) of `len` elements each
+__host__ __device__ inline void cos_stage_seq(int kind, int64_t I, int64_t* nl, int64_t* len) {
+  if (kind == kCosRow && I >= kCosVw) {
+    *nl = kCosVw;
+    *len = I / kCosVw;
+  } else {
+    *nl = 1;
+    *len = I;
+  }
+}
+
+// slabs (output blocks: B outputs of the column kind, one row of the row kind) per staged chunk;
+// 0 = the tensor runs the direct form
+inline int64_t cos_stage_slabs(int kind, int64_t A, int64_t I, int64_t B) {
+  if (kind == kCosElem || (kind == kCosCol && B >= 32)) return 0;  // coalesced as it is
+  const int64_t slab = I * B;
+  if (slab > kCosStageFloats) return 0;
+  int64_t nl, len;
+  cos_stage_seq(kind, I, &nl, &len);
+  const int64_t outs = kind == kCosCol ? B : 1;
+  const int64_t items = outs * nl * 4 * cos_runs(len);
+  if (items > kCosStageItems) return 0;
+  int64_t g = kCosStageFloats / slab;
+  g = std::min<int64_t>(g, kCosStageOut / outs);
+  if (kind == kCosRow) g = std::min<int64_t>(g, kCosStageRows);
+  if (items > 0) g = std::min<int64_t>(g, kCosStageItems / items);
+  return std::max<int64_t>(1, std::min(g, A));
+}
 
 struct CosPairs {
   const float* a[kCosMaxPairs];
@@ -3008,7 +3071,7 @@ __global__ __launch_bounds__(kCosBlock) void k_cosine_outputs(CosPairs pr, const
   const int pair = blockIdx.y;
   const int64_t n_out = plan[1];
   const int64_t* ch = plan + kCosHdr + kCosSegWords * static_cast<int64_t>(n_seg) +
-                      kCosChunkWords * static_cast<int64_t>(blockIdx.x);
+                      kCosChunkWords * (plan[3] + static_cast<int64_t>(blockIdx.x));  // after the staged chunks
   const int64_t* sg = plan + kCosHdr + kCosSegWords * ch[0];
   const int64_t first = ch[1], count = ch[2];
   const int64_t I = sg[2], B = sg[3];
@@ -3132,6 +3195,204 @@ __global__ __launch_bounds__(kCosBlock) void k_cosine_outputs(CosPairs pr, const
     for (int64_t k2 = nv * kCosVw; k2 < I; ++k2) tail = __fadd_rn(tail, prod(k2));
   const float fin = cos_group_fold(tail, lane_sum, gbase);
   if (l == 0 && live) s[q] = __fadd_rn(0.f, fin);
+}
+
+// ---- staged chunks (see kCosStageFloats) ---------------------------------------------------
+// The cascade of one row_sum stream of si elements from its level-0 run sums R(0..): the levels
+// are pushed at the element counts multi_row_sum pushes them (cos_multi_row), the partial last
+// run (si not a multiple of the run width) is the level-0 value at the end.  Every run sum
+// starts from 0, as acc[0] does after each push, so this is cos_multi_row's arithmetic exactly.
+template <class Runs>
+__device__ __forceinline__ float cos_cascade_runs(Runs R, int64_t si) {
+  const int64_t lp = cos_lp(si);
+  const int64_t step = int64_t{1} << lp, mask0 = step - 1;
+  const int64_t full = si / step;
+  float a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int64_t i = 0;
+  for (int64_t r = 0; r < full; ++r) {
+    i += step;
+    a1 = __fadd_rn(a1, R(r));
+    if (i & (mask0 << lp)) continue;
+    a2 = __fadd_rn(a2, a1);
+    a1 = 0.f;
+    if (i & (mask0 << (2 * lp))) continue;
+    a3 = __fadd_rn(a3, a2);
+    a2 = 0.f;
+  }
+  const float a0 = full * step < si ? R(full) : 0.f;
+  return __fadd_rn(__fadd_rn(__fadd_rn(a0, a1), a2), a3);
+}
+
+// ne floats from g into lds[0 .. ne) by 16-B loads from g's 16-B aligned base (a 16-B chunk that
+// holds one element of the range lies in that element's page); NT: non-temporal (read once)
+template <bool NT>
+__device__ __forceinline__ void cos_stage(const float* g, int64_t ne, float* lds) {
+  const int mis = static_cast<int>((reinterpret_cast<uintptr_t>(g) >> 2) & 3);
+  const v4f* g4 = reinterpret_cast<const v4f*>(g - mis);
+  const int n4 = static_cast<int>((ne + mis + 3) / 4);
+  constexpr int kU = (kCosStageFloats / 4 + kCosStageBlock - 1) / kCosStageBlock + 1;  // 6
+  for (int v0 = threadIdx.x; v0 < n4; v0 += kU * kCosStageBlock) {
+    v4f t[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int v = v0 + u * kCosStageBlock;
+      if (v < n4) t[u] = NT ? __builtin_nontemporal_load(g4 + v) : g4[v];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int v = v0 + u * kCosStageBlock;
+      if (v >= n4) continue;
+      const int e = 4 * v - mis;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (e + k >= 0 && e + k < ne) lds[e + k] = t[u][k];
+    }
+  }
+}
+
+// torch NormTwoOps over x[0], x[s], x[2 s], ... (n elements): fma in index order, the LDS reads
+// a batch ahead of the FMAs that use them
+__device__ __forceinline__ float cos_norm_chain(const float* x, int64_t s, int64_t n) {
+  constexpr int kB = 8;
+  float acc = 0.f;
+  float cur[kB], nxt[kB];
+  int64_t i = 0;
+  const int64_t nb = n / kB;
+  if (nb > 0) {
+#pragma unroll
+    for (int u = 0; u < kB; ++u) cur[u] = x[u * s];
+  }
+  for (int64_t b = 0; b < nb; ++b) {
+    const bool more = b + 1 < nb;
+#pragma unroll
+    for (int u = 0; u < kB; ++u) nxt[u] = more ? x[((b + 1) * kB + u) * s] : 0.f;
+#pragma unroll
+    for (int u = 0; u < kB; ++u) acc = __fmaf_rn(cur[u], cur[u], acc);
+#pragma unroll
+    for (int u = 0; u < kB; ++u) cur[u] = nxt[u];
+  }
+  for (i = nb * kB; i < n; ++i) acc = __fmaf_rn(x[i * s], x[i * s], acc);
+  return acc;
+}
+
+// One workgroup per (staged chunk, pair): the chunk's slabs of a and b in LDS, then the
+// outputs' norms, level-0 runs and sums in torch's order (k_cosine_outputs' arithmetic, the
+// independent parts spread over the workgroup's lanes).
+__global__ __launch_bounds__(kCosStageBlock) void k_cosine_staged(CosPairs pr, const int64_t* __restrict__ plan,
+                                                                 int n_seg, int cnt, float* __restrict__ s_all) {
+  __shared__ float sx[2][kCosStageFloats];
+  __shared__ float sn[2][kCosStageOut];             // per output (row kind: per row) norms of a, b
+  __shared__ float sl[2 * kCosVw * kCosStageRows];  // row kind: lane accumulators, then lane sums
+  __shared__ float sr[kCosStageItems];              // level-0 run sums
+  // XCD-aware order: dispatch deals workgroups round-robin over the 8 XCDs, so the pairs of one
+  // chunk (index 8 k + x) run one after another on XCD x, and every pair after the first finds
+  // the aggregating model's slab (each pair's `a`) in that XCD's L2
+  const int L = blockIdx.x;
+  const int kq = L >> 3;
+  const int pair = kq % cnt;
+  const int64_t c = static_cast<int64_t>(kq / cnt) * 8 + (L & 7);
+  if (c >= plan[3]) return;
+  const int64_t* ch = plan + kCosHdr + kCosSegWords * static_cast<int64_t>(n_seg) + kCosChunkWords * c;
+  const int64_t* sg = plan + kCosHdr + kCosSegWords * ch[0];
+  const int64_t first = ch[1], nq = ch[2];
+  const int64_t I = sg[2], B = sg[3];
+  const bool col = sg[5] == kCosCol;
+  const int tid = threadIdx.x;
+  // column kind: first = o0 * B, nq = G * B -> elements o0 I B .. (o0 + G) I B; row kind:
+  // first = o0, nq = G -> o0 I .. (o0 + G) I: both first * I, nq * I
+  cos_stage<false>(pr.a[pair] + sg[0] + first * I, nq * I, sx[0]);
+  cos_stage<true>(pr.b[pair] + sg[0] + first * I, nq * I, sx[1]);
+  __syncthreads();
+  if (col) {  // chains (model, output): x[(q / B) I B + q % B + i B], i < I
+    for (int64_t j = tid; j < 2 * nq; j += kCosStageBlock) {
+      const int m = j >= nq;
+      const int64_t q = j - m * nq;
+      sn[m][q] = cos_clamp(cos_sqrt_rn(cos_norm_chain(sx[m] + (q / B) * I * B + q % B, B, I)));
+    }
+  } else {  // torch's reduce-lastdim norm: 8 lane accumulators over whole vectors, then the fold
+    const int64_t nv = I / kCosVw;
+    for (int64_t j = tid; j < 2 * nq * kCosVw; j += kCosStageBlock) {
+      const int64_t m = j / (nq * kCosVw), r = j - m * nq * kCosVw;
+      sl[j] = cos_norm_chain(sx[m] + (r / kCosVw) * I + r % kCosVw, kCosVw, nv);
+    }
+    __syncthreads();
+    for (int64_t j = tid; j < 2 * nq; j += kCosStageBlock) {
+      const int64_t m = j / nq, g = j - m * nq;
+      const float* la = sl + (m * nq + g) * kCosVw;
+      float t = la[0];
+#pragma unroll
+      for (int l = 1; l < kCosVw; ++l) t = __fadd_rn(t, la[l]);
+      const float* x = sx[m] + g * I;
+      int64_t d = nv * kCosVw;
+      const int64_t sep = (I - d) / 4 * 4;  // the tail: groups of 4 as square-then-add, the rest fused
+      for (int64_t e = 0; e < sep; ++e, ++d) t = __fadd_rn(t, __fmul_rn(x[d], x[d]));
+      for (; d < I; ++d) t = __fmaf_rn(x[d], x[d], t);
+      sn[m][g] = cos_clamp(cos_sqrt_rn(t));
+    }
+  }
+  __syncthreads();
+  // each output's row_sum sequences: nl lanes of len elements, element stride es
+  int64_t nl, len;
+  cos_stage_seq(col ? kCosCol : kCosRow, I, &nl, &len);
+  const int64_t es = col ? B : (nl > 1 ? kCosVw : 1);
+  const int64_t si = len / 4;
+  const int64_t step = int64_t{1} << cos_lp(si);
+  const int64_t nr = (si + step - 1) / step;
+  auto base_of = [&](int64_t q, int64_t l) { return col ? (q / B) * I * B + q % B : q * I + l; };
+  auto prod = [&](int64_t e, float na, float nb) {
+    return __fmul_rn(__fdiv_rn(sx[0][e], na), __fdiv_rn(sx[1][e], nb));
+  };
+  // level-0 runs: item ((r * 4 + stream) * nq + q) * nl + l sums elements 4 i + stream of
+  // sequence (q, l), i in [r step, (r + 1) step) (the last run partial), from 0 in order
+  const int64_t n_items = nq * nl * 4 * nr;
+  for (int64_t it = tid; it < n_items; it += kCosStageBlock) {
+    const int64_t l = it % nl;
+    int64_t t = it / nl;
+    const int64_t q = t % nq;
+    t /= nq;
+    const int64_t st = t % 4, r = t / 4;
+    const float na = sn[0][q], nb = sn[1][q];
+    const int64_t b0 = base_of(q, l) + es * st;
+    const int64_t i1 = min((r + 1) * step, si);
+    float acc = 0.f;
+    for (int64_t i = r * step; i < i1; i += 8) {
+      float p[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) p[u] = i + u < i1 ? prod(b0 + 4 * es * (i + u), na, nb) : 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i + u < i1) acc = __fadd_rn(acc, p[u]);
+    }
+    sr[it] = acc;
+  }
+  __syncthreads();
+  // per sequence: the four streams' cascades, the row_sum remainder into stream 0, the streams
+  // in order (cos_row_sum); one lane: the output's sum; 8 lanes: their sums, folded below
+  float* s = s_all + static_cast<int64_t>(pair) * plan[1] + sg[4] + first;
+  for (int64_t j = tid; j < nq * nl; j += kCosStageBlock) {
+    const int64_t q = j / nl, l = j - q * nl;
+    const float na = sn[0][q], nb = sn[1][q];
+    float ps[4];
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+      ps[st] = cos_cascade_runs([&](int64_t r) { return sr[((r * 4 + st) * nq + q) * nl + l]; }, si);
+    const int64_t b0 = base_of(q, l);
+    for (int64_t i = si * 4; i < len; ++i) ps[0] = __fadd_rn(ps[0], prod(b0 + es * i, na, nb));
+    const float v = __fadd_rn(__fadd_rn(__fadd_rn(ps[0], ps[1]), ps[2]), ps[3]);
+    if (nl == 1) s[q] = __fadd_rn(0.f, v);
+    else sl[j] = v;  // the lane accumulators are spent
+  }
+  if (nl > 1) {  // vectorized_inner_sum: the scalar tail from 0, then the lanes in order
+    __syncthreads();
+    for (int64_t q = tid; q < nq; q += kCosStageBlock) {
+      const float na = sn[0][q], nb = sn[1][q];
+      float fin = 0.f;
+      for (int64_t k2 = len * kCosVw; k2 < I; ++k2) fin = __fadd_rn(fin, prod(q * I + k2, na, nb));
+#pragma unroll
+      for (int l = 0; l < kCosVw; ++l) fin = __fadd_rn(fin, sl[q * kCosVw + l]);
+      s[q] = __fadd_rn(0.f, fin);
+    }
+  }
 }
 
 // torch's serial full sum of s[0 .. n) (scalar_inner_sum below 8 elements, else
@@ -4244,13 +4505,23 @@ int32_t tal_agg_round_bf16(const uint16_t* pool_in, int64_t ld_in, uint16_t* poo
 
 static int cos_kind(int64_t I, int64_t B) { return I == 1 ? kCosElem : (B == 1 ? kCosRow : kCosCol); }
 
+// outputs per chunk of a tensor and whether its chunks are staged (k_cosine_staged: whole slabs
+// per chunk) or direct (k_cosine_outputs)
+static int64_t cos_seg_per(int64_t A, int64_t I, int64_t B, bool* staged) {
+  const int kind = cos_kind(I, B);
+  const int64_t g = cos_stage_slabs(kind, A, I, B);
+  *staged = g > 0;
+  return g > 0 ? g * (kind == kCosCol ? B : 1) : cos_chunk_outputs(kind);
+}
+
 int64_t tal_cosine_plan_words(const int64_t* seg_host, int32_t n_seg) {
   if (!seg_host || n_seg <= 0) return -1;
   int64_t chunks = 0;
   for (int s = 0; s < n_seg; ++s) {
     const int64_t A = seg_host[4 * s + 1], I = seg_host[4 * s + 2], B = seg_host[4 * s + 3];
     if (A <= 0 || I <= 0 || B <= 0 || seg_host[4 * s] < 0) return -1;
-    const int64_t per = cos_chunk_outputs(cos_kind(I, B));
+    bool staged;
+    const int64_t per = cos_seg_per(A, I, B, &staged);
     chunks += (A * B + per - 1) / per;
   }
   return kCosHdr + kCosSegWords * static_cast<int64_t>(n_seg) + kCosChunkWords * chunks;
@@ -4264,30 +4535,43 @@ int32_t tal_cosine_plan_build(const int64_t* seg_host, int32_t n_seg, int64_t* p
   if (plan_capacity_words < words) return fail(TAL_ERR_INVALID, "tal_cosine_plan_build: buffer too small");
   int64_t* sg = plan_host + kCosHdr;
   int64_t* ch = sg + kCosSegWords * static_cast<int64_t>(n_seg);
-  int64_t c = 0, out = 0;
+  int64_t c = 0, out = 0, n_staged = 0;
   for (int s = 0; s < n_seg; ++s) {
     const int64_t A = seg_host[4 * s + 1], I = seg_host[4 * s + 2], B = seg_host[4 * s + 3];
-    const int kind = cos_kind(I, B);
+    bool staged;
     sg[kCosSegWords * s + 0] = seg_host[4 * s];
     sg[kCosSegWords * s + 1] = A;
     sg[kCosSegWords * s + 2] = I;
     sg[kCosSegWords * s + 3] = B;
     sg[kCosSegWords * s + 4] = out;
-    sg[kCosSegWords * s + 5] = kind;
-    const int64_t total = A * B, per = cos_chunk_outputs(kind);
-    for (int64_t f = 0; f < total; f += per) {
-      ch[kCosChunkWords * c + 0] = s;
-      ch[kCosChunkWords * c + 1] = f;
-      ch[kCosChunkWords * c + 2] = std::min(per, total - f);
-      ch[kCosChunkWords * c + 3] = 0;
-      ++c;
+    sg[kCosSegWords * s + 5] = cos_kind(I, B);
+    sg[kCosSegWords * s + 6] = cos_seg_per(A, I, B, &staged);
+    if (staged) n_staged += (A * B + sg[kCosSegWords * s + 6] - 1) / sg[kCosSegWords * s + 6];
+    out += A * B;
+  }
+  // the staged chunks first (k_cosine_staged takes chunks 0 .. n_staged - 1, k_cosine_outputs
+  // the rest); a chunk writes only its own outputs, so the order is free
+  for (int pass = 1; pass >= 0; --pass) {
+    for (int s = 0; s < n_seg; ++s) {
+      const int64_t A = sg[kCosSegWords * s + 1], B = sg[kCosSegWords * s + 3], per = sg[kCosSegWords * s + 6];
+      bool staged;
+      cos_seg_per(A, sg[kCosSegWords * s + 2], B, &staged);
+      if (staged != (pass == 1)) continue;
+      const int64_t total = A * B;
+      for (int64_t f = 0; f < total; f += per) {
+        ch[kCosChunkWords * c + 0] = s;
+        ch[kCosChunkWords * c + 1] = f;
+        ch[kCosChunkWords * c + 2] = std::min(per, total - f);
+        ch[kCosChunkWords * c + 3] = staged ? 1 : 0;
+        ++c;
+      }
     }
-    out += total;
   }
   if (c > 0x7fffffff) return fail(TAL_ERR_INVALID, "tal_cosine_plan_build: too many chunks");
   plan_host[0] = n_seg;
   plan_host[1] = out;
   plan_host[2] = 1;  // serial sums until tal_cosine_plan_set_threads says otherwise
+  plan_host[3] = n_staged;
   *n_chunks = static_cast<int32_t>(c);
   g_err.clear();
   return TAL_OK;
@@ -4328,7 +4612,13 @@ int32_t tal_cosine_params(const float* const* a_ptrs_host, const float* const* b
     }
     float* s_all = static_cast<float*>(scratch);
     float* means = s_all + n_out * cnt;
-    k_cosine_outputs<<<dim3(n_chunks, cnt), kCosBlock, 0, s>>>(pr, plan_dev, n_seg, s_all);
+    const int64_t n_staged = plan_host[3];
+    if (n_staged > 0)  // XCD-aware 1-D grid: 8 k + x = (chunk 8 (k / cnt) + x, pair k % cnt)
+      k_cosine_staged<<<static_cast<unsigned>((n_staged + 7) / 8 * 8 * cnt), kCosStageBlock, 0, s>>>(
+          pr, plan_dev, n_seg, cnt, s_all);
+    if (n_chunks > n_staged)
+      k_cosine_outputs<<<dim3(static_cast<unsigned>(n_chunks - n_staged), cnt), kCosBlock, 0, s>>>(pr, plan_dev, n_seg,
+                                                                                                  s_all);
     k_cosine_means<<<dim3(n_seg, cnt), 64, 0, s>>>(plan_dev, n_seg, s_all, means);
     k_cosine_finish<<<cnt, 64, 0, s>>>(n_seg, means, out_dev, base);
   }
@@ -4997,8 +5287,7 @@ int32_t tal_host_cosine(const float* const* a_host, const float* const* b_host, 
   int64_t n_chunks = 0;  // chunk words follow the segment words; count them from the segments
   for (int64_t t = 0; t < n_seg; ++t) {
     const int64_t* sg = plan_host + kCosHdr + kCosSegWords * t;
-    const int64_t per = cos_chunk_outputs(static_cast<int>(sg[5]));
-    n_chunks += (sg[1] * sg[3] + per - 1) / per;
+    n_chunks += (sg[1] * sg[3] + sg[6] - 1) / sg[6];
   }
   std::vector<float> s_all(static_cast<size_t>(n_out));
   std::vector<float> means(static_cast<size_t>(n_seg));
