@@ -86,7 +86,11 @@ def parse():
                         "sends / receives)")
     p.add_argument("--exchange", default="auto", choices=["auto", "halo", "transpose"],
                    help="N > 1: neighbor models by RCCL P2P (halo) or column blocks by all-to-all "
-                        "(transpose); auto = fewer link bytes (transposed.choose_exchange)")
+                        "(transpose); auto = the smaller predicted time at the probed link rate "
+                        "(transposed.choose_exchange)")
+    p.add_argument("--link-probe-mb", type=int, default=1024,
+                   help="N > 1: bytes each rank sends to (and receives from) every other rank in the "
+                        "link probe before the round is built (gloo rehearsals: at most 8 MiB)")
     return p.parse_args()
 
 
@@ -475,10 +479,13 @@ def main():
 
         # per-rank progress on stderr: a first multi-GPU run that stalls names its phase
         rlog = (lambda msg: log(f"rank {rank}/{world}: {msg}"))
-        rlog(f"{n_dev_total} devices, {layout.n_f32 + layout.n_b16} float params per model; building the round")
+        rlog(f"{n_dev_total} devices, {layout.n_f32 + layout.n_b16} float params per model; probing the links")
+        probe = link_probe(dist, rank, world, dev, args.dist_backend, args.link_probe_mb)
+        rlog(f"link probe {probe['GBps']} GB/s per pair (min over ranks); building the round")
         sr = make_round(layout, orders, weights, rank, world, dev, exchange=args.exchange, mode=mode,
                         tune=not args.no_tune,
-                        transport="host" if args.dist_backend == "gloo" else args.halo_transport)
+                        transport="host" if args.dist_backend == "gloo" else args.halo_transport,
+                        link_gbps=probe["GBps"] if world > 1 else None)
         rlog(f"{sr.exchange_kind} exchange over {sr.transport}, {len(sr.own_ids)} own devices; first round")
         rowcheck.fill_owned(sr.pool_a, lay, sr.own_ids, seed_base)
         sr.step()
@@ -518,13 +525,14 @@ def main():
         # DESIGN §6's model next to the measurement: per exchange kind the busiest rank's HBM
         # bytes and the busiest GPU pair's link bytes over their peaks; the binding term
         from topology_aware_learning_amd.distributed import partition_contiguous
-        from topology_aware_learning_amd.transposed import link_model
+        from topology_aware_learning_amd.transposed import XGMI_LINK_GBPS, link_model
 
         model = link_model(orders, partition_contiguous(n_dev_total, world), world, layout.n_f32,
-                           layout.n_i64, layout.n_b16)
+                           layout.n_i64, layout.n_b16, link_gbps=probe["GBps"] if world > 1 else XGMI_LINK_GBPS)
         ms_step = 1e3 * el / args.steps
         chosen = model[sr.exchange_kind]
         result_extra = dict(kernel=",".join(sorted({ops.round_kernel_name(p) for p in sr.plans.values()})),
+                            link_probe_GBps=probe["GBps"], link_probe=probe,
                             parity_rows=parity_rows, exchange=sr.exchange_kind, transport=sr.transport, link_bytes_in_per_round=sr.link_bytes,
                             link_GBps_in=sr.link_bytes / (el / args.steps) / 1e9,
                             bound_model=dict(per_exchange={k: {kk: (round(vv, 3) if isinstance(vv, float) else vv)
@@ -590,6 +598,44 @@ def main():
     if sharded:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def link_probe(dist, rank: int, world: int, dev, backend: str, mb: int) -> dict:
+    """The per-pair link rate the exchange choice and the bound model use: every rank
+    sends `mb` MiB to every other rank and receives as much from each, all pairs at once in one
+    P2P group (as both exchanges load the links), timed after one warm-up group; rate = bytes
+    per pair / seconds, reduced with a MIN over ranks so every rank makes the same choice.
+    Replaces the assumed 153 GB/s per xGMI pair (neither skill guide states one).  Over gloo
+    (rehearsal) it is a host-memory rate, at most 8 MiB per pair."""
+    import torch
+
+    if world < 2:
+        return dict(GBps=None, bytes_per_pair=0, seconds=None, backend=backend)
+    nbytes = (min(mb, 8) if backend == "gloo" else mb) << 20
+    d = dev if backend == "nccl" else torch.device("cpu")
+    send = torch.ones(nbytes, dtype=torch.uint8, device=d)
+    peers = [p for p in range(world) if p != rank]
+    recv = [torch.empty(nbytes, dtype=torch.uint8, device=d) for _ in peers]
+    ops_ = [op for p, r in zip(peers, recv) for op in (dist.P2POp(dist.isend, send, p), dist.P2POp(dist.irecv, r, p))]
+
+    def group():
+        for w in dist.batch_isend_irecv(ops_):
+            w.wait()
+        if d.type == "cuda":
+            torch.cuda.synchronize(d)
+
+    group()
+    dist.barrier()
+    t0 = time.perf_counter()
+    group()
+    el = time.perf_counter() - t0
+    rate = torch.tensor([nbytes / el / 1e9], dtype=torch.float64, device=d)
+    dist.all_reduce(rate, op=dist.ReduceOp.MIN)
+    del send, recv
+    if d.type == "cuda":
+        torch.cuda.empty_cache()
+    return dict(GBps=float(rate.item()), bytes_per_pair=nbytes, seconds_local=el, backend=backend,
+                note="all pairs at once, one direction per pair; MIN over ranks")
 
 
 def _round_csr(orders, weights):

@@ -14,6 +14,6 @@ timeout -k 10 120 python tools/cosine_bench.py resnet50 > $o/bench1.log 2>&1 && 
 timeout -k 10 120 python tools/cosine_bench.py resnet50 > $o/bench2.log 2>&1 && \
 timeout -k 10 120 python tools/cosine_bench.py vit_b16 > $o/bench_vit.log 2>&1 && \
 timeout -k 10 120 python tools/cosine_kinds.py resnet50 > $o/kinds.log 2>&1 && \
-( cd /tmp && export TMPDIR=/tmp && timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $o/prof -o k2 -- python3 $R/tools/cosine_bench.py resnet50 > $o/prof.log 2>&1 )
+( cd /tmp && export TMPDIR=/tmp && timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $o/prof -o k2 -- python3 $R/tools/cosine_bench.py resnet50 > $o/prof.log 2>&1 )
 rc=$?
 echo EXIT $rc

@@ -223,6 +223,8 @@ def test_bench_world8_rehearsal(cuda, tmp_path, graph, model, dtype, exchange):
     assert pr["rows_checked"] == pr["devices"] == d["config"]["devices"] and pr["rows_differing"] == 0
     assert pr["reference"].startswith("K1")  # --max-params: no reference fixture for the cut layout
     assert d["value"] > 0 and d["link_bytes_in_per_round"] > 0
+    # the link probe ran before the round was built and fed the bound model and the choice
+    assert d["link_probe_GBps"] > 0 and d["link_probe"]["bytes_per_pair"] == 8 << 20
     if exchange != "auto":
         assert d["exchange"] == exchange
 

@@ -861,3 +861,60 @@ def test_pool_row_addresses_and_cpu_pool_refused():
     with pytest.raises(ValueError, match="device pool"):
         ops.agg_pool_rows(pool, [0, 1], [0.5, 0.5], 1)
     assert torch.equal(pool.f32, torch.zeros_like(pool.f32))
+
+
+def test_tune_candidates_by_workload_class():
+    """The tuner times only forms that won a workload of the same class: no broadcast form on
+    uniform-weight rounds (config 3: 6.2-9.9 ms against 2.0 in BENCH_r05), the measured winners
+    on per-operand-weight rounds (config 5 degree centrality)."""
+    import bench
+    from topology_aware_learning_amd.round import csr_from_lists
+
+    orders, ws = bench.round_spec(64, 8)  # config 3: unweighted
+    rp, col, w = csr_from_lists(orders, ws)
+    rows = np.arange(len(orders), dtype=np.int32)
+    assert ops.rows_uniform(rp, w)
+    keys = [k for k, _ in ops.tune_candidates(rp, col, w, rows)]
+    assert keys[0] == ("default",) and not any(k[0] == "bcast" for k in keys)
+    orders, ws = bench.round_spec(256, 8, kind="sbm", weights="degcent")
+    rp, col, w = csr_from_lists(orders, ws)
+    rows = np.arange(len(orders), dtype=np.int32)
+    assert not ops.rows_uniform(rp, w)
+    for bf16 in (False, True):
+        keys = [k for k, _ in ops.tune_candidates(rp, col, w, rows, bf16=bf16, mode=ops.MODE_FMA)]
+        bc = {k[1:] for k in keys if k[0] == "bcast"}
+        assert bc and bc <= set(ops.BCAST_CANDIDATES)
+
+
+def test_exchange_choice_follows_measured_link_rate():
+    """With a measured link rate (bench.py's probe) the 'auto' exchange is the one with the smaller
+    predicted time: below the crossover rate the link binds and the transpose's smaller busiest
+    pair wins; above it both are HBM-bound and the halo's fewer local bytes win.  Without a rate:
+    the busiest-pair byte rule (unchanged)."""
+    import bench
+    from topology_aware_learning_amd import synth
+    from topology_aware_learning_amd.arena import StateLayout
+    from topology_aware_learning_amd.distributed import partition_contiguous
+    from topology_aware_learning_amd.transposed import choose_exchange, exchange_crossover_gbps, link_model
+
+    cases = [("sbm", 256, "vit_b16", 8), ("random", None, "resnet50", 4), ("random", None, "resnet50", 8),
+             ("barbell", 128, "resnet50", 4)]
+    flipped = 0
+    for kind, nd, model, world in cases:
+        lay = StateLayout.from_layout(synth.get_layout(model))
+        orders, _ = bench.round_spec(nd or 64 * world, 8, kind=kind)
+        owner = partition_contiguous(len(orders), world)
+        args = (orders, owner, world, lay.n_f32, lay.n_i64, lay.n_b16)
+        x = exchange_crossover_gbps(*args)
+        if choose_exchange(*args) != "transpose":
+            continue
+        if x is None:  # the transpose also moves fewer local bytes (random graph at 8 ranks): any rate
+            assert choose_exchange(*args, link_gbps=1e6) == choose_exchange(*args, link_gbps=10.0) == "transpose"
+            continue
+        assert x > 153.0  # at the assumed 153 GB/s the byte rule's transpose stands
+        assert choose_exchange(*args, link_gbps=0.99 * x) == "transpose"
+        assert choose_exchange(*args, link_gbps=1.01 * x) == "halo"
+        m = link_model(*args, link_gbps=1.01 * x)
+        assert m["transpose"]["predicted_ms"] >= 0.9 * m["halo"]["predicted_ms"]
+        flipped += 1
+    assert flipped >= 2

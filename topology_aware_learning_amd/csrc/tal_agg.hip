@@ -2920,7 +2920,7 @@ constexpr int64_t cos_chunk_outputs(int kind) { return kind == kCosRow ? kCosBlo
 // runs (independent: each starts from 0), then each output's cascade / lane fold.  The direct
 // form (one thread or 8 lanes per output, loads strided by B or 8 lanes 32 B wide) was bound by
 // the strided gather (37.7 L1 accesses per load instruction, profiles/r05/r05k2pmc).
-constexpr int kCosStageFloats = 4608;  // per model (18 KiB): one ResNet-50 512 x 512 x 3 x 3 slab
+constexpr int kCosStageFloats = 4736;  // per model (18.5 KiB): one ResNet-50 512 x 512 x 3 x 3 slab, padded
 constexpr int kCosStageOut = 256;      // outputs per staged chunk
 constexpr int kCosStageRows = 32;      // row-kind rows per staged chunk (lane accumulators in LDS)
 constexpr int kCosStageItems = 1024;   // level-0 runs per staged chunk
@@ -2958,11 +2958,20 @@ __host__ __device__ inline void cos_stage_seq(int kind, int64_t I, int64_t* nl, 
   }
 }
 
+// LDS pitch of one staged column sequence (column kind, stored transposed: x[o, :, k] contiguous):
+// I rounded up to 4 floats (16-B aligned reads) + 4 (consecutive columns 4 banks apart)
+__host__ __device__ inline int64_t cos_col_pitch(int64_t I) { return (I + 3) / 4 * 4 + 4; }
+
+// LDS floats of one slab (column kind: B transposed sequences; row kind: the row as it is)
+__host__ __device__ inline int64_t cos_slab_floats(int kind, int64_t I, int64_t B) {
+  return kind == kCosCol ? B * cos_col_pitch(I) : I;
+}
+
 // slabs (output blocks: B outputs of the column kind, one row of the row kind) per staged chunk;
 // 0 = the tensor runs the direct form
 inline int64_t cos_stage_slabs(int kind, int64_t A, int64_t I, int64_t B) {
   if (kind == kCosElem || (kind == kCosCol && B >= 32)) return 0;  // coalesced as it is
-  const int64_t slab = I * B;
+  const int64_t slab = cos_slab_floats(kind, I, B);
   if (slab > kCosStageFloats) return 0;
   int64_t nl, len;
   cos_stage_seq(kind, I, &nl, &len);
@@ -3203,13 +3212,13 @@ __global__ __launch_bounds__(kCosBlock) void k_cosine_outputs(CosPairs pr, const
 // run (si not a multiple of the run width) is the level-0 value at the end.  Every run sum
 // starts from 0, as acc[0] does after each push, so this is cos_multi_row's arithmetic exactly.
 template <class Runs>
-__device__ __forceinline__ float cos_cascade_runs(Runs R, int64_t si) {
-  const int64_t lp = cos_lp(si);
-  const int64_t step = int64_t{1} << lp, mask0 = step - 1;
-  const int64_t full = si / step;
+__device__ __forceinline__ float cos_cascade_runs(Runs R, int si) {
+  const int lp = static_cast<int>(cos_lp(si));
+  const int step = 1 << lp, mask0 = step - 1;
+  const int full = si / step;
   float a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  int64_t i = 0;
-  for (int64_t r = 0; r < full; ++r) {
+  int i = 0;
+  for (int r = 0; r < full; ++r) {
     i += step;
     a1 = __fadd_rn(a1, R(r));
     if (i & (mask0 << lp)) continue;
@@ -3223,13 +3232,27 @@ __device__ __forceinline__ float cos_cascade_runs(Runs R, int64_t si) {
   return __fadd_rn(__fadd_rn(__fadd_rn(a0, a1), a2), a3);
 }
 
-// ne floats from g into lds[0 .. ne) by 16-B loads from g's 16-B aligned base (a 16-B chunk that
-// holds one element of the range lies in that element's page); NT: non-temporal (read once)
-template <bool NT>
-__device__ __forceinline__ void cos_stage(const float* g, int64_t ne, float* lds) {
+// q, r of e / d (e < 2^22, 0 < d): a float-reciprocal estimate within one of the quotient, fixed
+__device__ __forceinline__ int cos_divmod(int e, int d, float inv_d, int* rem) {
+  int q = static_cast<int>(static_cast<float>(e) * inv_d);
+  int r = e - q * d;
+  if (r < 0) { --q; r += d; }
+  else if (r >= d) { ++q; r -= d; }
+  *rem = r;
+  return q;
+}
+
+// The chunk's ne floats from g into LDS by 16-B loads from g's 16-B aligned base (a 16-B chunk
+// holding one element of the range lies in that element's page); NT: non-temporal (read once).
+// Column kind (COL): element (slab o, i, column k) of the [G, I, B] block goes to
+// lds[(o B + k) P + i] - each output's sequence contiguous, P = cos_col_pitch(I).
+template <bool NT, bool COL>
+__device__ __forceinline__ void cos_stage(const float* g, int ne, float* lds, int I, int B, int P) {
   const int mis = static_cast<int>((reinterpret_cast<uintptr_t>(g) >> 2) & 3);
   const v4f* g4 = reinterpret_cast<const v4f*>(g - mis);
-  const int n4 = static_cast<int>((ne + mis + 3) / 4);
+  const int n4 = (ne + mis + 3) / 4;
+  const int ib = I * B;
+  const float inv_ib = 1.f / static_cast<float>(ib), inv_b = 1.f / static_cast<float>(B);
   constexpr int kU = (kCosStageFloats / 4 + kCosStageBlock - 1) / kCosStageBlock + 1;  // 6
   for (int v0 = threadIdx.x; v0 < n4; v0 += kU * kCosStageBlock) {
     v4f t[kU];
@@ -3242,45 +3265,83 @@ __device__ __forceinline__ void cos_stage(const float* g, int64_t ne, float* lds
     for (int u = 0; u < kU; ++u) {
       const int v = v0 + u * kCosStageBlock;
       if (v >= n4) continue;
-      const int e = 4 * v - mis;
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (e + k >= 0 && e + k < ne) lds[e + k] = t[u][k];
+      for (int k = 0; k < 4; ++k) {
+        const int e = 4 * v - mis + k;
+        if (e < 0 || e >= ne) continue;
+        int dst = e;
+        if constexpr (COL) {
+          int rem, col;
+          const int o = cos_divmod(e, ib, inv_ib, &rem);
+          const int i = cos_divmod(rem, B, inv_b, &col);
+          dst = (o * B + col) * P + i;
+        }
+        lds[dst] = t[u][k];
+      }
     }
   }
 }
 
-// torch NormTwoOps over x[0], x[s], x[2 s], ... (n elements): fma in index order, the LDS reads
-// a batch ahead of the FMAs that use them
-__device__ __forceinline__ float cos_norm_chain(const float* x, int64_t s, int64_t n) {
-  constexpr int kB = 8;
+// torch NormTwoOps over x[0], x[S], x[2 S], ... (n elements): fma in index order; the reads a
+// batch ahead of the FMAs (S = 1: 16-B reads of a 16-B aligned sequence)
+template <int S>
+__device__ __forceinline__ float cos_norm_chain(const float* x, int n) {
+  constexpr int kB = 16;
   float acc = 0.f;
   float cur[kB], nxt[kB];
-  int64_t i = 0;
-  const int64_t nb = n / kB;
-  if (nb > 0) {
+  const int nb = n / kB;
+  auto load = [&](float* v, const float* p) {
+    if constexpr (S == 1) {
 #pragma unroll
-    for (int u = 0; u < kB; ++u) cur[u] = x[u * s];
-  }
-  for (int64_t b = 0; b < nb; ++b) {
-    const bool more = b + 1 < nb;
+      for (int u = 0; u < kB; u += 4) {
+        const v4f q = *reinterpret_cast<const v4f*>(p + u);
+        v[u] = q.x; v[u + 1] = q.y; v[u + 2] = q.z; v[u + 3] = q.w;
+      }
+    } else {
 #pragma unroll
-    for (int u = 0; u < kB; ++u) nxt[u] = more ? x[((b + 1) * kB + u) * s] : 0.f;
+      for (int u = 0; u < kB; ++u) v[u] = p[u * S];
+    }
+  };
+  if (nb > 0) load(cur, x);
+  for (int b = 0; b < nb; ++b) {
+    if (b + 1 < nb) load(nxt, x + (b + 1) * kB * S);
 #pragma unroll
     for (int u = 0; u < kB; ++u) acc = __fmaf_rn(cur[u], cur[u], acc);
 #pragma unroll
     for (int u = 0; u < kB; ++u) cur[u] = nxt[u];
   }
-  for (i = nb * kB; i < n; ++i) acc = __fmaf_rn(x[i * s], x[i * s], acc);
+  for (int i = nb * kB; i < n; ++i) acc = __fmaf_rn(x[i * S], x[i * S], acc);
+  return acc;
+}
+
+// ((x1 / na) * (x2 / nb)) for the two staged models (x2 = x1 + kCosStageFloats)
+__device__ __forceinline__ float cos_prod(const float* x, float na, float nb) {
+  return __fmul_rn(__fdiv_rn(x[0], na), __fdiv_rn(x[kCosStageFloats], nb));
+}
+
+// One level-0 run: elements 0, ST, 2 ST, ... (n of them) from 0 in order, products a batch ahead
+template <int ST>
+__device__ __forceinline__ float cos_run(const float* x, int n, float na, float nb) {
+  float acc = 0.f;
+  int i = 0;
+  for (; i + 8 <= n; i += 8, x += 8 * ST) {
+    float p[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) p[u] = cos_prod(x + u * ST, na, nb);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = __fadd_rn(acc, p[u]);
+  }
+  for (; i < n; ++i, x += ST) acc = __fadd_rn(acc, cos_prod(x, na, nb));
   return acc;
 }
 
 // One workgroup per (staged chunk, pair): the chunk's slabs of a and b in LDS, then the
 // outputs' norms, level-0 runs and sums in torch's order (k_cosine_outputs' arithmetic, the
-// independent parts spread over the workgroup's lanes).
+// independent parts spread over the workgroup's lanes).  LDS indices are 32-bit and every
+// chain walks a pointer with a compile-time stride.
 __global__ __launch_bounds__(kCosStageBlock) void k_cosine_staged(CosPairs pr, const int64_t* __restrict__ plan,
                                                                  int n_seg, int cnt, float* __restrict__ s_all) {
-  __shared__ float sx[2][kCosStageFloats];
+  __shared__ __attribute__((aligned(16))) float sx[2 * kCosStageFloats];
   __shared__ float sn[2][kCosStageOut];             // per output (row kind: per row) norms of a, b
   __shared__ float sl[2 * kCosVw * kCosStageRows];  // row kind: lane accumulators, then lane sums
   __shared__ float sr[kCosStageItems];              // level-0 run sums
@@ -3294,100 +3355,100 @@ __global__ __launch_bounds__(kCosStageBlock) void k_cosine_staged(CosPairs pr, c
   if (c >= plan[3]) return;
   const int64_t* ch = plan + kCosHdr + kCosSegWords * static_cast<int64_t>(n_seg) + kCosChunkWords * c;
   const int64_t* sg = plan + kCosHdr + kCosSegWords * ch[0];
-  const int64_t first = ch[1], nq = ch[2];
-  const int64_t I = sg[2], B = sg[3];
+  const int64_t first = ch[1];
+  const int nq = static_cast<int>(ch[2]);
+  const int I = static_cast<int>(sg[2]), B = static_cast<int>(sg[3]);
   const bool col = sg[5] == kCosCol;
+  const int P = col ? static_cast<int>(cos_col_pitch(I)) : I;  // LDS floats per sequence / row
   const int tid = threadIdx.x;
   // column kind: first = o0 * B, nq = G * B -> elements o0 I B .. (o0 + G) I B; row kind:
   // first = o0, nq = G -> o0 I .. (o0 + G) I: both first * I, nq * I
-  cos_stage<false>(pr.a[pair] + sg[0] + first * I, nq * I, sx[0]);
-  cos_stage<true>(pr.b[pair] + sg[0] + first * I, nq * I, sx[1]);
+  const float* ga = pr.a[pair] + sg[0] + first * I;
+  const float* gb = pr.b[pair] + sg[0] + first * I;
+  if (col) {
+    cos_stage<false, true>(ga, nq * I, sx, I, B, P);
+    cos_stage<true, true>(gb, nq * I, sx + kCosStageFloats, I, B, P);
+  } else {
+    cos_stage<false, false>(ga, nq * I, sx, I, B, P);
+    cos_stage<true, false>(gb, nq * I, sx + kCosStageFloats, I, B, P);
+  }
   __syncthreads();
-  if (col) {  // chains (model, output): x[(q / B) I B + q % B + i B], i < I
-    for (int64_t j = tid; j < 2 * nq; j += kCosStageBlock) {
+  if (col) {  // chains (model, output): the output's contiguous sequence
+    for (int j = tid; j < 2 * nq; j += kCosStageBlock) {
       const int m = j >= nq;
-      const int64_t q = j - m * nq;
-      sn[m][q] = cos_clamp(cos_sqrt_rn(cos_norm_chain(sx[m] + (q / B) * I * B + q % B, B, I)));
+      const int q = j - m * nq;
+      sn[m][q] = cos_clamp(cos_sqrt_rn(cos_norm_chain<1>(sx + m * kCosStageFloats + q * P, I)));
     }
   } else {  // torch's reduce-lastdim norm: 8 lane accumulators over whole vectors, then the fold
-    const int64_t nv = I / kCosVw;
-    for (int64_t j = tid; j < 2 * nq * kCosVw; j += kCosStageBlock) {
-      const int64_t m = j / (nq * kCosVw), r = j - m * nq * kCosVw;
-      sl[j] = cos_norm_chain(sx[m] + (r / kCosVw) * I + r % kCosVw, kCosVw, nv);
+    const int nv = I / kCosVw;
+    for (int j = tid; j < 2 * nq * kCosVw; j += kCosStageBlock) {
+      const int m = j / (nq * kCosVw), r = j - m * nq * kCosVw;
+      sl[j] = cos_norm_chain<kCosVw>(sx + m * kCosStageFloats + (r >> 3) * I + (r & 7), nv);
     }
     __syncthreads();
-    for (int64_t j = tid; j < 2 * nq; j += kCosStageBlock) {
-      const int64_t m = j / nq, g = j - m * nq;
+    for (int j = tid; j < 2 * nq; j += kCosStageBlock) {
+      const int m = j / nq, g = j - m * nq;
       const float* la = sl + (m * nq + g) * kCosVw;
       float t = la[0];
 #pragma unroll
       for (int l = 1; l < kCosVw; ++l) t = __fadd_rn(t, la[l]);
-      const float* x = sx[m] + g * I;
-      int64_t d = nv * kCosVw;
-      const int64_t sep = (I - d) / 4 * 4;  // the tail: groups of 4 as square-then-add, the rest fused
-      for (int64_t e = 0; e < sep; ++e, ++d) t = __fadd_rn(t, __fmul_rn(x[d], x[d]));
+      const float* x = sx + m * kCosStageFloats + g * I;
+      int d = nv * kCosVw;
+      const int sep = (I - d) / 4 * 4;  // the tail: groups of 4 as square-then-add, the rest fused
+      for (int e = 0; e < sep; ++e, ++d) t = __fadd_rn(t, __fmul_rn(x[d], x[d]));
       for (; d < I; ++d) t = __fmaf_rn(x[d], x[d], t);
       sn[m][g] = cos_clamp(cos_sqrt_rn(t));
     }
   }
   __syncthreads();
-  // each output's row_sum sequences: nl lanes of len elements, element stride es
-  int64_t nl, len;
-  cos_stage_seq(col ? kCosCol : kCosRow, I, &nl, &len);
-  const int64_t es = col ? B : (nl > 1 ? kCosVw : 1);
-  const int64_t si = len / 4;
-  const int64_t step = int64_t{1} << cos_lp(si);
-  const int64_t nr = (si + step - 1) / step;
-  auto base_of = [&](int64_t q, int64_t l) { return col ? (q / B) * I * B + q % B : q * I + l; };
-  auto prod = [&](int64_t e, float na, float nb) {
-    return __fmul_rn(__fdiv_rn(sx[0][e], na), __fdiv_rn(sx[1][e], nb));
-  };
+  // each output's row_sum sequences: nl lanes of len elements; in LDS sequence (q, l) starts at
+  // q P (column) / q I + l (row) with element stride es
+  const int nl = (!col && I >= kCosVw) ? kCosVw : 1;
+  const int len = nl > 1 ? I / kCosVw : I;
+  const int es = nl > 1 ? kCosVw : 1;
+  const int si = len / 4;
+  const int step = 1 << static_cast<int>(cos_lp(si));
+  const int nr = (si + step - 1) / step;
+  auto base_of = [&](int q, int l) { return col ? q * P : q * I + l; };
   // level-0 runs: item ((r * 4 + stream) * nq + q) * nl + l sums elements 4 i + stream of
   // sequence (q, l), i in [r step, (r + 1) step) (the last run partial), from 0 in order
-  const int64_t n_items = nq * nl * 4 * nr;
-  for (int64_t it = tid; it < n_items; it += kCosStageBlock) {
-    const int64_t l = it % nl;
-    int64_t t = it / nl;
-    const int64_t q = t % nq;
+  const int n_items = nq * nl * 4 * nr;
+  for (int it = tid; it < n_items; it += kCosStageBlock) {
+    const int l = it % nl;
+    int t = it / nl;
+    const int q = t % nq;
     t /= nq;
-    const int64_t st = t % 4, r = t / 4;
-    const float na = sn[0][q], nb = sn[1][q];
-    const int64_t b0 = base_of(q, l) + es * st;
-    const int64_t i1 = min((r + 1) * step, si);
-    float acc = 0.f;
-    for (int64_t i = r * step; i < i1; i += 8) {
-      float p[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) p[u] = i + u < i1 ? prod(b0 + 4 * es * (i + u), na, nb) : 0.f;
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (i + u < i1) acc = __fadd_rn(acc, p[u]);
-    }
-    sr[it] = acc;
+    const int st = t & 3, r = t >> 2;
+    const int i0 = r * step, n = min(step, si - i0);
+    const float* x = sx + base_of(q, l) + es * (4 * i0 + st);
+    sr[it] = es == 1 ? cos_run<4>(x, n, sn[0][q], sn[1][q]) : cos_run<4 * kCosVw>(x, n, sn[0][q], sn[1][q]);
   }
   __syncthreads();
   // per sequence: the four streams' cascades, the row_sum remainder into stream 0, the streams
   // in order (cos_row_sum); one lane: the output's sum; 8 lanes: their sums, folded below
   float* s = s_all + static_cast<int64_t>(pair) * plan[1] + sg[4] + first;
-  for (int64_t j = tid; j < nq * nl; j += kCosStageBlock) {
-    const int64_t q = j / nl, l = j - q * nl;
+  const int rstride = 4 * nq * nl;  // between a sequence's consecutive runs of one stream
+  for (int j = tid; j < nq * nl; j += kCosStageBlock) {
+    const int q = j / nl, l = j - q * nl;
     const float na = sn[0][q], nb = sn[1][q];
     float ps[4];
 #pragma unroll
-    for (int st = 0; st < 4; ++st)
-      ps[st] = cos_cascade_runs([&](int64_t r) { return sr[((r * 4 + st) * nq + q) * nl + l]; }, si);
-    const int64_t b0 = base_of(q, l);
-    for (int64_t i = si * 4; i < len; ++i) ps[0] = __fadd_rn(ps[0], prod(b0 + es * i, na, nb));
+    for (int st = 0; st < 4; ++st) {
+      const float* rs = sr + st * nq * nl + j;
+      ps[st] = cos_cascade_runs([&](int r) { return rs[r * rstride]; }, si);
+    }
+    const float* x = sx + base_of(q, l);
+    for (int i = si * 4; i < len; ++i) ps[0] = __fadd_rn(ps[0], cos_prod(x + es * i, na, nb));
     const float v = __fadd_rn(__fadd_rn(__fadd_rn(ps[0], ps[1]), ps[2]), ps[3]);
     if (nl == 1) s[q] = __fadd_rn(0.f, v);
     else sl[j] = v;  // the lane accumulators are spent
   }
   if (nl > 1) {  // vectorized_inner_sum: the scalar tail from 0, then the lanes in order
     __syncthreads();
-    for (int64_t q = tid; q < nq; q += kCosStageBlock) {
+    for (int q = tid; q < nq; q += kCosStageBlock) {
       const float na = sn[0][q], nb = sn[1][q];
       float fin = 0.f;
-      for (int64_t k2 = len * kCosVw; k2 < I; ++k2) fin = __fadd_rn(fin, prod(q * I + k2, na, nb));
+      for (int k2 = len * kCosVw; k2 < I; ++k2) fin = __fadd_rn(fin, cos_prod(sx + q * I + k2, na, nb));
 #pragma unroll
       for (int l = 0; l < kCosVw; ++l) fin = __fadd_rn(fin, sl[q * kCosVw + l]);
       s[q] = __fadd_rn(0.f, fin);

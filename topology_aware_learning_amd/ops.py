@@ -181,8 +181,14 @@ def host_agg(xs: Sequence[torch.Tensor], weights: Sequence[float], out: torch.Te
 LDS_BUDGET = 80 * 1024  # two workgroups per CU overlap one's HBM staging with the other's math
 LDS_BUDGETS = (80 * 1024, 160 * 1024)  # candidates: 2 workgroups / CU, or 1 with bigger groups
 TILE_WIDTHS = (64, 128, 32, 16)  # float4 per staged source per tile (ties keep the earlier)
-BCAST_WIDTHS = (16, 32)          # the narrow kernel's broadcast form (build_plan(bcast=...))
-BCAST_FORMS = ((8, 2), (12, 2), (16, 2), (16, 1))  # (wavefronts per workgroup, workgroups per CU)
+# the narrow kernel's broadcast form (build_plan(bcast=...)): (c4, wavefronts per workgroup,
+# workgroups per CU) of the forms that won a measured round - per-operand weights on a
+# community graph (config 5 degree-centrality: fp32 16/8/2, bf16 32/16/1 and 16/16/2).
+# The form is a candidate only for rounds with per-operand weights: on uniform-weight rows it
+# never won (config 3: 6.2-9.9 ms against 2.0 in BENCH_r05; config 5 bf16 unweighted: 23.6-103
+# against 22.3, profiles/r06/r06a)
+BCAST_CANDIDATES = ((16, 8, 2), (16, 16, 2), (32, 16, 1), (32, 8, 2))
+TUNE_DROP = 1.5  # a candidate whose first timed run exceeds the default's by this factor is dropped
 
 
 @dataclass
@@ -721,27 +727,17 @@ def build_stream_plan(row_ptr, col, w, out_row, max_group_rows: int = 64, max_gr
     return RoundPlan(info=info, host=blob[: info.words].copy(), rows=rows, nnz=len(col))
 
 
-def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.Tensor,
-              n: Optional[int] = None, reps: int = 5, mode: int = MODE_EXACT,
-              margin: float = 0.01) -> RoundPlan:
-    """Pick the plan by measurement, anchored on the untimed default (default_plan).
+def rows_uniform(row_ptr, w) -> bool:
+    """Every row's operands share one fp32 weight (unweighted_module_avg, scale_agg): the
+    narrow plans' row-weight form, on which the broadcast form never won."""
+    w32 = np.asarray(w, dtype=np.float64).astype(np.float32)
+    rp = np.asarray(row_ptr)
+    first = np.repeat(w32[rp[:-1]], np.diff(rp))
+    return bool(np.array_equal(w32, first))
 
-    Candidates are the forms that have won a measured round on some BASELINE config (DESIGN §4
-    "Plan forms and their selection"): the sparse form at every tile width and LDS budget whose
-    staging stays within 1.25 x the fewest staged sources of any candidate (multi-group plans
-    that re-read sources - config 3's 80 KiB c4 = 128 plan stages 3.7x - never won), the
-    broadcast forms, and the clique plan.  Dense row blocks, the streamed form and the
-    register-resident groups lost every measured A/B outside their probes (BENCH_r04: 5.9, 7.0
-    and 8.5-16 ms against 2.0 ms on config 3) and are built only on request (plan_from_spec).
 
-    Each candidate runs `reps` times, interleaved rep by rep with the others, and is judged by
-    its median.  A candidate replaces the default only when its median beats the default's by
-    more than `margin` (round 4: the tuner's single short timings once kept a plan slower than
-    the default - 23.74 vs 22.89 ms).  pool_out must not alias pool_in."""
-    if pool_in.data_ptr() == pool_out.data_ptr():
-        raise ValueError("tune_plan needs distinct input / output pools")
-    bf16 = pool_in.dtype == torch.bfloat16  # bf16 rounds: sparse and narrow plans only
-    run = round_bf16 if bf16 else round_f32
+def tune_candidates(row_ptr, col, w, out_row, bf16: bool = False, mode: int = MODE_EXACT):
+    """tune_plan's candidates [(key, plan)], the default plan first (host-side plans)."""
     base = default_plan(row_ptr, col, w, out_row, bf16=bf16, mode=mode)
     if base.spec is None:
         base.spec = {}
@@ -760,20 +756,48 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
             key = (p.info.c4, p.info.n_groups, p.info.total_src, p.info.max_src)
             if p.staged_rows() <= 1.25 * fewest and all(key != k for k, _ in cands) and p.spec != base.spec:
                 cands.append((key, p))
-    for c4 in BCAST_WIDTHS:  # the broadcast form of the narrow kernel
-        for waves, wg in BCAST_FORMS:
-            try:
-                p = build_plan(row_ptr, col, w, out_row, c4=c4, lds_bytes=LDS_BUDGETS[-1], bcast=waves, bcast_wg=wg)
-            except _lib.TalError:
-                continue
-            key = ("bcast", c4, waves, wg)
-            if all(key != k for k, _ in cands) and p.spec != base.spec:
-                cands.append((key, p))
+    for c4, waves, wg in (BCAST_CANDIDATES if not rows_uniform(row_ptr, w) else ()):
+        try:
+            p = build_plan(row_ptr, col, w, out_row, c4=c4, lds_bytes=LDS_BUDGETS[-1], bcast=waves, bcast_wg=wg)
+        except _lib.TalError:
+            continue
+        key = ("bcast", c4, waves, wg)
+        if all(key != k for k, _ in cands) and p.spec != base.spec:
+            cands.append((key, p))
     if not bf16 and not isinstance(base, CliquePlan):
         cp = build_clique_plan(row_ptr, col, w, out_row)
         if cp is not None:
             cp.spec = dict(clique=1, rest=cp.rest.spec if cp.rest is not None else None)
             cands.append((("clique",), cp))
+    return cands
+
+
+def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.Tensor,
+              n: Optional[int] = None, reps: int = 5, mode: int = MODE_EXACT,
+              margin: float = 0.01) -> RoundPlan:
+    """Pick the plan by measurement, anchored on the untimed default (default_plan).
+
+    Candidates are the forms that have won a measured round on some BASELINE config (DESIGN §4
+    "Plan forms and their selection"): the sparse form at every tile width and LDS budget whose
+    staging stays within 1.25 x the fewest staged sources of any candidate (multi-group plans
+    that re-read sources - config 3's 80 KiB c4 = 128 plan stages 3.7x - never won), the
+    broadcast forms that won (BCAST_CANDIDATES) on rounds with per-operand weights, and the
+    clique plan (tune_candidates).  Dense row blocks, the streamed form and the
+    register-resident groups lost every measured A/B outside their probes (BENCH_r04: 5.9, 7.0
+    and 8.5-16 ms against 2.0 ms on config 3) and are built only on request (plan_from_spec).
+
+    Each candidate runs `reps` times, interleaved rep by rep with the others, and is judged by
+    its median; one slower than TUNE_DROP x the default on its first timed run is not timed
+    again (its median comes from that run).  A candidate replaces the default only when its
+    median beats the default's by more than `margin` (round 4: the tuner's single short timings
+    once kept a plan slower than the default - 23.74 vs 22.89 ms).  pool_out must not alias
+    pool_in."""
+    if pool_in.data_ptr() == pool_out.data_ptr():
+        raise ValueError("tune_plan needs distinct input / output pools")
+    bf16 = pool_in.dtype == torch.bfloat16  # bf16 rounds: sparse and narrow plans only
+    run = round_bf16 if bf16 else round_f32
+    cands = tune_candidates(row_ptr, col, w, out_row, bf16=bf16, mode=mode)
+    base = cands[0][1]
     if isinstance(base, CliquePlan) and base.rest is not None:  # the rows outside the cliques: tuned too
         r_rp, r_col, r_w, r_out = _sub_csr(row_ptr, col, w, out_row, base.rest_rows)
         base.rest = tune_plan(r_rp, r_col, r_w, r_out, pool_in, pool_out, n=n, reps=reps, mode=mode, margin=margin)
@@ -787,13 +811,16 @@ def tune_plan(row_ptr, col, w, out_row, pool_in: torch.Tensor, pool_out: torch.T
     # candidates interleaved rep by rep, so a clock or thermal drift during tuning does not
     # favour the ones timed first
     ts = [[] for _ in cands]
-    for _ in range(reps):
-        for k, (_, p) in enumerate(cands):
+    live = list(range(len(cands)))
+    for rep in range(reps):
+        for k in live:
             s.record()
-            run(pool_in, pool_out, p, n=n, mode=mode)
+            run(pool_in, pool_out, cands[k][1], n=n, mode=mode)
             e.record()
             e.synchronize()
             ts[k].append(s.elapsed_time(e))
+        if rep == 0:  # far slower than the default on its first timed run: not timed again
+            live = [k for k in live if k == 0 or ts[k][0] <= TUNE_DROP * ts[0][0]]
     med = [float(np.median(tk)) for tk in ts]
     timings = [{"form": "/".join(map(str, key)), "ms": round(t, 4), "all_ms": [round(x, 4) for x in tk], "spec": p.spec}
                for (key, p), t, tk in zip(cands, med, ts)]

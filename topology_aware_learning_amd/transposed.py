@@ -120,12 +120,14 @@ HBM_GBPS = 8000.0       # MI355X HBM3E peak per GPU (MI355X_MICROARCH.md)
 XGMI_LINK_GBPS = 153.0  # one xGMI link per GPU pair, one direction (7 links per GPU)
 
 
-def link_model(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: int = 0) -> dict:
+def link_model(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: int = 0,
+               link_gbps: float = XGMI_LINK_GBPS) -> dict:
     """DESIGN §6's bound per exchange kind, for rank-level reporting next to a measured round:
     local HBM bytes of the busiest rank (halo: its staged sources - own and received - read once
     plus its own rows written; transpose: the round over every model's column block plus the
     packing and unpacking of its own models), the busiest directed GPU pair's bytes, each over
-    its peak (HBM 8 TB/s, one xGMI link 153 GB/s), predicted_ms = the larger, and which binds."""
+    its rate (HBM 8 TB/s; one GPU pair's link: `link_gbps`, the assumed 153 GB/s unless a run
+    measured it - bench.py's link probe), predicted_ms = the larger, and which binds."""
     owner = np.asarray(owner)
     row = 4 * n_f32 + 2 * n_b16 + 8 * n_i64
     specs = [build_shard(orders, [[1.0] * len(o) for o in orders], owner, r, world) for r in range(world)]
@@ -142,22 +144,46 @@ def link_model(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: int = 0
     for kind in ("halo", "transpose"):
         pair = vol[kind + "_link"]
         hbm_ms = local[kind] / (HBM_GBPS * 1e6)
-        link_ms = pair / (XGMI_LINK_GBPS * 1e6)
+        link_ms = pair / (link_gbps * 1e6)
         out[kind] = dict(local_bytes=int(local[kind]), busiest_pair_bytes=int(pair), rank_link_bytes=int(vol[kind]),
                          hbm_ms=hbm_ms, link_ms=link_ms, predicted_ms=max(hbm_ms, link_ms),
                          binds="xgmi" if link_ms > hbm_ms else "hbm")
     return out
 
 
-def choose_exchange(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: int = 0) -> str:
-    """'transpose' when its busiest link carries clearly fewer bytes than the halo's busiest
-    link (random expanders at 4+ ranks, 60-cliques spread over 4 GPUs), else 'halo' (rings,
-    community graphs, 2 ranks).  Both exchanges use the pairs' xGMI links concurrently, so the
-    round's link time is set by the busiest pair, not by a rank's total."""
+def choose_exchange(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: int = 0,
+                    link_gbps: Optional[float] = None) -> str:
+    """'transpose' when it is clearly (10 %) cheaper than the halo, else 'halo'.  Without a
+    measured link rate: by the busiest link's bytes (random expanders at 4+ ranks, 60-cliques
+    spread over 4 GPUs go to the transpose; rings, community graphs, 2 ranks to the halo) - both
+    exchanges use the pairs' links concurrently, so the busiest pair sets the link time.  With
+    one (`link_gbps`, bench.py's probe): by link_model's predicted time, max(HBM, busiest pair /
+    link_gbps), so a fast link hands the choice to the local bytes, which favour the halo (the
+    transpose packs and unpacks every own model and reduces every model's column block)."""
     if world < 2:
         return "halo"
-    b = exchange_bytes(orders, owner, world, n_f32, n_i64, n_b16)
-    return "transpose" if b["transpose_link"] < 0.9 * b["halo_link"] else "halo"
+    if link_gbps is None:
+        b = exchange_bytes(orders, owner, world, n_f32, n_i64, n_b16)
+        return "transpose" if b["transpose_link"] < 0.9 * b["halo_link"] else "halo"
+    m = link_model(orders, owner, world, n_f32, n_i64, n_b16, link_gbps=link_gbps)
+    return "transpose" if m["transpose"]["predicted_ms"] < 0.9 * m["halo"]["predicted_ms"] else "halo"
+
+
+def exchange_crossover_gbps(orders, owner, world: int, n_f32: int, n_i64: int, n_b16: int = 0) -> Optional[float]:
+    """The link rate above which choose_exchange(link_gbps=...) stops picking the transpose
+    (None when it never picks it, or picks it at any rate): the smallest r with
+    max(hbm_t, Lt / r) >= 0.9 max(hbm_h, Lh / r)."""
+    m = link_model(orders, owner, world, n_f32, n_i64, n_b16, link_gbps=1.0)
+    ht, hh = m["transpose"]["hbm_ms"], m["halo"]["hbm_ms"]
+    lt, lh = m["transpose"]["link_ms"], m["halo"]["link_ms"]  # ms at 1 GB/s: bytes / 1e6
+    lo, hi = 1e-3, 1e7
+    pick = lambda r: max(ht, lt / r) < 0.9 * max(hh, lh / r)  # noqa: E731
+    if not pick(lo) or pick(hi):
+        return None
+    for _ in range(200):  # monotone in r: transpose at low rates, halo at high ones
+        mid = (lo * hi) ** 0.5
+        lo, hi = (mid, hi) if pick(mid) else (lo, mid)
+    return hi
 
 
 @dataclass
@@ -449,15 +475,16 @@ class TransposedRound:
 
 def make_round(layout: StateLayout, orders, weights, rank: int, world: int, device, exchange: str = "auto",
                mode: int = ops.MODE_EXACT, owner: Optional[np.ndarray] = None, group=None, tune: bool = False,
-               transport: str = "device"):
+               transport: str = "device", link_gbps: Optional[float] = None):
     """This rank's sharded round with the given exchange ('halo' | 'transpose' | 'auto');
     transport 'device' = torch.distributed's RCCL, 'host' stages the exchange through host
     memory (gloo rehearsal runs only), 'cabi' moves either exchange through the library's own
     RCCL communicator (tal_comm_* / tal_halo_pack / tal_halo_exchange: per-peer messages in one
-    RCCL group; an all-to-all is such a group)."""
+    RCCL group; an all-to-all is such a group).  link_gbps: a measured per-pair link rate for
+    the 'auto' choice (choose_exchange)."""
     owner = partition_contiguous(len(orders), world) if owner is None else np.asarray(owner, np.int32)
     if exchange == "auto":
-        exchange = choose_exchange(orders, owner, world, layout.n_f32, layout.n_i64, layout.n_b16)
+        exchange = choose_exchange(orders, owner, world, layout.n_f32, layout.n_i64, layout.n_b16, link_gbps=link_gbps)
     cls = {"halo": ShardedRound, "transpose": TransposedRound}[exchange]
     r = cls(layout, orders, weights, rank, world, device, mode=mode, owner=owner, group=group, tune=tune,
             transport=transport)
