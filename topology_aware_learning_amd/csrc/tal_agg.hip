@@ -2920,10 +2920,12 @@ constexpr int64_t cos_chunk_outputs(int kind) { return kind == kCosRow ? kCosBlo
 // runs (independent: each starts from 0), then each output's cascade / lane fold.  The direct
 // form (one thread or 8 lanes per output, loads strided by B or 8 lanes 32 B wide) was bound by
 // the strided gather (37.7 L1 accesses per load instruction, profiles/r05/r05k2pmc).
-constexpr int kCosStageFloats = 4736;  // per model (18.5 KiB): one ResNet-50 512 x 512 x 3 x 3 slab, padded
-constexpr int kCosStageOut = 256;      // outputs per staged chunk
-constexpr int kCosStageRows = 32;      // row-kind rows per staged chunk (lane accumulators in LDS)
-constexpr int kCosStageItems = 1024;   // level-0 runs per staged chunk
+// LDS: 2 x 18 KiB of slabs + 4 KiB of norms, reciprocals, lane and run sums = 40 KiB: four
+// workgroups per CU
+constexpr int kCosStageFloats = 4608;  // per model (18 KiB): one ResNet-50 512 x 512 x 3 x 3 slab
+constexpr int kCosStageOut = 128;      // outputs per staged chunk
+constexpr int kCosStageRows = 16;      // row-kind rows per staged chunk (lane accumulators in LDS)
+constexpr int kCosStageItems = 512;    // level-0 runs per staged chunk
 constexpr int kCosStageBlock = 256;
 
 __host__ __device__ inline int64_t cos_log2_ceil(int64_t x) {
@@ -2958,13 +2960,14 @@ __host__ __device__ inline void cos_stage_seq(int kind, int64_t I, int64_t* nl, 
   }
 }
 
-// LDS pitch of one staged column sequence (column kind, stored transposed: x[o, :, k] contiguous):
-// I rounded up to 4 floats (16-B aligned reads) + 4 (consecutive columns 4 banks apart)
-__host__ __device__ inline int64_t cos_col_pitch(int64_t I) { return (I + 3) / 4 * 4 + 4; }
+// LDS pitch of a staged row (row kind): I padded to 8 (mod 64) floats, so the 8 rows a wave's
+// lanes read at once (8 lanes each: torch's vector lanes) sit on 8 different bank octets
+__host__ __device__ inline int64_t cos_row_pitch(int64_t I) { return I + (72 - I % 64) % 64; }
 
-// LDS floats of one slab (column kind: B transposed sequences; row kind: the row as it is)
+// LDS floats of one slab: the column kind's [I, B] block as it is in memory (a sequence x[o, :, k]
+// is strided by B; consecutive outputs' chains read consecutive words), a row at its pitch
 __host__ __device__ inline int64_t cos_slab_floats(int kind, int64_t I, int64_t B) {
-  return kind == kCosCol ? B * cos_col_pitch(I) : I;
+  return kind == kCosCol ? I * B : cos_row_pitch(I);
 }
 
 // slabs (output blocks: B outputs of the column kind, one row of the row kind) per staged chunk;
@@ -3218,9 +3221,12 @@ __device__ __forceinline__ float cos_cascade_runs(Runs R, int si) {
   const int full = si / step;
   float a1 = 0.f, a2 = 0.f, a3 = 0.f;
   int i = 0;
+  float nxt = full > 0 ? R(0) : 0.f;  // each run's sum read one iteration ahead
   for (int r = 0; r < full; ++r) {
+    const float cur = nxt;
+    if (r + 1 < full) nxt = R(r + 1);
     i += step;
-    a1 = __fadd_rn(a1, R(r));
+    a1 = __fadd_rn(a1, cur);
     if (i & (mask0 << lp)) continue;
     a2 = __fadd_rn(a2, a1);
     a1 = 0.f;
@@ -3242,75 +3248,81 @@ __device__ __forceinline__ int cos_divmod(int e, int d, float inv_d, int* rem) {
   return q;
 }
 
-// The chunk's ne floats from g into LDS by 16-B loads from g's 16-B aligned base (a 16-B chunk
-// holding one element of the range lies in that element's page); NT: non-temporal (read once).
-// Column kind (COL): element (slab o, i, column k) of the [G, I, B] block goes to
-// lds[(o B + k) P + i] - each output's sequence contiguous, P = cos_col_pitch(I).
-template <bool NT, bool COL>
-__device__ __forceinline__ void cos_stage(const float* g, int ne, float* lds, int I, int B, int P) {
-  const int mis = static_cast<int>((reinterpret_cast<uintptr_t>(g) >> 2) & 3);
-  const v4f* g4 = reinterpret_cast<const v4f*>(g - mis);
-  const int n4 = (ne + mis + 3) / 4;
-  const int ib = I * B;
-  const float inv_ib = 1.f / static_cast<float>(ib), inv_b = 1.f / static_cast<float>(B);
+// The chunk's ne floats of both models (ga: the aggregating model, default cache policy - every
+// pair re-reads it; gb: non-temporal, read once) into LDS (model 1 at kCosStageFloats) by 16-B
+// loads from each pointer's 16-B aligned base (a 16-B chunk holding one element of the range lies
+// in that element's page), every load of a batch in flight before the first LDS write.  The
+// column kind keeps the memory layout; a row (ROW) goes to lds[g Pr + i], Pr = cos_row_pitch(I)
+// (the row and column of a chunk's first element found once, the other three stepped).
+template <bool ROW>
+__device__ __forceinline__ void cos_stage(const float* ga, const float* gb, int ne, float* lds, int I, int Pr) {
+  const int mis_a = static_cast<int>((reinterpret_cast<uintptr_t>(ga) >> 2) & 3);
+  const int mis_b = static_cast<int>((reinterpret_cast<uintptr_t>(gb) >> 2) & 3);
+  const v4f* a4 = reinterpret_cast<const v4f*>(ga - mis_a);
+  const v4f* b4 = reinterpret_cast<const v4f*>(gb - mis_b);
+  const int na4 = (ne + mis_a + 3) / 4, nb4 = (ne + mis_b + 3) / 4;
+  const int n4 = na4 > nb4 ? na4 : nb4;
+  const float inv_i = 1.f / static_cast<float>(I);
   constexpr int kU = (kCosStageFloats / 4 + kCosStageBlock - 1) / kCosStageBlock + 1;  // 6
+  auto put = [&](const v4f& t, int v, int mis, float* dst0) {
+    const int e = 4 * v - mis;  // element of t[0]
+    const int e0 = e < 0 ? 0 : e;
+    int c = e0, g = 0;
+    if constexpr (ROW) g = cos_divmod(e0, I, inv_i, &c);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int ek = e + k;
+      if (ek < e0 || ek >= ne) continue;
+      if constexpr (ROW) {
+        dst0[g * Pr + c] = t[k];
+        if (++c == I) {
+          c = 0;
+          ++g;
+        }
+      } else {
+        dst0[ek] = t[k];
+      }
+    }
+  };
   for (int v0 = threadIdx.x; v0 < n4; v0 += kU * kCosStageBlock) {
-    v4f t[kU];
+    v4f ta[kU], tb[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int v = v0 + u * kCosStageBlock;
-      if (v < n4) t[u] = NT ? __builtin_nontemporal_load(g4 + v) : g4[v];
+      if (v < na4) ta[u] = a4[v];
+      if (v < nb4) tb[u] = __builtin_nontemporal_load(b4 + v);
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int v = v0 + u * kCosStageBlock;
-      if (v >= n4) continue;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int e = 4 * v - mis + k;
-        if (e < 0 || e >= ne) continue;
-        int dst = e;
-        if constexpr (COL) {
-          int rem, col;
-          const int o = cos_divmod(e, ib, inv_ib, &rem);
-          const int i = cos_divmod(rem, B, inv_b, &col);
-          dst = (o * B + col) * P + i;
-        }
-        lds[dst] = t[u][k];
-      }
+      if (v < na4) put(ta[u], v, mis_a, lds);
+      if (v < nb4) put(tb[u], v, mis_b, lds + kCosStageFloats);
     }
   }
 }
 
 // torch NormTwoOps over x[0], x[S], x[2 S], ... (n elements): fma in index order; the reads a
-// batch ahead of the FMAs (S = 1: 16-B reads of a 16-B aligned sequence)
+// batch ahead of the FMAs.  S > 0: compile-time stride (immediate LDS offsets); S == 0: `rs`
 template <int S>
-__device__ __forceinline__ float cos_norm_chain(const float* x, int n) {
+__device__ __forceinline__ float cos_norm_chain(const float* x, int n, int rs = 0) {
   constexpr int kB = 16;
+  const int st = S > 0 ? S : rs;
   float acc = 0.f;
   float cur[kB], nxt[kB];
   const int nb = n / kB;
   auto load = [&](float* v, const float* p) {
-    if constexpr (S == 1) {
 #pragma unroll
-      for (int u = 0; u < kB; u += 4) {
-        const v4f q = *reinterpret_cast<const v4f*>(p + u);
-        v[u] = q.x; v[u + 1] = q.y; v[u + 2] = q.z; v[u + 3] = q.w;
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < kB; ++u) v[u] = p[u * S];
-    }
+    for (int u = 0; u < kB; ++u) v[u] = p[u * st];
   };
   if (nb > 0) load(cur, x);
   for (int b = 0; b < nb; ++b) {
-    if (b + 1 < nb) load(nxt, x + (b + 1) * kB * S);
+    if (b + 1 < nb) load(nxt, x + (b + 1) * kB * st);
 #pragma unroll
     for (int u = 0; u < kB; ++u) acc = __fmaf_rn(cur[u], cur[u], acc);
 #pragma unroll
     for (int u = 0; u < kB; ++u) cur[u] = nxt[u];
   }
-  for (int i = nb * kB; i < n; ++i) acc = __fmaf_rn(x[i * S], x[i * S], acc);
+  for (int i = nb * kB; i < n; ++i) acc = __fmaf_rn(x[i * st], x[i * st], acc);
   return acc;
 }
 
@@ -3319,71 +3331,91 @@ __device__ __forceinline__ float cos_prod(const float* x, float na, float nb) {
   return __fmul_rn(__fdiv_rn(x[0], na), __fdiv_rn(x[kCosStageFloats], nb));
 }
 
-// One level-0 run: elements 0, ST, 2 ST, ... (n of them) from 0 in order, products a batch ahead
-template <int ST>
-__device__ __forceinline__ float cos_run(const float* x, int n, float na, float nb) {
+// x / n with the IEEE division's result, without its scaling steps (each writes VCC, which the
+// next division's v_div_fmas reads, so divisions serialise): y = RN(1 / n) once per norm, then
+// q0 = RN(x y) and q = RN(q0 + RN(x - n q0) y) (both fused).  Equal to RN(x / n) for n in
+// [2^-40, 2^40] and |x| in [2^-50, 2^60) (every intermediate is normal, so the result depends
+// only on the two mantissas: all 2^46 pairs checked on the GPU, tools/div_exhaustive.hip,
+// profiles/r05/r05div); callers take __fdiv_rn outside it.
+__device__ __forceinline__ float cos_rdiv(float x, float n, float y) {
+  const float q0 = __fmul_rn(x, y);
+  return __fmaf_rn(__fmaf_rn(-n, q0, x), y, q0);
+}
+__device__ __forceinline__ bool cos_rdiv_x(float x) {  // |x| in [2^-50, 2^60)
+  return (__float_as_uint(x) & 0x7fffffffu) - 0x26800000u < 0x37000000u;
+}
+__device__ __forceinline__ bool cos_rdiv_n(float n) {  // n in [2^-40, 2^40]
+  return __float_as_uint(n) - 0x2B800000u <= 0x28000000u;
+}
+
+// One level-0 run: elements 0, S, 2 S, ... (n of them; S == 0: stride rs) summed from 0 in order,
+// products a batch ahead.  FAST (both norms in cos_rdiv's range): the reciprocal division, a
+// batch falling back to __fdiv_rn on the lanes holding an element outside its range.
+template <int S, bool FAST>
+__device__ __forceinline__ float cos_run(const float* x, int n, float na, float nb, float ya, float yb, int rs = 0) {
+  const int st = S > 0 ? S : rs;
   float acc = 0.f;
   int i = 0;
-  for (; i + 8 <= n; i += 8, x += 8 * ST) {
+  for (; i + 8 <= n; i += 8, x += 8 * st) {
     float p[8];
+    if constexpr (FAST) {
+      bool ok = true;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) p[u] = cos_prod(x + u * ST, na, nb);
+      for (int u = 0; u < 8; ++u) {
+        const float xa = x[u * st], xb = x[u * st + kCosStageFloats];
+        ok = ok && cos_rdiv_x(xa) && cos_rdiv_x(xb);
+        p[u] = __fmul_rn(cos_rdiv(xa, na, ya), cos_rdiv(xb, nb, yb));
+      }
+      if (!ok) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) p[u] = cos_prod(x + u * st, na, nb);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) p[u] = cos_prod(x + u * st, na, nb);
+    }
 #pragma unroll
     for (int u = 0; u < 8; ++u) acc = __fadd_rn(acc, p[u]);
   }
-  for (; i < n; ++i, x += ST) acc = __fadd_rn(acc, cos_prod(x, na, nb));
+  for (; i < n; ++i, x += st) acc = __fadd_rn(acc, cos_prod(x, na, nb));
   return acc;
 }
 
-// One workgroup per (staged chunk, pair): the chunk's slabs of a and b in LDS, then the
-// outputs' norms, level-0 runs and sums in torch's order (k_cosine_outputs' arithmetic, the
-// independent parts spread over the workgroup's lanes).  LDS indices are 32-bit and every
-// chain walks a pointer with a compile-time stride.
-__global__ __launch_bounds__(kCosStageBlock) void k_cosine_staged(CosPairs pr, const int64_t* __restrict__ plan,
-                                                                 int n_seg, int cnt, float* __restrict__ s_all) {
-  __shared__ __attribute__((aligned(16))) float sx[2 * kCosStageFloats];
-  __shared__ float sn[2][kCosStageOut];             // per output (row kind: per row) norms of a, b
-  __shared__ float sl[2 * kCosVw * kCosStageRows];  // row kind: lane accumulators, then lane sums
-  __shared__ float sr[kCosStageItems];              // level-0 run sums
-  // XCD-aware order: dispatch deals workgroups round-robin over the 8 XCDs, so the pairs of one
-  // chunk (index 8 k + x) run one after another on XCD x, and every pair after the first finds
-  // the aggregating model's slab (each pair's `a`) in that XCD's L2
-  const int L = blockIdx.x;
-  const int kq = L >> 3;
-  const int pair = kq % cnt;
-  const int64_t c = static_cast<int64_t>(kq / cnt) * 8 + (L & 7);
-  if (c >= plan[3]) return;
-  const int64_t* ch = plan + kCosHdr + kCosSegWords * static_cast<int64_t>(n_seg) + kCosChunkWords * c;
-  const int64_t* sg = plan + kCosHdr + kCosSegWords * ch[0];
-  const int64_t first = ch[1];
-  const int nq = static_cast<int>(ch[2]);
-  const int I = static_cast<int>(sg[2]), B = static_cast<int>(sg[3]);
-  const bool col = sg[5] == kCosCol;
-  const int P = col ? static_cast<int>(cos_col_pitch(I)) : I;  // LDS floats per sequence / row
+template <int S>
+__device__ __forceinline__ float cos_run_any(const float* x, int n, float na, float nb, float ya, float yb, int rs) {
+  if (cos_rdiv_n(na) && cos_rdiv_n(nb)) return cos_run<S, true>(x, n, na, nb, ya, yb, rs);
+  return cos_run<S, false>(x, n, na, nb, ya, yb, rs);
+}
+
+// A staged chunk's arithmetic after its slabs are in LDS (sx: model a, model b at +
+// kCosStageFloats).  Column kind (ROW false): output q = o B + k is the sequence x[o I B + k + i B],
+// i < I (CB: B at compile time, 0: runtime); row kind: row q at q Pr, torch's 8 lanes (I >= 8) or
+// one sequence.  Norms, then the level-0 runs, then each sequence's cascades and the lane fold -
+// cos_row_sum / cos_multi_row's operations in their order.
+template <bool ROW, int CB>
+__device__ __forceinline__ void cos_staged_body(const float* sx, float (*sn)[kCosStageOut], float (*sy)[kCosStageOut],
+                                                float* sl, float* sr, int nq, int I, int Bq, int Pr, float* s) {
   const int tid = threadIdx.x;
-  // column kind: first = o0 * B, nq = G * B -> elements o0 I B .. (o0 + G) I B; row kind:
-  // first = o0, nq = G -> o0 I .. (o0 + G) I: both first * I, nq * I
-  const float* ga = pr.a[pair] + sg[0] + first * I;
-  const float* gb = pr.b[pair] + sg[0] + first * I;
-  if (col) {
-    cos_stage<false, true>(ga, nq * I, sx, I, B, P);
-    cos_stage<true, true>(gb, nq * I, sx + kCosStageFloats, I, B, P);
-  } else {
-    cos_stage<false, false>(ga, nq * I, sx, I, B, P);
-    cos_stage<true, false>(gb, nq * I, sx + kCosStageFloats, I, B, P);
-  }
-  __syncthreads();
-  if (col) {  // chains (model, output): the output's contiguous sequence
+  const int B = CB > 0 ? CB : Bq;
+  const float inv_b = 1.f / static_cast<float>(B);
+  auto col_base = [&](int q) {  // o I B + k
+    int k;
+    const int o = cos_divmod(q, B, inv_b, &k);
+    return o * I * B + k;
+  };
+  if constexpr (!ROW) {  // chains (model, output), strided by B; consecutive lanes, consecutive words
     for (int j = tid; j < 2 * nq; j += kCosStageBlock) {
       const int m = j >= nq;
       const int q = j - m * nq;
-      sn[m][q] = cos_clamp(cos_sqrt_rn(cos_norm_chain<1>(sx + m * kCosStageFloats + q * P, I)));
+      const float nrm = cos_clamp(cos_sqrt_rn(cos_norm_chain<CB>(sx + m * kCosStageFloats + col_base(q), I, B)));
+      sn[m][q] = nrm;
+      sy[m][q] = __fdiv_rn(1.f, nrm);
     }
   } else {  // torch's reduce-lastdim norm: 8 lane accumulators over whole vectors, then the fold
     const int nv = I / kCosVw;
     for (int j = tid; j < 2 * nq * kCosVw; j += kCosStageBlock) {
       const int m = j / (nq * kCosVw), r = j - m * nq * kCosVw;
-      sl[j] = cos_norm_chain<kCosVw>(sx + m * kCosStageFloats + (r >> 3) * I + (r & 7), nv);
+      sl[j] = cos_norm_chain<kCosVw>(sx + m * kCosStageFloats + (r >> 3) * Pr + (r & 7), nv);
     }
     __syncthreads();
     for (int j = tid; j < 2 * nq; j += kCosStageBlock) {
@@ -3392,24 +3424,25 @@ __global__ __launch_bounds__(kCosStageBlock) void k_cosine_staged(CosPairs pr, c
       float t = la[0];
 #pragma unroll
       for (int l = 1; l < kCosVw; ++l) t = __fadd_rn(t, la[l]);
-      const float* x = sx + m * kCosStageFloats + g * I;
+      const float* x = sx + m * kCosStageFloats + g * Pr;
       int d = nv * kCosVw;
       const int sep = (I - d) / 4 * 4;  // the tail: groups of 4 as square-then-add, the rest fused
       for (int e = 0; e < sep; ++e, ++d) t = __fadd_rn(t, __fmul_rn(x[d], x[d]));
       for (; d < I; ++d) t = __fmaf_rn(x[d], x[d], t);
-      sn[m][g] = cos_clamp(cos_sqrt_rn(t));
+      const float nrm = cos_clamp(cos_sqrt_rn(t));
+      sn[m][g] = nrm;
+      sy[m][g] = __fdiv_rn(1.f, nrm);
     }
   }
   __syncthreads();
-  // each output's row_sum sequences: nl lanes of len elements; in LDS sequence (q, l) starts at
-  // q P (column) / q I + l (row) with element stride es
-  const int nl = (!col && I >= kCosVw) ? kCosVw : 1;
+  // each output's row_sum sequences: nl lanes of len elements, element stride es
+  const int nl = (ROW && I >= kCosVw) ? kCosVw : 1;
   const int len = nl > 1 ? I / kCosVw : I;
-  const int es = nl > 1 ? kCosVw : 1;
+  const int es = ROW ? nl : B;
   const int si = len / 4;
   const int step = 1 << static_cast<int>(cos_lp(si));
   const int nr = (si + step - 1) / step;
-  auto base_of = [&](int q, int l) { return col ? q * P : q * I + l; };
+  auto base_of = [&](int q, int l) { return ROW ? q * Pr + l : col_base(q); };
   // level-0 runs: item ((r * 4 + stream) * nq + q) * nl + l sums elements 4 i + stream of
   // sequence (q, l), i in [r step, (r + 1) step) (the last run partial), from 0 in order
   const int n_items = nq * nl * 4 * nr;
@@ -3421,12 +3454,18 @@ __global__ __launch_bounds__(kCosStageBlock) void k_cosine_staged(CosPairs pr, c
     const int st = t & 3, r = t >> 2;
     const int i0 = r * step, n = min(step, si - i0);
     const float* x = sx + base_of(q, l) + es * (4 * i0 + st);
-    sr[it] = es == 1 ? cos_run<4>(x, n, sn[0][q], sn[1][q]) : cos_run<4 * kCosVw>(x, n, sn[0][q], sn[1][q]);
+    const float na = sn[0][q], nb = sn[1][q], ya = sy[0][q], yb = sy[1][q];
+    float v;
+    if constexpr (ROW) {
+      v = nl > 1 ? cos_run_any<4 * kCosVw>(x, n, na, nb, ya, yb, 0) : cos_run_any<4>(x, n, na, nb, ya, yb, 0);
+    } else {
+      v = cos_run_any<4 * CB>(x, n, na, nb, ya, yb, 4 * B);
+    }
+    sr[it] = v;
   }
   __syncthreads();
   // per sequence: the four streams' cascades, the row_sum remainder into stream 0, the streams
   // in order (cos_row_sum); one lane: the output's sum; 8 lanes: their sums, folded below
-  float* s = s_all + static_cast<int64_t>(pair) * plan[1] + sg[4] + first;
   const int rstride = 4 * nq * nl;  // between a sequence's consecutive runs of one stream
   for (int j = tid; j < nq * nl; j += kCosStageBlock) {
     const int q = j / nl, l = j - q * nl;
@@ -3448,12 +3487,49 @@ __global__ __launch_bounds__(kCosStageBlock) void k_cosine_staged(CosPairs pr, c
     for (int q = tid; q < nq; q += kCosStageBlock) {
       const float na = sn[0][q], nb = sn[1][q];
       float fin = 0.f;
-      for (int k2 = len * kCosVw; k2 < I; ++k2) fin = __fadd_rn(fin, cos_prod(sx + q * I + k2, na, nb));
+      for (int k2 = len * kCosVw; k2 < I; ++k2) fin = __fadd_rn(fin, cos_prod(sx + q * Pr + k2, na, nb));
 #pragma unroll
       for (int l = 0; l < kCosVw; ++l) fin = __fadd_rn(fin, sl[q * kCosVw + l]);
       s[q] = __fadd_rn(0.f, fin);
     }
   }
+}
+
+// One workgroup per (staged chunk, pair): the chunk's slabs of a and b in LDS by coalesced 16-B
+// loads, then cos_staged_body.  LDS indices are 32-bit and chains walk pointers.
+__global__ __launch_bounds__(kCosStageBlock) void k_cosine_staged(CosPairs pr, const int64_t* __restrict__ plan,
+                                                                 int n_seg, int cnt, float* __restrict__ s_all) {
+  __shared__ __attribute__((aligned(16))) float sx[2 * kCosStageFloats];
+  __shared__ float sn[2][kCosStageOut];             // per output (row kind: per row) norms of a, b
+  __shared__ float sy[2][kCosStageOut];             // their reciprocals RN(1 / n) (cos_rdiv)
+  __shared__ float sl[2 * kCosVw * kCosStageRows];  // row kind: lane accumulators, then lane sums
+  __shared__ float sr[kCosStageItems];              // level-0 run sums
+  // XCD-aware order: dispatch deals workgroups round-robin over the 8 XCDs, so the pairs of one
+  // chunk (index 8 k + x) run one after another on XCD x, and every pair after the first finds
+  // the aggregating model's slab (each pair's `a`) in that XCD's L2
+  const int L = blockIdx.x;
+  const int kq = L >> 3;
+  const int pair = kq % cnt;
+  const int64_t c = static_cast<int64_t>(kq / cnt) * 8 + (L & 7);
+  if (c >= plan[3]) return;
+  const int64_t* ch = plan + kCosHdr + kCosSegWords * static_cast<int64_t>(n_seg) + kCosChunkWords * c;
+  const int64_t* sg = plan + kCosHdr + kCosSegWords * ch[0];
+  const int64_t first = ch[1];
+  const int nq = static_cast<int>(ch[2]);
+  const int I = static_cast<int>(sg[2]), B = static_cast<int>(sg[3]);
+  const bool row = sg[5] == kCosRow;
+  const int Pr = static_cast<int>(cos_row_pitch(I));
+  // column kind: first = o0 * B, nq = G * B -> elements o0 I B .. (o0 + G) I B; row kind:
+  // first = o0, nq = G -> o0 I .. (o0 + G) I: both first * I, nq * I
+  const float* ga = pr.a[pair] + sg[0] + first * I;
+  const float* gb = pr.b[pair] + sg[0] + first * I;
+  if (row) cos_stage<true>(ga, gb, nq * I, sx, I, Pr);
+  else cos_stage<false>(ga, gb, nq * I, sx, I, Pr);
+  __syncthreads();
+  float* s = s_all + static_cast<int64_t>(pair) * plan[1] + sg[4] + first;
+  if (row) cos_staged_body<true, 0>(sx, sn, sy, sl, sr, nq, I, B, Pr, s);
+  else if (B == 9) cos_staged_body<false, 9>(sx, sn, sy, sl, sr, nq, I, B, Pr, s);  // 3 x 3 convolutions
+  else cos_staged_body<false, 0>(sx, sn, sy, sl, sr, nq, I, B, Pr, s);
 }
 
 // torch's serial full sum of s[0 .. n) (scalar_inner_sum below 8 elements, else
