@@ -2920,12 +2920,13 @@ constexpr int64_t cos_chunk_outputs(int kind) { return kind == kCosRow ? kCosBlo
 // runs (independent: each starts from 0), then each output's cascade / lane fold.  The direct
 // form (one thread or 8 lanes per output, loads strided by B or 8 lanes 32 B wide) was bound by
 // the strided gather (37.7 L1 accesses per load instruction, profiles/r05/r05k2pmc).
-// LDS: 2 x 18 KiB of slabs + 4 KiB of norms, reciprocals, lane and run sums = 40 KiB: four
-// workgroups per CU
+// A workgroup holds the aggregating model's slabs and those of kCosStagePairs neighbors: 4 x 18
+// KiB + 7.3 KiB of norms, reciprocals, lane and run sums < 80 KiB: two workgroups per CU
+constexpr int kCosStagePairs = 3;      // pairs per workgroup (the models: a, then each pair's b)
 constexpr int kCosStageFloats = 4608;  // per model (18 KiB): one ResNet-50 512 x 512 x 3 x 3 slab
-constexpr int kCosStageOut = 128;      // outputs per staged chunk
+constexpr int kCosStageOut = 64;       // outputs per staged chunk
 constexpr int kCosStageRows = 16;      // row-kind rows per staged chunk (lane accumulators in LDS)
-constexpr int kCosStageItems = 512;    // level-0 runs per staged chunk
+constexpr int kCosStageItems = 288;    // level-0 runs per staged chunk and pair
 constexpr int kCosStageBlock = 256;
 
 __host__ __device__ inline int64_t cos_log2_ceil(int64_t x) {
@@ -3248,24 +3249,28 @@ __device__ __forceinline__ int cos_divmod(int e, int d, float inv_d, int* rem) {
   return q;
 }
 
-// The chunk's ne floats of both models (ga: the aggregating model, default cache policy - every
-// pair re-reads it; gb: non-temporal, read once) into LDS (model 1 at kCosStageFloats) by 16-B
-// loads from each pointer's 16-B aligned base (a 16-B chunk holding one element of the range lies
-// in that element's page), every load of a batch in flight before the first LDS write.  The
-// column kind keeps the memory layout; a row (ROW) goes to lds[g Pr + i], Pr = cos_row_pitch(I)
-// (the row and column of a chunk's first element found once, the other three stepped).
+// The chunk's ne floats of nm models (model 0: the aggregating model, default cache policy - every
+// pair group re-reads it; the others non-temporal, read once) into LDS, model m at m
+// kCosStageFloats, by 16-B loads from each pointer's 16-B aligned base (a 16-B chunk holding one
+// element of the range lies in that element's page), every load of a batch in flight before the
+// first LDS write.  The column kind keeps the memory layout; a row (ROW) goes to lds[g Pr + i],
+// Pr = cos_row_pitch(I) (the row and column of a chunk's first element found once, then stepped).
 template <bool ROW>
-__device__ __forceinline__ void cos_stage(const float* ga, const float* gb, int ne, float* lds, int I, int Pr) {
-  const int mis_a = static_cast<int>((reinterpret_cast<uintptr_t>(ga) >> 2) & 3);
-  const int mis_b = static_cast<int>((reinterpret_cast<uintptr_t>(gb) >> 2) & 3);
-  const v4f* a4 = reinterpret_cast<const v4f*>(ga - mis_a);
-  const v4f* b4 = reinterpret_cast<const v4f*>(gb - mis_b);
-  const int na4 = (ne + mis_a + 3) / 4, nb4 = (ne + mis_b + 3) / 4;
-  const int n4 = na4 > nb4 ? na4 : nb4;
+__device__ __forceinline__ void cos_stage(const float* const* gm, int nm, int ne, float* lds, int I, int Pr) {
   const float inv_i = 1.f / static_cast<float>(I);
   constexpr int kU = (kCosStageFloats / 4 + kCosStageBlock - 1) / kCosStageBlock + 1;  // 6
-  auto put = [&](const v4f& t, int v, int mis, float* dst0) {
-    const int e = 4 * v - mis;  // element of t[0]
+  constexpr int kM = kCosStagePairs + 1;
+  int mis[kM], n4[kM];
+  const v4f* g4[kM];
+#pragma unroll
+  for (int m = 0; m < kM; ++m) {
+    const float* g = m < nm ? gm[m] : gm[0];
+    mis[m] = static_cast<int>((reinterpret_cast<uintptr_t>(g) >> 2) & 3);
+    g4[m] = reinterpret_cast<const v4f*>(g - mis[m]);
+    n4[m] = m < nm ? (ne + mis[m] + 3) / 4 : 0;
+  }
+  auto put = [&](const v4f& t, int v, int mis_, float* dst0) {
+    const int e = 4 * v - mis_;  // element of t[0]
     const int e0 = e < 0 ? 0 : e;
     int c = e0, g = 0;
     if constexpr (ROW) g = cos_divmod(e0, I, inv_i, &c);
@@ -3284,20 +3289,23 @@ __device__ __forceinline__ void cos_stage(const float* ga, const float* gb, int 
       }
     }
   };
-  for (int v0 = threadIdx.x; v0 < n4; v0 += kU * kCosStageBlock) {
-    v4f ta[kU], tb[kU];
+  const int nmax = (ne + 3 + 3) / 4;
+  for (int v0 = threadIdx.x; v0 < nmax; v0 += kU * kCosStageBlock) {
+    v4f t[kM][kU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int v = v0 + u * kCosStageBlock;
-      if (v < na4) ta[u] = a4[v];
-      if (v < nb4) tb[u] = __builtin_nontemporal_load(b4 + v);
-    }
+    for (int m = 0; m < kM; ++m)
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int v = v0 + u * kCosStageBlock;
-      if (v < na4) put(ta[u], v, mis_a, lds);
-      if (v < nb4) put(tb[u], v, mis_b, lds + kCosStageFloats);
-    }
+      for (int u = 0; u < kU; ++u) {
+        const int v = v0 + u * kCosStageBlock;
+        if (v < n4[m]) t[m][u] = m == 0 ? g4[m][v] : __builtin_nontemporal_load(g4[m] + v);
+      }
+#pragma unroll
+    for (int m = 0; m < kM; ++m)
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int v = v0 + u * kCosStageBlock;
+        if (v < n4[m]) put(t[m][u], v, mis[m], lds + m * kCosStageFloats);
+      }
   }
 }
 
@@ -3326,9 +3334,9 @@ __device__ __forceinline__ float cos_norm_chain(const float* x, int n, int rs = 
   return acc;
 }
 
-// ((x1 / na) * (x2 / nb)) for the two staged models (x2 = x1 + kCosStageFloats)
-__device__ __forceinline__ float cos_prod(const float* x, float na, float nb) {
-  return __fmul_rn(__fdiv_rn(x[0], na), __fdiv_rn(x[kCosStageFloats], nb));
+// ((x1 / na) * (x2 / nb)) for two staged models (x2 = x1 + ob: the pair's b)
+__device__ __forceinline__ float cos_prod(const float* x, int ob, float na, float nb) {
+  return __fmul_rn(__fdiv_rn(x[0], na), __fdiv_rn(x[ob], nb));
 }
 
 // x / n with the IEEE division's result, without its scaling steps (each writes VCC, which the
@@ -3352,50 +3360,55 @@ __device__ __forceinline__ bool cos_rdiv_n(float n) {  // n in [2^-40, 2^40]
 // products a batch ahead.  FAST (both norms in cos_rdiv's range): the reciprocal division, a
 // batch falling back to __fdiv_rn on the lanes holding an element outside its range.
 template <int S, bool FAST>
-__device__ __forceinline__ float cos_run(const float* x, int n, float na, float nb, float ya, float yb, int rs = 0) {
+__device__ __forceinline__ float cos_run(const float* x, int ob, int n, float na, float nb, float ya, float yb, int rs) {
   const int st = S > 0 ? S : rs;
+  const float* y = x + ob;
   float acc = 0.f;
   int i = 0;
-  for (; i + 8 <= n; i += 8, x += 8 * st) {
+  for (; i + 8 <= n; i += 8, x += 8 * st, y += 8 * st) {
     float p[8];
     if constexpr (FAST) {
       bool ok = true;
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const float xa = x[u * st], xb = x[u * st + kCosStageFloats];
+        const float xa = x[u * st], xb = y[u * st];
         ok = ok && cos_rdiv_x(xa) && cos_rdiv_x(xb);
         p[u] = __fmul_rn(cos_rdiv(xa, na, ya), cos_rdiv(xb, nb, yb));
       }
       if (!ok) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) p[u] = cos_prod(x + u * st, na, nb);
+        for (int u = 0; u < 8; ++u) p[u] = __fmul_rn(__fdiv_rn(x[u * st], na), __fdiv_rn(y[u * st], nb));
       }
     } else {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) p[u] = cos_prod(x + u * st, na, nb);
+      for (int u = 0; u < 8; ++u) p[u] = __fmul_rn(__fdiv_rn(x[u * st], na), __fdiv_rn(y[u * st], nb));
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) acc = __fadd_rn(acc, p[u]);
   }
-  for (; i < n; ++i, x += st) acc = __fadd_rn(acc, cos_prod(x, na, nb));
+  for (; i < n; ++i, x += st, y += st) acc = __fadd_rn(acc, __fmul_rn(__fdiv_rn(x[0], na), __fdiv_rn(y[0], nb)));
   return acc;
 }
 
 template <int S>
-__device__ __forceinline__ float cos_run_any(const float* x, int n, float na, float nb, float ya, float yb, int rs) {
-  if (cos_rdiv_n(na) && cos_rdiv_n(nb)) return cos_run<S, true>(x, n, na, nb, ya, yb, rs);
-  return cos_run<S, false>(x, n, na, nb, ya, yb, rs);
+__device__ __forceinline__ float cos_run_any(const float* x, int ob, int n, float na, float nb, float ya, float yb,
+                                             int rs) {
+  if (cos_rdiv_n(na) && cos_rdiv_n(nb)) return cos_run<S, true>(x, ob, n, na, nb, ya, yb, rs);
+  return cos_run<S, false>(x, ob, n, na, nb, ya, yb, rs);
 }
 
-// A staged chunk's arithmetic after its slabs are in LDS (sx: model a, model b at +
-// kCosStageFloats).  Column kind (ROW false): output q = o B + k is the sequence x[o I B + k + i B],
-// i < I (CB: B at compile time, 0: runtime); row kind: row q at q Pr, torch's 8 lanes (I >= 8) or
-// one sequence.  Norms, then the level-0 runs, then each sequence's cascades and the lane fold -
-// cos_row_sum / cos_multi_row's operations in their order.
+// A staged chunk's arithmetic after its slabs are in LDS (sx: model m at m kCosStageFloats;
+// model 0 = a, model p + 1 = pair p's b, np pairs).  Column kind (ROW false): output q = o B + k is
+// the sequence x[o I B + k + i B], i < I (CB: B at compile time, 0: runtime); row kind: row q at
+// q Pr, torch's 8 lanes (I >= 8) or one sequence.  Norms of every model, then every pair's level-0
+// runs, then each sequence's cascades and the lane fold - cos_row_sum / cos_multi_row's operations
+// in their order.  s: pair 0's outputs of the chunk; pair p's at s + p n_out.
 template <bool ROW, int CB>
 __device__ __forceinline__ void cos_staged_body(const float* sx, float (*sn)[kCosStageOut], float (*sy)[kCosStageOut],
-                                                float* sl, float* sr, int nq, int I, int Bq, int Pr, float* s) {
+                                                float* sl, float* sr, int np, int nq, int I, int Bq, int Pr, float* s,
+                                                int64_t n_out) {
   const int tid = threadIdx.x;
+  const int nm = np + 1;
   const int B = CB > 0 ? CB : Bq;
   const float inv_b = 1.f / static_cast<float>(B);
   auto col_base = [&](int q) {  // o I B + k
@@ -3404,21 +3417,20 @@ __device__ __forceinline__ void cos_staged_body(const float* sx, float (*sn)[kCo
     return o * I * B + k;
   };
   if constexpr (!ROW) {  // chains (model, output), strided by B; consecutive lanes, consecutive words
-    for (int j = tid; j < 2 * nq; j += kCosStageBlock) {
-      const int m = j >= nq;
-      const int q = j - m * nq;
+    for (int j = tid; j < nm * nq; j += kCosStageBlock) {
+      const int m = j / nq, q = j - m * nq;
       const float nrm = cos_clamp(cos_sqrt_rn(cos_norm_chain<CB>(sx + m * kCosStageFloats + col_base(q), I, B)));
       sn[m][q] = nrm;
       sy[m][q] = __fdiv_rn(1.f, nrm);
     }
   } else {  // torch's reduce-lastdim norm: 8 lane accumulators over whole vectors, then the fold
     const int nv = I / kCosVw;
-    for (int j = tid; j < 2 * nq * kCosVw; j += kCosStageBlock) {
+    for (int j = tid; j < nm * nq * kCosVw; j += kCosStageBlock) {
       const int m = j / (nq * kCosVw), r = j - m * nq * kCosVw;
       sl[j] = cos_norm_chain<kCosVw>(sx + m * kCosStageFloats + (r >> 3) * Pr + (r & 7), nv);
     }
     __syncthreads();
-    for (int j = tid; j < 2 * nq; j += kCosStageBlock) {
+    for (int j = tid; j < nm * nq; j += kCosStageBlock) {
       const int m = j / nq, g = j - m * nq;
       const float* la = sl + (m * nq + g) * kCosVw;
       float t = la[0];
@@ -3443,10 +3455,11 @@ __device__ __forceinline__ void cos_staged_body(const float* sx, float (*sn)[kCo
   const int step = 1 << static_cast<int>(cos_lp(si));
   const int nr = (si + step - 1) / step;
   auto base_of = [&](int q, int l) { return ROW ? q * Pr + l : col_base(q); };
-  // level-0 runs: item ((r * 4 + stream) * nq + q) * nl + l sums elements 4 i + stream of
-  // sequence (q, l), i in [r step, (r + 1) step) (the last run partial), from 0 in order
+  // level-0 runs: item ((r * 4 + stream) * nq + q) * nl + l of pair p sums elements 4 i + stream
+  // of sequence (q, l), i in [r step, (r + 1) step) (the last run partial), from 0 in order
   const int n_items = nq * nl * 4 * nr;
-  for (int it = tid; it < n_items; it += kCosStageBlock) {
+  for (int ia = tid; ia < np * n_items; ia += kCosStageBlock) {
+    const int p = ia / n_items, it = ia - p * n_items;
     const int l = it % nl;
     int t = it / nl;
     const int q = t % nq;
@@ -3454,64 +3467,74 @@ __device__ __forceinline__ void cos_staged_body(const float* sx, float (*sn)[kCo
     const int st = t & 3, r = t >> 2;
     const int i0 = r * step, n = min(step, si - i0);
     const float* x = sx + base_of(q, l) + es * (4 * i0 + st);
-    const float na = sn[0][q], nb = sn[1][q], ya = sy[0][q], yb = sy[1][q];
+    const int ob = (p + 1) * kCosStageFloats;
+    const float na = sn[0][q], nb = sn[p + 1][q], ya = sy[0][q], yb = sy[p + 1][q];
     float v;
     if constexpr (ROW) {
-      v = nl > 1 ? cos_run_any<4 * kCosVw>(x, n, na, nb, ya, yb, 0) : cos_run_any<4>(x, n, na, nb, ya, yb, 0);
+      v = nl > 1 ? cos_run_any<4 * kCosVw>(x, ob, n, na, nb, ya, yb, 0) : cos_run_any<4>(x, ob, n, na, nb, ya, yb, 0);
     } else {
-      v = cos_run_any<4 * CB>(x, n, na, nb, ya, yb, 4 * B);
+      v = cos_run_any<4 * CB>(x, ob, n, na, nb, ya, yb, 4 * B);
     }
-    sr[it] = v;
+    sr[ia] = v;
   }
   __syncthreads();
-  // per sequence: the four streams' cascades, the row_sum remainder into stream 0, the streams
-  // in order (cos_row_sum); one lane: the output's sum; 8 lanes: their sums, folded below
+  // per (pair, sequence): the four streams' cascades, the row_sum remainder into stream 0, the
+  // streams in order (cos_row_sum); one lane: the output's sum; 8 lanes: their sums, folded below
   const int rstride = 4 * nq * nl;  // between a sequence's consecutive runs of one stream
-  for (int j = tid; j < nq * nl; j += kCosStageBlock) {
+  for (int ja = tid; ja < np * nq * nl; ja += kCosStageBlock) {
+    const int p = ja / (nq * nl), j = ja - p * nq * nl;
     const int q = j / nl, l = j - q * nl;
-    const float na = sn[0][q], nb = sn[1][q];
+    const float na = sn[0][q], nb = sn[p + 1][q];
+    const int ob = (p + 1) * kCosStageFloats;
     float ps[4];
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
-      const float* rs = sr + st * nq * nl + j;
+      const float* rs = sr + p * n_items + st * nq * nl + j;
       ps[st] = cos_cascade_runs([&](int r) { return rs[r * rstride]; }, si);
     }
     const float* x = sx + base_of(q, l);
-    for (int i = si * 4; i < len; ++i) ps[0] = __fadd_rn(ps[0], cos_prod(x + es * i, na, nb));
+    for (int i = si * 4; i < len; ++i) ps[0] = __fadd_rn(ps[0], cos_prod(x + es * i, ob, na, nb));
     const float v = __fadd_rn(__fadd_rn(__fadd_rn(ps[0], ps[1]), ps[2]), ps[3]);
-    if (nl == 1) s[q] = __fadd_rn(0.f, v);
-    else sl[j] = v;  // the lane accumulators are spent
+    if (nl == 1) s[p * n_out + q] = __fadd_rn(0.f, v);
+    else sl[ja] = v;  // the lane accumulators are spent
   }
   if (nl > 1) {  // vectorized_inner_sum: the scalar tail from 0, then the lanes in order
     __syncthreads();
-    for (int q = tid; q < nq; q += kCosStageBlock) {
-      const float na = sn[0][q], nb = sn[1][q];
+    for (int qa = tid; qa < np * nq; qa += kCosStageBlock) {
+      const int p = qa / nq, q = qa - p * nq;
+      const float na = sn[0][q], nb = sn[p + 1][q];
+      const int ob = (p + 1) * kCosStageFloats;
       float fin = 0.f;
-      for (int k2 = len * kCosVw; k2 < I; ++k2) fin = __fadd_rn(fin, cos_prod(sx + q * Pr + k2, na, nb));
+      for (int k2 = len * kCosVw; k2 < I; ++k2) fin = __fadd_rn(fin, cos_prod(sx + q * Pr + k2, ob, na, nb));
 #pragma unroll
-      for (int l = 0; l < kCosVw; ++l) fin = __fadd_rn(fin, sl[q * kCosVw + l]);
-      s[q] = __fadd_rn(0.f, fin);
+      for (int l = 0; l < kCosVw; ++l) fin = __fadd_rn(fin, sl[qa * kCosVw + l]);
+      s[p * n_out + q] = __fadd_rn(0.f, fin);
     }
   }
 }
 
-// One workgroup per (staged chunk, pair): the chunk's slabs of a and b in LDS by coalesced 16-B
-// loads, then cos_staged_body.  LDS indices are 32-bit and chains walk pointers.
+// One workgroup per (staged chunk, group of kCosStagePairs pairs): the chunk's slabs of a and of
+// the group's b's in LDS by coalesced 16-B loads, then cos_staged_body.  LDS indices are 32-bit
+// and chains walk pointers.
 __global__ __launch_bounds__(kCosStageBlock) void k_cosine_staged(CosPairs pr, const int64_t* __restrict__ plan,
                                                                  int n_seg, int cnt, float* __restrict__ s_all) {
-  __shared__ __attribute__((aligned(16))) float sx[2 * kCosStageFloats];
-  __shared__ float sn[2][kCosStageOut];             // per output (row kind: per row) norms of a, b
-  __shared__ float sy[2][kCosStageOut];             // their reciprocals RN(1 / n) (cos_rdiv)
-  __shared__ float sl[2 * kCosVw * kCosStageRows];  // row kind: lane accumulators, then lane sums
-  __shared__ float sr[kCosStageItems];              // level-0 run sums
-  // XCD-aware order: dispatch deals workgroups round-robin over the 8 XCDs, so the pairs of one
-  // chunk (index 8 k + x) run one after another on XCD x, and every pair after the first finds
-  // the aggregating model's slab (each pair's `a`) in that XCD's L2
+  constexpr int kM = kCosStagePairs + 1;
+  __shared__ __attribute__((aligned(16))) float sx[kM * kCosStageFloats];
+  __shared__ float sn[kM][kCosStageOut];            // per model and output (row kind: row) norms
+  __shared__ float sy[kM][kCosStageOut];            // their reciprocals RN(1 / n) (cos_rdiv)
+  __shared__ float sl[kM * kCosVw * kCosStageRows];  // row kind: lane accumulators, then lane sums
+  __shared__ float sr[kCosStagePairs * kCosStageItems];  // level-0 run sums
+  // XCD-aware order: dispatch deals workgroups round-robin over the 8 XCDs, so the pair groups of
+  // one chunk (index 8 k + x) run one after another on XCD x, and every group after the first
+  // finds the aggregating model's slab (each pair's `a`) in that XCD's L2
+  const int npg = (cnt + kCosStagePairs - 1) / kCosStagePairs;
   const int L = blockIdx.x;
   const int kq = L >> 3;
-  const int pair = kq % cnt;
-  const int64_t c = static_cast<int64_t>(kq / cnt) * 8 + (L & 7);
+  const int pg = kq % npg;
+  const int64_t c = static_cast<int64_t>(kq / npg) * 8 + (L & 7);
   if (c >= plan[3]) return;
+  const int pair0 = pg * kCosStagePairs;
+  const int np = min(kCosStagePairs, cnt - pair0);
   const int64_t* ch = plan + kCosHdr + kCosSegWords * static_cast<int64_t>(n_seg) + kCosChunkWords * c;
   const int64_t* sg = plan + kCosHdr + kCosSegWords * ch[0];
   const int64_t first = ch[1];
@@ -3521,15 +3544,19 @@ __global__ __launch_bounds__(kCosStageBlock) void k_cosine_staged(CosPairs pr, c
   const int Pr = static_cast<int>(cos_row_pitch(I));
   // column kind: first = o0 * B, nq = G * B -> elements o0 I B .. (o0 + G) I B; row kind:
   // first = o0, nq = G -> o0 I .. (o0 + G) I: both first * I, nq * I
-  const float* ga = pr.a[pair] + sg[0] + first * I;
-  const float* gb = pr.b[pair] + sg[0] + first * I;
-  if (row) cos_stage<true>(ga, gb, nq * I, sx, I, Pr);
-  else cos_stage<false>(ga, gb, nq * I, sx, I, Pr);
+  const int64_t off = sg[0] + first * I;
+  const float* gm[kM];
+  gm[0] = pr.a[pair0] + off;
+#pragma unroll
+  for (int p = 0; p < kCosStagePairs; ++p) gm[p + 1] = pr.b[pair0 + (p < np ? p : 0)] + off;
+  if (row) cos_stage<true>(gm, np + 1, nq * I, sx, I, Pr);
+  else cos_stage<false>(gm, np + 1, nq * I, sx, I, Pr);
   __syncthreads();
-  float* s = s_all + static_cast<int64_t>(pair) * plan[1] + sg[4] + first;
-  if (row) cos_staged_body<true, 0>(sx, sn, sy, sl, sr, nq, I, B, Pr, s);
-  else if (B == 9) cos_staged_body<false, 9>(sx, sn, sy, sl, sr, nq, I, B, Pr, s);  // 3 x 3 convolutions
-  else cos_staged_body<false, 0>(sx, sn, sy, sl, sr, nq, I, B, Pr, s);
+  const int64_t n_out = plan[1];
+  float* s = s_all + static_cast<int64_t>(pair0) * n_out + sg[4] + first;
+  if (row) cos_staged_body<true, 0>(sx, sn, sy, sl, sr, np, nq, I, B, Pr, s, n_out);
+  else if (B == 9) cos_staged_body<false, 9>(sx, sn, sy, sl, sr, np, nq, I, B, Pr, s, n_out);  // 3 x 3 convolutions
+  else cos_staged_body<false, 0>(sx, sn, sy, sl, sr, np, nq, I, B, Pr, s, n_out);
 }
 
 // torch's serial full sum of s[0 .. n) (scalar_inner_sum below 8 elements, else
@@ -4750,9 +4777,9 @@ int32_t tal_cosine_params(const float* const* a_ptrs_host, const float* const* b
     float* s_all = static_cast<float*>(scratch);
     float* means = s_all + n_out * cnt;
     const int64_t n_staged = plan_host[3];
-    if (n_staged > 0)  // XCD-aware 1-D grid: 8 k + x = (chunk 8 (k / cnt) + x, pair k % cnt)
-      k_cosine_staged<<<static_cast<unsigned>((n_staged + 7) / 8 * 8 * cnt), kCosStageBlock, 0, s>>>(
-          pr, plan_dev, n_seg, cnt, s_all);
+    if (n_staged > 0)  // XCD-aware 1-D grid: 8 k + x = (chunk 8 (k / groups) + x, pair group k % groups)
+      k_cosine_staged<<<static_cast<unsigned>((n_staged + 7) / 8 * 8 * ((cnt + kCosStagePairs - 1) / kCosStagePairs)),
+                        kCosStageBlock, 0, s>>>(pr, plan_dev, n_seg, cnt, s_all);
     if (n_chunks > n_staged)
       k_cosine_outputs<<<dim3(static_cast<unsigned>(n_chunks - n_staged), cnt), kCosBlock, 0, s>>>(pr, plan_dev, n_seg,
                                                                                                   s_all);
