@@ -3517,7 +3517,7 @@ __device__ __forceinline__ void cos_staged_body(const float* sx, float (*sn)[kCo
 // the group's b's in LDS by coalesced 16-B loads, then cos_staged_body.  LDS indices are 32-bit
 // and chains walk pointers.
 __global__ __launch_bounds__(kCosStageBlock) void k_cosine_staged(CosPairs pr, const int64_t* __restrict__ plan,
-                                                                 int n_seg, int cnt, float* __restrict__ s_all) {
+                                                                 int n_seg, int cnt, int pgs, float* __restrict__ s_all) {
   constexpr int kM = kCosStagePairs + 1;
   __shared__ __attribute__((aligned(16))) float sx[kM * kCosStageFloats];
   __shared__ float sn[kM][kCosStageOut];            // per model and output (row kind: row) norms
@@ -3527,14 +3527,14 @@ __global__ __launch_bounds__(kCosStageBlock) void k_cosine_staged(CosPairs pr, c
   // XCD-aware order: dispatch deals workgroups round-robin over the 8 XCDs, so the pair groups of
   // one chunk (index 8 k + x) run one after another on XCD x, and every group after the first
   // finds the aggregating model's slab (each pair's `a`) in that XCD's L2
-  const int npg = (cnt + kCosStagePairs - 1) / kCosStagePairs;
+  const int npg = (cnt + pgs - 1) / pgs;  // pgs: pairs per group (1 when the pairs' a differ)
   const int L = blockIdx.x;
   const int kq = L >> 3;
   const int pg = kq % npg;
   const int64_t c = static_cast<int64_t>(kq / npg) * 8 + (L & 7);
   if (c >= plan[3]) return;
-  const int pair0 = pg * kCosStagePairs;
-  const int np = min(kCosStagePairs, cnt - pair0);
+  const int pair0 = pg * pgs;
+  const int np = min(pgs, cnt - pair0);
   const int64_t* ch = plan + kCosHdr + kCosSegWords * static_cast<int64_t>(n_seg) + kCosChunkWords * c;
   const int64_t* sg = plan + kCosHdr + kCosSegWords * ch[0];
   const int64_t first = ch[1];
@@ -4777,9 +4777,14 @@ int32_t tal_cosine_params(const float* const* a_ptrs_host, const float* const* b
     float* s_all = static_cast<float*>(scratch);
     float* means = s_all + n_out * cnt;
     const int64_t n_staged = plan_host[3];
+    // pairs sharing one `a` (sim_centrality_module_avg: the client against each neighbor) go
+    // kCosStagePairs to a workgroup, which stages and norms that a once; otherwise one pair each
+    bool same_a = true;
+    for (int j = 1; j < cnt; ++j) same_a = same_a && pr.a[j] == pr.a[0];
+    const int pgs = same_a ? kCosStagePairs : 1;
     if (n_staged > 0)  // XCD-aware 1-D grid: 8 k + x = (chunk 8 (k / groups) + x, pair group k % groups)
-      k_cosine_staged<<<static_cast<unsigned>((n_staged + 7) / 8 * 8 * ((cnt + kCosStagePairs - 1) / kCosStagePairs)),
-                        kCosStageBlock, 0, s>>>(pr, plan_dev, n_seg, cnt, s_all);
+      k_cosine_staged<<<static_cast<unsigned>((n_staged + 7) / 8 * 8 * ((cnt + pgs - 1) / pgs)), kCosStageBlock, 0,
+                        s>>>(pr, plan_dev, n_seg, cnt, pgs, s_all);
     if (n_chunks > n_staged)
       k_cosine_outputs<<<dim3(static_cast<unsigned>(n_chunks - n_staged), cnt), kCosBlock, 0, s>>>(pr, plan_dev, n_seg,
                                                                                                   s_all);
