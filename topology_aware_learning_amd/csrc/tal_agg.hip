@@ -2971,10 +2971,20 @@ __host__ __device__ inline int64_t cos_slab_floats(int kind, int64_t I, int64_t 
   return kind == kCosCol ? I * B : cos_row_pitch(I);
 }
 
+// The staged row form is kept for A/B measurement (tal_cosine_plan_build's tensors of the row
+// kind run the direct form unless TAL_COS_STAGE_ROWS=1 is set when the library loads).
+static const bool g_cos_stage_rows = [] {
+  const char* v = getenv("TAL_COS_STAGE_ROWS");
+  return v && v[0] == '1';
+}();
+
 // slabs (output blocks: B outputs of the column kind, one row of the row kind) per staged chunk;
 // 0 = the tensor runs the direct form
 inline int64_t cos_stage_slabs(int kind, int64_t A, int64_t I, int64_t B) {
   if (kind == kCosElem || (kind == kCosCol && B >= 32)) return 0;  // coalesced as it is
+  // rows: the direct form's 8 lanes per row read 32 contiguous bytes each and beat the staged
+  // form (ResNet-50's 37 row tensors, 8 pairs: 0.25 against 0.34-0.40 ms, profiles/r06/r06k4-5)
+  if (kind == kCosRow && !g_cos_stage_rows) return 0;
   const int64_t slab = cos_slab_floats(kind, I, B);
   if (slab > kCosStageFloats) return 0;
   int64_t nl, len;
