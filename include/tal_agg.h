@@ -423,6 +423,19 @@ int32_t tal_halo_exchange(void* comm, int32_t world, const void* const* send_buf
                           const int64_t* send_bytes, void* const* recv_bufs,
                           const int64_t* recv_bytes, void* stream);
 
+/* One process driving several GPUs (TAL_GPUS: the reference's single coordinator process,
+ * decentralized_app.py:605-641 / parsl_setup.py:75-78, with its clients' models spread over the
+ * node's GPUs).  tal_comm_init_local makes n communicators together, rank r on devices[r]
+ * (ncclCommInitAll; distinct devices).  tal_halo_exchange_local posts, in ONE RCCL group (a thread
+ * driving several ranks must group them), for every local rank r and peer p with a non-zero count:
+ * a send of send_bytes[r n + p] bytes from send_bufs[r n + p] and a receive of recv_bytes[r n + p]
+ * bytes into recv_bufs[r n + p], on rank r's stream streams[r].  The buffers obey
+ * tal_halo_exchange's rules (a contiguous block of ghost rows is a valid receive buffer). */
+int32_t tal_comm_init_local(void** comms_out, int32_t n, const int32_t* devices);
+int32_t tal_halo_exchange_local(void* const* comms, int32_t n, const void* const* send_bufs,
+                                const int64_t* send_bytes, void* const* recv_bufs,
+                                const int64_t* recv_bytes, void* const* streams);
+
 #ifdef __cplusplus
 }
 #endif

@@ -174,12 +174,24 @@ class DecentrallearnApp:
         if os.environ.get("TAL_DEVICE_POOL", "1") == "0" or not torch.cuda.is_available():
             return None
         from topology_aware_learning_amd.aggregate import layout_of_module
+        from topology_aware_learning_amd.multipool import MultiPool, devices_from_env
         from topology_aware_learning_amd.round import calibrated_pool
 
         layout = layout_of_module(self.clients[0].model)
+        trials = int(os.environ.get("TAL_POOL_PLACEMENT_TRIALS", "8"))
+        devs = devices_from_env()
+        if devs is not None:
+            # TAL_GPUS=N: the clients in contiguous blocks over N GPUs of this one process, each
+            # GPU's pool with ghost rows for the other GPUs' clients its clients can draw
+            # (the topology's non-zero entries); see topology_aware_learning_amd/multipool.py
+            mp = MultiPool(layout, len(self.clients), devs, adjacency=self.topology,
+                           make_pool=lambda rows, dev: calibrated_pool(layout, rows, dev, trials=trials))
+            for c in self.clients:
+                mp.bind(c.model, c.idx)
+            return mp
         # the pool the models live in for the whole run, placed where in-place rounds are fast
         pool = calibrated_pool(layout, len(self.clients), torch.device("cuda", torch.cuda.current_device()),
-                               trials=int(os.environ.get("TAL_POOL_PLACEMENT_TRIALS", "8")))
+                               trials=trials)
         for c in self.clients:
             c.model.to(pool.device)
             pool.bind(c.model, c.idx)
@@ -277,9 +289,13 @@ class DecentrallearnApp:
         decides; per call each result is the same arithmetic (same operands in the same order,
         same fp32 weights).  Returns each entry's aggregated (results, client) tuple, in order."""
         from topology_aware_learning_amd.arena import bound_row
+        from topology_aware_learning_amd.multipool import MultiPool
         from topology_aware_learning_amd.round import RoundExecutor
 
         from src.decentralized_client import manual_seed, weight_rule
+
+        if isinstance(self.pool, MultiPool):
+            return self._batched_aggregation_multi(batch)
 
         # each distinct future of the round resolved once (64 training futures behind 640 operand
         # references at config 3), each distinct model's pool row checked once
@@ -315,4 +331,58 @@ class DecentrallearnApp:
             if self._executor is None:
                 self._executor = RoundExecutor(self.pool)
             self._executor.run(orders, weights, out_rows)
+        return done
+
+    def _batched_aggregation_multi(self, batch) -> list:
+        """_batched_aggregation over a MultiPool (TAL_GPUS): the same weights and operand order;
+        the whole halo moves first (every GPU's ghost rows from their owners: RCCL sends /
+        receives between this process's per-device communicators), then each GPU's share of the
+        round runs as one K3 launch on its pool (own and ghost rows in, own rows out in place),
+        each on its device's stream behind that device's messages."""
+        from topology_aware_learning_amd.arena import bound_row
+        from topology_aware_learning_amd.round import RoundExecutor
+
+        from src.decentralized_client import manual_seed, weight_rule
+
+        mp = self.pool
+        memo: dict = {}
+        for _, _, agg_client, agg_neighbors, _ in batch:
+            for x in (agg_client, *agg_neighbors):
+                if id(x) not in memo:
+                    memo[id(x)] = x.result() if isinstance(x, Future) else x
+        gid_of: dict = {}  # id(model) -> global client id
+
+        def gid(m) -> int:
+            k = gid_of.get(id(m))
+            if k is None:
+                b = bound_row(m)
+                if b is None or mp.member(b[0]) is None:
+                    raise RuntimeError("TAL_BATCHED_ROUND needs every model bound to the device pools")
+                k = gid_of[id(m)] = mp.global_id(b[0], b[1])
+            return k
+
+        per_gpu = [([], [], []) for _ in range(mp.world)]  # (orders, weights, out rows) in local rows
+        done = []
+        rule = weight_rule(self.aggregation_function)  # None for test_agg: a no-op
+        for _, _, agg_client, agg_neighbors, kwargs in batch:
+            me = memo[id(agg_client)]
+            done.append(me)
+            if rule is None:
+                continue
+            got = rule(me, [memo[id(f)] for f in agg_neighbors], **kwargs)
+            g, out_row = mp.home(gid(me[1].model))
+            loc = mp.local[g]
+            per_gpu[g][0].append([loc[gid(m)] for m in got[0]])
+            per_gpu[g][1].append(list(map(float, got[1])))
+            per_gpu[g][2].append(out_row)
+        if self.seed is not None:  # the apps seed torch per call (reference :395); same end state
+            manual_seed(self.seed)
+        if any(o for o, _, _ in per_gpu):
+            if self._executor is None:
+                self._executor = [RoundExecutor(p) for p in mp.pools]
+            mp.exchange_halo()
+            for g, (orders, weights, out_rows) in enumerate(per_gpu):
+                if orders:
+                    with torch.cuda.device(mp.devices[g]):
+                        self._executor[g].run(orders, weights, out_rows)
         return done

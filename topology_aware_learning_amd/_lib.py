@@ -27,7 +27,7 @@ TAL_ERR_COMM = 4
 TAL_COMM_ID_BYTES = 128
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 23
+ABI_VERSION = 24
 
 EXPORTED = (
     "tal_last_error",
@@ -61,6 +61,8 @@ EXPORTED = (
     "tal_comm_destroy",
     "tal_halo_pack",
     "tal_halo_exchange",
+    "tal_comm_init_local",
+    "tal_halo_exchange_local",
     "tal_fill_counter",
     "tal_host_agg_f32",
     "tal_host_agg_i64",
@@ -171,6 +173,8 @@ _SIGS = {
     "tal_comm_destroy": (_I32, [_P]),
     "tal_halo_pack": (_I32, [_P, _I64, _I64, _P, _I32, _I64, _P, _P]),
     "tal_halo_exchange": (_I32, [_P, _I32, _PP, _PI64, _PP, _PI64, _P]),
+    "tal_comm_init_local": (_I32, [_PP, _I32, _PI32]),
+    "tal_halo_exchange_local": (_I32, [_PP, _I32, _PP, _PI64, _PP, _PI64, _PP]),
     "tal_fill_counter": (_I32, [_P, _I64, _I32, _P, _PI64, _P]),
     "tal_host_agg_f32": (_I32, [_PP, _PD, _I32, _P, _I64, _I32]),
     "tal_host_agg_i64": (_I32, [_PP, _PD, _I32, _P, _I64]),

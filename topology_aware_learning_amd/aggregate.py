@@ -403,6 +403,14 @@ def aggregate_models(operands: Sequence[nn.Module], weights: Sequence[float], ta
     # row); the target's pool then gives the layout without rebuilding its state_dict
     tb = bound_row(target)
     bounds = [bound_row(m) for m in operands]
+    mp = getattr(tb[0], "multi", None) if tb is not None else None
+    if mp is not None and all(b is not None and mp[0].member(b[0]) is not None for b in bounds):
+        # the driver's clients over several GPUs (multipool.MultiPool, TAL_GPUS): the operands
+        # other GPUs own are copied into this GPU's ghost rows, then K1 on rows of one pool
+        with torch.cuda.device(tb[0].device):
+            rows = mp[0].rows_for(mp[1], bounds)
+            ops.agg_pool_rows(tb[0], rows, [float(x) for x in weights], tb[1], mode)
+        return target
     if tb is not None and tb[0].device.type == "cuda" and all(b is not None and b[0] is tb[0] for b in bounds):
         # every model a row of one device pool (the driver's binding): K1 on the rows in place,
         # addresses from the pool instead of a view per row and segment

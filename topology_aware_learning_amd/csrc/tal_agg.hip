@@ -45,7 +45,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 23;
+constexpr int kAbiVersion = 24;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -5031,6 +5031,7 @@ struct Rccl {
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
   ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
   ncclResult_t (*CommCount)(const ncclComm_t, int*) = nullptr;
   ncclResult_t (*GroupStart)() = nullptr;
@@ -5061,6 +5062,7 @@ const Rccl& rccl() {
     sym(x.GetErrorString, "ncclGetErrorString");
     sym(x.GetUniqueId, "ncclGetUniqueId");
     sym(x.CommInitRank, "ncclCommInitRank");
+    sym(x.CommInitAll, "ncclCommInitAll");
     sym(x.CommDestroy, "ncclCommDestroy");
     sym(x.CommCount, "ncclCommCount");
     sym(x.GroupStart, "ncclGroupStart");
@@ -5120,6 +5122,65 @@ int32_t tal_comm_destroy(void* comm) {
   TAL_NEED_RCCL("tal_comm_destroy");
   const ncclResult_t r = rccl().CommDestroy(static_cast<ncclComm_t>(comm));
   if (r != ncclSuccess) return comm_fail("ncclCommDestroy", r);
+  g_err.clear();
+  return TAL_OK;
+}
+
+int32_t tal_comm_init_local(void** comms_out, int32_t n, const int32_t* devices) {
+  if (!comms_out || !devices || n <= 0) return fail(TAL_ERR_INVALID, "tal_comm_init_local: bad arguments");
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < i; ++j)
+      if (devices[i] == devices[j] || devices[i] < 0)
+        return fail(TAL_ERR_INVALID, "tal_comm_init_local: devices must be distinct (RCCL takes one rank per device)");
+  TAL_NEED_RCCL("tal_comm_init_local");
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess) return fail(TAL_ERR_HIP, "tal_comm_init_local: hipGetDevice");
+  std::vector<ncclComm_t> c(static_cast<size_t>(n), nullptr);
+  const ncclResult_t r = rccl().CommInitAll(c.data(), n, devices);
+  (void)hipSetDevice(prev);
+  if (r != ncclSuccess) return comm_fail("ncclCommInitAll", r);
+  for (int i = 0; i < n; ++i) comms_out[i] = c[i];
+  g_err.clear();
+  return TAL_OK;
+}
+
+int32_t tal_halo_exchange_local(void* const* comms, int32_t n, const void* const* send_bufs, const int64_t* send_bytes,
+                                void* const* recv_bufs, const int64_t* recv_bytes, void* const* streams) {
+  if (!comms || n <= 0 || !send_bytes || !recv_bytes || !streams)
+    return fail(TAL_ERR_INVALID, "tal_halo_exchange_local: bad arguments");
+  TAL_NEED_RCCL("tal_halo_exchange_local");
+  for (int r = 0; r < n; ++r) {
+    if (!comms[r]) return fail(TAL_ERR_INVALID, "tal_halo_exchange_local: null communicator");
+    int cnt = 0;
+    const ncclResult_t rc = rccl().CommCount(static_cast<ncclComm_t>(comms[r]), &cnt);
+    if (rc != ncclSuccess) return comm_fail("ncclCommCount", rc);
+    if (cnt != n) return fail(TAL_ERR_INVALID, "tal_halo_exchange_local: n differs from the communicators' size");
+    for (int p = 0; p < n; ++p) {
+      const int64_t k = static_cast<int64_t>(r) * n + p;
+      if (send_bytes[k] < 0 || recv_bytes[k] < 0 || (send_bytes[k] && (!send_bufs || !send_bufs[k])) ||
+          (recv_bytes[k] && (!recv_bufs || !recv_bufs[k])))
+        return fail(TAL_ERR_INVALID, "tal_halo_exchange_local: bad buffer for rank " + std::to_string(r) + ", peer " +
+                                         std::to_string(p));
+    }
+  }
+  // one group over every local rank's sends and receives: RCCL needs them together when one
+  // thread drives several of the communicator's ranks
+  ncclResult_t r = rccl().GroupStart();
+  if (r != ncclSuccess) return comm_fail("ncclGroupStart", r);
+  ncclResult_t first = ncclSuccess;
+  for (int q = 0; q < n && first == ncclSuccess; ++q) {
+    ncclComm_t c = static_cast<ncclComm_t>(comms[q]);
+    hipStream_t st = static_cast<hipStream_t>(streams[q]);
+    for (int p = 0; p < n && first == ncclSuccess; ++p) {
+      const int64_t k = static_cast<int64_t>(q) * n + p;
+      if (send_bytes[k]) first = rccl().Send(send_bufs[k], static_cast<size_t>(send_bytes[k]), ncclUint8, p, c, st);
+      if (first == ncclSuccess && recv_bytes[k])
+        first = rccl().Recv(recv_bufs[k], static_cast<size_t>(recv_bytes[k]), ncclUint8, p, c, st);
+    }
+  }
+  r = rccl().GroupEnd();
+  if (first != ncclSuccess) return comm_fail("ncclSend / ncclRecv", first);
+  if (r != ncclSuccess) return comm_fail("ncclGroupEnd", r);
   g_err.clear();
   return TAL_OK;
 }

@@ -67,6 +67,17 @@ def cosine_pairs(model: nn.Module, others: Sequence[nn.Module]) -> List[float]:
         flats = _host_flat([model, *others], layout)
         return [float(x) for x in ops.host_cosine([flats[0]] * len(others), flats[1:], plan).tolist()]
     device = _device_for([model, *others])
+    b0 = bound_row(model)
+    mp = getattr(b0[0], "multi", None) if b0 is not None else None
+    bounds = [bound_row(m) for m in others]
+    if mp is not None and all(b is not None and mp[0].member(b[0]) is not None for b in bounds):
+        # clients over several GPUs (multipool.MultiPool): the neighbors other GPUs own are read
+        # from this GPU's ghost rows, refreshed first
+        pool = b0[0]
+        with torch.cuda.device(pool.device):
+            rows = mp[0].rows_for(mp[1], bounds)
+            res = ops.cosine([pool.row_f32(b0[1])] * len(others), [pool.row_f32(r) for r in rows], plan)
+            return [float(x) for x in res.cpu().tolist()]
     flats = _flat([model, *others], layout, device)
     res = ops.cosine([flats[0]] * len(others), flats[1:], plan)
     return [float(x) for x in res.cpu().tolist()]
