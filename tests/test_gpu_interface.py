@@ -215,14 +215,28 @@ def test_driver_batched_round(cuda, tmp_path, monkeypatch):
         runs.append(len(orders))
 
     monkeypatch.setattr(RoundExecutor, "run", checked_run)
+    import src.decentralized_app as da
+
+    apps = []
+    real_batched = da.DecentrallearnApp._batched_aggregation
+
+    def spy(self, batch):
+        apps.append(self)
+        return real_batched(self, batch)
+
+    monkeypatch.setattr(da.DecentrallearnApp, "_batched_aggregation", spy)
     topo = tmp_path / "ring8.txt"
     np.savetxt(topo, nx.to_numpy_array(nx.cycle_graph(8)), fmt="%d")
     from src.experiments import decentralized_main
 
     rc = decentralized_main.main(["--dataset", "cifar10", "--aggregation_strategy", "degCent", "--softmax",
-                                  "--rounds", "2", "--epochs", "1", "--topology_file", str(topo), "--out_dir",
+                                  "--rounds", "3", "--epochs", "1", "--topology_file", str(topo), "--out_dir",
                                   str(tmp_path / "logs"), "--batch_size", "32"])
-    assert rc == 0 and runs == [8, 8]
+    assert rc == 0 and runs == [8, 8, 8]
+    # rounds 2 and 3 drew the same neighbor sets (a %d topology: every link probability 1), so
+    # they reused round 1's operand rows and weights (DecentrallearnApp._round_key), still
+    # bitwise the oracle's snapshot round (checked_run above)
+    assert apps[-1].round_cache_hits == 2
 
 
 @pytest.mark.parametrize("strategy,participation", [("weighted", 0.5), ("unweighted", 0.75), ("test_agg", 1.0)])
