@@ -83,7 +83,7 @@ def parse():
                    help="N > 1 over nccl, either exchange: torch.distributed's RCCL (device) or the "
                         "library's own communicator (cabi, include/tal_agg.h: tal_comm_* / "
                         "tal_halo_pack / tal_halo_exchange; the all-to-alls as groups of per-peer "
-                        "sends / receives)")
+                        "sends / receives; experimental: not yet run across GPUs)")
     p.add_argument("--exchange", default="auto", choices=["auto", "halo", "transpose"],
                    help="N > 1: neighbor models by RCCL P2P (halo) or column blocks by all-to-all "
                         "(transpose); auto = the smaller predicted time at the probed link rate "
@@ -585,7 +585,12 @@ def main():
                    "params_per_model": n_params, "parallelism": f"{result_extra.get('exchange', '')}-sharded x{world}" if sharded else "1 GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                     "bytes_per_launch": bytes_round, "kernel_ms": k_ms},
+                     "bytes_per_launch": bytes_round, "kernel_ms": k_ms,
+                     # the same plan on the first two pools allocated, before the placement
+                     # calibration kept the fastest pair (arena.select_pool_pair)
+                     "first_pair_frac": (bytes_round / (result_extra["placement"]["first_pair_ms"] * 1e-3) / 1e9
+                                         / HBM_PEAK_GBPS) if not sharded and "first_pair_ms" in result_extra.get(
+                                             "placement", {}) else None},
         "cpu_baseline": cpu,
         "parity": parity_ok,
         **result_extra,

@@ -195,7 +195,9 @@ def _host_binding(model: nn.Module, layout: StateLayout) -> Optional[Tuple[Model
         return _bind_pinned(model, layout)
 
 
-_bind_lock = threading.Lock()
+# re-entrant: a pool freed by garbage collection while this thread binds (weakref.finalize ->
+# _pin_release) takes it again on the same thread
+_bind_lock = threading.RLock()
 _PIN = {"used": 0, "budget": None}
 
 
@@ -222,7 +224,9 @@ def _pin_budget() -> int:
 
 
 def _pin_release(nbytes: int) -> None:
-    _PIN["used"] -= nbytes
+    # weakref.finalize runs on whichever thread collects the pool: the same lock as the binder's
+    with _bind_lock:
+        _PIN["used"] -= nbytes
 
 
 def _bind_pinned(model: nn.Module, layout: StateLayout) -> Optional[Tuple[ModelPool, int]]:
@@ -360,28 +364,34 @@ def _pipelined_host_call(hbs, target_hb, layout: StateLayout, w: List[float], mo
     src = [_row_segments(hb[0], hb[1], sizes) for hb in hbs]
     dst = _row_segments(target_hb[0], target_hb[1], sizes)
     keep = []
-    for g, n in sizes.items():
-        ld = (n + 63) // 64 * 64  # 256-B aligned operand rows: chunks keep K1's vector path
-        dev = torch.empty((m, ld), dtype=_SEG_DTYPE[g], device=device)
-        out = torch.empty(ld, dtype=_SEG_DTYPE[g], device=device)
-        keep += [dev, out]
-        step = n if g == "i64" else _PIPE_CHUNK
-        for a in range(0, n, step):
-            b = min(n, a + step)
-            with torch.cuda.stream(h2d):
-                for j in range(m):
-                    dev[j, a:b].copy_(src[j][g][a:b], non_blocking=True)
-            landed = torch.cuda.Event()
-            landed.record(h2d)
-            comp.wait_event(landed)
-            _k1(g, [dev[j, a:b] for j in range(m)], w, out[a:b], mode, comp)
-            done = torch.cuda.Event()
-            done.record(comp)
-            d2h.wait_event(done)
-            with torch.cuda.stream(d2h):
-                dst[g][a:b].copy_(out[a:b], non_blocking=True)
-    d2h.synchronize()  # the call returns with the model written, as the reference's load_state_dict
-    del keep
+    try:
+        for g, n in sizes.items():
+            ld = (n + 63) // 64 * 64  # 256-B aligned operand rows: chunks keep K1's vector path
+            dev = torch.empty((m, ld), dtype=_SEG_DTYPE[g], device=device)
+            out = torch.empty(ld, dtype=_SEG_DTYPE[g], device=device)
+            keep += [dev, out]
+            step = n if g == "i64" else _PIPE_CHUNK
+            for a in range(0, n, step):
+                b = min(n, a + step)
+                with torch.cuda.stream(h2d):
+                    for j in range(m):
+                        dev[j, a:b].copy_(src[j][g][a:b], non_blocking=True)
+                landed = torch.cuda.Event()
+                landed.record(h2d)
+                comp.wait_event(landed)
+                _k1(g, [dev[j, a:b] for j in range(m)], w, out[a:b], mode, comp)
+                done = torch.cuda.Event()
+                done.record(comp)
+                d2h.wait_event(done)
+                with torch.cuda.stream(d2h):
+                    dst[g][a:b].copy_(out[a:b], non_blocking=True)
+    finally:
+        # the call returns with the model written, as the reference's load_state_dict; and if a
+        # launch or copy raised part way, no queued copy may still touch `keep` (allocated on the
+        # caller's stream, used on the three side streams) once the allocator gets it back
+        for st in (h2d, comp, d2h):
+            st.synchronize()
+        del keep
 
 
 _AGG = {"f32": lambda xs, w, out, mode: ops.agg_f32(xs, w, out, mode=mode),

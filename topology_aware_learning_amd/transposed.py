@@ -483,6 +483,12 @@ def make_round(layout: StateLayout, orders, weights, rank: int, world: int, devi
     RCCL group; an all-to-all is such a group).  link_gbps: a measured per-pair link rate for
     the 'auto' choice (choose_exchange)."""
     owner = partition_contiguous(len(orders), world) if owner is None else np.asarray(owner, np.int32)
+    if transport == "cabi" and world > 1:
+        import warnings
+
+        warnings.warn("transport 'cabi' (the library's own RCCL communicator) is experimental across GPUs: "
+                      "tested on one rank and on virtual ranks only; no committed multi-GPU run yet",
+                      stacklevel=2)
     if exchange == "auto":
         exchange = choose_exchange(orders, owner, world, layout.n_f32, layout.n_i64, layout.n_b16, link_gbps=link_gbps)
     cls = {"halo": ShardedRound, "transpose": TransposedRound}[exchange]
