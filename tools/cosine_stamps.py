@@ -35,6 +35,9 @@ def main():
     st = buf.reshape(-1, 8).astype(np.int64)
     live = st[:, 5] > 0
     st = st[live]
+    if not len(st):
+        print(json.dumps(dict(shape=shape, staged=False, note="no staged chunk: the direct form")), flush=True)
+        return
     names = ["plan", "stage", "norms", "runs", "combine"]
     d = {nm: float(np.median(st[:, k + 1] - st[:, k])) for k, nm in enumerate(names)}
     d["total"] = float(np.median(st[:, 5] - st[:, 0]))

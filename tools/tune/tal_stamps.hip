@@ -32,7 +32,7 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>  // types only: the functions are resolved at run time (rccl())
 
-#include "../../include/tal_agg.h"
+#include "/root/repo/include/tal_agg.h"
 
 // The device code is gfx950 only: the inline asm below (v_mad_u32_u16 with op_sel, v_add_u32
 // with an inline constant, global_load_lds_dwordx4 through M0, counted s_waitcnt vmcnt) is CDNA4
@@ -2902,6 +2902,10 @@ int32_t launch_round_vec(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, i
 // one thread, strided); the per-tensor means and the final average follow in two small
 // kernels.  All arithmetic is single-rounding fp32 (__f*_rn), in torch's order.
 // ------------------------------------------------------------------------------------------
+__device__ unsigned long long g_stamps[16384 * 8];
+__device__ __forceinline__ void stamp(int k) {
+  if (threadIdx.x == 0 && blockIdx.x < 16384) g_stamps[blockIdx.x * 8 + k] = __builtin_amdgcn_s_memtime();
+}
 constexpr int kCosMaxPairs = 32;
 constexpr int kCosHdr = 4;         // plan words: {n_seg, n_out, torch intra-op threads, staged chunks}
 constexpr int kCosMaxThreads = 1024;
@@ -3482,6 +3486,7 @@ __device__ __forceinline__ void cos_staged_body(const float* sx, const int* mb, 
     }
   }
   __syncthreads();
+  stamp(3);
   // each output's row_sum sequences: nl lanes of len elements, element stride es
   const int nl = (ROW && I >= kCosVw) ? kCosVw : 1;
   const int len = nl > 1 ? I / kCosVw : I;
@@ -3513,6 +3518,7 @@ __device__ __forceinline__ void cos_staged_body(const float* sx, const int* mb, 
     sr[ia] = v;
   }
   __syncthreads();
+  stamp(4);
   // per (pair, sequence): the four streams' cascades, the row_sum remainder into stream 0, the
   // streams in order (cos_row_sum); one lane: the output's sum; 8 lanes: their sums, folded below
   const int rstride = 4 * nq * nl;  // between a sequence's consecutive runs of one stream
@@ -3560,6 +3566,7 @@ __global__ __launch_bounds__(kCosStageBlock) void k_cosine_staged(CosPairs pr, c
   // one chunk (index 8 k + x) run one after another on XCD x, and every group after the first
   // finds the aggregating model's slab (each pair's `a`) in that XCD's L2
   const int npg = (cnt + pgs - 1) / pgs;  // pgs: pairs per group (1 when the pairs' a differ)
+  stamp(0);
   const int L = blockIdx.x;
   const int kq = L >> 3;
   const int pg = kq % npg;
@@ -3581,6 +3588,7 @@ __global__ __launch_bounds__(kCosStageBlock) void k_cosine_staged(CosPairs pr, c
   gm[0] = pr.a[pair0] + off;
 #pragma unroll
   for (int p = 0; p < kCosStagePairs; ++p) gm[p + 1] = pr.b[pair0 + (p < np ? p : 0)] + off;
+  stamp(1);
   if (row) cos_stage<true>(gm, np + 1, nq * I, sx, I, Pr);
   else cos_stage<false>(gm, np + 1, nq * I, sx, I, Pr);
   int mb[kM];  // LDS offset of each model's element 0 (the column kind keeps the 16-B phase)
@@ -3588,11 +3596,13 @@ __global__ __launch_bounds__(kCosStageBlock) void k_cosine_staged(CosPairs pr, c
   for (int m = 0; m < kM; ++m)
     mb[m] = m * kCosStageStride + (row ? 0 : static_cast<int>((reinterpret_cast<uintptr_t>(gm[m]) >> 2) & 3));
   __syncthreads();
+  stamp(2);
   const int64_t n_out = plan[1];
   float* s = s_all + static_cast<int64_t>(pair0) * n_out + sg[4] + first;
   if (row) cos_staged_body<true, 0>(sx, mb, sn, sy, sl, sr, np, nq, I, B, Pr, s, n_out);
   else if (B == 9) cos_staged_body<false, 9>(sx, mb, sn, sy, sl, sr, np, nq, I, B, Pr, s, n_out);  // 3 x 3 convolutions
   else cos_staged_body<false, 0>(sx, mb, sn, sy, sl, sr, np, nq, I, B, Pr, s, n_out);
+  stamp(5);
 }
 
 // torch's serial full sum of s[0 .. n) (scalar_inner_sum below 8 elements, else
@@ -4245,6 +4255,10 @@ int32_t finish_plan(int32_t rows, const int32_t* row_ptr_host, const int32_t* co
 }  // namespace
 
 extern "C" {
+
+int32_t tal_debug_stamps(unsigned long long* out, int32_t n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 2;
+}
 
 const char* tal_last_error(void) { return g_err.c_str(); }
 
