@@ -19,6 +19,7 @@ import os
 import pathlib
 import shutil
 import sys
+import threading
 from concurrent.futures import Future
 from pathlib import Path
 
@@ -61,6 +62,22 @@ _DATASETS = {
     "cifar10_dropout": (DataChoices.CIFAR10_DROPOUT, 10),
     "cifar10_augment_dropout": (DataChoices.CIFAR10_AUGMENT_DROPOUT, 10),
 }
+
+
+class _Resolved(Future):
+    """A future created already resolved (the batched round's aggregation results): the
+    concurrent.futures.Future interface (result(), done(), add_done_callback, ...) without a
+    condition variable and lock per future - they never wait, so one shared condition serves."""
+
+    _cond = threading.Condition()
+
+    def __init__(self, result):  # noqa: D107 - Future.__init__ replaced on purpose
+        self._condition = _Resolved._cond
+        self._state = "FINISHED"
+        self._result = result
+        self._exception = None
+        self._waiters = []
+        self._done_callbacks = []
 
 
 class DecentrallearnApp:
@@ -254,6 +271,7 @@ class DecentrallearnApp:
             self.centrality_dict = update_random_agg_coeffs(seed=self.seed, round_idx=round_idx,
                                                             num_clients=len(self.clients),
                                                             centrality_dict=self.centrality_dict)
+        kwargs = None
         for client in self.clients:
             agg_client = nxt[client.idx]["train"]
             if client.idx not in sel:
@@ -267,8 +285,9 @@ class DecentrallearnApp:
                 continue
             neighbor_idxs.append(client.idx)  # self is the last operand (:625)
             agg_neighbors = [nxt[i]["train"] for i in neighbor_idxs]
-            kwargs = dict(centrality_metric=self.centrality_metric, centrality_dict=self.centrality_dict,
-                          softmax=self.softmax, softmax_coeff=self.aggregation_scheduler.get_softmax_coeff())
+            if kwargs is None:  # the same for every call of the round (the scheduler steps after it)
+                kwargs = dict(centrality_metric=self.centrality_metric, centrality_dict=self.centrality_dict,
+                              softmax=self.softmax, softmax_coeff=self.aggregation_scheduler.get_softmax_coeff())
             if batch is not None:  # collected; the whole round runs below as one K3 launch
                 batch.append((len(futures), client.idx, agg_client, agg_neighbors, kwargs, tuple(neighbor_idxs)))
                 futures.append(None)  # its future is made after the launch (below)
@@ -280,9 +299,7 @@ class DecentrallearnApp:
             # the launch first, then the round's futures (already resolved: the aggregation is
             # stream-ordered behind the launch), so their setup runs under the kernel
             for (pos, idx, *_), me in zip(batch, self._batched_aggregation(batch)):
-                future = Future()
-                future.set_result(me)
-                futures[pos] = nxt[idx]["agg"] = future
+                futures[pos] = nxt[idx]["agg"] = _Resolved(me)
         self.aggregation_scheduler.step(round_idx)
         return futures
 

@@ -15,6 +15,7 @@ place, CPU models are staged through pinned memory) — the values are the same.
 """
 from __future__ import annotations
 
+import itertools
 import json
 from typing import List, Optional
 
@@ -65,8 +66,10 @@ def draw_neighbors(clients) -> list:
     sizes = [len(c.neighbor_probs) for c in clients]
     if not any(sizes):
         return [[] for _ in clients]
-    keep = np.random.binomial(1, np.concatenate([np.asarray(c.neighbor_probs, dtype=np.float64)
-                                                 for c in clients])).tolist()
+    # one float64 array from the concatenated Python lists (one conversion, not one per client)
+    probs = np.fromiter(itertools.chain.from_iterable(c.neighbor_probs for c in clients), dtype=np.float64,
+                        count=sum(sizes))
+    keep = np.random.binomial(1, probs).tolist()
     out, k = [], 0
     for c, n in zip(clients, sizes):
         out.append([a for a, b in zip(c.neighbors, keep[k:k + n]) if b > 0])
