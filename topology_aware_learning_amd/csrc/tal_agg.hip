@@ -1801,6 +1801,95 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_round_stream(const float* __r
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ------------------------------------------------------------------------------------------
+// K3, wide-row form for bf16 pools (a streamed plan's groups, <= kWideRows rows each): rows with
+// more distinct sources than one LDS tile holds (the reference's `unweighted_fl`, every other
+// client a neighbor, decentralized_app.py:386-389) read each source once per group and column
+// tile instead of once per row.  Workgroup = (column tile of kWideC4 float4, group); thread =
+// (row of the group, float4 column).  The group's sources (ascending pool rows) pass through LDS
+// kWideSrc at a time, converted to fp32 (the next chunk's loads in flight while the current one
+// is reduced); each row walks its operands in reference order - ascending sources, its own model
+// last (kept in registers when its chunk passes) - with the bf16 arithmetic of the other round
+// kernels (EXACT: every product and sum rounded to bf16; FMA: fp32 fused, rounded by the store).
+// ------------------------------------------------------------------------------------------
+constexpr int kWideRows = 16;
+constexpr int kWideC4 = 16;
+constexpr int kWideSrc = 64;
+constexpr int kWideThreads = kWideRows * kWideC4;  // 256
+constexpr int kWideLoads = kWideSrc * kWideC4 / kWideThreads;  // 4 staged chunks per thread
+
+template <typename T, bool EXACT>
+__global__ __launch_bounds__(kWideThreads) void k_round_wide(const T* __restrict__ pin, int64_t ld_in4,
+                                                            T* __restrict__ pout, int64_t ld_out4, int64_t n4,
+                                                            PlanView p) {
+  __shared__ float4 s_x[kWideSrc * kWideC4];  // 16 KiB
+  const int g = blockIdx.y;
+  const int t = threadIdx.x;
+  const int rr = t / kWideC4, c = t % kWideC4;
+  const int s_beg = p.grp_src_ptr[g], ns = p.grp_src_ptr[g + 1] - s_beg;
+  const int r_beg = p.grp_row_ptr[g], nr = p.grp_row_ptr[g + 1] - r_beg;
+  const bool live = rr < nr;
+  const int row = r_beg + (live ? rr : 0);
+  const int q1 = p.row_ptr[row + 1];
+  int q = p.row_ptr[row];
+  const int last = q1 - 1;  // the row's own model: its last operand, applied after the others
+  const int self_slot = p.op_slot[last];
+  const float self_w = p.op_w[last];
+  const int64_t tile0 = static_cast<int64_t>(blockIdx.x) * kWideC4;
+  const int nch = (ns + kWideSrc - 1) / kWideSrc;
+  typename Io<T>::raw_t v[kWideLoads];
+  auto load = [&](int k) {
+#pragma unroll
+    for (int u = 0; u < kWideLoads; ++u) {
+      const int slot = t + u * kWideThreads;
+      const int src = k * kWideSrc + slot / kWideC4;
+      if (src < ns)  // past the row end: a duplicate of its last chunk (never stored)
+        v[u] = Io<T>::ld_raw(pin, static_cast<int64_t>(p.src_row[s_beg + src]) * ld_in4 +
+                                     min(tile0 + slot % kWideC4, n4 - 1));
+    }
+  };
+  load(0);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f), self_x = acc;
+  bool started = false;
+  for (int k = 0; k < nch; ++k) {
+    __syncthreads();  // the previous chunk's readers are done
+#pragma unroll
+    for (int u = 0; u < kWideLoads; ++u) {
+      const int slot = t + u * kWideThreads;
+      if (k * kWideSrc + slot / kWideC4 < ns) s_x[slot] = Io<T>::f4(v[u]);
+    }
+    __syncthreads();
+    if (k + 1 < nch) load(k + 1);  // in flight while this chunk is reduced
+    if (!live) continue;
+    const int lo = k * kWideSrc, hi = lo + kWideSrc;
+    if (self_slot >= lo && self_slot < hi) self_x = s_x[(self_slot - lo) * kWideC4 + c];
+    for (; q < last; ++q) {
+      const int sl = p.op_slot[q];
+      if (sl >= hi) break;
+      const float4 x = s_x[(sl - lo) * kWideC4 + c];
+      acc = started ? next4t<T, EXACT>(acc, p.op_w[q], x) : first4t<T, EXACT>(p.op_w[q], x);
+      started = true;
+    }
+  }
+  const int64_t col = tile0 + c;
+  if (live && col < n4) {
+    acc = started ? next4t<T, EXACT>(acc, self_w, self_x) : first4t<T, EXACT>(self_w, self_x);
+    Io<T>::st(pout, static_cast<int64_t>(p.out_row[row]) * ld_out4 + col, acc);
+  }
+}
+
+template <typename T>
+int32_t launch_round_wide(const T* pin, int64_t ld_in, T* pout, int64_t ld_out, int64_t n4, const PlanView& v,
+                          const tal_round_plan_info& in, bool exact, hipStream_t s) {
+  if (in.max_rows > kWideRows) return fail(TAL_ERR_INVALID, "wide-row round: groups of at most 16 rows");
+  const int64_t tiles = (n4 + kWideC4 - 1) / kWideC4;
+  if (tiles > 0x7fffffff || in.n_groups > 65535) return fail(TAL_ERR_INVALID, "wide-row round: grid too large");
+  const dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(in.n_groups));
+  if (exact) k_round_wide<T, true><<<grid, kWideThreads, 0, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v);
+  else k_round_wide<T, false><<<grid, kWideThreads, 0, s>>>(pin, ld_in / 4, pout, ld_out / 4, n4, v);
+  return check_launch("round kernel (wide rows)");
+}
+
 // Tail / int64 columns of a streamed plan: per (column chunk, group) workgroup, the group's
 // sources' columns are staged in LDS (as fp32), then each thread computes (row, column) pairs
 // walking the row's operands in reference order from the plan in global memory.
@@ -4666,9 +4755,10 @@ int32_t tal_agg_round_bf16(const uint16_t* pool_in, int64_t ld_in, uint16_t* poo
                            int32_t mode, void* stream) {
   int32_t rc = validate_info(info);
   if (rc) return rc;
-  if (info->dense_rb != 0 || info->stream_cs != 0)
-    return fail(TAL_ERR_INVALID, "tal_agg_round_bf16: bf16 rounds take sparse or narrow plans "
-                                 "(dense_rb 0, stream_cs 0)");
+  const bool wide = info->stream_cs != 0;  // a streamed plan: the wide-row form (<= 16 rows per group)
+  if ((info->dense_rb != 0 && !wide) || (wide && info->max_rows > kWideRows))
+    return fail(TAL_ERR_INVALID, "tal_agg_round_bf16: bf16 rounds take sparse or narrow plans (dense_rb 0), or "
+                                 "streamed plans of at most 16 rows per group (the wide-row form)");
   if (!pool_in || !pool_out || !plan_dev) return fail(TAL_ERR_INVALID, "tal_agg_round_bf16: null pointer");
   if (n < 0 || ld_in < n || ld_out < n) return fail(TAL_ERR_INVALID, "tal_agg_round_bf16: bad n / ld");
   if (pool_in == pool_out && info->n_groups > 1)
@@ -4683,7 +4773,10 @@ int32_t tal_agg_round_bf16(const uint16_t* pool_in, int64_t ld_in, uint16_t* poo
   if (vec) {
     const int64_t n4 = n / 4;
     e_vec = n4 * 4;
-    if (n4 > 0) {
+    if (n4 > 0 && wide) {
+      rc = launch_round_wide<uint16_t>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, exact, s);
+      if (rc) return rc;
+    } else if (n4 > 0) {
       switch (info->c4 * 2 + (exact ? 1 : 0)) {
         case 33: rc = launch_round_narrow<16, true, uint16_t>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;
         case 32: rc = launch_round_narrow<16, false, uint16_t>(pool_in, ld_in, pool_out, ld_out, n4, v, *info, s); break;

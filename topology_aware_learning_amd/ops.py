@@ -876,8 +876,9 @@ def default_plan(row_ptr, col, w, out_row, bf16: bool = False, mode: int = MODE_
     only when it has no more groups than the sparse plan; RoundExecutor runs a single-group
     plan (config 5's: every source in one tile) in place and a multi-group one through its
     scratch pool.  A round with a row of more distinct sources than one LDS tile holds (e.g.
-    `unweighted_fl` over > ~620 clients) gets the streamed form (fp32) or one K1 call per row
-    (RowCallPlan, bf16 pools)."""
+    `unweighted_fl` over > ~620 clients) gets a streamed plan - the fp32 streamed kernel, or for
+    bf16 pools the wide-row kernel - or, rows out of reference order, one K1 call per row
+    (RowCallPlan)."""
     try:
         if not bf16:
             cp = build_clique_plan(row_ptr, col, w, out_row)
@@ -889,16 +890,16 @@ def default_plan(row_ptr, col, w, out_row, bf16: bool = False, mode: int = MODE_
         if exc.code != _lib.TAL_ERR_CAPACITY:
             raise
         # a row with more distinct sources than one LDS tile holds: fp32 rounds stream their
-        # sources through an LDS ring (any group size; rows in reference order); bf16 pools,
-        # which the streamed kernel does not take, and other operand orders run one K1 call
-        # per row
-        if not bf16:
-            try:
-                p = build_stream_plan(row_ptr, col, w, out_row)
-                p.spec = {"stream_rows": 64, "stream_src": 0}
-                return p
-            except _lib.TalError:
-                pass
+        # sources through an LDS ring (k_round_stream), bf16 rounds through LDS chunks in groups
+        # of 16 rows (k_round_wide); rows in reference order either way; other operand orders
+        # run one K1 call per row
+        try:  # fp32: the streamed kernel's groups of 64 rows; bf16: the wide-row form's 16
+            rows = 64 if not bf16 else WIDE_ROWS
+            p = build_stream_plan(row_ptr, col, w, out_row, max_group_rows=rows)
+            p.spec = {"stream_rows": rows, "stream_src": 0}
+            return p
+        except _lib.TalError:
+            pass
         return row_call_plan(row_ptr, col, w, out_row)
     if p.info.c4 < 64 and not p.info.narrow_roww and (not bf16 or mode == MODE_FMA):
         # per-operand weights on a narrow plan: the broadcast form with every source in one LDS
@@ -916,9 +917,13 @@ def default_plan(row_ptr, col, w, out_row, bf16: bool = False, mode: int = MODE_
     return p
 
 
-def round_kernel_name(plan) -> str:
-    """Which K3 kernel tal_agg_round_f32 launches for this plan or plan info (mirrors
-    launch_round_vec); clique plans name the K3c kernel (their rest rows run a second one)."""
+WIDE_ROWS = 16  # rows per group of the bf16 wide-row form (k_round_wide, kWideRows)
+
+
+def round_kernel_name(plan, bf16: bool = False) -> str:
+    """Which K3 kernel tal_agg_round_f32 (bf16: tal_agg_round_bf16) launches for this plan or plan
+    info (mirrors launch_round_vec); clique plans name the K3c kernel (their rest rows run a
+    second one)."""
     if isinstance(plan, CliquePlan):
         return "k_round_clique"
     if isinstance(plan, RegPlan):
@@ -927,7 +932,7 @@ def round_kernel_name(plan) -> str:
         return "k_agg (one call per row)"
     info = plan.info if isinstance(plan, RoundPlan) else plan
     if info.stream_cs:
-        return "k_round_stream"
+        return "k_round_wide" if bf16 else "k_round_stream"
     if info.c4 < 64:
         return "k_round_f32_narrow"
     threads = 1024 if info.c4 == 64 else 512
@@ -1009,7 +1014,8 @@ def round_i64(pool_in: torch.Tensor, pool_out: torch.Tensor, plan: RoundPlan, n:
 
 def round_bf16(pool_in: torch.Tensor, pool_out: torch.Tensor, plan: RoundPlan, n: Optional[int] = None,
                mode: int = MODE_EXACT, stream=None) -> torch.Tensor:
-    """K3 on [models, ld] bf16 pools (sparse or narrow plans; modes as agg_bf16)."""
+    """K3 on [models, ld] bf16 pools (sparse, narrow or - rows wider than one LDS tile - streamed
+    plans of at most 16 rows per group, the wide-row kernel; modes as agg_bf16)."""
     if isinstance(plan, CliquePlan):
         plan = plan.full
     if isinstance(plan, RegPlan):
