@@ -824,8 +824,9 @@ def test_app_seed_matches_torch_manual_seed_cpu():
 
 def test_default_plan_rows_wider_than_a_tile():
     """A row of more distinct sources than one LDS tile holds (unweighted_fl over 700 clients):
-    fp32 rounds get the streamed form, bf16 rounds and rows out of reference order one K1 call
-    per row - never a capacity error (host-side plan building, no GPU)."""
+    fp32 rounds get the streamed form, bf16 rounds the wide-row form (groups of 16 rows), rows
+    out of reference order one K1 call per row - never a capacity error (host-side plan
+    building, no GPU)."""
     import networkx as nx
 
     from topology_aware_learning_amd import ops
@@ -838,11 +839,13 @@ def test_default_plan_rows_wider_than_a_tile():
     p = ops.default_plan(rp, col, w, rows)
     assert ops.round_kernel_name(p) == "k_round_stream" and not p.single_group
     q = ops.default_plan(rp, col, w, rows, bf16=True)
-    assert isinstance(q, ops.RowCallPlan) and q.staged_rows() == 700 * 700 and not q.single_group
-    assert isinstance(ops.plan_from_spec(rp, col, w, rows, q.spec), ops.RowCallPlan)
+    assert ops.round_kernel_name(q, bf16=True) == "k_round_wide" and not q.single_group
+    assert q.spec == {"stream_rows": ops.WIDE_ROWS, "stream_src": 0}
+    assert ops.round_kernel_name(ops.plan_from_spec(rp, col, w, rows, q.spec), bf16=True) == "k_round_wide"
     self_first = [[i] + sorted(g.neighbors(i)) for i in range(700)]
     rp2, col2, w2 = csr_from_lists(self_first, [[1 / 700] * 700 for _ in self_first])
     assert isinstance(ops.default_plan(rp2, col2, w2, rows), ops.RowCallPlan)
+    assert isinstance(ops.default_plan(rp2, col2, w2, rows, bf16=True), ops.RowCallPlan)
 
 
 def test_pool_row_addresses_and_cpu_pool_refused():
