@@ -284,32 +284,37 @@ class DecentrallearnApp:
                 futures.append(agg_client)
                 continue
             neighbor_idxs.append(client.idx)  # self is the last operand (:625)
-            agg_neighbors = [nxt[i]["train"] for i in neighbor_idxs]
             if kwargs is None:  # the same for every call of the round (the scheduler steps after it)
                 kwargs = dict(centrality_metric=self.centrality_metric, centrality_dict=self.centrality_dict,
                               softmax=self.softmax, softmax_coeff=self.aggregation_scheduler.get_softmax_coeff())
             if batch is not None:  # collected; the whole round runs below as one K3 launch
-                batch.append((len(futures), client.idx, agg_client, agg_neighbors, kwargs, tuple(neighbor_idxs)))
+                # (the operand futures are nxt[i]["train"] for i in the drawn tuple: looked up
+                # only when the round's weights are computed, not on a cached round)
+                batch.append((len(futures), client.idx, agg_client, tuple(neighbor_idxs), kwargs))
                 futures.append(None)  # its future is made after the launch (below)
                 continue
+            agg_neighbors = [nxt[i]["train"] for i in neighbor_idxs]
             future = self.aggregation_function(agg_client, self.seed, *agg_neighbors, **kwargs)
             futures.append(future)
             nxt[client.idx]["agg"] = future
         if batch:
             # the launch first, then the round's futures (already resolved: the aggregation is
             # stream-ordered behind the launch), so their setup runs under the kernel
-            for (pos, idx, *_), me in zip(batch, self._batched_aggregation(batch)):
+            for (pos, idx, *_), me in zip(batch, self._batched_aggregation(batch, nxt)):
                 futures[pos] = nxt[idx]["agg"] = _Resolved(me)
         self.aggregation_scheduler.step(round_idx)
         return futures
 
-    def _batched_aggregation(self, batch) -> list:
+    def _batched_aggregation(self, batch, nxt) -> list:
         """The round's aggregations as ONE K3 launch over the device pool (RoundExecutor):
         every aggregation reads the models as they were after training (snapshot semantics,
         SURVEY §8(a)).  The reference's per-call apps instead read neighbors that an earlier
         call of the same round may already have overwritten, in an order its 2-thread pool
         decides; per call each result is the same arithmetic (same operands in the same order,
-        same fp32 weights).  Returns each entry's aggregated (results, client) tuple, in order."""
+        same fp32 weights).  batch: (future position, client, its training future, drawn
+        operand ids with self last, kwargs) per aggregation; nxt: the round's
+        {client: {"train": future}}.  Returns each entry's aggregated (results, client) tuple,
+        in order."""
         from topology_aware_learning_amd import arena
         from topology_aware_learning_amd.arena import bound_row
         from topology_aware_learning_amd.multipool import MultiPool
@@ -318,15 +323,11 @@ class DecentrallearnApp:
         from src.decentralized_client import manual_seed, weight_rule
 
         if isinstance(self.pool, MultiPool):
-            return self._batched_aggregation_multi(batch)
+            return self._batched_aggregation_multi(batch, nxt)
 
-        # each distinct future of the round resolved once (64 training futures behind 640 operand
-        # references at config 3), each distinct model's pool row checked once
-        memo: dict = {}
-        for _, _, agg_client, agg_neighbors, *_ in batch:
-            for x in (agg_client, *agg_neighbors):
-                if id(x) not in memo:
-                    memo[id(x)] = x.result() if isinstance(x, Future) else x
+        # every operand is some client's training future (nxt[i]["train"]): each resolved once
+        # (64 futures behind 640 operand references at config 3), each model's row checked once
+        memo = self._resolve_round(nxt)
         rule = weight_rule(self.aggregation_function)  # None for test_agg: a no-op
         key = self._round_key(batch, rule)
         hit = self._round_cache.get(key) if key is not None else None
@@ -359,12 +360,12 @@ class DecentrallearnApp:
         orders, weights, out_rows, done = [], [], [], []
         text = io.StringIO()
         with contextlib.redirect_stdout(text) if key is not None else contextlib.nullcontext():
-            for _, _, agg_client, agg_neighbors, kwargs, _ in batch:
+            for _, _, agg_client, idxs, kwargs in batch:
                 me = memo[id(agg_client)]
                 done.append(me)
                 if rule is None:
                     continue
-                got = rule(me, [memo[id(f)] for f in agg_neighbors], **kwargs)
+                got = rule(me, [memo[id(nxt[i]["train"])] for i in idxs], **kwargs)
                 orders.append([row_of[id(m)] if id(m) in row_of else pool_row(m) for m in got[0]])
                 weights.append(list(map(float, got[1])))
                 m = me[1].model
@@ -397,9 +398,19 @@ class DecentrallearnApp:
             return None
         kw = batch[0][4]
         return (rule.__name__, kw.get("softmax"), float(kw.get("softmax_coeff") or 0.0), kw.get("centrality_metric"),
-                tuple((e[1], e[5]) for e in batch))
+                tuple((e[1], e[3]) for e in batch))
 
-    def _batched_aggregation_multi(self, batch) -> list:
+    @staticmethod
+    def _resolve_round(nxt) -> dict:
+        """id(future) -> its result, for every client's training future of the round."""
+        memo: dict = {}
+        for v in nxt.values():
+            x = v["train"]
+            if id(x) not in memo:
+                memo[id(x)] = x.result() if isinstance(x, Future) else x
+        return memo
+
+    def _batched_aggregation_multi(self, batch, nxt) -> list:
         """_batched_aggregation over a MultiPool (TAL_GPUS): the same weights and operand order;
         the whole halo moves first (every GPU's ghost rows from their owners: RCCL sends /
         receives between this process's per-device communicators), then each GPU's share of the
@@ -411,11 +422,7 @@ class DecentrallearnApp:
         from src.decentralized_client import manual_seed, weight_rule
 
         mp = self.pool
-        memo: dict = {}
-        for _, _, agg_client, agg_neighbors, *_ in batch:
-            for x in (agg_client, *agg_neighbors):
-                if id(x) not in memo:
-                    memo[id(x)] = x.result() if isinstance(x, Future) else x
+        memo = self._resolve_round(nxt)
         gid_of: dict = {}  # id(model) -> global client id
 
         def gid(m) -> int:
@@ -430,12 +437,12 @@ class DecentrallearnApp:
         per_gpu = [([], [], []) for _ in range(mp.world)]  # (orders, weights, out rows) in local rows
         done = []
         rule = weight_rule(self.aggregation_function)  # None for test_agg: a no-op
-        for _, _, agg_client, agg_neighbors, kwargs, _ in batch:
+        for _, _, agg_client, idxs, kwargs in batch:
             me = memo[id(agg_client)]
             done.append(me)
             if rule is None:
                 continue
-            got = rule(me, [memo[id(f)] for f in agg_neighbors], **kwargs)
+            got = rule(me, [memo[id(nxt[i]["train"])] for i in idxs], **kwargs)
             g, out_row = mp.home(gid(me[1].model))
             loc = mp.local[g]
             per_gpu[g][0].append([loc[gid(m)] for m in got[0]])
@@ -445,7 +452,8 @@ class DecentrallearnApp:
             manual_seed(self.seed)
         if any(o for o, _, _ in per_gpu):
             if self._executor is None:
-                self._executor = [RoundExecutor(p) for p in mp.pools]
+                # in place per GPU pool: a spare would also carry the ghost rows every round
+                self._executor = [RoundExecutor(p, double_buffer=False) for p in mp.pools]
             mp.exchange_halo()
             for g, (orders, weights, out_rows) in enumerate(per_gpu):
                 if orders:

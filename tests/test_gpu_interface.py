@@ -220,9 +220,9 @@ def test_driver_batched_round(cuda, tmp_path, monkeypatch):
     apps = []
     real_batched = da.DecentrallearnApp._batched_aggregation
 
-    def spy(self, batch):
+    def spy(self, batch, nxt):
         apps.append(self)
-        return real_batched(self, batch)
+        return real_batched(self, batch, nxt)
 
     monkeypatch.setattr(da.DecentrallearnApp, "_batched_aggregation", spy)
     topo = tmp_path / "ring8.txt"

@@ -121,7 +121,9 @@ def test_draw_neighbors_is_the_sequential_stream():
         clients.append(DecentralClient(idx=i, prox_coeff=0.0, model=torch.nn.Linear(1, 1), train_data=None,
                                        test_data=None, valid_data=None, global_test_data=ds,
                                        global_backdoor_test_data=None, neighbors=nb, neighbor_probs=pr))
-    for sub in (clients, clients[::3], clients[:1], []):
+    ones = [c.model_copy(update=dict(neighbor_probs=[1.0] * len(c.neighbors))) for c in clients]
+
+    def same(sub):
         np.random.seed(4)
         seq = [c.get_neighbors() for c in sub]
         st = np.random.get_state()
@@ -129,6 +131,13 @@ def test_draw_neighbors_is_the_sequential_stream():
         assert draw_neighbors(sub) == seq
         st2 = np.random.get_state()
         assert np.array_equal(st[1], st2[1]) and st[2] == st2[2]
+
+    # each set twice in a row (the second call reuses the concatenated probabilities); `ones`:
+    # every link kept (the no-filter path)
+    for sub in (clients, clients, clients[::3], clients[::3], clients[:1], [], ones, ones, ones[5:]):
+        same(sub)
+    clients[7].neighbor_probs[:] = [0.5] * len(clients[7].neighbor_probs)  # changed in place
+    same(clients)
 
 
 def test_layouts_match_reference_models():

@@ -11,8 +11,8 @@ back to back with one synchronisation at the end (throughput: *_back_to_back).
 
 Training is replaced by an already resolved future holding the model as it stands (no app is
 submitted) so a round is the driver's own Python plus the aggregation.  Also
-times RoundExecutor(pool).run directly on the round (its default plan, in place) against the
-bench's K1 floor (64 x one K1 call).  One JSON line per measurement.
+times RoundExecutor(pool).run directly on the round (its default plan; double-buffered, the
+default, and in place) against the bench's K1 floor (64 x one K1 call).  One JSON line per measurement.
 
 usage: python tools/dropin_rate.py [rounds] [--profile[=per_call]] [--switch-us=N]   (--profile: cProfile of the
 batched rounds only, or of the per-call rounds with =per_call; top functions by cumulative and by
@@ -183,9 +183,9 @@ def main():
     marks = {}
     orig_batched, orig_run = app._batched_aggregation, rmod.RoundExecutor.run
 
-    def batched(batch):
+    def batched(batch, nxt):
         marks["collected"] = time.perf_counter()
-        return orig_batched(batch)
+        return orig_batched(batch, nxt)
 
     def run(self, *a, **k):
         marks["run_entered"] = time.perf_counter()
@@ -238,19 +238,26 @@ def main():
     e.synchronize()
     k1 = s.elapsed_time(e)
     print(json.dumps(dict(k1_floor_ms_per_round=round(k1, 3), k1_ms_per_call=round(k1 / 64, 4))), flush=True)
-    # RoundExecutor.run on the whole round (default plan; single group -> in place on the pool)
-    ex = RoundExecutor(pool)
-    ex.run(orders, ws)
-    ts = []
-    for _ in range(10):
-        s.record()
+    # RoundExecutor.run on the whole round (default plan): double-buffered (the default since
+    # round 6: out of place into the executor's placed spare, then the storage exchange) and
+    # in place on the pool (double_buffer=False, round 5's form), interleaved
+    exs = dict(double_buffered=RoundExecutor(pool), in_place=RoundExecutor(pool, double_buffer=False))
+    for ex in exs.values():
         ex.run(orders, ws)
-        e.record()
-        e.synchronize()
-        ts.append(s.elapsed_time(e))
-    p = ex.plan(orders, ws, list(range(64)))
-    print(json.dumps(dict(round_executor_ms=round(float(np.median(ts)), 3), plan=p.spec,
-                          kernel=ops.round_kernel_name(p), in_place=bool(p.single_group))), flush=True)
+    ts = {k: [] for k in exs}
+    for _ in range(10):
+        for k, ex in exs.items():
+            s.record()
+            ex.run(orders, ws)
+            e.record()
+            e.synchronize()
+            ts[k].append(s.elapsed_time(e))
+    p = exs["in_place"].plan(orders, ws, list(range(64)))
+    for k, ex in exs.items():
+        print(json.dumps(dict(round_executor_ms=round(float(np.median(ts[k])), 3), form=k,
+                              all_ms=[round(t, 3) for t in ts[k]], plan=p.spec, kernel=ops.round_kernel_name(p),
+                              spare_placement=ex.placement, swaps=ex.swaps)), flush=True)
+    del exs
     # the same round out of place into a scratch pool: default plan vs the tuner's pick (bench)
     from topology_aware_learning_amd.arena import ModelPool
     from topology_aware_learning_amd.round import csr_from_lists

@@ -2,7 +2,8 @@
 `unweighted_fl` over 700 clients (every other client a neighbor), CIFAR-CNN-sized bf16 rows
 (5,851,338 elements), EXACT and FMA: the wide-row form (k_round_wide, the default since round 6)
 against round 5's one K1 call per row (RowCallPlan), kernel time by HIP events.  One JSON line
-per measurement."""
+per measurement.  --pmc: one EXACT launch of each form only, for a rocprofv3 --pmc FETCH_SIZE
+pass (source reads once per group against once per row)."""
 import json
 import sys
 from pathlib import Path
@@ -30,6 +31,15 @@ def main():
     pout = torch.empty_like(pin)
     wide = ops.default_plan(rp, col, w, rows, bf16=True)
     percall = ops.row_call_plan(rp, col, w, rows)
+    if "--pmc" in sys.argv:  # one EXACT launch of each form, nothing else (for rocprofv3 --pmc)
+        ops.round_bf16(pin, pout, wide, n=n, mode=ops.MODE_EXACT)
+        torch.cuda.synchronize()
+        ops.round_bf16(pin, pout, percall, n=n, mode=ops.MODE_EXACT)
+        torch.cuda.synchronize()
+        print(json.dumps(dict(pmc_pass=True, groups=wide.info.n_groups,
+                              wide_source_bytes=2 * n * nc * wide.info.n_groups,
+                              per_row_source_bytes=2 * n * nc * nc, out_bytes=2 * n * nc)), flush=True)
+        return
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for mode, name in ((ops.MODE_EXACT, "exact"), (ops.MODE_FMA, "fma")):
         res = {}

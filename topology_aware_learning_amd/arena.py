@@ -301,15 +301,34 @@ class ModelPool:
                     table[attr] = v
             else:  # pragma: no cover - state_dict keys always resolve to a param or buffer
                 raise KeyError(e.name)
-            slots.append((table, attr, v.data_ptr()))
+            slots.append((table, attr, e.seg, v.data_ptr() - getattr(self, e.seg).data_ptr()))
         _install_hooks()
         module._tal_pool = self  # type: ignore[attr-defined]
         module._tal_row = r  # type: ignore[attr-defined]
         module._tal_gen = _GEN[0]  # type: ignore[attr-defined]
-        module._tal_slots = [(table, attr) for table, attr, _ in slots]  # type: ignore[attr-defined]
-        module._tal_ptrs = [ptr for _, _, ptr in slots]  # type: ignore[attr-defined]
+        module._tal_slots = [(table, attr) for table, attr, _, _ in slots]  # type: ignore[attr-defined]
+        # each entry's byte offset from its segment's base: the base moves when a double-buffered
+        # round exchanges the pool's storage (swap_storage), the offsets do not
+        module._tal_segs = [seg for _, _, seg, _ in slots]  # type: ignore[attr-defined]
+        module._tal_offs = [off for _, _, _, off in slots]  # type: ignore[attr-defined]
         self._bound[id(module)] = r
         return module
+
+    def swap_with(self, other: "ModelPool") -> None:
+        """Exchange this pool's memory with `other`'s (same layout, rows and device), segment by
+        segment: every view of either pool - the bound models' parameters and buffers included -
+        then reads the other's bytes.  No data moves (swap_storage)."""
+        if other.layout != self.layout or other.rows != self.rows or other.device != self.device:
+            raise ValueError("swap_with: pools differ in layout, rows or device")
+        if not (self.whole_storage() and other.whole_storage()):
+            raise ValueError("swap_with: a pool segment that is not a whole storage")
+        for k in ("f32", "b16", "i64"):
+            swap_storage(getattr(self, k), getattr(other, k))
+
+    def whole_storage(self) -> bool:
+        """Every segment tensor is its storage, whole (what swap_with exchanges)."""
+        return all(not t.storage_offset() and t.untyped_storage().nbytes() == t.numel() * t.element_size()
+                   for t in (self.f32, self.b16, self.i64))
 
     def row_of(self, module: nn.Module) -> Optional[int]:
         """Row the module is bound to, if its state still lives there: O(1) while no re-pointing
@@ -321,11 +340,11 @@ class ModelPool:
         if _HOOKS and module._tal_gen == _GEN[0]:  # type: ignore[attr-defined]
             # no re-pointing hook fired since the last full check (see _GEN); the first and
             # the last entry are compared as well (unhooked re-pointing of either is seen)
-            ptrs = module._tal_ptrs  # type: ignore[attr-defined]
+            segs, offs = module._tal_segs, module._tal_offs  # type: ignore[attr-defined]
             for k in (0, len(slots) - 1):
                 table, attr = slots[k]
                 t = table.get(attr)
-                if t is None or t.data_ptr() != ptrs[k]:
+                if t is None or t.data_ptr() - getattr(self, segs[k]).data_ptr() != offs[k]:
                     return None
             return r
         # after a hook event: every state entry, resolved by name again (a replaced submodule
@@ -339,10 +358,11 @@ class ModelPool:
                 mod = mods[path]
                 table = mod._parameters if attr in mod._parameters else mod._buffers
                 fresh.append((table, attr))
-            ptrs = [table[attr].data_ptr() for table, attr in fresh]
+            base = {k: getattr(self, k).data_ptr() for k in ("f32", "b16", "i64")}
+            offs = [table[attr].data_ptr() - base[k] for (table, attr), k in zip(fresh, module._tal_segs)]
         except (KeyError, AttributeError):  # an entry removed or set to None
             return None
-        if ptrs != module._tal_ptrs:  # type: ignore[attr-defined]
+        if offs != module._tal_offs:  # type: ignore[attr-defined]
             return None
         table, attr = fresh[0]
         if table[attr].device != self.device:
@@ -358,6 +378,29 @@ def bound_row(module: nn.Module) -> Optional[Tuple[ModelPool, int]]:
         return None
     r = pool.row_of(module)
     return None if r is None else (pool, r)
+
+
+_SWAP: list = []  # the loaded libtal_swap.so
+
+
+def swap_storage(a: torch.Tensor, b: torch.Tensor) -> None:
+    """Exchange the memory behind the storages of `a` and `b` (same size and device): every view
+    of either then reads the other's bytes (csrc/storage_swap.cpp, built by build.build_swap)."""
+    import ctypes
+
+    if not _SWAP:
+        from .build import SWAP_LIB
+
+        if not SWAP_LIB.exists():
+            raise RuntimeError(f"{SWAP_LIB} is missing: run __graft_entry__.build() (double-buffered rounds "
+                               "exchange pool storages through it)")
+        lib = ctypes.CDLL(str(SWAP_LIB))
+        lib.tal_swap_storage.restype = ctypes.c_int32
+        lib.tal_swap_storage.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        _SWAP.append(lib)
+    rc = _SWAP[0].tal_swap_storage(a.untyped_storage()._cdata, b.untyped_storage()._cdata)
+    if rc:
+        raise ValueError("swap_storage: " + ("the same storage" if rc == 1 else "sizes or devices differ"))
 
 
 def select_pool_pair(make_pool: Callable[[], "ModelPool"], score: Callable[["ModelPool", "ModelPool"], float],

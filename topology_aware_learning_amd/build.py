@@ -18,6 +18,8 @@ ROOT = PKG.parent
 SRC = PKG / "csrc" / "tal_agg.hip"
 HDR = ROOT / "include" / "tal_agg.h"
 LIB = PKG / "libtal_agg.so"
+SWAP_SRC = PKG / "csrc" / "storage_swap.cpp"
+SWAP_LIB = PKG / "libtal_swap.so"
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950",
@@ -62,5 +64,24 @@ def build_library(force: bool = False, verbose: bool = False) -> Path:
     return LIB
 
 
+def build_swap(force: bool = False, verbose: bool = False) -> Path:
+    """Compile csrc/storage_swap.cpp -> libtal_swap.so (host C++ against torch's c10 headers:
+    the double-buffered round's storage exchange; skipped when up to date)."""
+    if not force and not _stale(SWAP_LIB, [SWAP_SRC]):
+        return SWAP_LIB
+    import torch
+
+    tdir = Path(torch.__file__).resolve().parent
+    tmp = SWAP_LIB.with_suffix(".so.tmp")
+    cmd = [shutil.which("g++") or "g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-isystem", str(tdir / "include"),
+           str(SWAP_SRC), "-L" + str(tdir / "lib"), "-lc10", "-Wl,-rpath," + str(tdir / "lib"), "-o", str(tmp)]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, SWAP_LIB)
+    return SWAP_LIB
+
+
 if __name__ == "__main__":
     print(build_library(force="--force" in sys.argv, verbose=True))
+    print(build_swap(force="--force" in sys.argv, verbose=True))

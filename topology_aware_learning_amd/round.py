@@ -38,28 +38,49 @@ def csr_from_lists(orders: Sequence[Sequence[int]], weights: Sequence[Sequence[f
 
 
 class RoundExecutor:
-    """Rounds over one pool.  Multi-group plans write a scratch pool (snapshot semantics);
-    placement_trials > 1 allocates that many scratch candidates the first time one is needed
-    (at most as many as fit in 60 % of the free HBM), times the round into each and keeps the
-    fastest (where in HBM the written pool sits changes the round time by up to 25 %, see
-    arena.select_pool_pair and DESIGN §5 "Pool placement"); `placement` records the times.
-    The default is 4 candidates.  Single-group plans run in place on `pool` itself, whose
-    placement is the caller's: `calibrated_pool` places it before models are bound."""
+    """Rounds over one pool.
+
+    Double-buffered (the default for device pools, `double_buffer=None`): the executor keeps a
+    spare pool of the same shape; each round reads `pool` and writes the spare (rows the round
+    does not aggregate are copied across), then the two pools exchange their memory
+    (ModelPool.swap_with: one storage pointer exchange per segment, no bytes moved), so the
+    models bound to `pool` read the round's output and the spare holds the previous state, the
+    next round's destination.  Every plan runs out of place this way, at the out-of-place rate:
+    an in-place round costs 5-6 % more on the same destination (profiles/r05/r05p).
+    The spare is allocated on the first round: `placement_trials` candidates (at most as many
+    as fit in 60 % of the free HBM) are each timed as the round's destination and the fastest is
+    kept (where in HBM the written pool sits changes the round time by up to 25 %, see
+    arena.select_pool_pair and DESIGN §5 "Pool placement"); `placement` records the times.  With
+    no room for a spare the executor falls back to the form below.
+
+    double_buffer=False (and pools sharing memory with something else, e.g. MultiPool's): single
+    -group plans run in place on `pool`, whose placement is the caller's (`calibrated_pool`
+    places it before models are bound); multi-group plans write a scratch pool (snapshot
+    semantics, placed like the spare) and copy the aggregated rows back."""
 
     def __init__(self, pool: ModelPool, scratch: Optional[ModelPool] = None, mode: int = ops.MODE_EXACT,
-                 placement_trials: int = 4):
+                 placement_trials: int = 4, double_buffer: Optional[bool] = None):
         self.pool = pool
         self.scratch = scratch
         self.mode = mode
         self.placement_trials = placement_trials
         self.placement: Optional[dict] = None
         self._plans: Dict[Tuple, ops.RoundPlan] = {}
+        if double_buffer is None:
+            double_buffer = scratch is None and pool.device.type == "cuda" and pool.whole_storage()
+        self.double_buffer = double_buffer
+        self.spare: Optional[ModelPool] = None
+        self.swaps = 0
 
-    def _new_scratch(self, plan) -> ModelPool:
+    def _new_scratch(self, plan, need: int = 1) -> Optional[ModelPool]:
+        """The scratch / spare pool, placed by timing `placement_trials` candidates as the
+        round's destination; None when fewer than `need` pools fit in 60 % of the free HBM."""
         lay = self.pool.layout
         make = lambda: ModelPool(lay, self.pool.rows, self.pool.device)  # noqa: E731
         pool_bytes = sum(t.numel() * t.element_size() for _, t, _ in self.pool.segments())
         fit = int(0.6 * torch.cuda.mem_get_info(self.pool.device)[0] // max(1, pool_bytes))
+        if fit < need:
+            return None
         trials = min(self.placement_trials, fit)
         if trials <= 1:
             return make()
@@ -92,6 +113,9 @@ class RoundExecutor:
             row_ptr, col, w = csr_from_lists(orders, weights)
             p = ops.default_plan(row_ptr, col, w, np.asarray(out_rows, np.int32),
                                  bf16=bool(self.pool.layout.n_b16), mode=self.mode).to(self.pool.device)
+            rest = sorted(set(range(self.pool.rows)) - set(int(r) for r in out_rows))
+            # rows a double-buffered round does not aggregate: copied into the spare before the swap
+            p.rest_rows = torch.as_tensor(rest, dtype=torch.long, device=self.pool.device) if rest else None
             if len(self._plans) > 64:
                 self._plans.clear()
             self._plans[key] = p
@@ -115,17 +139,26 @@ class RoundExecutor:
                     ops.agg_i64([self.pool.row_i64(j) for j in o], w, self.pool.row_i64(r))
             return
         plan = self.plan(orders, weights, out_rows)
+        if self.double_buffer:
+            if self.spare is None:
+                self.spare = self._new_scratch(plan, need=1)
+                if self.spare is None:  # no room for a second pool: in place / scratch from now on
+                    self.double_buffer = False
+            if self.spare is not None:
+                self._launch(plan, self.spare)
+                if plan.rest_rows is not None:
+                    for (_, src, _), (_, dst, _) in zip(self.pool.segments(), self.spare.segments()):
+                        dst.index_copy_(0, plan.rest_rows, src.index_select(0, plan.rest_rows))
+                # stream-ordered: the next reader of either pool runs behind this round's writes
+                self.pool.swap_with(self.spare)
+                self.swaps += 1
+                return
         # every workgroup stages all sources of its tile before writing: with one group in place
         # is safe; otherwise the round goes through the scratch pool
         if not plan.single_group and self.scratch is None:
             self.scratch = self._new_scratch(plan)
         dst = self.pool if plan.single_group else self.scratch
-        if lay.n_f32:
-            ops.round_f32(self.pool.f32, dst.f32, plan, n=lay.n_f32, mode=self.mode)
-        if lay.n_b16:
-            ops.round_bf16(self.pool.b16, dst.b16, plan, n=lay.n_b16, mode=self.mode)
-        if lay.n_i64:
-            ops.round_i64(self.pool.i64, dst.i64, plan, n=lay.n_i64)
+        self._launch(plan, dst)
         if dst is self.pool:
             return
         idx = torch.as_tensor(list(out_rows), dtype=torch.long, device=self.pool.device)
@@ -133,6 +166,16 @@ class RoundExecutor:
             src = {id(self.pool.f32): self.scratch.f32, id(self.pool.b16): self.scratch.b16,
                    id(self.pool.i64): self.scratch.i64}[id(t)]
             t.index_copy_(0, idx, src.index_select(0, idx))
+
+
+    def _launch(self, plan, dst: ModelPool) -> None:
+        lay = self.pool.layout
+        if lay.n_f32:
+            ops.round_f32(self.pool.f32, dst.f32, plan, n=lay.n_f32, mode=self.mode)
+        if lay.n_b16:
+            ops.round_bf16(self.pool.b16, dst.b16, plan, n=lay.n_b16, mode=self.mode)
+        if lay.n_i64:
+            ops.round_i64(self.pool.i64, dst.i64, plan, n=lay.n_i64)
 
 
 def calibrated_pool(layout, rows: int, device, trials: int = 8, degree: int = 8) -> ModelPool:
