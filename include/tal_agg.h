@@ -315,12 +315,16 @@ int32_t tal_agg_round_reg(const void* pool_in, int64_t ld_in, void* pool_out, in
  *
  * seg_host: 4*n_seg int64 {offset (elements into the flat parameter arena), A, I, B}.
  * The plan (int64 words, tal_cosine_plan_words; copied to the device by the caller, and the
- * host copy passed too) = {n_seg, n_outputs, threads}, per tensor {offset, A, I, B, first output,
- * kind}, per workgroup chunk {tensor, first output, count, 0}.
+ * host copy passed too) = {n_seg, n_outputs, threads, streamed chunks}, per tensor {offset, A,
+ * I, B, first output, kind, outputs per chunk}, per workgroup chunk {tensor, first output, count,
+ * streamed}.  Column tensors with B < 32 (3 x 3 convolutions) run streamed (ABI 25): every
+ * model's norms in one launch, then each pair's products, both walking i in 16-element steps
+ * through LDS; the others one thread (or 8 lanes) per output.
  *
  * a_ptrs_host / b_ptrs_host: n_pairs device pointers; pair j compares model a_j with b_j
  * (flat fp32 parameter arenas of the same layout).  scratch: device buffer of at least
- * tal_cosine_scratch_bytes(plan_host, n_pairs) bytes.  out_dev: n_pairs fp32 results. */
+ * tal_cosine_scratch_bytes(plan_host, n_pairs) bytes (ABI 25: 4 (3 n_outputs + n_seg) per pair
+ * of a launch of up to 32 pairs).  out_dev: n_pairs fp32 results. */
 int64_t tal_cosine_plan_words(const int64_t* seg_host, int32_t n_seg);
 int32_t tal_cosine_plan_build(const int64_t* seg_host, int32_t n_seg, int64_t* plan_host,
                               int64_t plan_capacity_words, int32_t* n_chunks);

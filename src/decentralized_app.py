@@ -346,7 +346,7 @@ class DecentrallearnApp:
             self.round_cache_hits += 1
             if self.seed is not None:
                 manual_seed(self.seed)
-            self._executor.run(hit["orders"], hit["weights"], hit["out_rows"])
+            self._executor.run(hit["orders"], hit["weights"], hit["out_rows"], plan=hit["plan"])
             return [memo[id(e[2])] for e in batch]
         row_of: dict = {}  # id(model) -> pool row
 
@@ -377,12 +377,13 @@ class DecentrallearnApp:
         if orders:
             if self._executor is None:
                 self._executor = RoundExecutor(self.pool)
-            self._executor.run(orders, weights, out_rows)
+            plan = self._executor.plan(orders, weights, out_rows)
+            self._executor.run(orders, weights, out_rows, plan=plan)
             if key is not None:
                 if len(self._round_cache) > 16:
                     self._round_cache.clear()
                 rows = {v[1].idx: row_of[id(v[1].model)] for v in memo.values() if id(v[1].model) in row_of}
-                self._round_cache[key] = dict(orders=orders, weights=weights, out_rows=out_rows,
+                self._round_cache[key] = dict(orders=orders, weights=weights, out_rows=out_rows, plan=plan,
                                               text=text.getvalue(), gen=arena._GEN[0], rows=sorted(rows.items()))
         return done
 

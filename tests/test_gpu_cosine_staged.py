@@ -1,12 +1,14 @@
-"""K2's staged chunks (round 6): whole output slabs of both models of a pair in LDS, the norms'
-chains, the level-0 cascade runs and each output's cascade / lane fold computed from there
-(k_cosine_staged).  Bitwise the oracle (torch's CPU order, oracle/cosine_oracle.c) at the
-edges of the staging: column tensors with B < 32 at every chunk size (the ResNet 3 x 3 convs'
-one slab per chunk at I = 512 up to 28 slabs for conv1's I = 3; the last chunk partial), slabs
-at the LDS capacity and one element past it (the direct form), streams whose length is not a
-multiple of the run width (a partial last run), row tensors of I < 8 (one sequence), 8 <= I
-with a tail past the last vector and rows at the capacity; segments starting at every 4-byte
-offset inside a 16-byte chunk; more pairs than one launch takes; a whole ResNet-50 model.
+"""K2's streamed column chunks (round 6): a column tensor [A, I, B] with B < 32 runs as two
+kernels that walk i in 16-element steps through LDS - every model's norms (torch's FMA chains),
+then each pair's products (the four streams' level-0 runs pushed into their cascades every 64
+elements) - k_cos_col_norms / k_cos_col_prods; the other tensors run the direct form.  Bitwise
+the oracle (torch's CPU order, oracle/cosine_oracle.c) at the edges: column tensors with B from
+2 to 31 (output blocks per chunk 14 .. 1, the tensor's last chunk partial), I below 4 (only the
+remainder), I not a multiple of the step (a partial last step) or of 4 (row_sum's remainder),
+streams whose length is not a multiple of the run (a partial last run), 1,024 and 16,400
+elements (the cascade's second and third levels), B = 32 (the direct form); row tensors of every
+size class; segments starting at every 4-byte offset inside a 16-byte chunk; pairs sharing one
+`a` and pairs that do not; more pairs than one launch takes; a whole ResNet-50 model.
 Reference: cosine_similarity, /root/reference/src/decentralized_client.py:661-681.
 """
 from __future__ import annotations
@@ -30,6 +32,7 @@ _SHAPES = [
     (3, 4609, 1), (2, 513, 9),         # one element past the capacity: the direct form
     (5, 4608, 1), (7, 2048, 1), (33, 512, 1),
     (40, 7, 1), (9, 8, 1), (11, 13, 1), (6, 100, 1), (3, 1030, 1),
+    (2, 1024, 9), (1, 16400, 3), (3, 1001, 5), (2, 70, 28), (5, 33, 14), (4, 2, 7), (3, 50, 32),
 ]
 
 
@@ -73,11 +76,12 @@ def test_staged_more_pairs_than_one_launch(cuda):
     segs = [(0, 8, 64, 9), (4608, 16, 72, 1), (4608 + 1152, 30, 1, 1)]
     rows = _models(np.random.default_rng(3), segs, 36)
     _check(cuda, rows, segs, [0] * 35, list(range(1, 36)))
+    _check(cuda, rows, segs, list(range(18)), list(range(18, 36)))  # 18 pairs, each its own a
 
 
 def test_staged_resnet50_model(cuda):
-    """A whole ResNet-50 parameter set (161 tensors: 3 x 3 convs staged one slab per chunk, 1 x 1
-    convs as staged rows, 1-D parameters direct) for 3 pairs, against the oracle."""
+    """A whole ResNet-50 parameter set (161 tensors: 3 x 3 convs streamed, 1 x 1 convs and 1-D
+    parameters direct) for 3 pairs, against the oracle."""
     lay = synth.get_layout("resnet50")
     layout = StateLayout.from_layout(lay)
     segs = layout.param_segments(synth.param_names(lay))

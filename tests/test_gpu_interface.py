@@ -202,11 +202,11 @@ def test_driver_batched_round(cuda, tmp_path, monkeypatch):
     real_run = RoundExecutor.run
     runs = []
 
-    def checked_run(self, orders, weights, out_rows=None, sequential=False):
+    def checked_run(self, orders, weights, out_rows=None, sequential=False, plan=None):
         lay = self.pool.layout
         f_in = self.pool.f32[:, : lay.n_f32].cpu().numpy().copy()
         i_in = self.pool.i64[:, : lay.n_i64].cpu().numpy().copy()
-        real_run(self, orders, weights, out_rows, sequential)
+        real_run(self, orders, weights, out_rows, sequential, plan)
         rp, col, w = ra.round_csr(orders, weights)
         ref = oracle.round_f32(f_in, rp, col, w, np.asarray(out_rows))
         iref = oracle.round_i64(i_in, rp, col, w, np.asarray(out_rows))
@@ -253,11 +253,11 @@ def test_driver_batched_round_partial(cuda, tmp_path, monkeypatch, strategy, par
     real_run = RoundExecutor.run
     runs = []
 
-    def checked_run(self, orders, weights, out_rows=None, sequential=False):
+    def checked_run(self, orders, weights, out_rows=None, sequential=False, plan=None):
         lay = self.pool.layout
         f_in = self.pool.f32[:, : lay.n_f32].cpu().numpy().copy()
         i_in = self.pool.i64[:, : lay.n_i64].cpu().numpy().copy()
-        real_run(self, orders, weights, out_rows, sequential)
+        real_run(self, orders, weights, out_rows, sequential, plan)
         rp, col, w = ra.round_csr(orders, weights)
         ref = f_in.copy()
         iref = i_in.copy()

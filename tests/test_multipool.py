@@ -149,11 +149,11 @@ def test_driver_batched_round_virtual_gpus(cuda, tmp_path, monkeypatch, strategy
                 assert torch.equal(self.pools[q].i64[gr], self.pools[h].i64[r]), (q, gid)
         seen["halos"] += 1
 
-    def checked_run(self, orders, weights, out_rows=None, sequential=False):
+    def checked_run(self, orders, weights, out_rows=None, sequential=False, plan=None):
         lay = self.pool.layout
         f_in = self.pool.f32[:, : lay.n_f32].cpu().numpy().copy()
         i_in = self.pool.i64[:, : lay.n_i64].cpu().numpy().copy()
-        real_run(self, orders, weights, out_rows, sequential)
+        real_run(self, orders, weights, out_rows, sequential, plan)
         rp, col, w = ra.round_csr(orders, weights)
         ref, iref = f_in.copy(), i_in.copy()
         oracle.round_f32(f_in, rp, col, w, np.asarray(out_rows), pool_out=ref)

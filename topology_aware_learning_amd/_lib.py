@@ -27,7 +27,7 @@ TAL_ERR_COMM = 4
 TAL_COMM_ID_BYTES = 128
 TAL_MODE_FMA = 0
 TAL_MODE_EXACT = 1
-ABI_VERSION = 24
+ABI_VERSION = 25
 
 EXPORTED = (
     "tal_last_error",

@@ -45,7 +45,7 @@
 
 namespace {
 
-constexpr int kAbiVersion = 24;
+constexpr int kAbiVersion = 25;
 constexpr int kMaxOps = 256;     // operands per K1 launch (kernel-argument table, 3 KiB)
 constexpr int kBlock = 256;      // 4 wavefronts of 64 lanes
 constexpr uint32_t kMaskUniform = 0x80000000u;  // dense table mask flag: one weight for all rows
@@ -3002,25 +3002,24 @@ constexpr int kCosVw = 8;          // Vectorized<float> width of torch's sum ker
 enum { kCosElem = 0, kCosRow = 1, kCosCol = 2 };
 constexpr int64_t cos_chunk_outputs(int kind) { return kind == kCosRow ? kCosBlock / kCosVw : kCosBlock; }
 
-// Staged chunks (round 6): a workgroup stages whole output slabs of both models of one pair -
-// consecutive rows x[o, :] (row kind) or consecutive [I, B] blocks x[o, :, :] (column kind
-// with B < 32), contiguous in memory - into LDS with coalesced 16-B loads, then runs every
-// chain from LDS: the norms' serial FMA chains (torch's order), the products' level-0 cascade
-// runs (independent: each starts from 0), then each output's cascade / lane fold.  The direct
-// form (one thread or 8 lanes per output, loads strided by B or 8 lanes 32 B wide) was bound by
-// the strided gather (37.7 L1 accesses per load instruction, profiles/r05/r05k2pmc).
-// A workgroup holds the aggregating model's slabs and those of kCosStagePairs neighbors: 4 x 18
-// KiB + 7.3 KiB of norms, reciprocals, lane and run sums < 80 KiB: two workgroups per CU
-constexpr int kCosStagePairs = 3;      // pairs per workgroup (the models: a, then each pair's b)
-constexpr int kCosStageFloats = 4608;  // per model (18 KiB): one ResNet-50 512 x 512 x 3 x 3 slab
-// LDS stride between staged models: 16 floats of slack (a column chunk is stored at its global
-// 16-B phase, up to 3 floats past the model's base) and 16 (mod 64) so that the same element of
-// the four models falls in four different bank groups (the norm chains of one wave read them at once)
-constexpr int kCosStageStride = kCosStageFloats + 16;
-constexpr int kCosStageOut = 64;       // outputs per staged chunk
-constexpr int kCosStageRows = 16;      // row-kind rows per staged chunk (lane accumulators in LDS)
-constexpr int kCosStageItems = 288;    // level-0 runs per staged chunk and pair
-constexpr int kCosStageBlock = 256;
+// Streamed column chunks (round 6): a column tensor [A, I, B] with B < 32 (the 3 x 3
+// convolutions) reduces every output (o, k) over i with stride B; the direct form's lanes gather
+// from ~7 slabs 18 KB apart (37.7 L1 accesses per load instruction, profiles/r05/r05k2pmc).  The
+// streamed form walks i in steps of kColIc: each step moves x[o0 .. o0 + Ob, i0 .. i0 + kColIc, :]
+// of every model of the workgroup (Ob contiguous runs of kColIc B floats each) into LDS with
+// coalesced loads, kColDepth steps in flight in registers, and every chain - one thread per
+// (output, model) or (output, pair) - advances kColIc elements from LDS in its own order.  Two
+// kernels: the norms (torch's FMA chains, every distinct model once, k_cos_col_norms), then the
+// products (each pair's four streams' level-0 runs, pushed into their cascades every 64 elements
+// as multi_row_sum pushes them, k_cos_col_prods).  Every chain of a chunk runs at once: the
+// round-6 slab-staged form ran one 512 x 9 slab per workgroup, 36 norm chains on 256 threads.
+constexpr int kColIc = 16;       // i per step: a quarter of the four streams' 16-element runs
+constexpr int kColThreads = 256;
+constexpr int kColModels = 9;    // LDS models per workgroup: 9 models' norms, or a + 8 pairs' b
+constexpr int kColPairs = 8;     // pairs per product workgroup when they share a (else 4)
+constexpr int kColMS = 1024;     // LDS floats per model at most (Ob pitch-padded output blocks)
+constexpr int kColDepth = 4;     // steps in flight
+static_assert(31 * kColIc <= 2 * kColThreads, "a model's step is at most two elements per thread");
 
 __host__ __device__ inline int64_t cos_log2_ceil(int64_t x) {
   int64_t r = 0;
@@ -3034,62 +3033,21 @@ __host__ __device__ inline int64_t cos_lp(int64_t size) {
   return l > 4 ? l : 4;
 }
 
-// row_sum over `len` elements: 4 interleaved streams of len / 4, each cut into level-0 runs of
-// 2^lp (the last one partial); runs per stream
-__host__ __device__ inline int64_t cos_runs(int64_t len) {
-  const int64_t si = len / 4;
-  const int64_t step = int64_t{1} << cos_lp(si);
-  return (si + step - 1) / step;
+// output blocks (B outputs each) per streamed chunk: chains Ob B <= 28 (B < 29)
+__host__ __device__ inline int cos_col_ob(int64_t B) { return B >= 28 ? 1 : static_cast<int>(28 / B); }
+
+// LDS pitch of one output block's kColIc x B floats, = B (mod 64): chain c = o B + k of model
+// slot g (model stride Ob P = Ob B = C, mod 64) reads bank (g C + c + i B) mod 64 = (lane + i B)
+// mod 64, so a wave's reads of one element index are conflict-free
+__host__ __device__ inline int cos_col_pitch(int64_t B) {
+  const int b = static_cast<int>(B);
+  return b * kColIc + ((b * (1 - kColIc)) % 64 + 64) % 64;
 }
 
-// A staged output's row_sum sequences: nl lanes (8: torch's vector lanes over a contiguous row
-// of >= 8; else 1) of `len` elements each
-__host__ __device__ inline void cos_stage_seq(int kind, int64_t I, int64_t* nl, int64_t* len) {
-  if (kind == kCosRow && I >= kCosVw) {
-    *nl = kCosVw;
-    *len = I / kCosVw;
-  } else {
-    *nl = 1;
-    *len = I;
-  }
-}
-
-// LDS pitch of a staged row (row kind): I padded to 8 (mod 64) floats, so the 8 rows a wave's
-// lanes read at once (8 lanes each: torch's vector lanes) sit on 8 different bank octets
-__host__ __device__ inline int64_t cos_row_pitch(int64_t I) { return I + (72 - I % 64) % 64; }
-
-// LDS floats of one slab: the column kind's [I, B] block as it is in memory (a sequence x[o, :, k]
-// is strided by B; consecutive outputs' chains read consecutive words), a row at its pitch
-__host__ __device__ inline int64_t cos_slab_floats(int kind, int64_t I, int64_t B) {
-  return kind == kCosCol ? I * B : cos_row_pitch(I);
-}
-
-// The staged row form is kept for A/B measurement (tal_cosine_plan_build's tensors of the row
-// kind run the direct form unless TAL_COS_STAGE_ROWS=1 is set when the library loads).
-static const bool g_cos_stage_rows = [] {
-  const char* v = getenv("TAL_COS_STAGE_ROWS");
-  return v && v[0] == '1';
-}();
-
-// slabs (output blocks: B outputs of the column kind, one row of the row kind) per staged chunk;
-// 0 = the tensor runs the direct form
-inline int64_t cos_stage_slabs(int kind, int64_t A, int64_t I, int64_t B) {
-  if (kind == kCosElem || (kind == kCosCol && B >= 32)) return 0;  // coalesced as it is
-  // rows: the direct form's 8 lanes per row read 32 contiguous bytes each and beat the staged
-  // form (ResNet-50's 37 row tensors, 8 pairs: 0.25 against 0.34-0.40 ms, profiles/r06/r06k4-5)
-  if (kind == kCosRow && !g_cos_stage_rows) return 0;
-  const int64_t slab = cos_slab_floats(kind, I, B);
-  if (slab > kCosStageFloats) return 0;
-  int64_t nl, len;
-  cos_stage_seq(kind, I, &nl, &len);
-  const int64_t outs = kind == kCosCol ? B : 1;
-  const int64_t items = outs * nl * 4 * cos_runs(len);
-  if (items > kCosStageItems) return 0;
-  int64_t g = kCosStageFloats / slab;
-  g = std::min<int64_t>(g, kCosStageOut / outs);
-  if (kind == kCosRow) g = std::min<int64_t>(g, kCosStageRows);
-  if (items > 0) g = std::min<int64_t>(g, kCosStageItems / items);
-  return std::max<int64_t>(1, std::min(g, A));
+// a column tensor runs the streamed form when B < 32 and its streams' level-0 runs are 16 long
+// (multi_row_sum's level width 2^4: every I below 2^22)
+inline bool cos_col_streamed(int kind, int64_t I, int64_t B) {
+  return kind == kCosCol && B < 32 && cos_lp(I / 4) == 4 && cos_col_ob(B) * cos_col_pitch(B) <= kColMS;
 }
 
 struct CosPairs {
@@ -3313,155 +3271,6 @@ __global__ __launch_bounds__(kCosBlock) void k_cosine_outputs(CosPairs pr, const
   if (l == 0 && live) s[q] = __fadd_rn(0.f, fin);
 }
 
-// ---- staged chunks (see kCosStageFloats) ---------------------------------------------------
-// The cascades of a row_sum's four streams (si elements each) from their level-0 run sums
-// R(run, stream): the levels are pushed at the element counts multi_row_sum pushes them
-// (cos_multi_row; the same counts for the four streams, so they advance together and each
-// step's four run sums are read at once), the partial last run (si not a multiple of the run
-// width) is the level-0 value at the end.  Every run sum starts from 0, as acc[0] does after each
-// push, so this is cos_multi_row's arithmetic exactly; out[st] = stream st's result.
-template <class Runs>
-__device__ __forceinline__ void cos_cascade_runs4(Runs R, int si, float* out) {
-  const int lp = static_cast<int>(cos_lp(si));
-  const int step = 1 << lp, mask0 = step - 1;
-  const int full = si / step;
-  float a1[4] = {0.f, 0.f, 0.f, 0.f}, a2[4] = {0.f, 0.f, 0.f, 0.f}, a3[4] = {0.f, 0.f, 0.f, 0.f};
-  float nxt[4];
-#pragma unroll
-  for (int st = 0; st < 4; ++st) nxt[st] = full > 0 ? R(0, st) : 0.f;
-  int i = 0;
-  for (int r = 0; r < full; ++r) {
-    float cur[4];
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      cur[st] = nxt[st];
-      if (r + 1 < full) nxt[st] = R(r + 1, st);
-    }
-    i += step;
-#pragma unroll
-    for (int st = 0; st < 4; ++st) a1[st] = __fadd_rn(a1[st], cur[st]);
-    if (i & (mask0 << lp)) continue;
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      a2[st] = __fadd_rn(a2[st], a1[st]);
-      a1[st] = 0.f;
-    }
-    if (i & (mask0 << (2 * lp))) continue;
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      a3[st] = __fadd_rn(a3[st], a2[st]);
-      a2[st] = 0.f;
-    }
-  }
-  const bool part = full * step < si;
-#pragma unroll
-  for (int st = 0; st < 4; ++st) {
-    const float a0 = part ? R(full, st) : 0.f;
-    out[st] = __fadd_rn(__fadd_rn(__fadd_rn(a0, a1[st]), a2[st]), a3[st]);
-  }
-}
-
-// q, r of e / d (e < 2^22, 0 < d): a float-reciprocal estimate within one of the quotient, fixed
-__device__ __forceinline__ int cos_divmod(int e, int d, float inv_d, int* rem) {
-  int q = static_cast<int>(static_cast<float>(e) * inv_d);
-  int r = e - q * d;
-  if (r < 0) { --q; r += d; }
-  else if (r >= d) { ++q; r -= d; }
-  *rem = r;
-  return q;
-}
-
-// The chunk's ne floats of nm models (model 0: the aggregating model, default cache policy - every
-// pair group re-reads it; the others non-temporal, read once) into LDS, model m at m
-// kCosStageStride (the column kind at its global 16-B phase: element e at + e + mis, one 16-B
-// LDS write per load), by 16-B loads from each pointer's 16-B aligned base (a 16-B chunk holding one
-// element of the range lies in that element's page), every load of a batch in flight before the
-// first LDS write.  The column kind keeps the memory layout; a row (ROW) goes to lds[g Pr + i],
-// Pr = cos_row_pitch(I) (the row and column of a chunk's first element found once, then stepped).
-template <bool ROW>
-__device__ __forceinline__ void cos_stage(const float* const* gm, int nm, int ne, float* lds, int I, int Pr) {
-  const float inv_i = 1.f / static_cast<float>(I);
-  constexpr int kU = (kCosStageFloats / 4 + kCosStageBlock - 1) / kCosStageBlock + 1;  // 6
-  constexpr int kM = kCosStagePairs + 1;
-  int mis[kM], n4[kM];
-  const v4f* g4[kM];
-#pragma unroll
-  for (int m = 0; m < kM; ++m) {
-    const float* g = m < nm ? gm[m] : gm[0];
-    mis[m] = static_cast<int>((reinterpret_cast<uintptr_t>(g) >> 2) & 3);
-    g4[m] = reinterpret_cast<const v4f*>(g - mis[m]);
-    n4[m] = m < nm ? (ne + mis[m] + 3) / 4 : 0;
-  }
-  auto put = [&](const v4f& t, int v, int mis_, float* dst0) {
-    if constexpr (!ROW) {  // the chunk at its global 16-B phase: element e at dst0[e + mis]
-      *reinterpret_cast<v4f*>(dst0 + 4 * v) = t;
-      return;
-    }
-    const int e = 4 * v - mis_;  // element of t[0]
-    const int e0 = e < 0 ? 0 : e;
-    int c = e0;
-    int g = cos_divmod(e0, I, inv_i, &c);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int ek = e + k;
-      if (ek < e0 || ek >= ne) continue;
-      dst0[g * Pr + c] = t[k];
-      if (++c == I) {
-        c = 0;
-        ++g;
-      }
-    }
-  };
-  const int nmax = (ne + 3 + 3) / 4;
-  for (int v0 = threadIdx.x; v0 < nmax; v0 += kU * kCosStageBlock) {
-    v4f t[kM][kU];
-#pragma unroll
-    for (int m = 0; m < kM; ++m)
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int v = v0 + u * kCosStageBlock;
-        if (v < n4[m]) t[m][u] = m == 0 ? g4[m][v] : __builtin_nontemporal_load(g4[m] + v);
-      }
-#pragma unroll
-    for (int m = 0; m < kM; ++m)
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int v = v0 + u * kCosStageBlock;
-        if (v < n4[m]) put(t[m][u], v, mis[m], lds + m * kCosStageStride);
-      }
-  }
-}
-
-// torch NormTwoOps over x[0], x[S], x[2 S], ... (n elements): fma in index order; the reads a
-// batch ahead of the FMAs.  S > 0: compile-time stride (immediate LDS offsets); S == 0: `rs`
-template <int S>
-__device__ __forceinline__ float cos_norm_chain(const float* x, int n, int rs = 0) {
-  constexpr int kB = 16;
-  const int st = S > 0 ? S : rs;
-  float acc = 0.f;
-  float cur[kB], nxt[kB];
-  const int nb = n / kB;
-  auto load = [&](float* v, const float* p) {
-#pragma unroll
-    for (int u = 0; u < kB; ++u) v[u] = p[u * st];
-  };
-  if (nb > 0) load(cur, x);
-  for (int b = 0; b < nb; ++b) {
-    if (b + 1 < nb) load(nxt, x + (b + 1) * kB * st);
-#pragma unroll
-    for (int u = 0; u < kB; ++u) acc = __fmaf_rn(cur[u], cur[u], acc);
-#pragma unroll
-    for (int u = 0; u < kB; ++u) cur[u] = nxt[u];
-  }
-  for (int i = nb * kB; i < n; ++i) acc = __fmaf_rn(x[i * st], x[i * st], acc);
-  return acc;
-}
-
-// ((x1 / na) * (x2 / nb)) for two staged models (x2 = x1 + ob: the pair's b)
-__device__ __forceinline__ float cos_prod(const float* x, int ob, float na, float nb) {
-  return __fmul_rn(__fdiv_rn(x[0], na), __fdiv_rn(x[ob], nb));
-}
-
 // x / n with the IEEE division's result, without its scaling steps (each writes VCC, which the
 // next division's v_div_fmas reads, so divisions serialise): y = RN(1 / n) once per norm, then
 // q0 = RN(x y) and q = RN(q0 + RN(x - n q0) y) (both fused).  Equal to RN(x / n) for n in
@@ -3479,209 +3288,248 @@ __device__ __forceinline__ bool cos_rdiv_n(float n) {  // n in [2^-40, 2^40]
   return __float_as_uint(n) - 0x2B800000u <= 0x28000000u;
 }
 
-// One level-0 run: elements 0, S, 2 S, ... (n of them; S == 0: stride rs) summed from 0 in order,
-// products a batch ahead.  FAST (both norms in cos_rdiv's range): the reciprocal division, a
-// batch falling back to __fdiv_rn on the lanes holding an element outside its range.
-template <int S, bool FAST>
-__device__ __forceinline__ float cos_run(const float* x, int ob, int n, float na, float nb, float ya, float yb, int rs) {
-  const int st = S > 0 ? S : rs;
-  const float* y = x + ob;
-  float acc = 0.f;
-  int i = 0;
-  for (; i + 8 <= n; i += 8, x += 8 * st, y += 8 * st) {
-    float p[8];
-    if constexpr (FAST) {
-      bool ok = true;
+// ---- streamed column chunks (see kColIc) ---------------------------------------------------
+struct ColChunk {
+  int I, B, C, Cf, P, MS, Ob;
+  int64_t off;   // element offset of the chunk's first output block in a model
+  int64_t out0;  // the chunk's first output (plan-wide)
+};
+
+__device__ __forceinline__ ColChunk col_chunk(const int64_t* __restrict__ plan, int n_seg, int64_t c) {
+  const int64_t* ch = plan + kCosHdr + kCosSegWords * static_cast<int64_t>(n_seg) + kCosChunkWords * c;
+  const int64_t* sg = plan + kCosHdr + kCosSegWords * ch[0];
+  ColChunk k;
+  k.I = static_cast<int>(sg[2]);
+  k.B = static_cast<int>(sg[3]);
+  k.C = static_cast<int>(ch[2]);  // the chunk's outputs: Ob B (the tensor's last chunk: fewer blocks)
+  k.Ob = k.C / k.B;
+  k.Cf = cos_col_ob(k.B) * k.B;   // a full chunk's chains: the thread and bank pattern
+  k.P = cos_col_pitch(k.B);
+  k.MS = cos_col_ob(k.B) * k.P;
+  k.off = sg[0] + ch[1] * k.I;     // first output o0 B -> element o0 I B
+  k.out0 = sg[4] + ch[1];
+  return k;
+}
+
+// One thread's share of a step.  A model's part of a step is Ob blocks x kColIc B floats <= 2
+// kColThreads (Ob B <= 31), so thread t moves elements t and t + kColThreads of every model: one
+// per-thread offset pair serves all the models, whose base pointers are uniform (SGPRs).
+struct ColLoads {
+  const float* gm[kColModels];  // model m's first element of the chunk
+  int64_t go[2];                // offset of element h kColThreads + t in a model (without i0 B)
+  int lo[2];                    // its LDS index in model 0's area (+ m MS)
+  int r[2];                     // its position inside its block's kColIc B run; INT_MAX: none
+  int nmod, MS;
+};
+
+__device__ __forceinline__ void col_loads_init(ColLoads& L, const float* const* gm, int nmod, const ColChunk& k) {
+  const int run = kColIc * k.B;
+  const int per_m = k.Ob * run;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float xa = x[u * st], xb = y[u * st];
-        ok = ok && cos_rdiv_x(xa) && cos_rdiv_x(xb);
-        p[u] = __fmul_rn(cos_rdiv(xa, na, ya), cos_rdiv(xb, nb, yb));
+  for (int m = 0; m < kColModels; ++m) L.gm[m] = gm[m] + k.off;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int e = static_cast<int>(threadIdx.x) + h * kColThreads;
+    const int o = e / run, r = e - o * run;
+    L.go[h] = static_cast<int64_t>(o) * k.I * k.B + r;
+    L.lo[h] = o * k.P + r;
+    L.r[h] = e < per_m ? r : 0x7fffffff;
+  }
+  L.nmod = nmod;
+  L.MS = k.MS;
+}
+
+// The chunk's steps: kColDepth steps' loads in flight in a register ring; each step waits for
+// its loads, writes them to LDS and issues the loads kColDepth steps ahead, then every chain
+// advances over the step's n <= kColIc elements (step(i0, n)).  The loads are unconditional
+// (a load outside the chunk re-reads the model's first chunk element and is not stored) and
+// the steps run in whole groups of kColDepth, so the loop body is straight-line code and each
+// step waits only for its own loads.
+template <class Step>
+__device__ __forceinline__ void col_stream(const ColLoads& L, int I, int B, float* lds, Step step) {
+  const int nsteps = (I + kColIc - 1) / kColIc;
+  float ring[kColDepth][2 * kColModels];
+  int64_t go[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) go[h] = L.r[h] == 0x7fffffff ? 0 : L.go[h];
+  auto issue = [&](float* v, int s) {
+    const int i0 = s * kColIc;
+    const int lim = min(kColIc, I - i0) * B;  // <= 0 past the last step
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t a = L.r[h] < lim ? go[h] + static_cast<int64_t>(i0) * B : 0;
+#pragma unroll
+      for (int m = 0; m < kColModels; ++m) v[2 * m + h] = L.gm[m][a];  // m >= nmod: the last model again
+    }
+  };
+#pragma unroll
+  for (int d = 0; d < kColDepth; ++d) issue(ring[d], d);
+  for (int s0 = 0; s0 < nsteps; s0 += kColDepth) {
+#pragma unroll
+    for (int d = 0; d < kColDepth; ++d) {
+      const int s = s0 + d;
+      const int n = min(kColIc, I - s * kColIc);  // <= 0: no step (the group's tail)
+      __syncthreads();  // the previous step's chains are done with the LDS
+#pragma unroll
+      for (int m = 0; m < kColModels; ++m)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          if (m < L.nmod && L.r[h] < n * B) lds[m * L.MS + L.lo[h]] = ring[d][2 * m + h];
+      issue(ring[d], s + kColDepth);
+      __syncthreads();
+      if (n > 0) step(s * kColIc, n);
+    }
+  }
+}
+
+// Norms: one workgroup per (streamed chunk, group of model slots); thread (g, c): model slot
+// m0 + g, output c of the chunk: |x| = sqrt(fma chain over i in index order), clamped (torch's
+// NormTwoOps over dim 1, cosine_similarity's clamp_min), into nrm[slot n_out + output].
+__global__ __launch_bounds__(kColThreads) void k_cos_col_norms(CosPairs pr, const int64_t* __restrict__ plan, int n_seg,
+                                                              int cnt, int same_a, float* __restrict__ nrm) {
+  __shared__ float lds[kColModels * kColMS];
+  const ColChunk k = col_chunk(plan, n_seg, blockIdx.x);
+  const int n_models = same_a ? 1 + cnt : 2 * cnt;
+  const int nmw = min(kColModels, kColThreads / k.Cf);
+  const int m0 = static_cast<int>(blockIdx.y) * nmw;
+  if (m0 >= n_models) return;
+  const int nmod = min(nmw, n_models - m0);
+  const float* gm[kColModels];
+#pragma unroll
+  for (int m = 0; m < kColModels; ++m) {
+    // model slot s: one a shared by all pairs (slot 0 = a, 1 + p = b_p) or one per pair (2 p = a_p,
+    // 2 p + 1 = b_p); the kernel argument is indexed in place (a reference to it would copy it
+    // to scratch)
+    const int sl = m0 + min(m, nmod - 1);
+    gm[m] = same_a ? (sl == 0 ? pr.a[0] : pr.b[sl - 1]) : ((sl & 1) ? pr.b[sl >> 1] : pr.a[sl >> 1]);
+  }
+  ColLoads L;
+  col_loads_init(L, gm, nmod, k);
+  const int t = threadIdx.x, g = t / k.Cf, c = t - g * k.Cf;
+  const bool live = g < nmod && c < k.C;
+  const int o = c / k.B, kk = c - o * k.B;
+  const float* x = lds + (live ? g * k.MS + o * k.P + kk : 0);
+  const int B = k.B;
+  float acc = 0.f;
+  col_stream(L, k.I, B, lds, [&](int, int n) {
+    if (!live) return;
+    if (n == kColIc) {
+      float v[kColIc];
+#pragma unroll
+      for (int i = 0; i < kColIc; ++i) v[i] = x[i * B];
+#pragma unroll
+      for (int i = 0; i < kColIc; ++i) acc = __fmaf_rn(v[i], v[i], acc);
+    } else {
+      for (int i = 0; i < n; ++i) acc = __fmaf_rn(x[i * B], x[i * B], acc);
+    }
+  });
+  if (live) nrm[static_cast<int64_t>(m0 + g) * plan[1] + k.out0 + c] = cos_clamp(cos_sqrt_rn(acc));
+}
+
+// Products: one workgroup per (streamed chunk, group of pairs); thread (g, c): pair p0 + g, output
+// c.  row_sum over the I products (x_a / n_a) (x_b / n_b): four interleaved streams of I / 4,
+// each summed in 16-element level-0 runs from 0 (cos_run) that are pushed into the stream's
+// cascade (cos_cascade: level 1 every run, level 2 every 16, level 3 every 256 - multi_row_sum's
+// counts at width 2^4), the partial last run at the end, the I mod 4 remainder into stream 0,
+// then the streams in order; s = 0 + that.  Divisions: cos_rdiv where both norms and the element
+// are in its range (equal to the IEEE quotient there), else __fdiv_rn.
+__global__ __launch_bounds__(kColThreads) void k_cos_col_prods(CosPairs pr, const int64_t* __restrict__ plan, int n_seg,
+                                                              int cnt, int same_a, const float* __restrict__ nrm,
+                                                              float* __restrict__ s_all) {
+  __shared__ float lds[kColModels * kColMS];
+  const ColChunk k = col_chunk(plan, n_seg, blockIdx.x);
+  const int ppw = same_a ? kColPairs : kColPairs / 2;
+  const int p0 = static_cast<int>(blockIdx.y) * ppw;
+  if (p0 >= cnt) return;
+  const int np = min(ppw, cnt - p0);
+  const int nmod = same_a ? 1 + np : 2 * np;
+  const float* gm[kColModels];
+#pragma unroll
+  for (int m = 0; m < kColModels; ++m) {
+    const int mm = min(m, nmod - 1);
+    gm[m] = same_a ? (mm == 0 ? pr.a[p0] : pr.b[p0 + mm - 1]) : ((mm & 1) ? pr.b[p0 + (mm >> 1)] : pr.a[p0 + (mm >> 1)]);
+  }
+  ColLoads L;
+  col_loads_init(L, gm, nmod, k);
+  const int t = threadIdx.x, g = t / k.Cf, c = t - g * k.Cf;
+  const bool live = g < np && c < k.C;
+  const int o = c / k.B, kk = c - o * k.B;
+  const int ma = same_a ? 0 : 2 * g, mb = same_a ? 1 + g : 2 * g + 1;
+  const int64_t n_out = plan[1];
+  float na = 1.f, nb = 1.f;
+  if (live) {
+    const int sa = same_a ? 0 : 2 * (p0 + g), sb = same_a ? 1 + p0 + g : 2 * (p0 + g) + 1;
+    na = nrm[sa * n_out + k.out0 + c];
+    nb = nrm[sb * n_out + k.out0 + c];
+  }
+  const float ya = __fdiv_rn(1.f, na), yb = __fdiv_rn(1.f, nb);
+  const bool fast = cos_rdiv_n(na) && cos_rdiv_n(nb);
+  const float* xa = lds + (live ? ma * k.MS + o * k.P + kk : 0);
+  const float* xb = lds + (live ? mb * k.MS + o * k.P + kk : 0);
+  const int B = k.B;
+  const int e4 = 4 * (k.I / 4);  // the streams' elements; the rest is row_sum's remainder
+  auto prod = [&](float u, float w) {
+    const float qa = fast && cos_rdiv_x(u) ? cos_rdiv(u, na, ya) : __fdiv_rn(u, na);
+    const float qb = fast && cos_rdiv_x(w) ? cos_rdiv(w, nb, yb) : __fdiv_rn(w, nb);
+    return __fmul_rn(qa, qb);
+  };
+  float acc[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f}, a2[4] = {0.f, 0.f, 0.f, 0.f},
+        a3[4] = {0.f, 0.f, 0.f, 0.f};
+  int pushed = 0;  // elements per stream in completed runs
+  col_stream(L, k.I, B, lds, [&](int i0, int n) {
+    if (!live) return;
+    float p[kColIc];
+    if (n == kColIc && i0 + kColIc <= e4) {  // a whole step of stream elements (all but the last)
+      // the reciprocal division for all 16, the IEEE one for the step if any element (or norm)
+      // is outside its range: one branch per step
+      bool ok = fast;
+#pragma unroll
+      for (int i = 0; i < kColIc; ++i) {
+        const float u = xa[i * B], w = xb[i * B];
+        ok = ok && cos_rdiv_x(u) && cos_rdiv_x(w);
+        p[i] = __fmul_rn(cos_rdiv(u, na, ya), cos_rdiv(w, nb, yb));
       }
       if (!ok) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) p[u] = __fmul_rn(__fdiv_rn(x[u * st], na), __fdiv_rn(y[u * st], nb));
+        for (int i = 0; i < kColIc; ++i) p[i] = __fmul_rn(__fdiv_rn(xa[i * B], na), __fdiv_rn(xb[i * B], nb));
       }
+#pragma unroll
+      for (int i = 0; i < kColIc; ++i) acc[i & 3] = __fadd_rn(acc[i & 3], p[i]);
     } else {
-#pragma unroll
-      for (int u = 0; u < 8; ++u) p[u] = __fmul_rn(__fdiv_rn(x[u * st], na), __fdiv_rn(y[u * st], nb));
+      for (int i = 0; i < n && i0 + i < e4; ++i) acc[i & 3] = __fadd_rn(acc[i & 3], prod(xa[i * B], xb[i * B]));
     }
+    if (((i0 + kColIc) & 63) == 0 && i0 + kColIc <= e4) {  // every stream's run of 16 complete
+      pushed += 16;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc = __fadd_rn(acc, p[u]);
-  }
-  for (; i < n; ++i, x += st, y += st) acc = __fadd_rn(acc, __fmul_rn(__fdiv_rn(x[0], na), __fdiv_rn(y[0], nb)));
-  return acc;
-}
-
-template <int S>
-__device__ __forceinline__ float cos_run_any(const float* x, int ob, int n, float na, float nb, float ya, float yb,
-                                             int rs) {
-  if (cos_rdiv_n(na) && cos_rdiv_n(nb)) return cos_run<S, true>(x, ob, n, na, nb, ya, yb, rs);
-  return cos_run<S, false>(x, ob, n, na, nb, ya, yb, rs);
-}
-
-// A staged chunk's arithmetic after its slabs are in LDS (sx: model m at m kCosStageFloats;
-// model 0 = a, model p + 1 = pair p's b, np pairs).  Column kind (ROW false): output q = o B + k is
-// the sequence x[o I B + k + i B], i < I (CB: B at compile time, 0: runtime); row kind: row q at
-// q Pr, torch's 8 lanes (I >= 8) or one sequence.  Norms of every model, then every pair's level-0
-// runs, then each sequence's cascades and the lane fold - cos_row_sum / cos_multi_row's operations
-// in their order.  s: pair 0's outputs of the chunk; pair p's at s + p n_out.
-template <bool ROW, int CB>
-__device__ __forceinline__ void cos_staged_body(const float* sx, const int* mb, float (*sn)[kCosStageOut],
-                                                float (*sy)[kCosStageOut], float* sl, float* sr, int np, int nq, int I,
-                                                int Bq, int Pr, float* s, int64_t n_out) {
-  // mb[m]: LDS offset of model m's element 0 (model 0 = a)
-  const int tid = threadIdx.x;
-  const int nm = np + 1;
-  const int B = CB > 0 ? CB : Bq;
-  const float inv_b = 1.f / static_cast<float>(B);
-  auto col_base = [&](int q) {  // o I B + k
-    int k;
-    const int o = cos_divmod(q, B, inv_b, &k);
-    return o * I * B + k;
-  };
-  if constexpr (!ROW) {  // chains (model, output), strided by B; consecutive lanes, consecutive words
-    for (int j = tid; j < nm * nq; j += kCosStageBlock) {
-      const int m = j / nq, q = j - m * nq;
-      const float nrm = cos_clamp(cos_sqrt_rn(cos_norm_chain<CB>(sx + mb[m] + col_base(q), I, B)));
-      sn[m][q] = nrm;
-      sy[m][q] = __fdiv_rn(1.f, nrm);
-    }
-  } else {  // torch's reduce-lastdim norm: 8 lane accumulators over whole vectors, then the fold
-    const int nv = I / kCosVw;
-    for (int j = tid; j < nm * nq * kCosVw; j += kCosStageBlock) {
-      const int m = j / (nq * kCosVw), r = j - m * nq * kCosVw;
-      sl[j] = cos_norm_chain<kCosVw>(sx + mb[m] + (r >> 3) * Pr + (r & 7), nv);
-    }
-    __syncthreads();
-    for (int j = tid; j < nm * nq; j += kCosStageBlock) {
-      const int m = j / nq, g = j - m * nq;
-      const float* la = sl + (m * nq + g) * kCosVw;
-      float t = la[0];
+      for (int st = 0; st < 4; ++st) {
+        a1[st] = __fadd_rn(a1[st], acc[st]);
+        acc[st] = 0.f;
+      }
+      if ((pushed & (15 << 4)) == 0) {
 #pragma unroll
-      for (int l = 1; l < kCosVw; ++l) t = __fadd_rn(t, la[l]);
-      const float* x = sx + mb[m] + g * Pr;
-      int d = nv * kCosVw;
-      const int sep = (I - d) / 4 * 4;  // the tail: groups of 4 as square-then-add, the rest fused
-      for (int e = 0; e < sep; ++e, ++d) t = __fadd_rn(t, __fmul_rn(x[d], x[d]));
-      for (; d < I; ++d) t = __fmaf_rn(x[d], x[d], t);
-      const float nrm = cos_clamp(cos_sqrt_rn(t));
-      sn[m][g] = nrm;
-      sy[m][g] = __fdiv_rn(1.f, nrm);
-    }
-  }
-  __syncthreads();
-  // each output's row_sum sequences: nl lanes of len elements, element stride es
-  const int nl = (ROW && I >= kCosVw) ? kCosVw : 1;
-  const int len = nl > 1 ? I / kCosVw : I;
-  const int es = ROW ? nl : B;
-  const int si = len / 4;
-  const int step = 1 << static_cast<int>(cos_lp(si));
-  const int nr = (si + step - 1) / step;
-  auto base_of = [&](int q, int l) { return ROW ? q * Pr + l : col_base(q); };
-  // level-0 runs: item ((r * 4 + stream) * nq + q) * nl + l of pair p sums elements 4 i + stream
-  // of sequence (q, l), i in [r step, (r + 1) step) (the last run partial), from 0 in order
-  const int n_items = nq * nl * 4 * nr;
-  for (int ia = tid; ia < np * n_items; ia += kCosStageBlock) {
-    const int p = ia / n_items, it = ia - p * n_items;
-    const int l = it % nl;
-    int t = it / nl;
-    const int q = t % nq;
-    t /= nq;
-    const int st = t & 3, r = t >> 2;
-    const int i0 = r * step, n = min(step, si - i0);
-    const float* x = sx + mb[0] + base_of(q, l) + es * (4 * i0 + st);
-    const int ob = mb[p + 1] - mb[0];
-    const float na = sn[0][q], nb = sn[p + 1][q], ya = sy[0][q], yb = sy[p + 1][q];
-    float v;
-    if constexpr (ROW) {
-      v = nl > 1 ? cos_run_any<4 * kCosVw>(x, ob, n, na, nb, ya, yb, 0) : cos_run_any<4>(x, ob, n, na, nb, ya, yb, 0);
-    } else {
-      v = cos_run_any<4 * CB>(x, ob, n, na, nb, ya, yb, 4 * B);
-    }
-    sr[ia] = v;
-  }
-  __syncthreads();
-  // per (pair, sequence): the four streams' cascades, the row_sum remainder into stream 0, the
-  // streams in order (cos_row_sum); one lane: the output's sum; 8 lanes: their sums, folded below
-  const int rstride = 4 * nq * nl;  // between a sequence's consecutive runs of one stream
-  for (int ja = tid; ja < np * nq * nl; ja += kCosStageBlock) {
-    const int p = ja / (nq * nl), j = ja - p * nq * nl;
-    const int q = j / nl, l = j - q * nl;
-    const float na = sn[0][q], nb = sn[p + 1][q];
-    const int ob = mb[p + 1] - mb[0];
-    float ps[4];
-    const float* rs = sr + p * n_items + j;
-    cos_cascade_runs4([&](int r, int st) { return rs[r * rstride + st * nq * nl]; }, si, ps);
-    const float* x = sx + mb[0] + base_of(q, l);
-    for (int i = si * 4; i < len; ++i) ps[0] = __fadd_rn(ps[0], cos_prod(x + es * i, ob, na, nb));
-    const float v = __fadd_rn(__fadd_rn(__fadd_rn(ps[0], ps[1]), ps[2]), ps[3]);
-    if (nl == 1) s[p * n_out + q] = __fadd_rn(0.f, v);
-    else sl[ja] = v;  // the lane accumulators are spent
-  }
-  if (nl > 1) {  // vectorized_inner_sum: the scalar tail from 0, then the lanes in order
-    __syncthreads();
-    for (int qa = tid; qa < np * nq; qa += kCosStageBlock) {
-      const int p = qa / nq, q = qa - p * nq;
-      const float na = sn[0][q], nb = sn[p + 1][q];
-      const int ob = mb[p + 1] - mb[0];
-      float fin = 0.f;
-      for (int k2 = len * kCosVw; k2 < I; ++k2) fin = __fadd_rn(fin, cos_prod(sx + mb[0] + q * Pr + k2, ob, na, nb));
+        for (int st = 0; st < 4; ++st) {
+          a2[st] = __fadd_rn(a2[st], a1[st]);
+          a1[st] = 0.f;
+        }
+        if ((pushed & (15 << 8)) == 0) {
 #pragma unroll
-      for (int l = 0; l < kCosVw; ++l) fin = __fadd_rn(fin, sl[qa * kCosVw + l]);
-      s[p * n_out + q] = __fadd_rn(0.f, fin);
+          for (int st = 0; st < 4; ++st) {
+            a3[st] = __fadd_rn(a3[st], a2[st]);
+            a2[st] = 0.f;
+          }
+        }
+      }
     }
-  }
-}
-
-// One workgroup per (staged chunk, group of kCosStagePairs pairs): the chunk's slabs of a and of
-// the group's b's in LDS by coalesced 16-B loads, then cos_staged_body.  LDS indices are 32-bit
-// and chains walk pointers.
-__global__ __launch_bounds__(kCosStageBlock) void k_cosine_staged(CosPairs pr, const int64_t* __restrict__ plan,
-                                                                 int n_seg, int cnt, int pgs, float* __restrict__ s_all) {
-  constexpr int kM = kCosStagePairs + 1;
-  __shared__ __attribute__((aligned(16))) float sx[kM * kCosStageStride];
-  __shared__ float sn[kM][kCosStageOut];            // per model and output (row kind: row) norms
-  __shared__ float sy[kM][kCosStageOut];            // their reciprocals RN(1 / n) (cos_rdiv)
-  __shared__ float sl[kM * kCosVw * kCosStageRows];  // row kind: lane accumulators, then lane sums
-  __shared__ float sr[kCosStagePairs * kCosStageItems];  // level-0 run sums
-  // XCD-aware order: dispatch deals workgroups round-robin over the 8 XCDs, so the pair groups of
-  // one chunk (index 8 k + x) run one after another on XCD x, and every group after the first
-  // finds the aggregating model's slab (each pair's `a`) in that XCD's L2
-  const int npg = (cnt + pgs - 1) / pgs;  // pgs: pairs per group (1 when the pairs' a differ)
-  const int L = blockIdx.x;
-  const int kq = L >> 3;
-  const int pg = kq % npg;
-  const int64_t c = static_cast<int64_t>(kq / npg) * 8 + (L & 7);
-  if (c >= plan[3]) return;
-  const int pair0 = pg * pgs;
-  const int np = min(pgs, cnt - pair0);
-  const int64_t* ch = plan + kCosHdr + kCosSegWords * static_cast<int64_t>(n_seg) + kCosChunkWords * c;
-  const int64_t* sg = plan + kCosHdr + kCosSegWords * ch[0];
-  const int64_t first = ch[1];
-  const int nq = static_cast<int>(ch[2]);
-  const int I = static_cast<int>(sg[2]), B = static_cast<int>(sg[3]);
-  const bool row = sg[5] == kCosRow;
-  const int Pr = static_cast<int>(cos_row_pitch(I));
-  // column kind: first = o0 * B, nq = G * B -> elements o0 I B .. (o0 + G) I B; row kind:
-  // first = o0, nq = G -> o0 I .. (o0 + G) I: both first * I, nq * I
-  const int64_t off = sg[0] + first * I;
-  const float* gm[kM];
-  gm[0] = pr.a[pair0] + off;
+  });
+  if (!live) return;
+  float ps[4];
 #pragma unroll
-  for (int p = 0; p < kCosStagePairs; ++p) gm[p + 1] = pr.b[pair0 + (p < np ? p : 0)] + off;
-  if (row) cos_stage<true>(gm, np + 1, nq * I, sx, I, Pr);
-  else cos_stage<false>(gm, np + 1, nq * I, sx, I, Pr);
-  int mb[kM];  // LDS offset of each model's element 0 (the column kind keeps the 16-B phase)
-#pragma unroll
-  for (int m = 0; m < kM; ++m)
-    mb[m] = m * kCosStageStride + (row ? 0 : static_cast<int>((reinterpret_cast<uintptr_t>(gm[m]) >> 2) & 3));
-  __syncthreads();
-  const int64_t n_out = plan[1];
-  float* s = s_all + static_cast<int64_t>(pair0) * n_out + sg[4] + first;
-  if (row) cos_staged_body<true, 0>(sx, mb, sn, sy, sl, sr, np, nq, I, B, Pr, s, n_out);
-  else if (B == 9) cos_staged_body<false, 9>(sx, mb, sn, sy, sl, sr, np, nq, I, B, Pr, s, n_out);  // 3 x 3 convolutions
-  else cos_staged_body<false, 0>(sx, mb, sn, sy, sl, sr, np, nq, I, B, Pr, s, n_out);
+  for (int st = 0; st < 4; ++st) ps[st] = __fadd_rn(__fadd_rn(__fadd_rn(acc[st], a1[st]), a2[st]), a3[st]);
+  // the remainder (I mod 4 elements) lies in the last step, whose data is still in LDS
+  const int last = (k.I - 1) / kColIc * kColIc;
+  for (int gi = e4; gi < k.I; ++gi) ps[0] = __fadd_rn(ps[0], prod(xa[(gi - last) * B], xb[(gi - last) * B]));
+  const float v = __fadd_rn(__fadd_rn(__fadd_rn(ps[0], ps[1]), ps[2]), ps[3]);
+  s_all[static_cast<int64_t>(p0 + g) * n_out + k.out0 + c] = __fadd_rn(0.f, v);
 }
 
 // torch's serial full sum of s[0 .. n) (scalar_inner_sum below 8 elements, else
@@ -4798,13 +4646,13 @@ int32_t tal_agg_round_bf16(const uint16_t* pool_in, int64_t ld_in, uint16_t* poo
 
 static int cos_kind(int64_t I, int64_t B) { return I == 1 ? kCosElem : (B == 1 ? kCosRow : kCosCol); }
 
-// outputs per chunk of a tensor and whether its chunks are staged (k_cosine_staged: whole slabs
-// per chunk) or direct (k_cosine_outputs)
+// outputs per chunk of a tensor and whether its chunks are streamed (k_cos_col_norms /
+// k_cos_col_prods: Ob output blocks of the column kind) or direct (k_cosine_outputs)
 static int64_t cos_seg_per(int64_t A, int64_t I, int64_t B, bool* staged) {
   const int kind = cos_kind(I, B);
-  const int64_t g = cos_stage_slabs(kind, A, I, B);
-  *staged = g > 0;
-  return g > 0 ? g * (kind == kCosCol ? B : 1) : cos_chunk_outputs(kind);
+  *staged = cos_col_streamed(kind, I, B);
+  (void)A;
+  return *staged ? cos_col_ob(B) * B : cos_chunk_outputs(kind);
 }
 
 int64_t tal_cosine_plan_words(const int64_t* seg_host, int32_t n_seg) {
@@ -4842,8 +4690,8 @@ int32_t tal_cosine_plan_build(const int64_t* seg_host, int32_t n_seg, int64_t* p
     if (staged) n_staged += (A * B + sg[kCosSegWords * s + 6] - 1) / sg[kCosSegWords * s + 6];
     out += A * B;
   }
-  // the staged chunks first (k_cosine_staged takes chunks 0 .. n_staged - 1, k_cosine_outputs
-  // the rest); a chunk writes only its own outputs, so the order is free
+  // the streamed chunks first (k_cos_col_norms / k_cos_col_prods take chunks 0 .. n_staged - 1,
+  // k_cosine_outputs the rest); a chunk writes only its own outputs, so the order is free
   for (int pass = 1; pass >= 0; --pass) {
     for (int s = 0; s < n_seg; ++s) {
       const int64_t A = sg[kCosSegWords * s + 1], B = sg[kCosSegWords * s + 3], per = sg[kCosSegWords * s + 6];
@@ -4882,7 +4730,36 @@ int32_t tal_cosine_plan_set_threads(int64_t* plan_host, int32_t threads) {
 
 int64_t tal_cosine_scratch_bytes(const int64_t* plan_host, int32_t n_pairs) {
   if (!plan_host || n_pairs <= 0 || plan_host[0] <= 0 || plan_host[1] <= 0) return -1;
-  return static_cast<int64_t>(sizeof(float)) * (plan_host[1] + plan_host[0]) * std::min(n_pairs, kCosMaxPairs);
+  // per pair of one launch: its outputs and per-tensor means, and two model slots of norms
+  return static_cast<int64_t>(sizeof(float)) * (3 * plan_host[1] + plan_host[0]) * std::min(n_pairs, kCosMaxPairs);
+}
+
+// K2's side stream of the calling thread on the current device, and its fork / join events
+// (created on first use, kept for the thread's life: one per device it ran K2 on)
+struct CosSide {
+  int dev = -1;
+  hipStream_t stream = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
+static CosSide* cos_side() {
+  thread_local CosSide sides[16];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) {
+    g_err = "no current device";
+    return nullptr;
+  }
+  CosSide& c = sides[dev];
+  if (c.dev != dev) {
+    if (hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c.join, hipEventDisableTiming) != hipSuccess) {
+      g_err = "stream / event creation failed";
+      return nullptr;
+    }
+    c.dev = dev;
+  }
+  return &c;
 }
 
 int32_t tal_cosine_params(const float* const* a_ptrs_host, const float* const* b_ptrs_host,
@@ -4906,17 +4783,37 @@ int32_t tal_cosine_params(const float* const* a_ptrs_host, const float* const* b
     float* s_all = static_cast<float*>(scratch);
     float* means = s_all + n_out * cnt;
     const int64_t n_staged = plan_host[3];
-    // pairs sharing one `a` (sim_centrality_module_avg: the client against each neighbor) go
-    // kCosStagePairs to a workgroup, which stages and norms that a once; otherwise one pair each
+    // pairs sharing one `a` (sim_centrality_module_avg: the client against each neighbor): its
+    // norms once, and up to kColPairs pairs per product workgroup read its chunk once
     bool same_a = true;
     for (int j = 1; j < cnt; ++j) same_a = same_a && pr.a[j] == pr.a[0];
-    const int pgs = same_a ? kCosStagePairs : 1;
-    if (n_staged > 0)  // XCD-aware 1-D grid: 8 k + x = (chunk 8 (k / groups) + x, pair group k % groups)
-      k_cosine_staged<<<static_cast<unsigned>((n_staged + 7) / 8 * 8 * ((cnt + pgs - 1) / pgs)), kCosStageBlock, 0,
-                        s>>>(pr, plan_dev, n_seg, cnt, pgs, s_all);
+    // the direct chunks do not depend on the streamed ones: with both present they run on this
+    // thread's side stream for the device, forked from and joined back into `s`, so they fill the
+    // GPU beside the streamed kernels' workgroups
+    const bool fork = n_staged > 0 && n_chunks > n_staged;
+    hipStream_t so = s;
+    CosSide* side = nullptr;
+    if (fork) {
+      side = cos_side();
+      if (!side) return fail(TAL_ERR_HIP, "tal_cosine_params: side stream: " + g_err);
+      if (hipEventRecord(side->fork, s) != hipSuccess || hipStreamWaitEvent(side->stream, side->fork, 0) != hipSuccess)
+        return fail(TAL_ERR_HIP, "tal_cosine_params: fork");
+      so = side->stream;
+    }
     if (n_chunks > n_staged)
-      k_cosine_outputs<<<dim3(static_cast<unsigned>(n_chunks - n_staged), cnt), kCosBlock, 0, s>>>(pr, plan_dev, n_seg,
-                                                                                                  s_all);
+      k_cosine_outputs<<<dim3(static_cast<unsigned>(n_chunks - n_staged), cnt), kCosBlock, 0, so>>>(pr, plan_dev, n_seg,
+                                                                                                   s_all);
+    if (n_staged > 0) {
+      float* nrm = means + static_cast<int64_t>(n_seg) * cnt;  // model slots x n_out
+      const int n_models = same_a ? 1 + cnt : 2 * cnt;
+      const int ppw = same_a ? kColPairs : kColPairs / 2;
+      k_cos_col_norms<<<dim3(static_cast<unsigned>(n_staged), (n_models + 7) / 8), kColThreads, 0, s>>>(
+          pr, plan_dev, n_seg, cnt, same_a ? 1 : 0, nrm);
+      k_cos_col_prods<<<dim3(static_cast<unsigned>(n_staged), (cnt + ppw - 1) / ppw), kColThreads, 0, s>>>(
+          pr, plan_dev, n_seg, cnt, same_a ? 1 : 0, nrm, s_all);
+    }
+    if (fork && (hipEventRecord(side->join, so) != hipSuccess || hipStreamWaitEvent(s, side->join, 0) != hipSuccess))
+      return fail(TAL_ERR_HIP, "tal_cosine_params: join");
     k_cosine_means<<<dim3(n_seg, cnt), 64, 0, s>>>(plan_dev, n_seg, s_all, means);
     k_cosine_finish<<<cnt, 64, 0, s>>>(n_seg, means, out_dev, base);
   }

@@ -122,8 +122,11 @@ class RoundExecutor:
         return p
 
     def run(self, orders: Sequence[Sequence[int]], weights: Sequence[Sequence[float]],
-            out_rows: Optional[Sequence[int]] = None, sequential: bool = False) -> None:
-        """Aggregate pool rows: out_rows[r] <- sum_k weights[r][k] * pool[orders[r][k]]."""
+            out_rows: Optional[Sequence[int]] = None, sequential: bool = False,
+            plan: Optional[ops.RoundPlan] = None) -> None:
+        """Aggregate pool rows: out_rows[r] <- sum_k weights[r][k] * pool[orders[r][k]].
+        plan: what self.plan(orders, weights, out_rows) returned for these same lists (a caller
+        that repeats a round passes it back instead of having the lists hashed again)."""
         if out_rows is None:
             out_rows = list(range(len(orders)))
         if len(orders) == 0:
@@ -138,7 +141,8 @@ class RoundExecutor:
                 if lay.n_i64:
                     ops.agg_i64([self.pool.row_i64(j) for j in o], w, self.pool.row_i64(r))
             return
-        plan = self.plan(orders, weights, out_rows)
+        if plan is None:
+            plan = self.plan(orders, weights, out_rows)
         if self.double_buffer:
             if self.spare is None:
                 self.spare = self._new_scratch(plan, need=1)
