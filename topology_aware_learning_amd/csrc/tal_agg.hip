@@ -3411,6 +3411,7 @@ __global__ __launch_bounds__(kColThreads) void k_cos_col_norms(CosPairs pr, cons
   const float* x = lds + (live ? g * k.MS + o * k.P + kk : 0);
   const int B = k.B;
   float acc = 0.f;
+  bool in_range = true;  // every element zero or in cos_rdiv's range
   col_stream(L, k.I, B, lds, [&](int, int n) {
     if (!live) return;
     if (n == kColIc) {
@@ -3418,12 +3419,21 @@ __global__ __launch_bounds__(kColThreads) void k_cos_col_norms(CosPairs pr, cons
 #pragma unroll
       for (int i = 0; i < kColIc; ++i) v[i] = x[i * B];
 #pragma unroll
-      for (int i = 0; i < kColIc; ++i) acc = __fmaf_rn(v[i], v[i], acc);
+      for (int i = 0; i < kColIc; ++i) {
+        acc = __fmaf_rn(v[i], v[i], acc);
+        in_range = in_range && (cos_rdiv_x(v[i]) || v[i] == 0.f);
+      }
     } else {
-      for (int i = 0; i < n; ++i) acc = __fmaf_rn(x[i * B], x[i * B], acc);
+      for (int i = 0; i < n; ++i) {
+        acc = __fmaf_rn(x[i * B], x[i * B], acc);
+        in_range = in_range && (cos_rdiv_x(x[i * B]) || x[i * B] == 0.f);
+      }
     }
   });
-  if (live) nrm[static_cast<int64_t>(m0 + g) * plan[1] + k.out0 + c] = cos_clamp(cos_sqrt_rn(acc));
+  // the norm, negated when the chain has an element outside cos_rdiv's range (the products then
+  // check element by element); a NaN norm stays NaN either way
+  const float nv = cos_clamp(cos_sqrt_rn(acc));
+  if (live) nrm[static_cast<int64_t>(m0 + g) * plan[1] + k.out0 + c] = in_range ? nv : -nv;
 }
 
 // Products: one workgroup per (streamed chunk, group of pairs); thread (g, c): pair p0 + g, output
@@ -3437,7 +3447,9 @@ __global__ __launch_bounds__(kColThreads) void k_cos_col_prods(CosPairs pr, cons
                                                               int cnt, int same_a, const float* __restrict__ nrm,
                                                               float* __restrict__ s_all) {
   __shared__ float lds[kColModels * kColMS];
-  const ColChunk k = col_chunk(plan, n_seg, blockIdx.x);
+  // chunks in the reverse of the norms' order: the first workgroups read what the norms kernel
+  // read last, still in the 256 MiB last-level cache
+  const ColChunk k = col_chunk(plan, n_seg, gridDim.x - 1 - blockIdx.x);
   const int ppw = same_a ? kColPairs : kColPairs / 2;
   const int p0 = static_cast<int>(blockIdx.y) * ppw;
   if (p0 >= cnt) return;
@@ -3462,8 +3474,15 @@ __global__ __launch_bounds__(kColThreads) void k_cos_col_prods(CosPairs pr, cons
     na = nrm[sa * n_out + k.out0 + c];
     nb = nrm[sb * n_out + k.out0 + c];
   }
+  // a negative norm: its chain has an element outside cos_rdiv's range (k_cos_col_norms)
+  const bool checked = __float_as_uint(na) >> 31 || __float_as_uint(nb) >> 31;
+  na = fabsf(na);
+  nb = fabsf(nb);
   const float ya = __fdiv_rn(1.f, na), yb = __fdiv_rn(1.f, nb);
   const bool fast = cos_rdiv_n(na) && cos_rdiv_n(nb);
+  // both chains entirely in range (zeros included: a zero quotient's sign never reaches a sum,
+  // whose terms are added to +0): the reciprocal division without element checks
+  const bool sure = fast && !checked;
   const float* xa = lds + (live ? ma * k.MS + o * k.P + kk : 0);
   const float* xb = lds + (live ? mb * k.MS + o * k.P + kk : 0);
   const int B = k.B;
@@ -3479,7 +3498,12 @@ __global__ __launch_bounds__(kColThreads) void k_cos_col_prods(CosPairs pr, cons
   col_stream(L, k.I, B, lds, [&](int i0, int n) {
     if (!live) return;
     float p[kColIc];
-    if (n == kColIc && i0 + kColIc <= e4) {  // a whole step of stream elements (all but the last)
+    if (sure && n == kColIc && i0 + kColIc <= e4) {
+#pragma unroll
+      for (int i = 0; i < kColIc; ++i) p[i] = __fmul_rn(cos_rdiv(xa[i * B], na, ya), cos_rdiv(xb[i * B], nb, yb));
+#pragma unroll
+      for (int i = 0; i < kColIc; ++i) acc[i & 3] = __fadd_rn(acc[i & 3], p[i]);
+    } else if (n == kColIc && i0 + kColIc <= e4) {  // a whole step of stream elements (all but the last)
       // the reciprocal division for all 16, the IEEE one for the step if any element (or norm)
       // is outside its range: one branch per step
       bool ok = fast;
