@@ -3131,6 +3131,23 @@ __device__ __forceinline__ float cos_sqrt_rn(float x) { return __builtin_sqrtf(x
 
 __device__ __forceinline__ float cos_clamp(float n) { return n < 1e-6f ? 1e-6f : n; }  // NaN stays NaN
 
+// x / n with the IEEE division's result, without its scaling steps (each writes VCC, which the
+// next division's v_div_fmas reads, so divisions serialise): y = RN(1 / n) once per norm, then
+// q0 = RN(x y) and q = RN(q0 + RN(x - n q0) y) (both fused).  Equal to RN(x / n) for n in
+// [2^-40, 2^40] and |x| in [2^-50, 2^60) (every intermediate is normal, so the result depends
+// only on the two mantissas: all 2^46 pairs checked on the GPU, tools/div_exhaustive.hip,
+// profiles/r05/r05div); callers take __fdiv_rn outside it.
+__device__ __forceinline__ float cos_rdiv(float x, float n, float y) {
+  const float q0 = __fmul_rn(x, y);
+  return __fmaf_rn(__fmaf_rn(-n, q0, x), y, q0);
+}
+__device__ __forceinline__ bool cos_rdiv_x(float x) {  // |x| in [2^-50, 2^60)
+  return (__float_as_uint(x) & 0x7fffffffu) - 0x26800000u < 0x37000000u;
+}
+__device__ __forceinline__ bool cos_rdiv_n(float n) {  // n in [2^-40, 2^40]
+  return __float_as_uint(n) - 0x2B800000u <= 0x28000000u;
+}
+
 // Lane sums of one 8-thread group (threads g*8 .. g*8+7 of the wave) delivered to its thread 0
 // in lane order: out = first + v_0 + v_1 + ... + v_7 (every thread of the wave must call it).
 __device__ __forceinline__ float cos_group_fold(float first, float v, int gbase) {
@@ -3255,6 +3272,8 @@ __global__ __launch_bounds__(kCosBlock) void k_cosine_outputs(CosPairs pr, const
   }
   n1 = __shfl(n1, gbase, 64);
   n2 = __shfl(n2, gbase, 64);
+  // (the reciprocal division of the streamed column kernels, with its range checks here, ran
+  // the row tensors slower: 0.255 -> 0.335 ms for ResNet-50's, profiles/r06/r06k/r06k14)
   auto prod = [&](int64_t i) { return __fmul_rn(__fdiv_rn(x1[i], n1), __fdiv_rn(x2[i], n2)); };
   if (I < kCosVw) {  // scalar_inner_sum
     if (l == 0 && live) s[q] = __fadd_rn(0.f, cos_row_sum(prod, I));
@@ -3271,22 +3290,6 @@ __global__ __launch_bounds__(kCosBlock) void k_cosine_outputs(CosPairs pr, const
   if (l == 0 && live) s[q] = __fadd_rn(0.f, fin);
 }
 
-// x / n with the IEEE division's result, without its scaling steps (each writes VCC, which the
-// next division's v_div_fmas reads, so divisions serialise): y = RN(1 / n) once per norm, then
-// q0 = RN(x y) and q = RN(q0 + RN(x - n q0) y) (both fused).  Equal to RN(x / n) for n in
-// [2^-40, 2^40] and |x| in [2^-50, 2^60) (every intermediate is normal, so the result depends
-// only on the two mantissas: all 2^46 pairs checked on the GPU, tools/div_exhaustive.hip,
-// profiles/r05/r05div); callers take __fdiv_rn outside it.
-__device__ __forceinline__ float cos_rdiv(float x, float n, float y) {
-  const float q0 = __fmul_rn(x, y);
-  return __fmaf_rn(__fmaf_rn(-n, q0, x), y, q0);
-}
-__device__ __forceinline__ bool cos_rdiv_x(float x) {  // |x| in [2^-50, 2^60)
-  return (__float_as_uint(x) & 0x7fffffffu) - 0x26800000u < 0x37000000u;
-}
-__device__ __forceinline__ bool cos_rdiv_n(float n) {  // n in [2^-40, 2^40]
-  return __float_as_uint(n) - 0x2B800000u <= 0x28000000u;
-}
 
 // ---- streamed column chunks (see kColIc) ---------------------------------------------------
 struct ColChunk {
