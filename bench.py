@@ -55,7 +55,7 @@ def parse():
     p.add_argument("--stream-rows", type=int, default=0,
                    help="force a streamed plan with groups of at most this many rows (profiling)")
     p.add_argument("--in-place", action="store_true",
-                   help="N = 1, single-group plans: every round in place on one pool (RoundExecutor's own form)")
+                   help="N = 1, single-group plans: every round in place on one pool (RoundExecutor(double_buffer=False); the executor's default double-buffers like the timed loop)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bound of the CPU baseline sample (one call at a time; the two-concurrent-calls "

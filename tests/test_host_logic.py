@@ -930,3 +930,39 @@ def test_exchange_choice_follows_measured_link_rate():
         assert m["transpose"]["predicted_ms"] >= 0.9 * m["halo"]["predicted_ms"]
         flipped += 1
     assert flipped >= 2
+
+
+def test_cosine_plan_streams_column_tensors():
+    """K2's plan (host code, no GPU): column tensors with B < 32 (and 16-element runs) are the
+    streamed chunks, first, each Ob = 28 // B output blocks (1 from B = 28); the others direct;
+    the scratch covers outputs, means and two model slots of norms per pair of a launch."""
+    from topology_aware_learning_amd import ops
+    from topology_aware_learning_amd.arena import StateLayout
+
+    lay = synth.get_layout("resnet50")
+    segs = StateLayout.from_layout(lay).param_segments(synth.param_names(lay))
+    segs += [(0, 3, 50, 32), (0, 2, 70, 28), (0, 4, 2, 7)]
+    plan = ops.build_cosine_plan(segs)
+    h = plan.host
+    n_seg, n_out, n_staged = int(h[0]), int(h[1]), int(h[3])
+    sg = h[4: 4 + 7 * n_seg].reshape(n_seg, 7)
+    ch = h[4 + 7 * n_seg:].reshape(-1, 4)
+    assert len(ch) == plan.n_chunks
+    streamed = [(s, a, i, b) for s, (o, a, i, b) in enumerate(segs) if i > 1 and 1 < b < 32]
+    want = sum(-(-a // max(1, 28 // b)) for _, a, _, b in streamed)
+    assert n_staged == want
+    assert all(ch[:n_staged, 3] == 1) and all(ch[n_staged:, 3] == 0)
+    for s, a, i, b in streamed:
+        per = max(1, 28 // b) * b
+        assert sg[s][6] == per
+        rows = ch[:n_staged][ch[:n_staged, 0] == s]
+        assert list(rows[:, 1]) == list(range(0, a * b, per)) and rows[:, 2].sum() == a * b
+    assert set(ch[n_staged:, 0]) == set(range(n_seg)) - {s for s, *_ in streamed}
+    import ctypes
+
+    from topology_aware_learning_amd import _lib
+
+    P64 = ctypes.POINTER(ctypes.c_int64)
+    for n_pairs in (1, 8, 40):
+        got = _lib.load().tal_cosine_scratch_bytes(h.ctypes.data_as(P64), n_pairs)
+        assert got == 4 * (3 * n_out + n_seg) * min(n_pairs, 32)
