@@ -90,3 +90,40 @@ def test_staged_resnet50_model(cuda):
         sd = synth.synth_state_dict(lay, s)
         flat.append(torch.cat([v.reshape(-1) for (n, _, d), v in zip(lay, sd.values()) if d == "float32"]).numpy())
     _check(cuda, flat, segs, [0, 0, 0], [1, 2, 3])
+
+
+def test_streamed_and_direct_from_two_threads(cuda):
+    """A plan with streamed and direct chunks forks its direct chunks onto the calling thread's
+    side stream: two host threads, each on its own torch stream, calling K2 at once get the
+    oracle's values (each thread has its own side stream and events)."""
+    import threading
+
+    segs, off = [], 1
+    for a, i, b in [(8, 512, 9), (33, 512, 1), (61, 3, 9), (40, 7, 1), (30, 1, 1)]:
+        segs.append((off, a, i, b))
+        off += a * i * b + 5
+    rows = _models(np.random.default_rng(21), segs, 5)
+    dev = [torch.from_numpy(r).to(cuda) for r in rows]
+    plan = ops.build_cosine_plan(segs)
+    ref = [np.float32(oracle.cosine_model(rows[0], rows[j], segs)) for j in (1, 2, 3, 4)]
+    got, errs = {}, []
+
+    def run(k):
+        try:
+            s = torch.cuda.Stream(cuda)
+            with torch.cuda.stream(s):
+                for _ in range(5):
+                    out = ops.cosine([dev[0]] * 4, dev[1:], plan)
+                s.synchronize()
+            got[k] = out.cpu().numpy()
+        except Exception as exc:  # pragma: no cover - reported below
+            errs.append(exc)
+
+    ts = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs
+    for k in range(2):
+        assert [int(v.view(np.uint32)) for v in got[k]] == [int(v.view(np.uint32)) for v in ref]
