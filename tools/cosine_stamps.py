@@ -2,7 +2,9 @@
 diagnostic build of the library that stamps s_memtime at each phase boundary of k_cosine_staged
 (tools/tune/libtal_agg_stamps.so, TAL_LIB_PATH).  Prints per-phase median cycles over
 workgroups: plan reads, staging (loads + LDS writes + barrier), norms, level-0 runs, combine.
-usage: TAL_LIB_PATH=tools/tune/libtal_agg_stamps.so python tools/cosine_stamps.py 512,512,3,3"""
+usage: TAL_LIB_PATH=tools/tune/libtal_agg_stamps.so python tools/cosine_stamps.py 512,512,3,3
+Historical: it patches the slab-staged K2 kernel, which the streamed column kernels replaced
+(run it on a checkout of commit 17a9a02 or earlier; profiles/r06/stamps holds its output)."""
 import ctypes
 import json
 import sys

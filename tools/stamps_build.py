@@ -3,7 +3,9 @@ tools/tune/libtal_agg_stamps.so = csrc/tal_agg.hip with s_memtime stamps at the 
 of k_cosine_staged (kernel start, after the plan reads, after staging, after the norms, after the
 level-0 runs, end) written by thread 0 of each workgroup to a device array, and an extra export
 tal_debug_stamps(out, n) that copies them out.  tools/cosine_stamps.py reads them.
-usage: python tools/stamps_build.py"""
+usage: python tools/stamps_build.py
+Historical: it patches the slab-staged K2 kernel, which the streamed column kernels replaced
+(run it on a checkout of commit 17a9a02 or earlier; profiles/r06/stamps holds its output)."""
 import subprocess
 import sys
 from pathlib import Path
