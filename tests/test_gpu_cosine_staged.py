@@ -93,9 +93,9 @@ def test_staged_resnet50_model(cuda):
 
 
 def test_streamed_and_direct_from_two_threads(cuda):
-    """A plan with streamed and direct chunks forks its direct chunks onto the calling thread's
-    side stream: two host threads, each on its own torch stream, calling K2 at once get the
-    oracle's values (each thread has its own side stream and events)."""
+    """A plan with streamed and direct chunks forks its direct chunks onto the device's side
+    stream and joins them back through per-call events: two host threads, each on its own torch
+    stream, calling K2 at once get the oracle's values."""
     import threading
 
     segs, off = [], 1

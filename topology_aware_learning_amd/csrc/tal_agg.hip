@@ -4761,32 +4761,29 @@ int64_t tal_cosine_scratch_bytes(const int64_t* plan_host, int32_t n_pairs) {
   return static_cast<int64_t>(sizeof(float)) * (3 * plan_host[1] + plan_host[0]) * std::min(n_pairs, kCosMaxPairs);
 }
 
-// K2's side stream of the calling thread on the current device, and its fork / join events
-// (created on first use, kept for the thread's life: one per device it ran K2 on)
-struct CosSide {
-  int dev = -1;
-  hipStream_t stream = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
+// K2's side stream on the current device: created on first use and kept for the process (one
+// per device, shared by every calling thread: each call joins its own caller's stream through
+// its own events, so calls from several threads stay correct - their direct chunks queue on the
+// one side stream).  The fork / join events are made per call and released right after their
+// waits are enqueued (HIP frees a pending event's resources when it completes).
+static std::mutex g_cos_side_mu;
 
-static CosSide* cos_side() {
-  thread_local CosSide sides[16];
+static hipStream_t cos_side_stream() {
+  static hipStream_t side[64] = {};
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) {
-    g_err = "no current device";
-    return nullptr;
-  }
-  CosSide& c = sides[dev];
-  if (c.dev != dev) {
-    if (hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c.join, hipEventDisableTiming) != hipSuccess) {
-      g_err = "stream / event creation failed";
-      return nullptr;
-    }
-    c.dev = dev;
-  }
-  return &c;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(g_cos_side_mu);
+  if (!side[dev] && hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking) != hipSuccess) side[dev] = nullptr;
+  return side[dev];
+}
+
+// record an event on `from` and make `to` wait for it
+static bool cos_stream_wait(hipStream_t to, hipStream_t from) {
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+  const bool ok = hipEventRecord(e, from) == hipSuccess && hipStreamWaitEvent(to, e, 0) == hipSuccess;
+  hipEventDestroy(e);
+  return ok;
 }
 
 int32_t tal_cosine_params(const float* const* a_ptrs_host, const float* const* b_ptrs_host,
@@ -4814,18 +4811,15 @@ int32_t tal_cosine_params(const float* const* a_ptrs_host, const float* const* b
     // norms once, and up to kColPairs pairs per product workgroup read its chunk once
     bool same_a = true;
     for (int j = 1; j < cnt; ++j) same_a = same_a && pr.a[j] == pr.a[0];
-    // the direct chunks do not depend on the streamed ones: with both present they run on this
-    // thread's side stream for the device, forked from and joined back into `s`, so they fill the
-    // GPU beside the streamed kernels' workgroups
+    // the direct chunks do not depend on the streamed ones: with both present they run on the
+    // device's side stream, forked from and joined back into `s`, so they fill the GPU beside the
+    // streamed kernels' workgroups
     const bool fork = n_staged > 0 && n_chunks > n_staged;
     hipStream_t so = s;
-    CosSide* side = nullptr;
     if (fork) {
-      side = cos_side();
-      if (!side) return fail(TAL_ERR_HIP, "tal_cosine_params: side stream: " + g_err);
-      if (hipEventRecord(side->fork, s) != hipSuccess || hipStreamWaitEvent(side->stream, side->fork, 0) != hipSuccess)
-        return fail(TAL_ERR_HIP, "tal_cosine_params: fork");
-      so = side->stream;
+      so = cos_side_stream();
+      if (!so) return fail(TAL_ERR_HIP, "tal_cosine_params: side stream");
+      if (!cos_stream_wait(so, s)) return fail(TAL_ERR_HIP, "tal_cosine_params: fork");
     }
     if (n_chunks > n_staged)
       k_cosine_outputs<<<dim3(static_cast<unsigned>(n_chunks - n_staged), cnt), kCosBlock, 0, so>>>(pr, plan_dev, n_seg,
@@ -4839,8 +4833,7 @@ int32_t tal_cosine_params(const float* const* a_ptrs_host, const float* const* b
       k_cos_col_prods<<<dim3(static_cast<unsigned>(n_staged), (cnt + ppw - 1) / ppw), kColThreads, 0, s>>>(
           pr, plan_dev, n_seg, cnt, same_a ? 1 : 0, nrm, s_all);
     }
-    if (fork && (hipEventRecord(side->join, so) != hipSuccess || hipStreamWaitEvent(s, side->join, 0) != hipSuccess))
-      return fail(TAL_ERR_HIP, "tal_cosine_params: join");
+    if (fork && !cos_stream_wait(s, so)) return fail(TAL_ERR_HIP, "tal_cosine_params: join");
     k_cosine_means<<<dim3(n_seg, cnt), 64, 0, s>>>(plan_dev, n_seg, s_all, means);
     k_cosine_finish<<<cnt, 64, 0, s>>>(n_seg, means, out_dev, base);
   }
