@@ -453,8 +453,9 @@ class DecentrallearnApp:
             manual_seed(self.seed)
         if any(o for o, _, _ in per_gpu):
             if self._executor is None:
-                # in place per GPU pool: a spare would also carry the ghost rows every round
-                self._executor = [RoundExecutor(p, double_buffer=False) for p in mp.pools]
+                # double-buffered per GPU pool; the ghost rows are not carried into the spare (the
+                # next halo, or a per-call read, refreshes every ghost row before it is read)
+                self._executor = [RoundExecutor(p, carried_rows=len(mp.own[g])) for g, p in enumerate(mp.pools)]
             mp.exchange_halo()
             for g, (orders, weights, out_rows) in enumerate(per_gpu):
                 if orders:

@@ -125,7 +125,8 @@ def _barbell_file(tmp_path):
 def test_driver_batched_round_virtual_gpus(cuda, tmp_path, monkeypatch, strategy, world):
     """TAL_VIRTUAL_GPUS + TAL_BATCHED_ROUND: decentralized_main.py unchanged over `world` pools;
     after every halo each ghost row equals its owner's row bitwise, and each GPU's share of the
-    round equals the oracle's snapshot round over that pool (own and ghost rows), so the whole
+    round (double-buffered, the ghost rows not carried into the spare) equals the oracle's
+    snapshot round over that pool (own and ghost rows in) on the pool's own rows, so the whole
     round is the snapshot round of the models after training."""
     import oracle
     from oracle import reference_alg as ra
@@ -158,8 +159,10 @@ def test_driver_batched_round_virtual_gpus(cuda, tmp_path, monkeypatch, strategy
         ref, iref = f_in.copy(), i_in.copy()
         oracle.round_f32(f_in, rp, col, w, np.asarray(out_rows), pool_out=ref)
         oracle.round_i64(i_in, rp, col, w, np.asarray(out_rows), pool_out=iref)
-        assert np.array_equal(self.pool.f32[:, : lay.n_f32].cpu().numpy().view(np.uint32), ref.view(np.uint32))
-        assert np.array_equal(self.pool.i64[:, : lay.n_i64].cpu().numpy(), iref)
+        k = self.carried_rows  # the pool's own rows (ghost rows: stale until the next halo)
+        assert self.double_buffer and self.swaps >= 1 and k < self.pool.rows
+        assert np.array_equal(self.pool.f32[:k, : lay.n_f32].cpu().numpy().view(np.uint32), ref[:k].view(np.uint32))
+        assert np.array_equal(self.pool.i64[:k, : lay.n_i64].cpu().numpy(), iref[:k])
         seen["rows"].append(len(out_rows))
 
     monkeypatch.setattr(MultiPool, "exchange_halo", checked_halo)

@@ -53,13 +53,17 @@ class RoundExecutor:
     arena.select_pool_pair and DESIGN §5 "Pool placement"); `placement` records the times.  With
     no room for a spare the executor falls back to the form below.
 
-    double_buffer=False (and pools sharing memory with something else, e.g. MultiPool's): single
-    -group plans run in place on `pool`, whose placement is the caller's (`calibrated_pool`
+    carried_rows=k: rows >= k are not carried into the spare (MultiPool's ghost rows, refreshed
+    from their owners before every read).
+
+    double_buffer=False (and pools whose segments are views of a larger storage): single-group
+    plans run in place on `pool`, whose placement is the caller's (`calibrated_pool`
     places it before models are bound); multi-group plans write a scratch pool (snapshot
     semantics, placed like the spare) and copy the aggregated rows back."""
 
     def __init__(self, pool: ModelPool, scratch: Optional[ModelPool] = None, mode: int = ops.MODE_EXACT,
-                 placement_trials: int = 4, double_buffer: Optional[bool] = None):
+                 placement_trials: int = 4, double_buffer: Optional[bool] = None,
+                 carried_rows: Optional[int] = None):
         self.pool = pool
         self.scratch = scratch
         self.mode = mode
@@ -69,6 +73,10 @@ class RoundExecutor:
         if double_buffer is None:
             double_buffer = scratch is None and pool.device.type == "cuda" and pool.whole_storage()
         self.double_buffer = double_buffer
+        # rows a double-buffered round carries into the spare when it does not aggregate them:
+        # all (None), or rows below this (a MultiPool pool: its ghost rows are refreshed from their
+        # owners before every read, so the stale copies the exchange leaves there are never read)
+        self.carried_rows = pool.rows if carried_rows is None else int(carried_rows)
         self.spare: Optional[ModelPool] = None
         self.swaps = 0
 
@@ -113,7 +121,7 @@ class RoundExecutor:
             row_ptr, col, w = csr_from_lists(orders, weights)
             p = ops.default_plan(row_ptr, col, w, np.asarray(out_rows, np.int32),
                                  bf16=bool(self.pool.layout.n_b16), mode=self.mode).to(self.pool.device)
-            rest = sorted(set(range(self.pool.rows)) - set(int(r) for r in out_rows))
+            rest = sorted(set(range(self.carried_rows)) - set(int(r) for r in out_rows))
             # rows a double-buffered round does not aggregate: copied into the spare before the swap
             p.rest_rows = torch.as_tensor(rest, dtype=torch.long, device=self.pool.device) if rest else None
             if len(self._plans) > 64:
