@@ -3272,8 +3272,10 @@ __global__ __launch_bounds__(kCosBlock) void k_cosine_outputs(CosPairs pr, const
   }
   n1 = __shfl(n1, gbase, 64);
   n2 = __shfl(n2, gbase, 64);
-  // (the reciprocal division of the streamed column kernels, with its range checks here, ran
-  // the row tensors slower: 0.255 -> 0.335 ms for ResNet-50's, profiles/r06/r06k/r06k14)
+  // (the reciprocal division of the streamed column kernels does not pay here: with per-element
+  // range checks the row tensors ran 0.255 -> 0.335 ms for ResNet-50's, with one check per row
+  // (bounds of |x| gathered in the norm loop, a templated product phase) 0.259 ms; the row kind
+  // is bound by its loads, not its divisions; profiles/r06/r06k/r06k14, r06k17)
   auto prod = [&](int64_t i) { return __fmul_rn(__fdiv_rn(x1[i], n1), __fdiv_rn(x2[i], n2)); };
   if (I < kCosVw) {  // scalar_inner_sum
     if (l == 0 && live) s[q] = __fadd_rn(0.f, cos_row_sum(prod, I));
