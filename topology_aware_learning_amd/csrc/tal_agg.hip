@@ -3158,11 +3158,18 @@ __device__ __forceinline__ float cos_group_fold(float first, float v, int gbase)
 }
 
 __global__ __launch_bounds__(kCosBlock) void k_cosine_outputs(CosPairs pr, const int64_t* __restrict__ plan,
-                                                              int n_seg, float* __restrict__ s_all) {
-  const int pair = blockIdx.y;
+                                                              int n_seg, int cnt, int64_t n_direct,
+                                                              float* __restrict__ s_all) {
+  // XCD-aware order: dispatch deals workgroups round-robin over the 8 XCDs, so workgroup 8 k + x
+  // takes pair k % cnt of direct chunk 8 (k / cnt) + x: a chunk's pairs run one after another
+  // on XCD x, and all but the first find the chunk's `a` rows in that XCD's L2
+  const int64_t kq = blockIdx.x >> 3;
+  const int pair = static_cast<int>(kq % cnt);
+  const int64_t c = kq / cnt * 8 + (blockIdx.x & 7);
+  if (c >= n_direct) return;
   const int64_t n_out = plan[1];
   const int64_t* ch = plan + kCosHdr + kCosSegWords * static_cast<int64_t>(n_seg) +
-                      kCosChunkWords * (plan[3] + static_cast<int64_t>(blockIdx.x));  // after the staged chunks
+                      kCosChunkWords * (plan[3] + c);  // after the streamed chunks
   const int64_t* sg = plan + kCosHdr + kCosSegWords * ch[0];
   const int64_t first = ch[1], count = ch[2];
   const int64_t I = sg[2], B = sg[3];
@@ -4823,9 +4830,11 @@ int32_t tal_cosine_params(const float* const* a_ptrs_host, const float* const* b
       if (!so) return fail(TAL_ERR_HIP, "tal_cosine_params: side stream");
       if (!cos_stream_wait(so, s)) return fail(TAL_ERR_HIP, "tal_cosine_params: fork");
     }
-    if (n_chunks > n_staged)
-      k_cosine_outputs<<<dim3(static_cast<unsigned>(n_chunks - n_staged), cnt), kCosBlock, 0, so>>>(pr, plan_dev, n_seg,
-                                                                                                   s_all);
+    if (n_chunks > n_staged) {
+      const int64_t n_direct = n_chunks - n_staged;
+      k_cosine_outputs<<<static_cast<unsigned>((n_direct + 7) / 8 * 8 * cnt), kCosBlock, 0, so>>>(pr, plan_dev, n_seg,
+                                                                                                 cnt, n_direct, s_all);
+    }
     if (n_staged > 0) {
       float* nrm = means + static_cast<int64_t>(n_seg) * cnt;  // model slots x n_out
       const int n_models = same_a ? 1 + cnt : 2 * cnt;
